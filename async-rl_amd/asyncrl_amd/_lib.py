@@ -1,0 +1,101 @@
+"""ctypes binding of libasyncrl_hip.so (C ABI in include/asyncrl_hip.h).
+
+torch is imported first on purpose: torch ships its own libamdhip64.so
+(SONAME libamdhip64.so.7), so the extension resolves to the SAME HIP runtime
+instance and torch's streams / device pointers are valid in our calls.
+
+There is no fallback: if the shared object is missing the import fails loudly
+(build it with `python -c "import __graft_entry__ as g; g.build()"` or
+`make -C async-rl_amd/csrc`).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module doc)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libasyncrl_hip.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"asyncrl_amd: native extension not built ({LIB_PATH} missing); "
+        "run `make -C async-rl_amd/csrc` or __graft_entry__.build()")
+
+lib = ctypes.CDLL(LIB_PATH)
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_i64 = ctypes.c_int64
+c_u64 = ctypes.c_uint64
+c_double = ctypes.c_double
+
+# name -> (restype, argtypes); every symbol declared in include/asyncrl_hip.h
+SIGNATURES = {
+    "arl_abi_version": (c_int, []),
+    "arl_last_error": (ctypes.c_char_p, []),
+    "arl_current_screen": (c_int, [c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p]),
+    "arl_max_luminance": (c_int, [c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
+    "arl_phi_stack": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p]),
+    "arl_dqn_phi": (c_int, [c_void_p, c_void_p, c_i64, c_void_p]),
+    "arl_net_create": (c_int, [ctypes.POINTER(c_void_p), c_int, c_int, c_int, c_int, c_int, c_u64]),
+    "arl_net_destroy": (None, [c_void_p]),
+    "arl_net_param_floats": (c_i64, [c_void_p]),
+    "arl_net_param_count": (c_int, [c_void_p]),
+    "arl_net_param_info": (c_int, [c_void_p, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),
+                                   ctypes.c_char_p, c_int]),
+    "arl_net_workspace_bytes": (c_i64, [c_void_p]),
+    "arl_net_buffer": (c_int, [c_void_p, ctypes.c_char_p, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
+    "arl_net_bind": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "arl_net_reset": (c_int, [c_void_p, c_void_p]),
+    "arl_observe": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int, c_void_p]),
+    "arl_act": (c_int, [c_void_p, c_int, c_void_p]),
+    "arl_learn": (c_int, [c_void_p, c_double, c_double, c_double, c_int, c_void_p]),
+    "arl_optimize": (c_int, [c_void_p, c_double, c_i64, c_i64, c_double, c_double, c_double, c_void_p]),
+    "arl_advance": (c_int, [c_void_p, c_void_p]),
+    "arl_forward_states": (c_int, [c_void_p, c_void_p, c_i64, c_void_p]),
+    "arl_rmsprop": (c_int, [c_void_p, c_void_p, c_void_p, c_i64, c_double, c_double, c_double, c_double,
+                            c_void_p, c_void_p]),
+    "arl_policy": (c_int, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_u64, c_void_p,
+                           c_i64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                           c_void_p, c_void_p]),
+    "arl_returns_lossgrad": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_i64,
+                                     c_int, c_double, c_double, c_double, c_int, c_void_p, c_void_p, c_void_p,
+                                     c_void_p]),
+}
+
+for _name, (_res, _args) in SIGNATURES.items():
+    _fn = getattr(lib, _name)
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+ARCH_FF = 0
+ARCH_LSTM = 1
+RESIZE_SCALAR = 0
+RESIZE_SIMD = 1
+
+
+class ArlError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib.arl_last_error().decode(errors="replace")
+        raise ArlError(f"{what or 'asyncrl_hip'} failed (code {rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None passes NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ArlError("asyncrl_amd: tensors must live on the GPU (HIP device)")
+    if not t.is_contiguous():
+        raise ArlError("asyncrl_amd: tensors must be contiguous")
+    return t.data_ptr()
+
+
+def stream_handle(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream

@@ -1,0 +1,194 @@
+"""A3C agent and models on the MI355X hot path (drop-in for a3c.py / a3c_ale.py).
+
+Reference surfaces kept: `A3CModel` (a3c.py:15-24: pi_and_v, reset_state,
+unchain_backward), `A3CFF` / `A3CLSTM` (a3c_ale.py:28-70), `A3C` (a3c.py:27-185:
+__init__ arguments, act(state, reward, is_state_terminal), sync_parameters,
+load_model / save_model).
+
+What changes: the reference runs one env per process and updates
+shared parameters Hogwild-style whenever that env finishes a t_max window or
+an episode.  Here N envs step in lockstep on the GPU; every t_max steps one
+update is made from the sum of all envs' window-segment gradients at fixed
+parameters (a terminal inside a window closes that env's segment with R = 0,
+exactly like a3c.py:82-83), all-reduced over ranks with RCCL when
+torch.distributed is initialised, then clipped (40) and applied by
+RMSpropAsync.  Hogwild races are gone; replicas stay bitwise identical.
+
+`act` takes the raw frame pair of each env (frame 3 and frame 4 of the
+4-frame skip, ale.py:118-119,134-135) -- the phi pre-stage runs on the GPU --
+together with the reward and terminal flag of the transition into it.
+Following batched-env convention, a terminal env's observation is already the
+first frame of its next episode (auto-reset); the reference spends a separate
+act(.., is_state_terminal=True) call on the terminal state instead.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ._lib import ARCH_FF, ARCH_LSTM, RESIZE_SCALAR
+from .net import DeviceNet, init_like_torch
+from .policy_output import SoftmaxPolicyOutput
+
+
+class A3CModel:
+    """a3c.py:15-24."""
+
+    arch = ARCH_FF
+
+    def __init__(self, n_actions: int, n_envs: int = 1, t_max: int = 5, seed: int = 0, env_offset: int = 0,
+                 init_seed: int | None = 0, device=None):
+        self.n_actions = n_actions
+        self.net = DeviceNet(self.arch, n_actions, n_envs, t_max, env_offset=env_offset, seed=seed,
+                             device=device)
+        if init_seed is not None:
+            self.net.load_params(init_like_torch(self.arch, n_actions, np.random.default_rng(init_seed)))
+
+    def pi_and_v(self, state: torch.Tensor, keep_same_state: bool = False):
+        """state: (n, 4, 84, 84) f32 (dqn_phi output).  FF only; the LSTM
+        model's recurrent forward runs inside A3C.act."""
+        self.net.forward_states(state.contiguous())
+        o = self.net.step_outputs(self.net.t_max)
+        n = state.shape[0]
+        o = {k: v[:n] for k, v in o.items()}
+        return SoftmaxPolicyOutput(o), o["v"]
+
+    def reset_state(self):
+        pass
+
+    def unchain_backward(self):
+        pass
+
+    def namedparams(self):
+        return self.net.state_dict()
+
+
+class A3CFF(A3CModel):
+    """a3c_ale.py:28-40: NIPSDQNHead -> FCSoftmaxPolicy + FCVFunction."""
+    arch = ARCH_FF
+
+
+class A3CLSTM(A3CModel):
+    """a3c_ale.py:43-70: NIPSDQNHead -> L.LSTM(256, 256) -> policy + value."""
+    arch = ARCH_LSTM
+
+    def pi_and_v(self, state, keep_same_state=False):
+        raise NotImplementedError("A3CLSTM forward runs inside A3C.act (recurrent state is on device)")
+
+
+class A3C:
+    """a3c.py:27-185, lockstep-batched.  One `act` call = one env-step of all
+    n_envs envs; every t_max calls it also performs the update."""
+
+    def __init__(self, model: A3CModel, optimizer, t_max: int, gamma: float, beta: float = 1e-2,
+                 process_idx: int = 0, clip_reward: bool = True, phi=None, pi_loss_coef: float = 1.0,
+                 v_loss_coef: float = 0.5, keep_loss_scale_same: bool = False, resize_mode: int = RESIZE_SCALAR,
+                 process_group=None):
+        if pi_loss_coef != 1.0 or keep_loss_scale_same:
+            raise NotImplementedError("pi_loss_coef != 1 / keep_loss_scale_same are not supported yet")
+        if model.net.t_max != t_max:
+            raise ValueError("model was built for a different t_max")
+        self.shared_model = model          # device params are shared by construction
+        self.model = model
+        self.optimizer = optimizer
+        if optimizer.target is None:
+            optimizer.setup(model)
+        self.t_max, self.gamma, self.beta = t_max, gamma, beta
+        self.process_idx, self.clip_reward = process_idx, clip_reward
+        self.v_loss_coef = v_loss_coef
+        self.resize_mode = resize_mode
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.t = 0          # env-steps taken (per env)
+        self.net = model.net
+        self.net.reset()
+
+    def sync_parameters(self):
+        """a3c.py:63-65 -- a no-op: actors read the device parameters."""
+
+    # ------------------------------------------------------------ window pieces
+    def _update(self, stream=None):
+        net = self.net
+        net.learn(self.gamma, self.beta, self.v_loss_coef, self.clip_reward, stream=stream)
+        if self.world > 1:
+            dist.all_reduce(net.grads, op=dist.ReduceOp.SUM, group=self.pg)
+        self.optimizer.update(stream=stream)
+        net.advance(stream=stream)
+
+    def act(self, pairs: torch.Tensor, reward=None, is_state_terminal=None) -> torch.Tensor:
+        """a3c.py:67-167, batched.  pairs: (n, 2, 210, 160, 3) uint8 device
+        tensor (frame 4, frame 3 of the skip); reward: (n,) f32 (clipped to
+        [-1, 1] as at a3c.py:69-70); is_state_terminal: (n,) uint8/bool, the
+        transition into this observation ended the episode.  Returns the
+        sampled actions (n,) int32 (device)."""
+        net, T = self.net, self.t_max
+        r = None if reward is None else torch.as_tensor(reward, dtype=torch.float32, device=net.device).contiguous()
+        d = None if is_state_terminal is None else \
+            torch.as_tensor(is_state_terminal, device=net.device).to(torch.uint8).contiguous()
+        pairs = pairs.contiguous()
+        if self.t == 0:
+            net.observe(0, pairs, r, d, 1, force_reset=True, resize_mode=self.resize_mode)
+            net.act(0)
+            ta = 0
+        elif self.t % T == 0:
+            net.observe(T, pairs, r, d, 1, resize_mode=self.resize_mode)
+            net.act(T)                       # bootstrap v(s_T), pre-update params
+            self._update()
+            net.act(0)                       # a3c.py:154-164 with post-update params
+            ta = 0
+        else:
+            ta = self.t % T
+            net.observe(ta, pairs, r, d, 1, resize_mode=self.resize_mode)
+            net.act(ta)
+        self.t += 1
+        return net.step_outputs(ta)["actions"]
+
+    def run_window(self, pair_pool, reward_pool, done_pool, pool_len: int, first: bool = False, stream=None,
+                   split_update: bool = False):
+        """One full lockstep window over device-resident pools (graph
+        capturable when first=False): T x (phi, forward, sample), bootstrap,
+        learn, [all-reduce], clip + RMSProp, advance."""
+        net, T = self.net, self.t_max
+        if first:
+            net.observe(0, pair_pool, reward_pool, done_pool, pool_len, force_reset=True,
+                        resize_mode=self.resize_mode, stream=stream)
+        for t in range(T):
+            if t > 0:
+                net.observe(t, pair_pool, reward_pool, done_pool, pool_len, resize_mode=self.resize_mode,
+                            stream=stream)
+            net.act(t, stream=stream)
+        net.observe(T, pair_pool, reward_pool, done_pool, pool_len, resize_mode=self.resize_mode, stream=stream)
+        net.act(T, stream=stream)
+        net.learn(self.gamma, self.beta, self.v_loss_coef, self.clip_reward, stream=stream)
+        if split_update:
+            return
+        self.finish_window(stream=stream)
+
+    def finish_window(self, stream=None):
+        if self.world > 1:
+            dist.all_reduce(self.net.grads, op=dist.ReduceOp.SUM, group=self.pg)
+        self.optimizer.update(stream=stream)
+        self.net.advance(stream=stream)
+        self.t += self.t_max
+
+    # ------------------------------------------------------------ checkpoints
+    def save_model(self, model_filename: str):
+        """a3c.py:181-185: model params + optimizer state ('.opt').  Stored
+        as .npz with the Chainer HDF5 paths as keys ('0/0/W' -> '0|0|W')."""
+        net = self.net
+        np.savez(model_filename, **{k.replace("/", "|"): v for k, v in net.state_dict().items()})
+        np.savez(model_filename + ".opt", **{k.replace("/", "|"): v for k, v in net.state_dict(net.ms).items()})
+
+    def load_model(self, model_filename: str):
+        """a3c.py:169-179 (loads the '.opt' state when present)."""
+        net = self.net
+        with np.load(model_filename if model_filename.endswith(".npz") else model_filename + ".npz") as z:
+            net.load_params({k.replace("|", "/"): z[k] for k in z.files})
+        opt = model_filename + ".opt.npz"
+        if os.path.exists(opt):
+            with np.load(opt) as z:
+                for k in z.files:
+                    net.view(net.ms, k.replace("|", "/")).copy_(torch.from_numpy(z[k]))

@@ -1,0 +1,154 @@
+"""Device-resident A3C model + lockstep actor-learner workspace.
+
+Replaces the reference's process-shared parameters (async.py:11-65:
+RawArray-backed params and RMSProp `ms`, Hogwild writes) with ONE flat fp32
+parameter buffer, one flat gradient buffer and one flat `ms` buffer in HBM,
+laid out in Chainer namedparams order (a3c_ale.py:35,52) so checkpoints map
+1:1 (HDF5 paths "0/0/W", ...).  PyTorch only allocates the memory; all
+compute is in libasyncrl_hip.so.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from ._lib import ARCH_FF, ARCH_LSTM, RESIZE_SCALAR, check, lib, ptr, stream_handle
+
+
+def param_shapes(arch: int, n_actions: int):
+    """Chainer parameter shapes in link order (dqn_head.py:40-44,
+    policy.py:49, v_function.py:25, Chainer L.LSTM upward/lateral)."""
+    head = [("0/0/W", (16, 4, 8, 8)), ("0/0/b", (16,)), ("0/1/W", (32, 16, 4, 4)), ("0/1/b", (32,)),
+            ("0/2/W", (256, 2592)), ("0/2/b", (256,))]
+    if arch == ARCH_FF:
+        return head + [("1/0/W", (n_actions, 256)), ("1/0/b", (n_actions,)), ("2/0/W", (1, 256)),
+                       ("2/0/b", (1,))]
+    return head + [("1/upward/W", (1024, 256)), ("1/upward/b", (1024,)), ("1/lateral/W", (1024, 256)),
+                   ("2/0/W", (n_actions, 256)), ("2/0/b", (n_actions,)), ("3/0/W", (1, 256)),
+                   ("3/0/b", (1,))]
+
+
+def init_like_torch(arch: int, n_actions: int, rng: np.random.Generator):
+    """init_like_torch.py:5-22: U(+-1/sqrt(fan_in)) for every W and b
+    (fan_in = in*kh*kw); host-side setup, not on the hot path."""
+    shapes = dict(param_shapes(arch, n_actions))
+    out = {}
+    for name, shape in param_shapes(arch, n_actions):
+        w = shapes[name.rsplit("/", 1)[0] + "/W"]
+        stdv = 1.0 / np.sqrt(int(np.prod(w[1:])))
+        out[name] = rng.uniform(-stdv, stdv, size=shape).astype(np.float32)
+    return out
+
+
+class DeviceNet:
+    """One arl_net handle + the device memory it borrows."""
+
+    def __init__(self, arch: int, n_actions: int, n_envs: int, t_max: int = 5, env_offset: int = 0,
+                 seed: int = 0, device=None):
+        self.device = torch.device(device if device is not None else "cuda")
+        self.arch, self.n_actions, self.n_envs, self.t_max = arch, n_actions, n_envs, t_max
+        self.env_offset, self.seed = env_offset, seed
+        h = ctypes.c_void_p()
+        check(lib.arl_net_create(ctypes.byref(h), arch, n_actions, n_envs, t_max, env_offset, seed),
+              "arl_net_create")
+        self._h = h
+        P = lib.arl_net_param_floats(h)
+        self.param_floats = P
+        self.params = torch.zeros(P, dtype=torch.float32, device=self.device)
+        self.grads = torch.zeros(P, dtype=torch.float32, device=self.device)
+        self.ms = torch.zeros(P, dtype=torch.float32, device=self.device)
+        self.workspace = torch.zeros(lib.arl_net_workspace_bytes(h), dtype=torch.uint8, device=self.device)
+        check(lib.arl_net_bind(h, ptr(self.params), ptr(self.grads), ptr(self.ms), ptr(self.workspace)),
+              "arl_net_bind")
+        self.layout = {}
+        shapes = dict(param_shapes(arch, n_actions))
+        name = ctypes.create_string_buffer(64)
+        for i in range(lib.arl_net_param_count(h)):
+            off, num = ctypes.c_int64(), ctypes.c_int64()
+            check(lib.arl_net_param_info(h, i, ctypes.byref(off), ctypes.byref(num), name, 64))
+            key = name.value.decode()
+            assert int(np.prod(shapes[key])) == num.value, key
+            self.layout[key] = (off.value, shapes[key])
+        self.n_params = sum(int(np.prod(s)) for _, s in self.layout.values())
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.arl_net_destroy(h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ------------------------------------------------------------ params
+    def view(self, flat: torch.Tensor, name: str) -> torch.Tensor:
+        off, shape = self.layout[name]
+        return flat[off:off + int(np.prod(shape))].view(shape)
+
+    def param(self, name: str) -> torch.Tensor:
+        return self.view(self.params, name)
+
+    def grad(self, name: str) -> torch.Tensor:
+        return self.view(self.grads, name)
+
+    def load_params(self, arrays: dict) -> None:
+        for name, (off, shape) in self.layout.items():
+            a = np.asarray(arrays[name], dtype=np.float32).reshape(shape)
+            self.param(name).copy_(torch.from_numpy(a))
+
+    def state_dict(self, flat: torch.Tensor | None = None) -> dict:
+        flat = self.params if flat is None else flat
+        return {n: self.view(flat, n).detach().cpu().numpy().copy() for n in self.layout}
+
+    # ------------------------------------------------------------ workspace
+    def buffer(self, name: str, dtype=torch.uint8, shape=None) -> torch.Tensor:
+        off, nb = ctypes.c_int64(), ctypes.c_int64()
+        check(lib.arl_net_buffer(self._h, name.encode(), ctypes.byref(off), ctypes.byref(nb)), "arl_net_buffer")
+        raw = self.workspace[off.value:off.value + nb.value]
+        t = raw.view(dtype)
+        return t.view(shape) if shape is not None else t
+
+    # ------------------------------------------------------------ hot path
+    def reset(self, stream=None):
+        check(lib.arl_net_reset(self._h, stream_handle(stream)), "arl_net_reset")
+
+    def observe(self, t: int, pair_pool: torch.Tensor, reward_pool=None, done_pool=None, pool_len: int = 1,
+                force_reset: bool = False, resize_mode: int = RESIZE_SCALAR, stream=None):
+        check(lib.arl_observe(self._h, t, ptr(pair_pool), ptr(reward_pool), ptr(done_pool), pool_len,
+                              int(force_reset), resize_mode, stream_handle(stream)), "arl_observe")
+
+    def act(self, t: int, stream=None):
+        check(lib.arl_act(self._h, t, stream_handle(stream)), "arl_act")
+
+    def learn(self, gamma=0.99, beta=1e-2, v_loss_coef=0.5, clip_reward=True, stream=None):
+        check(lib.arl_learn(self._h, gamma, beta, v_loss_coef, int(clip_reward), stream_handle(stream)),
+              "arl_learn")
+
+    def optimize(self, lr0=7e-4, total_steps=0, n_total=0, alpha=0.99, eps=0.1, clip=40.0, stream=None):
+        check(lib.arl_optimize(self._h, lr0, int(total_steps), int(n_total), alpha, eps, clip,
+                               stream_handle(stream)), "arl_optimize")
+
+    def advance(self, stream=None):
+        check(lib.arl_advance(self._h, stream_handle(stream)), "arl_advance")
+
+    def forward_states(self, states: torch.Tensor, stream=None):
+        n = states.shape[0]
+        check(lib.arl_forward_states(self._h, ptr(states), n, stream_handle(stream)), "arl_forward_states")
+
+    # ------------------------------------------------------------ outputs
+    def step_outputs(self, t: int) -> dict:
+        """Views of the policy / value outputs of window step t."""
+        N, A, T1 = self.n_envs, self.n_actions, self.t_max + 1
+        f32 = torch.float32
+        return {
+            "logits": self.buffer("logits", f32, (T1, N, A))[t],
+            "probs": self.buffer("probs", f32, (T1, N, A))[t],
+            "log_probs": self.buffer("logp", f32, (T1, N, A))[t],
+            "v": self.buffer("v", f32, (T1, N))[t],
+            "entropy": self.buffer("entropy", f32, (T1, N))[t],
+            "actions": self.buffer("actions", torch.int32, (T1, N))[t],
+            "action_log_probs": self.buffer("logp_a", f32, (T1, N))[t],
+        }

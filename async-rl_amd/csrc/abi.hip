@@ -1,0 +1,239 @@
+// C ABI of libasyncrl_hip.so (declared in include/asyncrl_hip.h).
+// Argument validation lives here; kernels assume validated shapes.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+
+#include "../../include/asyncrl_hip.h"
+#include "arl_internal.hpp"
+
+struct arl_net {
+  arl::Net net;
+  bool bound = false;
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+int hip_status(hipError_t e, const char* what) {
+  if (e == hipSuccess) return ARL_OK;
+  return fail(ARL_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
+hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+}  // namespace
+
+extern "C" {
+
+int arl_abi_version(void) { return 1; }
+const char* arl_last_error(void) { return g_err.c_str(); }
+
+int arl_current_screen(const uint8_t* cur, const uint8_t* prev, uint8_t* out, int64_t n, int mode, void* s) {
+  if (n < 0 || (n > 0 && (!cur || !prev || !out))) return fail(ARL_EINVAL, "current_screen: null pointer / n < 0");
+  if (!aligned(cur, 16) || !aligned(prev, 16) || !aligned(out, 4))
+    return fail(ARL_EINVAL, "current_screen: frames must be 16-byte aligned, out 4-byte aligned");
+  if (mode != ARL_RESIZE_SCALAR && mode != ARL_RESIZE_SIMD) return fail(ARL_EINVAL, "bad resize_mode");
+  if (n > 65535) return fail(ARL_EINVAL, "current_screen: n > 65535 per call");
+  return hip_status(arl::launch_current_screen(cur, prev, out, n, mode, S(s)), "current_screen");
+}
+
+int arl_max_luminance(const uint8_t* cur, const uint8_t* prev, uint8_t* gray, int64_t npix, void* s) {
+  if (npix < 0 || (npix > 0 && (!cur || !prev || !gray))) return fail(ARL_EINVAL, "max_luminance: null / npix < 0");
+  if (npix > ((int64_t)1 << 31) * 255) return fail(ARL_EINVAL, "max_luminance: npix too large");
+  return hip_status(arl::launch_max_luminance(cur, prev, gray, npix, S(s)), "max_luminance");
+}
+
+int arl_phi_stack(const uint8_t* pairs, const uint8_t* prev_stack, const uint8_t* reset, uint8_t* out_stack,
+                  int64_t n, int mode, void* s) {
+  if (n < 0 || (n > 0 && (!pairs || !prev_stack || !out_stack)))
+    return fail(ARL_EINVAL, "phi_stack: null pointer / n < 0");
+  if (!aligned(pairs, 16) || !aligned(prev_stack, 16) || !aligned(out_stack, 16))
+    return fail(ARL_EINVAL, "phi_stack: buffers must be 16-byte aligned");
+  if (prev_stack == out_stack && n > 0) return fail(ARL_EINVAL, "phi_stack: prev_stack and out_stack alias");
+  if (mode != ARL_RESIZE_SCALAR && mode != ARL_RESIZE_SIMD) return fail(ARL_EINVAL, "bad resize_mode");
+  if (n > 65535) return fail(ARL_EINVAL, "phi_stack: n > 65535 per call");
+  return hip_status(arl::launch_phi_stack(pairs, prev_stack, reset, out_stack, n, mode, S(s)), "phi_stack");
+}
+
+int arl_dqn_phi(const uint8_t* in, float* out, int64_t n, void* s) {
+  if (n < 0 || (n > 0 && (!in || !out))) return fail(ARL_EINVAL, "dqn_phi: null pointer / n < 0");
+  if (!aligned(in, 4) || !aligned(out, 16)) return fail(ARL_EINVAL, "dqn_phi: in 4-byte, out 16-byte aligned");
+  return hip_status(arl::launch_dqn_phi(in, out, n * 4 * arl::PLANE, S(s)), "dqn_phi");
+}
+
+int arl_net_create(arl_net** out, int arch, int n_actions, int n_envs, int t_max, int env_offset, uint64_t seed) {
+  if (!out) return fail(ARL_EINVAL, "net_create: out is null");
+  arl_net* h = new arl_net();
+  std::string err;
+  if (!arl::net_init(h->net, arch, n_actions, n_envs, t_max, env_offset, seed, err)) {
+    delete h;
+    return fail(ARL_EINVAL, "net_create: " + err);
+  }
+  *out = h;
+  return ARL_OK;
+}
+
+void arl_net_destroy(arl_net* h) { delete h; }
+
+int64_t arl_net_param_floats(const arl_net* h) { return h ? h->net.param_floats : -1; }
+int arl_net_param_count(const arl_net* h) { return h ? (int)h->net.params.size() : -1; }
+
+int arl_net_param_info(const arl_net* h, int idx, int64_t* offset, int64_t* numel, char* name, int cap) {
+  if (!h || idx < 0 || idx >= (int)h->net.params.size()) return fail(ARL_EINVAL, "param_info: bad index");
+  const arl::ParamInfo& p = h->net.params[idx];
+  if (offset) *offset = p.offset;
+  if (numel) *numel = p.numel;
+  if (name && cap > 0) {
+    strncpy(name, p.name.c_str(), (size_t)cap - 1);
+    name[cap - 1] = 0;
+  }
+  return ARL_OK;
+}
+
+int64_t arl_net_workspace_bytes(const arl_net* h) { return h ? h->net.ws_bytes : -1; }
+
+int arl_net_buffer(const arl_net* h, const char* name, int64_t* offset, int64_t* bytes) {
+  if (!h || !name) return fail(ARL_EINVAL, "net_buffer: null");
+  for (const auto& b : h->net.bufs)
+    if (strcmp(b.name, name) == 0) {
+      if (offset) *offset = b.off;
+      if (bytes) *bytes = b.bytes;
+      return ARL_OK;
+    }
+  return fail(ARL_EINVAL, std::string("net_buffer: unknown buffer ") + name);
+}
+
+int arl_net_bind(arl_net* h, float* params, float* grads, float* ms, void* ws) {
+  if (!h || !params || !grads || !ms || !ws) return fail(ARL_EINVAL, "net_bind: null pointer");
+  if (!aligned(params, 16) || !aligned(grads, 16) || !aligned(ms, 16) || !aligned(ws, 256))
+    return fail(ARL_EINVAL, "net_bind: params/grads/ms 16-byte aligned, workspace 256-byte aligned");
+  h->net.p = params;
+  h->net.g = grads;
+  h->net.ms = ms;
+  h->net.ws = reinterpret_cast<char*>(ws);
+  h->bound = true;
+  return ARL_OK;
+}
+
+#define NEED_BOUND(h)                                                         \
+  do {                                                                        \
+    if (!(h)) return fail(ARL_EINVAL, "null net");                            \
+    if (!(h)->bound) return fail(ARL_ESTATE, "net not bound (arl_net_bind)"); \
+  } while (0)
+
+int arl_net_reset(arl_net* h, void* s) {
+  NEED_BOUND(h);
+  arl::Net& n = h->net;
+  hipError_t e = hipMemsetAsync(n.ws + n.w_ctl, 0, arl::CTL_SIZE * 8, S(s));
+  if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_nvalid, 0, (size_t)n.R * n.N, S(s));
+  if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_reset, 1, (size_t)(n.T + 1) * n.N, S(s));
+  if (e == hipSuccess && n.arch == arl::ARCH_LSTM) {
+    e = hipMemsetAsync(n.ws + n.w_hbuf, 0, (size_t)(n.T + 2) * n.N * arl::HID * 4, S(s));
+    if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_cbuf, 0, (size_t)(n.T + 2) * n.N * arl::HID * 4, S(s));
+  }
+  return hip_status(e, "net_reset");
+}
+
+int arl_observe(arl_net* h, int t, const uint8_t* pair_pool, const float* reward_pool, const uint8_t* done_pool,
+                int64_t pool_len, int force_reset, int mode, void* s) {
+  NEED_BOUND(h);
+  arl::Net& n = h->net;
+  if (t < 0 || t > n.T) return fail(ARL_EINVAL, "observe: t out of [0, t_max]");
+  if (!pair_pool || pool_len < 1) return fail(ARL_EINVAL, "observe: need pair_pool and pool_len >= 1");
+  if (!aligned(pair_pool, 16)) return fail(ARL_EINVAL, "observe: pair_pool must be 16-byte aligned");
+  if (mode != ARL_RESIZE_SCALAR && mode != ARL_RESIZE_SIMD) return fail(ARL_EINVAL, "bad resize_mode");
+  if (n.N > 65535) return fail(ARL_EINVAL, "observe: n_envs > 65535");
+  arl::RingArgs a;
+  a.pair_pool = pair_pool;
+  a.reward_pool = reward_pool;
+  a.done_pool = done_pool;
+  a.pool_len = pool_len;
+  a.frames = n.at<uint8_t>(n.w_frames);
+  a.nvalid = n.at<uint8_t>(n.w_nvalid);
+  a.reset_flags = n.at<uint8_t>(n.w_reset);
+  a.rewards = n.at<float>(n.w_rewards);
+  a.dones = n.at<uint8_t>(n.w_dones);
+  a.ctl = n.at<int64_t>(n.w_ctl);
+  a.n = n.N;
+  a.R = n.R;
+  a.t = t;
+  a.mode = mode;
+  a.force_reset = force_reset ? 1 : 0;
+  return hip_status(arl::launch_phi_ring(a, S(s)), "observe");
+}
+
+int arl_act(arl_net* h, int t, void* s) {
+  NEED_BOUND(h);
+  if (t < 0 || t > h->net.T) return fail(ARL_EINVAL, "act: t out of [0, t_max]");
+  return hip_status(arl::net_act(h->net, t, 1, S(s)), "act");
+}
+
+int arl_learn(arl_net* h, double gamma, double beta, double vcoef, int clip_reward, void* s) {
+  NEED_BOUND(h);
+  return hip_status(arl::net_learn(h->net, gamma, (float)beta, (float)vcoef, clip_reward, S(s)), "learn");
+}
+
+int arl_optimize(arl_net* h, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps, double clip,
+                 void* s) {
+  NEED_BOUND(h);
+  return hip_status(arl::net_optimize(h->net, lr0, total_steps, n_total, alpha, eps, (float)clip, S(s)), "optimize");
+}
+
+int arl_advance(arl_net* h, void* s) {
+  NEED_BOUND(h);
+  return hip_status(arl::net_advance(h->net, S(s)), "advance");
+}
+
+int arl_forward_states(arl_net* h, const float* x, int64_t n, void* s) {
+  NEED_BOUND(h);
+  if (h->net.arch != arl::ARCH_FF) return fail(ARL_ESTATE, "forward_states: FF only (LSTM keeps state)");
+  if (!x || n < 1 || n > h->net.N) return fail(ARL_EINVAL, "forward_states: need 1 <= n <= n_envs");
+  return hip_status(arl::net_forward_f32(h->net, x, (int)n, nullptr, nullptr, S(s)), "forward_states");
+}
+
+int arl_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, double alpha, double eps, double clip,
+                double* parts, void* s) {
+  if (n < 0 || (n > 0 && (!p || !ms || !g))) return fail(ARL_EINVAL, "rmsprop: null pointer / n < 0");
+  if (!aligned(p, 16) || !aligned(ms, 16) || !aligned(g, 16)) return fail(ARL_EINVAL, "rmsprop: 16-byte alignment");
+  if (clip > 0 && !parts) return fail(ARL_EINVAL, "rmsprop: clip needs norm_partials scratch");
+  hipError_t e = hipSuccess;
+  const int blocks = 1024;
+  if (clip > 0) e = arl::launch_grad_sqnorm(g, n, parts, blocks, S(s));
+  if (e == hipSuccess)
+    e = arl::launch_rmsprop(p, ms, g, n, lr, alpha, eps, clip > 0 ? parts : nullptr, blocks, (float)clip, nullptr, 0,
+                            0, 0, S(s));
+  return hip_status(e, "rmsprop");
+}
+
+int arl_policy(const float* hh, int64_t n, const float* Wpi, const float* bpi, const float* Wv, const float* bv,
+               int A, uint64_t seed, const int64_t* step_dev, int64_t step_off, int env_offset, int sample,
+               float* logits, float* probs, float* logp, float* v, float* ent, int32_t* act, float* logp_a,
+               void* s) {
+  if (n < 0 || A < 1 || A > arl::MAXA) return fail(ARL_EINVAL, "policy: bad n / n_actions");
+  if (n > 0 && (!hh || !Wpi || !bpi || !Wv || !bv || !logits || !probs || !logp || !v || !ent))
+    return fail(ARL_EINVAL, "policy: null pointer");
+  if (sample && (!step_dev || !act || !logp_a)) return fail(ARL_EINVAL, "policy: sampling needs step/act/logp_a");
+  if (!aligned(hh, 16) || !aligned(Wpi, 16) || !aligned(Wv, 16)) return fail(ARL_EINVAL, "policy: 16-byte alignment");
+  return hip_status(arl::launch_policy(hh, n, Wpi, bpi, Wv, bv, A, seed, step_dev, step_off, env_offset, sample,
+                                       logits, probs, logp, v, ent, act, logp_a, S(s)),
+                    "policy");
+}
+
+int arl_returns_lossgrad(const float* rewards, const uint8_t* dones, const float* v, const float* probs,
+                         const float* logp, const int32_t* act, int T, int64_t n, int A, double gamma, double beta,
+                         double vcoef, int clip_reward, float* dlogits, float* dv, float* loss, void* s) {
+  if (T < 1 || n < 0 || A < 1) return fail(ARL_EINVAL, "returns: bad T / n / A");
+  if (n > 0 && (!rewards || !dones || !v || !probs || !logp || !act || !dlogits || !dv))
+    return fail(ARL_EINVAL, "returns: null pointer");
+  return hip_status(arl::launch_returns(rewards, dones, v, probs, logp, act, T, (int)n, A, gamma, (float)beta,
+                                        (float)vcoef, clip_reward, dlogits, dv, loss, S(s)),
+                    "returns");
+}
+
+}  // extern "C"

@@ -1,0 +1,103 @@
+// Internal declarations shared by the HIP translation units of libasyncrl_hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace arl {
+
+// control block (device int64[16]), read by kernels so that a captured window
+// replays with advancing step counters (no frozen kernel arguments)
+enum { CTL_STEP = 0, CTL_WINDOW = 1, CTL_SIZE = 16 };
+
+enum Arch { ARCH_FF = 0, ARCH_LSTM = 1 };
+
+constexpr int PLANE = 84 * 84;         // 7056 B per screen
+constexpr int PAIR = 2 * 210 * 160 * 3; // 201,600 B per frame pair
+constexpr int C1_OC = 16, C1_P = 400;  // conv1: 16 x 20 x 20
+constexpr int C2_OC = 32, C2_P = 81;   // conv2: 32 x 9 x 9
+constexpr int A1 = C1_OC * C1_P;       // 6400
+constexpr int A2 = C2_OC * C2_P;       // 2592
+constexpr int HID = 256;
+constexpr int GATES = 4 * HID;
+constexpr int MAXA = 32;               // max actions supported by the policy kernel
+
+struct RingArgs {
+  const uint8_t* pair_pool;   // (pool_len, n, 2, 210, 160, 3)
+  const float* reward_pool;   // (pool_len, n) or null
+  const uint8_t* done_pool;   // (pool_len, n) or null
+  int64_t pool_len;
+  uint8_t* frames;            // (R, n, 84, 84)
+  uint8_t* nvalid;            // (R, n)
+  uint8_t* reset_flags;       // (T+1, n)
+  float* rewards;             // (T, n)
+  uint8_t* dones;             // (T, n)
+  const int64_t* ctl;
+  int n, R, t, mode, force_reset;
+};
+
+hipError_t launch_current_screen(const uint8_t* cur, const uint8_t* prev, uint8_t* out, int64_t n,
+                                 int mode, hipStream_t s);
+hipError_t launch_phi_stack(const uint8_t* pairs, const uint8_t* prev_stack, const uint8_t* reset,
+                            uint8_t* out_stack, int64_t n, int mode, hipStream_t s);
+hipError_t launch_phi_ring(const RingArgs& a, hipStream_t s);
+hipError_t launch_max_luminance(const uint8_t* cur, const uint8_t* prev, uint8_t* gray, int64_t npix,
+                                hipStream_t s);
+hipError_t launch_dqn_phi(const uint8_t* in, float* out, int64_t count, hipStream_t s);
+
+// ---------------------------------------------------------------- network
+struct ParamInfo {
+  std::string name;   // Chainer namedparam / HDF5 path, e.g. "0/0/W"
+  int64_t offset;     // floats into the flat buffer (64-float aligned)
+  int64_t numel;
+};
+
+struct Net {
+  int arch, A, N, T, R;
+  int env_offset;          // global id of env 0 on this rank (RNG stream)
+  uint64_t seed;
+  std::vector<ParamInfo> params;
+  int64_t param_floats;    // padded flat length
+  // parameter offsets (floats)
+  int64_t o_c1W, o_c1b, o_c2W, o_c2b, o_fcW, o_fcb, o_luW, o_lub, o_llW, o_piW, o_pib, o_vW, o_vb;
+  // workspace layout (byte offsets)
+  struct Buf { const char* name; int64_t off, bytes; };
+  std::vector<Buf> bufs;
+  int64_t ws_bytes;
+  int64_t w_ctl, w_frames, w_nvalid, w_reset, w_rewards, w_dones, w_a1, w_a2, w_hfc, w_gates, w_hbuf,
+      w_cbuf, w_logits, w_probs, w_logp, w_v, w_ent, w_logpa, w_act, w_dlogits, w_dv, w_dh, w_dfc,
+      w_dG, w_dhn, w_dcn, w_da2, w_da1, w_slab, w_norm, w_loss;
+  int64_t slab_floats;
+  int norm_blocks;
+  // bound pointers
+  float* p = nullptr;
+  float* g = nullptr;
+  float* ms = nullptr;
+  char* ws = nullptr;
+  template <class T> T* at(int64_t off) const { return reinterpret_cast<T*>(ws + off); }
+};
+
+bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_offset, uint64_t seed,
+              std::string& err);
+hipError_t net_act(Net& net, int t, int sample, hipStream_t s);
+hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s);
+hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
+                        float clip, hipStream_t s);
+hipError_t net_advance(Net& net, hipStream_t s);
+hipError_t net_forward_f32(Net& net, const float* x, int n, float* logits, float* v, hipStream_t s);
+
+hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, double alpha, double eps,
+                          const double* norm_partials, int norm_blocks, float clip, const int64_t* ctl,
+                          int64_t total_steps, int64_t n_total, int t_max, hipStream_t s);
+hipError_t launch_grad_sqnorm(const float* g, int64_t n, double* partials, int blocks, hipStream_t s);
+hipError_t launch_policy(const float* h, int64_t n, const float* Wpi, const float* bpi, const float* Wv,
+                         const float* bv, int A, uint64_t seed, const int64_t* ctl, int64_t step_off,
+                         int env_offset, int sample, float* logits, float* probs, float* logp, float* v,
+                         float* ent, int32_t* act, float* logp_a, hipStream_t s);
+hipError_t launch_returns(const float* rewards, const uint8_t* dones, const float* v, const float* probs,
+                          const float* logp, const int32_t* act, int T, int n, int A, double gamma, float beta,
+                          float vcoef, int clip_reward, float* dlogits, float* dv, float* loss, hipStream_t s);
+
+}  // namespace arl

@@ -1,0 +1,623 @@
+// A3C FF / LSTM network on gfx950: batched-env forward, lockstep-window
+// backward, parameter layout and workspace layout.
+//
+// Reference: a3c_ale.py:28-70 (A3CFF, A3CLSTM), dqn_head.py:31-52
+// (NIPSDQNHead: conv 4->16 k8 s4, conv 16->32 k4 s2, Linear 2592->256, ReLU
+// after each), policy.py:32-58, v_function.py:10-34, Chainer 1.8.1 L.LSTM /
+// F.lstm (interleaved a,i,f,o gates), a3c.py:129-130 (backward of the window
+// loss), a3c.py:144 (unchain_backward: truncated BPTT at the window edge).
+//
+// Every contraction runs through the fp32 MFMA implicit-GEMM template
+// (gemm.hpp).  Forward: conv1 M = 400*n rows (env, oy, ox) x 16 oc x K 256
+// gathered straight from the uint8 frame ring (stack order oldest->newest,
+// planes older than the env's last reset read as 0, /255 folded into the
+// gather); conv2 M = 81*n x 32 x 256 from conv1's activations; FC M = n x 256
+// x 2592 split over K into partial slabs + a bias/ReLU reduce.  Backward over
+// the whole window (S = T*n samples): weight gradients are split-K GEMMs whose
+// reduction axis is the sample (and position) axis, with a ones-column that
+// yields the bias gradient in the same pass; slabs are summed in f64 in slice
+// order (deterministic) straight into the flat gradient buffer.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "arl_internal.hpp"
+#include "gemm.hpp"
+
+namespace arl {
+
+// ---------------------------------------------------------------- accessors
+
+// conv1 operand from the frame ring.  Sample s (relative to activation step
+// t0) = (t = t0 + s / n, env e = s % n); state = ring slots k-3..k of obs step
+// k = ctl[STEP] + t, planes before the env's last reset are zero.
+struct RingIm2col {
+  const uint8_t* __restrict__ frames;
+  const uint8_t* __restrict__ nvalid;
+  const int64_t* __restrict__ ctl;
+  int n, R, t0;
+  // element (s*400 + p, k): p = oy*20 + ox, k = ic*64 + ky*8 + kx
+  __device__ float at(int s, int p, int k) const {
+    const int t = t0 + s / n, e = s - (s / n) * n;
+    const int64_t ks = ctl[CTL_STEP] + t;
+    const int ic = k >> 6, ky = (k >> 3) & 7, kx = k & 7;
+    const int nv = nvalid[(ks % R) * n + e];
+    if (ic < 4 - nv) return 0.f;
+    const int slot = (int)((ks + R - 3 + ic) % R);
+    const int oy = p / 20, ox = p - oy * 20;
+    const uint8_t v = frames[((int64_t)slot * n + e) * PLANE + (4 * oy + ky) * 84 + 4 * ox + kx];
+    return __fdiv_rn((float)v, 255.f);   // dqn_phi.py:16
+  }
+};
+
+struct Conv1FwdA {      // A(m, k), m = s*400 + p
+  RingIm2col x;
+  __device__ float load(int m, int k) const { const int s = m / C1_P; return x.at(s, m - s * C1_P, k); }
+};
+struct Conv1F32A {      // same from an f32 (n,4,84,84) state tensor (dqn_phi output)
+  const float* __restrict__ x;
+  __device__ float load(int m, int k) const {
+    const int s = m / C1_P, p = m - s * C1_P;
+    const int ic = k >> 6, ky = (k >> 3) & 7, kx = k & 7;
+    const int oy = p / 20, ox = p - oy * 20;
+    return x[((int64_t)s * 4 + ic) * PLANE + (4 * oy + ky) * 84 + 4 * ox + kx];
+  }
+};
+struct Conv2A {         // A(m, k) = a1[s][ic][2oy+ky][2ox+kx], m = s*81 + p, k = ic*16+ky*4+kx
+  const float* __restrict__ a1;
+  __device__ float load(int m, int k) const {
+    const int s = m / C2_P, p = m - s * C2_P;
+    const int oy = p / 9, ox = p - oy * 9;
+    const int ic = k >> 4, ky = (k >> 2) & 3, kx = k & 3;
+    return a1[(int64_t)s * A1 + ic * C1_P + (2 * oy + ky) * 20 + 2 * ox + kx];
+  }
+};
+struct WeightT {        // B(k, n) = W[n][k]  (Chainer W is (out, in...))
+  const float* __restrict__ w; int K;
+  __device__ float load(int k, int n) const { return w[(int64_t)n * K + k]; }
+};
+struct LstmGateA {      // A(m, k): [x | h_prev (0 after reset)]
+  const float* __restrict__ x; const float* __restrict__ h; const uint8_t* __restrict__ reset;
+  __device__ float load(int m, int k) const {
+    if (k < HID) return x[(int64_t)m * HID + k];
+    return reset[m] ? 0.f : h[(int64_t)m * HID + k - HID];
+  }
+};
+struct LstmGateB {      // B(k, j) = [Wu^T ; Wl^T]
+  const float* __restrict__ wu; const float* __restrict__ wl;
+  __device__ float load(int k, int j) const {
+    return k < HID ? wu[(int64_t)j * HID + k] : wl[(int64_t)j * HID + k - HID];
+  }
+};
+struct HeadsGA {        // A(m, s) = m < A ? dlogits[s][m] : dv[s]
+  const float* __restrict__ dl; const float* __restrict__ dv; int A;
+  __device__ float load(int m, int s) const { return m < A ? dl[(int64_t)s * A + m] : dv[s]; }
+};
+struct OnesColB {       // B(s, j) = j < K ? X[s][j] : 1   (bias gradient column)
+  const float* __restrict__ x; int K;
+  __device__ float load(int s, int j) const { return j < K ? x[(int64_t)s * K + j] : 1.f; }
+};
+struct Conv2GA {        // A(oc, q) = da2[s][oc][p], q = s*81 + p
+  const float* __restrict__ da2;
+  __device__ float load(int oc, int q) const {
+    const int s = q / C2_P;
+    return da2[(int64_t)s * A2 + oc * C2_P + (q - s * C2_P)];
+  }
+};
+struct Conv2GB {        // B(q, kk) = im2col(a1)[q][kk] | 1
+  Conv2A a;
+  __device__ float load(int q, int kk) const { return kk < 256 ? a.load(q, kk) : 1.f; }
+};
+struct ConvT2A {        // A(m, k) for da1 = conv_transpose(da2, W2); m = s*400 + y*20 + x
+  const float* __restrict__ da2;
+  __device__ float load(int m, int k) const {
+    const int s = m / C1_P, p = m - s * C1_P;
+    const int y = p / 20, x = p - y * 20;
+    const int oc = k >> 4, ky = (k >> 2) & 3, kx = k & 3;
+    const int yy = y - ky, xx = x - kx;
+    if (yy < 0 || xx < 0 || (yy & 1) || (xx & 1)) return 0.f;
+    const int oy = yy >> 1, ox = xx >> 1;
+    if (oy >= 9 || ox >= 9) return 0.f;
+    return da2[(int64_t)s * A2 + oc * C2_P + oy * 9 + ox];
+  }
+};
+struct ConvT2B {        // B(k, ic) = W2[oc][ic][ky][kx], k = oc*16 + ky*4 + kx
+  const float* __restrict__ w2;
+  __device__ float load(int k, int ic) const {
+    const int oc = k >> 4, t = k & 15;
+    return w2[(oc * 16 + ic) * 16 + t];
+  }
+};
+struct Conv1GA {        // A(oc, q) = da1[s][oc][p], q = s*400 + p
+  const float* __restrict__ da1;
+  __device__ float load(int oc, int q) const {
+    const int s = q / C1_P;
+    return da1[(int64_t)s * A1 + oc * C1_P + (q - s * C1_P)];
+  }
+};
+struct Conv1GB {        // B(q, kk) = im2col(x)[q][kk] | 1
+  RingIm2col x;
+  __device__ float load(int q, int kk) const {
+    if (kk >= 256) return 1.f;
+    const int s = q / C1_P;
+    return x.at(s, q - s * C1_P, kk);
+  }
+};
+struct LstmWB {         // B(s, j) = [x (256) | 1 | h_prev (256, 0 after reset)]
+  const float* __restrict__ x; const float* __restrict__ h; const uint8_t* __restrict__ reset;
+  __device__ float load(int s, int j) const {
+    if (j < HID) return x[(int64_t)s * HID + j];
+    if (j == HID) return 1.f;
+    return reset[s] ? 0.f : h[(int64_t)s * HID + j - HID - 1];
+  }
+};
+
+// ---------------------------------------------------------------- epilogues
+struct EpiConv {        // out[s][n][p] = relu(v + b[n]); m = s*P + p
+  float* __restrict__ out; const float* __restrict__ b; int OC, P;
+  __device__ void store(int m, int n, float v, int) const {
+    const int s = m / P, p = m - s * P;
+    out[((int64_t)s * OC + n) * P + p] = fmaxf(__fadd_rn(v, b[n]), 0.f);
+  }
+};
+struct EpiSlab {
+  float* __restrict__ slab; int M, N;
+  __device__ void store(int m, int n, float v, int z) const {
+    slab[((int64_t)z * M + m) * N + n] = v;
+  }
+};
+struct EpiBias {        // out[m][n] = v + b[n]
+  float* __restrict__ out; const float* __restrict__ b; int ld;
+  __device__ void store(int m, int n, float v, int) const { out[(int64_t)m * ld + n] = __fadd_rn(v, b[n]); }
+};
+struct EpiMask {        // out[m][n] = mask[m][n] > 0 ? v : 0  (ReLU backward)
+  float* __restrict__ out; const float* __restrict__ mask; int ld;
+  __device__ void store(int m, int n, float v, int) const {
+    const int64_t i = (int64_t)m * ld + n;
+    out[i] = mask[i] > 0.f ? v : 0.f;
+  }
+};
+struct EpiConvMask {    // da1[s][ic][p] masked by a1 > 0; m = s*400 + p, n = ic
+  float* __restrict__ out; const float* __restrict__ mask;
+  __device__ void store(int m, int n, float v, int) const {
+    const int s = m / C1_P, p = m - s * C1_P;
+    const int64_t i = ((int64_t)s * C1_OC + n) * C1_P + p;
+    out[i] = mask[i] > 0.f ? v : 0.f;
+  }
+};
+struct EpiResetMask {   // out[m][n] = reset[m] ? 0 : v
+  float* __restrict__ out; const uint8_t* __restrict__ reset; int ld;
+  __device__ void store(int m, int n, float v, int) const {
+    out[(int64_t)m * ld + n] = reset[m] ? 0.f : v;
+  }
+};
+
+// ---------------------------------------------------------------- reductions
+__global__ void reduce_bias_relu_kernel(const float* __restrict__ slab, int splits, int64_t MN, int N,
+                                        const float* __restrict__ b, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= MN) return;
+  float s = 0.f;
+  for (int z = 0; z < splits; ++z) s = __fadd_rn(s, slab[(int64_t)z * MN + i]);
+  out[i] = fmaxf(__fadd_rn(s, b[i % N]), 0.f);
+}
+
+// dense weight + bias: n < K -> g[oW + m*K + n]; n == K -> g[ob + m];
+// (LSTM) n > K -> g[oL + m*K + n-K-1]
+struct MapDense {
+  float* g; int64_t oW, ob, oL; int K;
+  __device__ void put(int m, int n, float v) const {
+    if (n < K) g[oW + (int64_t)m * K + n] = v;
+    else if (n == K) g[ob + m] = v;
+    else g[oL + (int64_t)m * K + (n - K - 1)] = v;
+  }
+};
+struct MapHeads {
+  float* g; int64_t oPW, oPB, oVW, oVB; int A;
+  __device__ void put(int m, int n, float v) const {
+    if (m < A) { if (n < HID) g[oPW + (int64_t)m * HID + n] = v; else g[oPB + m] = v; }
+    else { if (n < HID) g[oVW + n] = v; else g[oVB] = v; }
+  }
+};
+
+template <class Map>
+__global__ void reduce_grad_kernel(const float* __restrict__ slab, int splits, int M, int N, Map map) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t MN = (int64_t)M * N;
+  if (i >= MN) return;
+  double s = 0.0;
+  for (int z = 0; z < splits; ++z) s += (double)slab[(int64_t)z * MN + i];
+  map.put((int)(i / N), (int)(i % N), (float)s);
+}
+
+template <class Map>
+static hipError_t launch_reduce_grad(const float* slab, int splits, int M, int N, const Map& map, hipStream_t s) {
+  const int64_t MN = (int64_t)M * N;
+  hipLaunchKernelGGL((reduce_grad_kernel<Map>), dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, s, slab, splits,
+                     M, N, map);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- elementwise
+__device__ inline float sigm(float x) { return __fdiv_rn(1.f, __fadd_rn(1.f, expf(-x))); }
+
+// Chainer F.lstm forward: a,i,f,o interleaved per unit (reshape(n, 256, 4))
+__global__ void lstm_cell_fwd_kernel(const float* __restrict__ gates, const float* __restrict__ c_prev,
+                                     const uint8_t* __restrict__ reset, float* __restrict__ c_out,
+                                     float* __restrict__ h_out, int64_t count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // (m, j)
+  if (i >= count) return;
+  const int64_t m = i / HID;
+  const float4 g = reinterpret_cast<const float4*>(gates)[i];
+  const float a = tanhf(g.x), ig = sigm(g.y), fg = sigm(g.z), og = sigm(g.w);
+  const float cp = reset[m] ? 0.f : c_prev[i];
+  const float c = __fadd_rn(__fmul_rn(a, ig), __fmul_rn(fg, cp));
+  c_out[i] = c;
+  h_out[i] = __fmul_rn(og, tanhf(c));
+}
+
+// F.lstm backward for step t.  dH: dL/dh_t from the heads; dhn/dcn: carried
+// from step t+1 (ignored when first); writes dG (interleaved) and dcn for t-1.
+__global__ void lstm_cell_bwd_kernel(const float* __restrict__ gates, const float* __restrict__ c_t,
+                                     const float* __restrict__ c_prev, const uint8_t* __restrict__ reset,
+                                     const float* __restrict__ dH, const float* __restrict__ dhn,
+                                     float* __restrict__ dcn, float* __restrict__ dG, int first, int64_t count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const int64_t m = i / HID;
+  const float4 g = reinterpret_cast<const float4*>(gates)[i];
+  const float a = tanhf(g.x), ig = sigm(g.y), fg = sigm(g.z), og = sigm(g.w);
+  const float c = c_t[i];
+  const float tc = tanhf(c);
+  const float dh = first ? dH[i] : __fadd_rn(dH[i], dhn[i]);
+  float dc = __fmul_rn(__fmul_rn(dh, og), __fsub_rn(1.f, __fmul_rn(tc, tc)));
+  if (!first) dc = __fadd_rn(dc, dcn[i]);
+  const bool rs = reset[m] != 0;
+  const float cp = rs ? 0.f : c_prev[i];
+  float4 d;
+  d.x = __fmul_rn(__fmul_rn(dc, ig), __fsub_rn(1.f, __fmul_rn(a, a)));
+  d.y = __fmul_rn(__fmul_rn(__fmul_rn(dc, a), ig), __fsub_rn(1.f, ig));
+  d.z = __fmul_rn(__fmul_rn(__fmul_rn(dc, cp), fg), __fsub_rn(1.f, fg));
+  d.w = __fmul_rn(__fmul_rn(__fmul_rn(dh, tc), og), __fsub_rn(1.f, og));
+  reinterpret_cast<float4*>(dG)[i] = d;
+  dcn[i] = rs ? 0.f : __fmul_rn(dc, fg);
+}
+
+// dh[s][j] = sum_k dlogits[s][k] Wpi[k][j] + dv[s] Wv[j]; with mask: * (h > 0)
+__global__ void heads_bwd_kernel(const float* __restrict__ dl, const float* __restrict__ dv,
+                                 const float* __restrict__ Wpi, const float* __restrict__ Wv, int A,
+                                 const float* __restrict__ mask, float* __restrict__ out, int64_t count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const int64_t s = i / HID;
+  const int j = (int)(i - s * HID);
+  float acc = 0.f;
+  for (int k = 0; k < A; ++k) acc = __fadd_rn(acc, __fmul_rn(dl[s * A + k], Wpi[k * HID + j]));
+  acc = __fadd_rn(acc, __fmul_rn(dv[s], Wv[j]));
+  if (mask) acc = mask[i] > 0.f ? acc : 0.f;
+  out[i] = acc;
+}
+
+__global__ void advance_kernel(int64_t* ctl, int T, uint8_t* reset, int n, float* hbuf, float* cbuf) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) reset[i] = reset[(int64_t)T * n + i];
+  if (hbuf != nullptr && i < (int64_t)n * HID) {
+    hbuf[i] = hbuf[(int64_t)T * n * HID + i];
+    cbuf[i] = cbuf[(int64_t)T * n * HID + i];
+  }
+  if (i == 0) {
+    ctl[CTL_STEP] += T;
+    ctl[CTL_WINDOW] += 1;
+  }
+}
+
+// ---------------------------------------------------------------- planning
+static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// split-K factor: aim at ~1024 workgroups, each slice >= 4 K-chunks
+static int plan_splits(int tiles, int64_t K, int BK, int target = 1024) {
+  int s = std::max(1, target / std::max(1, tiles));
+  const int maxs = std::max(1, ceil_div(K, (int64_t)BK * 4));
+  s = std::min(s, maxs);
+  return s;
+}
+
+struct Plans {   // effective split counts (launch_gemm may shrink a request)
+  int fc_fwd, heads_w, fc_w, c2_w, c1_w, lstm_w;
+};
+
+static Plans make_plans(const Net& net) {
+  const int n = net.N, S = net.T * net.N;
+  Plans p;
+  p.fc_fwd = effective_splits<32>(A2, plan_splits(ceil_div(n, 32) * ceil_div(HID, 64), A2, 32, 256));
+  p.heads_w = effective_splits<32>(S, plan_splits(ceil_div(net.A + 1, 16) * ceil_div(HID + 1, 64), S, 32));
+  p.fc_w = effective_splits<32>(S, plan_splits(ceil_div(HID, 64) * ceil_div(A2 + 1, 64), S, 32));
+  p.c2_w = effective_splits<32>((int64_t)S * C2_P, plan_splits(ceil_div(C2_OC, 32) * ceil_div(257, 64),
+                                                               (int64_t)S * C2_P, 32));
+  p.c1_w = effective_splits<32>((int64_t)S * C1_P, plan_splits(ceil_div(C1_OC, 16) * ceil_div(257, 64),
+                                                               (int64_t)S * C1_P, 32));
+  p.lstm_w = effective_splits<32>(S, plan_splits(ceil_div(GATES, 64) * ceil_div(2 * HID + 1, 64), S, 32));
+  return p;
+}
+
+static int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_offset, uint64_t seed,
+              std::string& err) {
+  if (arch != ARCH_FF && arch != ARCH_LSTM) { err = "arch must be 0 (FF) or 1 (LSTM)"; return false; }
+  if (n_actions < 1 || n_actions > MAXA) { err = "n_actions must be in [1, 32]"; return false; }
+  if (n_envs < 1 || n_envs > (1 << 20)) { err = "n_envs out of range"; return false; }
+  if (t_max < 1 || t_max > 64) { err = "t_max must be in [1, 64]"; return false; }
+  if ((int64_t)t_max * n_envs * C1_P >= (int64_t)1 << 31) { err = "t_max * n_envs too large"; return false; }
+  net.arch = arch; net.A = n_actions; net.N = n_envs; net.T = t_max; net.R = t_max + 4;
+  net.env_offset = env_offset; net.seed = seed;
+  // ---- parameters, Chainer link order (a3c_ale.py:35,52)
+  net.params.clear();
+  int64_t off = 0;
+  auto add = [&](const char* name, int64_t numel) {
+    ParamInfo pi; pi.name = name; pi.offset = off; pi.numel = numel;
+    net.params.push_back(pi);
+    off = align_up(off + numel, 64);
+    return pi.offset;
+  };
+  net.o_c1W = add("0/0/W", 16 * 4 * 8 * 8);
+  net.o_c1b = add("0/0/b", 16);
+  net.o_c2W = add("0/1/W", 32 * 16 * 4 * 4);
+  net.o_c2b = add("0/1/b", 32);
+  net.o_fcW = add("0/2/W", (int64_t)HID * A2);
+  net.o_fcb = add("0/2/b", HID);
+  net.o_luW = net.o_lub = net.o_llW = -1;
+  if (arch == ARCH_FF) {
+    net.o_piW = add("1/0/W", (int64_t)n_actions * HID);
+    net.o_pib = add("1/0/b", n_actions);
+    net.o_vW = add("2/0/W", HID);
+    net.o_vb = add("2/0/b", 1);
+  } else {
+    net.o_luW = add("1/upward/W", (int64_t)GATES * HID);
+    net.o_lub = add("1/upward/b", GATES);
+    net.o_llW = add("1/lateral/W", (int64_t)GATES * HID);
+    net.o_piW = add("2/0/W", (int64_t)n_actions * HID);
+    net.o_pib = add("2/0/b", n_actions);
+    net.o_vW = add("3/0/W", HID);
+    net.o_vb = add("3/0/b", 1);
+  }
+  net.param_floats = off;
+  // ---- workspace
+  const int64_t n = n_envs, T = t_max, T1 = T + 1, S = T * n, A = n_actions;
+  net.norm_blocks = 1024;
+  Plans pl = make_plans(net);
+  int64_t slab = 0;
+  slab = std::max(slab, (int64_t)pl.fc_fwd * n * HID);
+  slab = std::max(slab, (int64_t)pl.heads_w * (A + 1) * (HID + 1));
+  slab = std::max(slab, (int64_t)pl.fc_w * HID * (A2 + 1));
+  slab = std::max(slab, (int64_t)pl.c2_w * C2_OC * 257);
+  slab = std::max(slab, (int64_t)pl.c1_w * C1_OC * 257);
+  if (arch == ARCH_LSTM) slab = std::max(slab, (int64_t)pl.lstm_w * GATES * (2 * HID + 1));
+  net.slab_floats = slab;
+  net.bufs.clear();
+  int64_t wo = 0;
+  auto buf = [&](const char* name, int64_t bytes) {
+    Net::Buf b; b.name = name; b.off = wo; b.bytes = bytes;
+    net.bufs.push_back(b);
+    wo = align_up(wo + std::max<int64_t>(bytes, 1), 256);
+    return b.off;
+  };
+  const bool L = arch == ARCH_LSTM;
+  net.w_ctl = buf("ctl", CTL_SIZE * 8);
+  net.w_frames = buf("frames", (int64_t)net.R * n * PLANE);
+  net.w_nvalid = buf("nvalid", (int64_t)net.R * n);
+  net.w_reset = buf("reset", T1 * n);
+  net.w_rewards = buf("rewards", S * 4);
+  net.w_dones = buf("dones", S);
+  net.w_a1 = buf("a1", T1 * n * A1 * 4);
+  net.w_a2 = buf("a2", T1 * n * A2 * 4);
+  net.w_hfc = buf("hfc", T1 * n * HID * 4);
+  net.w_gates = buf("gates", L ? T1 * n * GATES * 4 : 0);
+  net.w_hbuf = buf("hbuf", L ? (T + 2) * n * HID * 4 : 0);
+  net.w_cbuf = buf("cbuf", L ? (T + 2) * n * HID * 4 : 0);
+  net.w_logits = buf("logits", T1 * n * A * 4);
+  net.w_probs = buf("probs", T1 * n * A * 4);
+  net.w_logp = buf("logp", T1 * n * A * 4);
+  net.w_v = buf("v", T1 * n * 4);
+  net.w_ent = buf("entropy", T1 * n * 4);
+  net.w_logpa = buf("logp_a", T1 * n * 4);
+  net.w_act = buf("actions", T1 * n * 4);
+  net.w_dlogits = buf("dlogits", S * A * 4);
+  net.w_dv = buf("dv", S * 4);
+  net.w_dh = buf("dh", S * HID * 4);
+  net.w_dfc = buf("dfc", S * HID * 4);
+  net.w_dG = buf("dG", L ? S * GATES * 4 : 0);
+  net.w_dhn = buf("dhn", L ? n * HID * 4 : 0);
+  net.w_dcn = buf("dcn", L ? n * HID * 4 : 0);
+  net.w_da2 = buf("da2", S * A2 * 4);
+  net.w_da1 = buf("da1", S * A1 * 4);
+  net.w_slab = buf("slab", slab * 4);
+  net.w_norm = buf("norm_partials", (int64_t)net.norm_blocks * 8);
+  net.w_loss = buf("loss", n * 2 * 4);
+  net.ws_bytes = wo;
+  return true;
+}
+
+// ---------------------------------------------------------------- forward
+static RingIm2col ring_of(const Net& net, int t0) {
+  RingIm2col r;
+  r.frames = net.at<uint8_t>(net.w_frames);
+  r.nvalid = net.at<uint8_t>(net.w_nvalid);
+  r.ctl = net.at<int64_t>(net.w_ctl);
+  r.n = net.N; r.R = net.R; r.t0 = t0;
+  return r;
+}
+
+#define ARL_TRY(x) do { hipError_t _e = (x); if (_e != hipSuccess) return _e; } while (0)
+
+// head (conv1 -> conv2 -> fc) for n rows whose conv1 operand is `c1a`,
+// writing activations at a1/a2/hfc (row-major per sample)
+template <class C1A>
+static hipError_t head_forward(const Net& net, const C1A& c1a, int n, float* a1, float* a2, float* hfc,
+                               hipStream_t s) {
+  const float* P = net.p;
+  ARL_TRY((launch_gemm<64, 16, 32, 4, 1>(c1a, WeightT{P + net.o_c1W, 256}, EpiConv{a1, P + net.o_c1b, C1_OC, C1_P},
+                                         n * C1_P, C1_OC, 256, 1, s)));
+  ARL_TRY((launch_gemm<32, 32, 32, 2, 2>(Conv2A{a1}, WeightT{P + net.o_c2W, 256}, EpiConv{a2, P + net.o_c2b, C2_OC, C2_P},
+                                         n * C2_P, C2_OC, 256, 1, s)));
+  const int req = plan_splits(ceil_div(n, 32) * ceil_div(HID, 64), A2, 32, 256);
+  const int sp = effective_splits<32>(A2, req);
+  float* slab = net.at<float>(net.w_slab);
+  ARL_TRY((launch_gemm<32, 64, 32, 2, 2>(RowMajor{a2, A2}, WeightT{P + net.o_fcW, A2}, EpiSlab{slab, n, HID},
+                                         n, HID, A2, req, s)));
+  const int64_t MN = (int64_t)n * HID;
+  hipLaunchKernelGGL(reduce_bias_relu_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, s, slab, sp, MN, HID,
+                     P + net.o_fcb, hfc);
+  return hipGetLastError();
+}
+
+hipError_t net_act(Net& net, int t, int sample, hipStream_t s) {
+  const int n = net.N, A = net.A;
+  float* a1 = net.at<float>(net.w_a1) + (int64_t)t * n * A1;
+  float* a2 = net.at<float>(net.w_a2) + (int64_t)t * n * A2;
+  float* hfc = net.at<float>(net.w_hfc) + (int64_t)t * n * HID;
+  ARL_TRY(head_forward(net, Conv1FwdA{ring_of(net, t)}, n, a1, a2, hfc, s));
+  const float* P = net.p;
+  const float* hpol = hfc;
+  if (net.arch == ARCH_LSTM) {
+    float* gates = net.at<float>(net.w_gates) + (int64_t)t * n * GATES;
+    const float* hprev = net.at<float>(net.w_hbuf) + (int64_t)t * n * HID;
+    const float* cprev = net.at<float>(net.w_cbuf) + (int64_t)t * n * HID;
+    float* hout = net.at<float>(net.w_hbuf) + (int64_t)(t + 1) * n * HID;
+    float* cout = net.at<float>(net.w_cbuf) + (int64_t)(t + 1) * n * HID;
+    const uint8_t* rs = net.at<uint8_t>(net.w_reset) + (int64_t)t * n;
+    ARL_TRY((launch_gemm<32, 64, 32, 2, 2>(LstmGateA{hfc, hprev, rs}, LstmGateB{P + net.o_luW, P + net.o_llW},
+                                           EpiBias{gates, P + net.o_lub, GATES}, n, GATES, 2 * HID, 1, s)));
+    const int64_t cnt = (int64_t)n * HID;
+    hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, gates, cprev, rs,
+                       cout, hout, cnt);
+    ARL_TRY(hipGetLastError());
+    hpol = hout;
+  }
+  const int64_t o = (int64_t)t * n;
+  return launch_policy(hpol, n, P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
+                       net.at<int64_t>(net.w_ctl), t, net.env_offset, (sample && t < net.T) ? 1 : 0,
+                       net.at<float>(net.w_logits) + o * A, net.at<float>(net.w_probs) + o * A,
+                       net.at<float>(net.w_logp) + o * A, net.at<float>(net.w_v) + o, net.at<float>(net.w_ent) + o,
+                       net.at<int32_t>(net.w_act) + o, net.at<float>(net.w_logpa) + o, s);
+}
+
+// Drop-in pi_and_v on explicit f32 states (dqn_phi output), FF only; results
+// land in activation slot T (the bootstrap slot) of the workspace.
+hipError_t net_forward_f32(Net& net, const float* x, int n, float*, float*, hipStream_t s) {
+  if (net.arch != ARCH_FF || n > net.N) return hipErrorInvalidValue;
+  const int T = net.T, A = net.A, N = net.N;
+  float* a1 = net.at<float>(net.w_a1) + (int64_t)T * N * A1;
+  float* a2 = net.at<float>(net.w_a2) + (int64_t)T * N * A2;
+  float* hfc = net.at<float>(net.w_hfc) + (int64_t)T * N * HID;
+  ARL_TRY(head_forward(net, Conv1F32A{x}, n, a1, a2, hfc, s));
+  const float* P = net.p;
+  const int64_t o = (int64_t)T * N;
+  return launch_policy(hfc, n, P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
+                       net.at<int64_t>(net.w_ctl), T, net.env_offset, 0, net.at<float>(net.w_logits) + o * A,
+                       net.at<float>(net.w_probs) + o * A, net.at<float>(net.w_logp) + o * A,
+                       net.at<float>(net.w_v) + o, net.at<float>(net.w_ent) + o, net.at<int32_t>(net.w_act) + o,
+                       net.at<float>(net.w_logpa) + o, s);
+}
+
+// ---------------------------------------------------------------- backward
+hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s) {
+  const int n = net.N, T = net.T, A = net.A, S = T * n;
+  const float* P = net.p;
+  float* G = net.g;
+  float* slab = net.at<float>(net.w_slab);
+  const Plans pl = make_plans(net);
+  float* dl = net.at<float>(net.w_dlogits);
+  float* dv = net.at<float>(net.w_dv);
+  // 1. n-step returns + loss gradient wrt logits / v  (a3c.py:82-126)
+  ARL_TRY(launch_returns(net.at<float>(net.w_rewards), net.at<uint8_t>(net.w_dones), net.at<float>(net.w_v),
+                         net.at<float>(net.w_probs), net.at<float>(net.w_logp), net.at<int32_t>(net.w_act), T, n, A,
+                         gamma, beta, vcoef, clip_reward, dl, dv, net.at<float>(net.w_loss), s));
+  const bool L = net.arch == ARCH_LSTM;
+  const float* hfc = net.at<float>(net.w_hfc);
+  const float* hheads = L ? net.at<float>(net.w_hbuf) + (int64_t)n * HID : hfc;   // h fed to pi / v
+  float* dfc = net.at<float>(net.w_dfc);
+  // 2. heads: weight grads (ones column = bias) and dh
+  ARL_TRY((launch_gemm<16, 64, 32, 1, 4>(HeadsGA{dl, dv, A}, OnesColB{hheads, HID}, EpiSlab{slab, A + 1, HID + 1},
+                                         A + 1, HID + 1, S, pl.heads_w, s)));
+  ARL_TRY(launch_reduce_grad(slab, pl.heads_w, A + 1, HID + 1,
+                             MapHeads{G, net.o_piW, net.o_pib, net.o_vW, net.o_vb, A}, s));
+  {
+    const int64_t cnt = (int64_t)S * HID;
+    float* dst = L ? net.at<float>(net.w_dh) : dfc;
+    hipLaunchKernelGGL(heads_bwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, dl, dv, P + net.o_piW,
+                       P + net.o_vW, A, L ? nullptr : hfc, dst, cnt);
+    ARL_TRY(hipGetLastError());
+  }
+  // 3. LSTM: truncated BPTT over the window
+  if (L) {
+    const float* gates = net.at<float>(net.w_gates);
+    const float* cbuf = net.at<float>(net.w_cbuf);
+    const float* hbuf = net.at<float>(net.w_hbuf);
+    const uint8_t* rs = net.at<uint8_t>(net.w_reset);
+    float* dG = net.at<float>(net.w_dG);
+    float* dhn = net.at<float>(net.w_dhn);
+    float* dcn = net.at<float>(net.w_dcn);
+    const float* dH = net.at<float>(net.w_dh);
+    const int64_t cnt = (int64_t)n * HID;
+    for (int t = T - 1; t >= 0; --t) {
+      const int64_t o = (int64_t)t * n;
+      hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s,
+                         gates + o * GATES, cbuf + (o + n) * HID, cbuf + o * HID, rs + o, dH + o * HID, dhn, dcn,
+                         dG + o * GATES, t == T - 1 ? 1 : 0, cnt);
+      ARL_TRY(hipGetLastError());
+      if (t > 0)
+        ARL_TRY((launch_gemm<32, 64, 32, 2, 2>(RowMajor{dG + o * GATES, GATES}, RowMajor{P + net.o_llW, HID},
+                                               EpiResetMask{dhn, rs + o, HID}, n, HID, GATES, 1, s)));
+    }
+    ARL_TRY((launch_gemm<64, 64, 32, 2, 2>(ColMajor{dG, GATES}, LstmWB{hfc, hbuf, rs},
+                                           EpiSlab{slab, GATES, 2 * HID + 1}, GATES, 2 * HID + 1, S, pl.lstm_w, s)));
+    ARL_TRY(launch_reduce_grad(slab, pl.lstm_w, GATES, 2 * HID + 1,
+                               MapDense{G, net.o_luW, net.o_lub, net.o_llW, HID}, s));
+    ARL_TRY((launch_gemm<64, 64, 32, 2, 2>(RowMajor{dG, GATES}, RowMajor{P + net.o_luW, HID}, EpiMask{dfc, hfc, HID},
+                                           S, HID, GATES, 1, s)));
+  }
+  // 4. FC: dW (+ bias via ones column) and da2 = (dfc W) * (a2 > 0)
+  const float* a2 = net.at<float>(net.w_a2);
+  const float* a1 = net.at<float>(net.w_a1);
+  float* da2 = net.at<float>(net.w_da2);
+  float* da1 = net.at<float>(net.w_da1);
+  ARL_TRY((launch_gemm<64, 64, 32, 2, 2>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab, HID, A2 + 1}, HID,
+                                         A2 + 1, S, pl.fc_w, s)));
+  ARL_TRY(launch_reduce_grad(slab, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s));
+  ARL_TRY((launch_gemm<64, 64, 32, 2, 2>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2}, EpiMask{da2, a2, A2}, S, A2,
+                                         HID, 1, s)));
+  // 5. conv2: dW, db; da1 = conv_transpose(da2, W2) * (a1 > 0)
+  ARL_TRY((launch_gemm<32, 64, 32, 2, 2>(Conv2GA{da2}, Conv2GB{Conv2A{a1}}, EpiSlab{slab, C2_OC, 257}, C2_OC, 257,
+                                         S * C2_P, pl.c2_w, s)));
+  ARL_TRY(launch_reduce_grad(slab, pl.c2_w, C2_OC, 257, MapDense{G, net.o_c2W, net.o_c2b, -1, 256}, s));
+  ARL_TRY((launch_gemm<64, 16, 32, 4, 1>(ConvT2A{da2}, ConvT2B{P + net.o_c2W}, EpiConvMask{da1, a1}, S * C1_P, C1_OC,
+                                         C2_OC * 16, 1, s)));
+  // 6. conv1: dW, db (no dx needed)
+  ARL_TRY((launch_gemm<16, 64, 32, 1, 4>(Conv1GA{da1}, Conv1GB{ring_of(net, 0)}, EpiSlab{slab, C1_OC, 257}, C1_OC,
+                                         257, S * C1_P, pl.c1_w, s)));
+  ARL_TRY(launch_reduce_grad(slab, pl.c1_w, C1_OC, 257, MapDense{G, net.o_c1W, net.o_c1b, -1, 256}, s));
+  return hipSuccess;
+}
+
+hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
+                        float clip, hipStream_t s) {
+  double* parts = net.at<double>(net.w_norm);
+  const bool do_clip = clip > 0.f;
+  if (do_clip) ARL_TRY(launch_grad_sqnorm(net.g, net.param_floats, parts, net.norm_blocks, s));
+  return launch_rmsprop(net.p, net.ms, net.g, net.param_floats, lr0, alpha, eps, do_clip ? parts : nullptr,
+                        net.norm_blocks, clip, total_steps > 0 ? net.at<int64_t>(net.w_ctl) : nullptr, total_steps,
+                        n_total, net.T, s);
+}
+
+hipError_t net_advance(Net& net, hipStream_t s) {
+  const bool L = net.arch == ARCH_LSTM;
+  const int64_t cnt = L ? (int64_t)net.N * HID : net.N;
+  hipLaunchKernelGGL(advance_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, net.at<int64_t>(net.w_ctl),
+                     net.T, net.at<uint8_t>(net.w_reset), net.N, L ? net.at<float>(net.w_hbuf) : nullptr,
+                     L ? net.at<float>(net.w_cbuf) : nullptr);
+  return hipGetLastError();
+}
+
+}  // namespace arl

@@ -1,0 +1,154 @@
+// GradientClipping(40) + RMSpropAsync over one flat parameter buffer.
+//
+// Reference: a3c_ale.py:224-226 (RMSpropAsync(lr=7e-4, eps=1e-1, alpha=0.99)
+// + GradientClipping(40) hook), rmsprop_async.py:23-29 (update_one_cpu) and
+// the dormant CuPy kernel rmsprop_async.py:31-38; Chainer's GradientClipping
+// (norm = sqrt(sum of per-array squared norms); if 40/norm < 1: g *= 40/norm).
+//
+// Two launches per update, both HBM-streaming over the padded flat buffer:
+//   grad_sqnorm_kernel: per-block partial sum of g^2 (f32 per thread over a
+//     grid-stride, f64 across the block) -> partials[block];
+//   rmsprop_kernel: every block first re-reduces the (<= 1024) f64 partials
+//     (4-8 KB, L2-resident) to the global norm, so the clip rate needs no host
+//     round trip and no extra launch; then 4 parameters per thread per
+//     iteration: g' = clip ? g*f32(rate) : g; ms = ms*alpha; ms += (c*g')*g';
+//     p -= (lr*g') / sqrt(ms + eps) -- every op an explicit round-to-nearest
+//     f32 op in the reference's order (NumPy f32 semantics, no FMA), so the
+//     result is bit-identical to update_one_cpu.
+// 20 bytes move per parameter (read p, g, ms; write p, ms) + 4 for the norm.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "arl_internal.hpp"
+
+namespace arl {
+
+__device__ inline double block_sum_f64(double x, double* sh) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) sh[w] = x;
+  __syncthreads();
+  double t = 0.0;
+  const int nw = blockDim.x >> 6;
+  for (int i = 0; i < nw; ++i) t += sh[i];
+  return t;
+}
+
+__global__ void __launch_bounds__(256)
+grad_sqnorm_kernel(const float* __restrict__ g, int64_t n, double* __restrict__ partials) {
+  __shared__ double sh[8];
+  const int64_t n4 = n >> 2;
+  float acc = 0.f;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = g4[i];
+    acc = __fadd_rn(acc, __fadd_rn(__fadd_rn(__fmul_rn(v.x, v.x), __fmul_rn(v.y, v.y)),
+                                   __fadd_rn(__fmul_rn(v.z, v.z), __fmul_rn(v.w, v.w))));
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const float v = g[(n4 << 2) + threadIdx.x];
+    acc = __fadd_rn(acc, __fmul_rn(v, v));
+  }
+  const double t = block_sum_f64((double)acc, sh);
+  if (threadIdx.x == 0) partials[blockIdx.x] = t;
+}
+
+struct RmsConst {
+  float lr, alpha, one_minus_alpha, eps;
+  // optional on-device lr anneal (a3c_ale.py:111-112):
+  // lr = (total - global_t - 1) / total * lr0, global_t = (ctl[STEP] + t_max) * n_total
+  double lr0;
+  int64_t total, n_total, t_max;
+  const int64_t* ctl;
+};
+
+__device__ inline void rms1(float& p, float& ms, float g, const RmsConst& c) {
+  ms = __fmul_rn(ms, c.alpha);                                   // ms *= alpha
+  ms = __fadd_rn(ms, __fmul_rn(__fmul_rn(c.one_minus_alpha, g), g));   // ms += (1-a)*g*g
+  p = __fsub_rn(p, __fdiv_rn(__fmul_rn(c.lr, g), __fsqrt_rn(__fadd_rn(ms, c.eps))));  // p -= lr*g/sqrt(ms+eps)
+}
+
+__global__ void __launch_bounds__(256)
+rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __restrict__ g, int64_t n, RmsConst c,
+               const double* __restrict__ partials, int nparts, float clip) {
+  __shared__ double sh[8];
+  if (c.ctl != nullptr && c.total > 0) {
+    const int64_t gt = (c.ctl[CTL_STEP] + c.t_max) * c.n_total;
+    c.lr = (float)(((double)(c.total - gt - 1) / (double)c.total) * c.lr0);
+  }
+  float scale = 1.f;
+  bool do_clip = false;
+  if (partials != nullptr) {
+    double t = 0.0;
+    for (int i = threadIdx.x; i < nparts; i += blockDim.x) t += partials[i];
+    t = block_sum_f64(t, sh);
+    const double norm = sqrt(t);
+    const double rate = (double)clip / norm;
+    if (norm > 0.0 && rate < 1.0) {
+      do_clip = true;
+      scale = (float)rate;
+    }
+  }
+  const int64_t n4 = n >> 2;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  float4* m4 = reinterpret_cast<float4*>(ms);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 pv = p4[i], mv = m4[i], gv = g4[i];
+    if (do_clip) {
+      gv.x = __fmul_rn(gv.x, scale); gv.y = __fmul_rn(gv.y, scale);
+      gv.z = __fmul_rn(gv.z, scale); gv.w = __fmul_rn(gv.w, scale);
+    }
+    rms1(pv.x, mv.x, gv.x, c);
+    rms1(pv.y, mv.y, gv.y, c);
+    rms1(pv.z, mv.z, gv.z, c);
+    rms1(pv.w, mv.w, gv.w, c);
+    p4[i] = pv;
+    m4[i] = mv;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const int64_t j = (n4 << 2) + threadIdx.x;
+    float gv = g[j];
+    if (do_clip) gv = __fmul_rn(gv, scale);
+    float pv = p[j], mv = ms[j];
+    rms1(pv, mv, gv, c);
+    p[j] = pv;
+    ms[j] = mv;
+  }
+}
+
+static int stream_blocks(int64_t n) {
+  int64_t b = (n / 4 + 255) / 256;
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+hipError_t launch_grad_sqnorm(const float* g, int64_t n, double* partials, int blocks, hipStream_t s) {
+  hipLaunchKernelGGL(grad_sqnorm_kernel, dim3(blocks), dim3(256), 0, s, g, n, partials);
+  return hipGetLastError();
+}
+
+hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, double alpha, double eps,
+                          const double* norm_partials, int norm_blocks, float clip, const int64_t* ctl,
+                          int64_t total_steps, int64_t n_total, int t_max, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  // each Python-float hyperparameter meets the f32 arrays as f32(value)
+  RmsConst c;
+  c.lr = (float)lr;
+  c.alpha = (float)alpha;
+  c.one_minus_alpha = (float)(1.0 - alpha);   // (1 - self.alpha) in Python double, then f32
+  c.eps = (float)eps;
+  c.lr0 = lr;
+  c.total = total_steps;
+  c.n_total = n_total;
+  c.t_max = t_max;
+  c.ctl = ctl;
+  hipLaunchKernelGGL(rmsprop_kernel, dim3(stream_blocks(n)), dim3(256), 0, s, p, ms, g, n, c, norm_partials,
+                     norm_blocks, clip);
+  return hipGetLastError();
+}
+
+}  // namespace arl

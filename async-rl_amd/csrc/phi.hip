@@ -1,0 +1,267 @@
+// Frame preprocessing (phi) on gfx950.
+//
+// Reference: ale.py:59-89 (current_screen: np.maximum of the two captured RGB
+// frames, float64 luminance R*0.2126 + G*0.0722 + B*0.7152, astype(uint8),
+// cv2.resize(img, (84, 84), INTER_LINEAR)), ale.py:135 / :155-158 (4-plane
+// deque, reset to three zero planes + the new screen), dqn_phi.py:14-16
+// (f32 /= 255).
+//
+// One workgroup (256 threads) = one env x one band of 12 output rows (7 bands
+// per 84x84 screen).  Only the source rows the bilinear taps touch are read
+// (2 per output row: for 210->84 that is 4 of every 5 rows), 48 contiguous
+// bytes (16 RGB pixels) per thread per frame as three 16-byte loads, both
+// frames of the pair.  Max + luminance run in registers (fp64, explicit
+// round-to-nearest ops so nothing can be contracted into an FMA: bit-exact
+// with NumPy), the uint8 gray rows land in LDS, and the separable fixed-point
+// resize reads them back and writes 4 output pixels per thread as one u32.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "arl_internal.hpp"
+
+namespace arl {
+
+constexpr int SRC_H = 210, SRC_W = 160, DST = 84;
+constexpr int BAND = 12;                   // output rows per workgroup
+constexpr int NBANDS = DST / BAND;         // 7
+constexpr int FRAME_BYTES = SRC_H * SRC_W * 3;   // 100,800
+
+
+// OpenCV INTER_LINEAR coefficients for one axis (see oracle.resize_coeffs):
+// f = (float)((d+0.5)*scale-0.5); s = floor(f); f -= s; clamps; a = rint(c*2048)
+__device__ inline void resize_coeff(int d, int ssize, int dsize, int& ofs, int& a0, int& a1) {
+  const double inv_scale = (double)dsize / (double)ssize;
+  const double scale = 1.0 / inv_scale;
+  float f = (float)__dsub_rn(__dmul_rn((double)d + 0.5, scale), 0.5);
+  int s = (int)floorf(f);
+  f = __fsub_rn(f, (float)s);
+  if (s < 0) { f = 0.f; s = 0; }
+  if (s >= ssize - 1) { f = 0.f; s = ssize - 1; }
+  const float c0 = __fsub_rn(1.f, f);
+  ofs = s;
+  a0 = (int)rintf(__fmul_rn(c0, 2048.f));
+  a1 = (int)rintf(__fmul_rn(f, 2048.f));
+}
+
+__device__ inline uint32_t umax_bytes(uint32_t a, uint32_t b) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint32_t x = (a >> (8 * i)) & 0xffu, y = (b >> (8 * i)) & 0xffu;
+    r |= (x > y ? x : y) << (8 * i);
+  }
+  return r;
+}
+
+// ale.py:67-69, float64, left-to-right, explicit RN ops (no FMA contraction)
+__device__ inline uint32_t luminance(uint32_t r, uint32_t g, uint32_t b) {
+  const double v = __dadd_rn(__dadd_rn(__dmul_rn((double)r, 0.2126), __dmul_rn((double)g, 0.0722)),
+                             __dmul_rn((double)b, 0.7152));
+  return (uint32_t)v;   // astype(uint8): truncation (v in [0, 255))
+}
+
+struct PhiShared {
+  uint8_t gray[BAND][2][SRC_W];   // [output row][tap][x]
+  int16_t xofs[DST];
+  int16_t xa0[DST], xa1[DST];
+  int16_t yofs[BAND];
+  int16_t yb0[BAND], yb1[BAND];
+};
+
+// Computes output rows [dy0, dy0+BAND) of one env's screen into `out`
+// (row stride 84).  cur/prev: the env's two RGB frames (HWC, uint8).
+__device__ inline void phi_band(const uint8_t* __restrict__ cur, const uint8_t* __restrict__ prev,
+                                uint8_t* __restrict__ out, int dy0, int mode, PhiShared& sh) {
+  const int tid = threadIdx.x;
+  if (tid < DST) {
+    int o, a0, a1;
+    resize_coeff(tid, SRC_W, DST, o, a0, a1);
+    sh.xofs[tid] = (int16_t)o; sh.xa0[tid] = (int16_t)a0; sh.xa1[tid] = (int16_t)a1;
+  } else if (tid >= 96 && tid < 96 + BAND) {
+    int o, b0, b1;
+    resize_coeff(dy0 + tid - 96, SRC_H, DST, o, b0, b1);
+    sh.yofs[tid - 96] = (int16_t)o; sh.yb0[tid - 96] = (int16_t)b0; sh.yb1[tid - 96] = (int16_t)b1;
+  }
+  __syncthreads();
+  // stage: task = (local row r in 0..23 -> (dy, tap), chunk c in 0..9 of 16 px)
+  if (tid < 2 * BAND * 10) {
+    const int r = tid / 10, c = tid % 10;
+    const int ly = r >> 1, tap = r & 1;
+    int sy = sh.yofs[ly] + tap;
+    if (sy > SRC_H - 1) sy = SRC_H - 1;
+    const uint4* pc = reinterpret_cast<const uint4*>(cur + (size_t)sy * SRC_W * 3 + c * 48);
+    const uint4* pp = reinterpret_cast<const uint4*>(prev + (size_t)sy * SRC_W * 3 + c * 48);
+    uint4 c0 = pc[0], c1 = pc[1], c2 = pc[2];
+    uint4 p0 = pp[0], p1 = pp[1], p2 = pp[2];
+    uint32_t w[12] = {umax_bytes(c0.x, p0.x), umax_bytes(c0.y, p0.y), umax_bytes(c0.z, p0.z),
+                      umax_bytes(c0.w, p0.w), umax_bytes(c1.x, p1.x), umax_bytes(c1.y, p1.y),
+                      umax_bytes(c1.z, p1.z), umax_bytes(c1.w, p1.w), umax_bytes(c2.x, p2.x),
+                      umax_bytes(c2.y, p2.y), umax_bytes(c2.z, p2.z), umax_bytes(c2.w, p2.w)};
+    uint32_t g[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const int b = 3 * p;
+      const uint32_t R = (w[b >> 2] >> (8 * (b & 3))) & 0xffu;
+      const uint32_t G = (w[(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 0xffu;
+      const uint32_t B = (w[(b + 2) >> 2] >> (8 * ((b + 2) & 3))) & 0xffu;
+      g[p >> 2] |= luminance(R, G, B) << (8 * (p & 3));
+    }
+    *reinterpret_cast<uint4*>(&sh.gray[ly][tap][c * 16]) = make_uint4(g[0], g[1], g[2], g[3]);
+  }
+  __syncthreads();
+  // resize: task = (local row ly, group of 4 output columns q) -> 12*21 = 252
+  if (tid < BAND * (DST / 4)) {
+    const int ly = tid / (DST / 4), q = tid % (DST / 4);
+    const int b0 = sh.yb0[ly], b1 = sh.yb1[ly];
+    uint32_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int dx = q * 4 + j;
+      const int sx = sh.xofs[dx];
+      const int sx1 = sx + 1 < SRC_W ? sx + 1 : SRC_W - 1;
+      const int a0 = sh.xa0[dx], a1 = sh.xa1[dx];
+      const int r0 = (int)sh.gray[ly][0][sx] * a0 + (int)sh.gray[ly][0][sx1] * a1;
+      const int r1 = (int)sh.gray[ly][1][sx] * a0 + (int)sh.gray[ly][1][sx1] * a1;
+      int v;
+      if (mode == 0) {         // FixedPtCast<int, uchar, 22>
+        v = (b0 * r0 + b1 * r1 + (1 << 21)) >> 22;
+      } else {                 // VResizeLinearVec_32s8u (mulhi form)
+        v = ((((r0 >> 4) * b0) >> 16) + (((r1 >> 4) * b1) >> 16) + 2) >> 2;
+      }
+      v = v < 0 ? 0 : (v > 255 ? 255 : v);
+      packed |= (uint32_t)v << (8 * j);
+    }
+    *reinterpret_cast<uint32_t*>(out + (size_t)(dy0 + ly) * DST + q * 4) = packed;
+  }
+}
+
+// ---------------------------------------------------------------- kernels
+// ale.py:59-89: one 84x84 screen per env.
+__global__ void __launch_bounds__(256)
+current_screen_kernel(const uint8_t* __restrict__ cur, const uint8_t* __restrict__ prev,
+                      uint8_t* __restrict__ out, int mode) {
+  __shared__ PhiShared sh;
+  const int64_t e = blockIdx.y;
+  phi_band(cur + e * FRAME_BYTES, prev + e * FRAME_BYTES, out + e * PLANE, blockIdx.x * BAND, mode, sh);
+}
+
+// Materialised 4-plane stack: out[e] = reset ? [0,0,0,new]
+// : [prev[1], prev[2], prev[3], new]; pairs laid out (n, 2, 210, 160, 3).
+__global__ void __launch_bounds__(256)
+phi_stack_kernel(const uint8_t* __restrict__ pairs, const uint8_t* __restrict__ prev_stack,
+                 const uint8_t* __restrict__ reset, uint8_t* __restrict__ out_stack, int mode) {
+  __shared__ PhiShared sh;
+  const int64_t e = blockIdx.y;
+  const int dy0 = blockIdx.x * BAND;
+  const uint8_t* pr = pairs + e * (2 * FRAME_BYTES);
+  uint8_t* os = out_stack + e * (4 * PLANE);
+  phi_band(pr, pr + FRAME_BYTES, os + 3 * PLANE, dy0, mode, sh);
+  // shift the three older planes (rows of this band only), 16 B per thread
+  const bool rs = reset != nullptr && reset[e] != 0;
+  const uint8_t* ps = prev_stack + e * (4 * PLANE);
+  constexpr int BAND_BYTES = BAND * DST;           // 1008 = 63 x 16
+  const int tid = threadIdx.x;
+  if (tid < 3 * (BAND_BYTES / 16)) {
+    const int p = tid / (BAND_BYTES / 16), c = tid % (BAND_BYTES / 16);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (!rs) v = *reinterpret_cast<const uint4*>(ps + (p + 1) * PLANE + dy0 * DST + c * 16);
+    *reinterpret_cast<uint4*>(os + p * PLANE + dy0 * DST + c * 16) = v;
+  }
+}
+
+// In-loop ring: the new screen of obs step k = ctl[0] + t goes to slot k % R;
+// nvalid[slot][e] = reset ? 1 : min(nvalid[prev slot][e] + 1, 4).  Also
+// ingests the reward / done that arrived with this obs (a3c.py:69-70,75):
+// rewards[t-1], dones[t-1] (t >= 1) and reset_flags[t].
+__global__ void __launch_bounds__(256)
+phi_ring_kernel(RingArgs a) {
+  __shared__ PhiShared sh;
+  const int e = blockIdx.y;
+  const int64_t k = a.ctl[CTL_STEP] + a.t;
+  const int slot = (int)(k % a.R);
+  const int64_t pidx = k % a.pool_len;
+  const uint8_t* pr = a.pair_pool + (pidx * a.n + e) * (int64_t)(2 * FRAME_BYTES);
+  uint8_t* dst = a.frames + ((int64_t)slot * a.n + e) * PLANE;
+  phi_band(pr, pr + FRAME_BYTES, dst, blockIdx.x * BAND, a.mode, sh);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint8_t d = a.done_pool ? a.done_pool[pidx * a.n + e] : 0;
+    const bool rs = a.force_reset || d != 0;
+    const int pslot = (int)((k + a.R - 1) % a.R);
+    int nv = rs ? 1 : (int)a.nvalid[(int64_t)pslot * a.n + e] + 1;
+    a.nvalid[(int64_t)slot * a.n + e] = (uint8_t)(nv > 4 ? 4 : nv);
+    a.reset_flags[(int64_t)a.t * a.n + e] = rs ? 1 : 0;
+    if (a.t >= 1) {
+      float r = a.reward_pool ? a.reward_pool[pidx * a.n + e] : 0.f;
+      a.rewards[(int64_t)(a.t - 1) * a.n + e] = r;
+      a.dones[(int64_t)(a.t - 1) * a.n + e] = d;
+    }
+  }
+}
+
+// dqn_phi.py:14-16: float32(x) / 255.0 (IEEE correctly rounded division).
+__global__ void dqn_phi_kernel(const uint8_t* __restrict__ in, float* __restrict__ out, int64_t count) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 3 < count) {
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(in + i);
+    float4 o;
+    o.x = __fdiv_rn((float)(w & 0xff), 255.f);
+    o.y = __fdiv_rn((float)((w >> 8) & 0xff), 255.f);
+    o.z = __fdiv_rn((float)((w >> 16) & 0xff), 255.f);
+    o.w = __fdiv_rn((float)(w >> 24), 255.f);
+    *reinterpret_cast<float4*>(out + i) = o;
+  } else {
+    for (int64_t j = i; j < count; ++j) out[j] = __fdiv_rn((float)in[j], 255.f);
+  }
+}
+
+// ale.py:62-69 alone (max of the pair + luminance + uint8), one pixel per
+// thread; same device function as the fused path (used to verify all 2^24
+// RGB triples against NumPy).
+__global__ void max_luminance_kernel(const uint8_t* __restrict__ cur, const uint8_t* __restrict__ prev,
+                                     uint8_t* __restrict__ gray, int64_t npix) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npix) return;
+  const uint8_t* c = cur + 3 * i;
+  const uint8_t* p = prev + 3 * i;
+  const uint32_t r = c[0] > p[0] ? c[0] : p[0];
+  const uint32_t g = c[1] > p[1] ? c[1] : p[1];
+  const uint32_t b = c[2] > p[2] ? c[2] : p[2];
+  gray[i] = (uint8_t)luminance(r, g, b);
+}
+
+hipError_t launch_max_luminance(const uint8_t* cur, const uint8_t* prev, uint8_t* gray, int64_t npix,
+                                hipStream_t s) {
+  if (npix <= 0) return hipSuccess;
+  hipLaunchKernelGGL(max_luminance_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, s, cur, prev, gray,
+                     npix);
+  return hipGetLastError();
+}
+
+hipError_t launch_current_screen(const uint8_t* cur, const uint8_t* prev, uint8_t* out, int64_t n,
+                                 int mode, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(current_screen_kernel, dim3(NBANDS, (unsigned)n), dim3(256), 0, s, cur, prev, out, mode);
+  return hipGetLastError();
+}
+
+hipError_t launch_phi_stack(const uint8_t* pairs, const uint8_t* prev_stack, const uint8_t* reset,
+                            uint8_t* out_stack, int64_t n, int mode, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(phi_stack_kernel, dim3(NBANDS, (unsigned)n), dim3(256), 0, s, pairs, prev_stack,
+                     reset, out_stack, mode);
+  return hipGetLastError();
+}
+
+hipError_t launch_phi_ring(const RingArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(phi_ring_kernel, dim3(NBANDS, (unsigned)a.n), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_dqn_phi(const uint8_t* in, float* out, int64_t count, hipStream_t s) {
+  if (count <= 0) return hipSuccess;
+  const int64_t threads = (count + 3) / 4;
+  hipLaunchKernelGGL(dqn_phi_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, in, out, count);
+  return hipGetLastError();
+}
+
+}  // namespace arl

@@ -1,0 +1,215 @@
+"""Throughput of the batched A3C hot path (phi + forward + sample + n-step
+update) on MI355X -- BASELINE.json metric, configs[1] workload at N=1.
+
+One bench *step* = one lockstep window: t_max x (phi of every env's frame
+pair into the ring, NIPS-head forward, softmax policy, Philox sample), the
+bootstrap phi + forward, n-step returns + loss gradient, backward, [RCCL
+all-reduce of the flat gradient over ranks], GradientClipping(40) +
+RMSpropAsync, advance.  Units = envs_per_gpu * t_max * world env-steps per
+step.  Inputs are synthetic 210x160x3 RGB frame pairs, rewards and terminal
+flags pre-generated in HBM (a pool of `--pool` steps, cycled).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "async-rl_amd"))
+
+from asyncrl_amd import A3C, A3CFF, A3CLSTM, GradientClipping, RMSpropAsync  # noqa: E402
+from asyncrl_amd import _lib  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+F32_MFMA_PEAK_TFS = 157.3      # dense fp32 matrix peak (spec)
+PHI_BYTES_PER_ENV_STEP = 201600 + 7056      # pair read + plane write (ring)
+RMSPROP_BYTES_PER_PARAM = 20                # r p,g,ms; w p,ms
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--envs-per-gpu", type=int, default=256)
+    ap.add_argument("--t-max", type=int, default=5)
+    ap.add_argument("--arch", choices=["ff", "lstm"], default="ff")
+    ap.add_argument("--actions", type=int, default=0, help="0: 4 for ff (Breakout), 6 for lstm (Space Invaders)")
+    ap.add_argument("--pool", type=int, default=8)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="0 disables the CPU baseline leg")
+    ap.add_argument("--kernel-reps", type=int, default=50)
+    return ap.parse_args()
+
+
+def init_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def synth_pools(n, pool, seed, dev):
+    """SURVEY 8(d) synthetic inputs: uniform RGB frames (rng 1), rewards in
+    {-1,0,+1} with P(!=0)=0.05 (rng 2), terminals Bernoulli(1/500) (rng 3)."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(1 + 1000 * seed)
+    pairs = torch.randint(0, 256, (pool, n, 2, 210, 160, 3), dtype=torch.uint8, device=dev, generator=g)
+    r2 = np.random.default_rng(2 + 1000 * seed)
+    rewards = r2.choice(np.array([-1.0, 0.0, 1.0], np.float32), (pool, n), p=[0.025, 0.95, 0.025])
+    r3 = np.random.default_rng(3 + 1000 * seed)
+    dones = (r3.random((pool, n)) < 1 / 500).astype(np.uint8)
+    return pairs, torch.from_numpy(rewards).to(dev), torch.from_numpy(dones).to(dev)
+
+
+def main():
+    a = parse()
+    world, rank, local = init_dist()
+    dev = torch.device("cuda", local)
+    arch = a.arch
+    A = a.actions or (4 if arch == "ff" else 6)
+    N, T = a.envs_per_gpu, a.t_max
+    Model = A3CFF if arch == "ff" else A3CLSTM
+    model = Model(A, n_envs=N, t_max=T, seed=1234, env_offset=rank * N, init_seed=0, device=dev)
+    opt = RMSpropAsync(lr=7e-4, eps=1e-1, alpha=0.99).setup(model)
+    opt.add_hook(GradientClipping(40))
+    opt.anneal_total_steps = 8 * 10 ** 7        # a3c_ale.py:200 --steps default
+    opt.n_total_envs = N * world
+    agent = A3C(model, opt, T, 0.99, beta=1e-2)
+    pairs, rewards, dones = synth_pools(N, a.pool, rank, dev)
+    P = a.pool
+
+    use_graph = not a.no_graph
+    graph = None
+    stream = torch.cuda.Stream(device=dev)
+    stream.wait_stream(torch.cuda.current_stream())
+
+    def window():
+        if graph is not None:
+            graph.replay()
+            if world > 1:
+                agent.finish_window(stream=stream)
+            else:
+                agent.t += T
+        else:
+            agent.run_window(pairs, rewards, dones, P, first=False, stream=stream)
+
+    with torch.cuda.stream(stream):
+        agent.run_window(pairs, rewards, dones, P, first=True, stream=stream)
+        for _ in range(max(0, a.warmup - 1)):
+            agent.run_window(pairs, rewards, dones, P, stream=stream)
+        if use_graph:
+            stream.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=stream):
+                # one window; with >1 rank the all-reduce + optimizer stay eager
+                agent.run_window(pairs, rewards, dones, P, stream=stream, split_update=(world > 1))
+            graph = g
+            agent.t -= T if world == 1 else 0
+            for _ in range(2):
+                window()
+    stream.synchronize()
+
+    # ---------------------------------------------------------------- timed region
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        for _ in range(a.steps):
+            window()
+    stream.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    units = N * T * world * a.steps
+    value = units / elapsed
+    ms_step = 1e3 * elapsed / a.steps
+    finite = bool(torch.isfinite(model.net.params).all())
+
+    # ---------------------------------------------------------------- per-kernel roofline
+    # phi (arl_observe) on the same stream and buffers, HIP events around
+    # kernel-reps back-to-back launches -> average launch duration.
+    roof = None
+    if rank == 0:
+        with torch.cuda.stream(stream):
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            for t in range(3):
+                model.net.observe(1 + t % T, pairs, rewards, dones, P, stream=stream)
+            ev0.record(stream)
+            for i in range(a.kernel_reps):
+                model.net.observe(1 + i % T, pairs, rewards, dones, P, stream=stream)
+            ev1.record(stream)
+            ev1.synchronize()
+            phi_us = 1e3 * ev0.elapsed_time(ev1) / a.kernel_reps
+            ev0.record(stream)
+            for i in range(a.kernel_reps):
+                model.net.optimize(lr0=1e-12, clip=0.0, stream=stream)
+            ev1.record(stream)
+            ev1.synchronize()
+            rms_us = 1e3 * ev0.elapsed_time(ev1) / a.kernel_reps
+        phi_bytes = N * PHI_BYTES_PER_ENV_STEP
+        phi_gbs = phi_bytes / (phi_us * 1e-6) / 1e9
+        rms_bytes = model.net.n_params * RMSPROP_BYTES_PER_PARAM
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "traffic_r01.json")
+        if os.path.exists(tf):
+            try:
+                with open(tf) as f:
+                    tj = json.load(f)
+                if tj.get("envs") == N:
+                    traffic = tj.get("phi_ring_kernel_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roof = {"bound": "hbm", "kernel": "phi_ring_kernel (arl_observe)", "achieved": round(phi_gbs, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(phi_gbs / HBM_PEAK_GBS, 4),
+                "traffic": traffic, "bytes_per_launch": phi_bytes, "avg_launch_us": round(phi_us, 2),
+                "rmsprop": {"achieved": round(rms_bytes / (rms_us * 1e-6) / 1e9, 1), "unit": "GB/s",
+                            "avg_launch_us": round(rms_us, 2), "bytes_per_launch": rms_bytes,
+                            "note": "sqnorm disabled (clip=0) in this isolated timing"}}
+
+    cpu = None
+    if rank == 0 and world == 1 and a.cpu_seconds > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import cpu_baseline  # noqa: E402  (oracle/, CPU baseline leg only)
+        cpu = cpu_baseline.run(seconds=a.cpu_seconds, t_max=T, n_actions=4)
+
+    if rank == 0:
+        out = {
+            "metric": "env-steps/sec (phi+forward+sample+update) at 1/2/4/8 MI355X; % roofline",
+            "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (uniform RGB 210x160 frame pairs, rewards P(!=0)=0.05, terminals p=1/500)",
+            "config": {"workload": ("A3C %s NIPS-DQN head, %d envs x t_max=%d per GPU (phi + conv head + sampling "
+                                    "+ n-step returns + backward + clip + RMSProp)") % (arch.upper(), N, T),
+                       "envs_per_gpu": N, "global_envs": N * world, "t_max": T, "n_actions": A, "arch": arch,
+                       "graph": use_graph, "parallelism": "dp%d" % world,
+                       "units_per_step": N * T * world},
+            "roofline": roof, "cpu_baseline": cpu, "params_finite": finite,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,151 @@
+/*
+ * asyncrl_hip.h -- C ABI of libasyncrl_hip.so, the MI355X (gfx950) hot path of
+ * batched A3C (phi + forward + sample + n-step update) for PeerM/async-rl.
+ *
+ * Every entry point takes plain device pointers, sizes and a hipStream_t
+ * (passed as void*; NULL = the default stream).  Calls are asynchronous on
+ * that stream, never allocate, never synchronise, and are graph-capturable.
+ * Return value: 0 (ARL_OK) or an error code; arl_last_error() describes the
+ * last failure of the calling thread.
+ *
+ * Each function names the reference interface it replaces (file:line in
+ * PeerM/async-rl @ v0).  INTEGRATION.md shows the ctypes binding a maintainer
+ * adds on the reference side.
+ */
+#ifndef ASYNCRL_HIP_H
+#define ASYNCRL_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ARL_OK 0
+#define ARL_EINVAL 1   /* bad argument (shape, pointer, alignment) */
+#define ARL_EHIP 2     /* HIP runtime error (launch failure) */
+#define ARL_ESTATE 3   /* handle not bound / wrong arch for this call */
+
+#define ARL_ARCH_FF 0     /* A3CFF   (a3c_ale.py:28-40) */
+#define ARL_ARCH_LSTM 1   /* A3CLSTM (a3c_ale.py:43-70) */
+
+#define ARL_RESIZE_SCALAR 0  /* OpenCV FixedPtCast vertical pass (canonical) */
+#define ARL_RESIZE_SIMD 1    /* OpenCV VResizeLinearVec_32s8u (mulhi) pass */
+
+int arl_abi_version(void);
+const char* arl_last_error(void);
+
+/* ------------------------------------------------------------------ phi */
+
+/* ale.py:59-89 ALE.current_screen (crop_or_scale='scale'), batched.
+ * rgb_cur, rgb_prev: (n, 210, 160, 3) uint8, 16-byte aligned.
+ * out: (n, 84, 84) uint8.  max -> fp64 luminance -> uint8 -> 84x84 resize. */
+int arl_current_screen(const uint8_t* rgb_cur, const uint8_t* rgb_prev, uint8_t* out, int64_t n,
+                       int resize_mode, void* stream);
+
+/* ale.py:62-69 alone: np.maximum of the two frames + float64 luminance +
+ * astype(uint8), for npix pixels (rgb: (npix, 3) uint8) -> gray (npix,). */
+int arl_max_luminance(const uint8_t* rgb_cur, const uint8_t* rgb_prev, uint8_t* gray, int64_t npix,
+                      void* stream);
+
+/* ale.py:135 + ale.py:155-158 (frame-stack deque), batched, materialised.
+ * rgb_pairs: (n, 2, 210, 160, 3) uint8 (frame 4 and frame 3 of the skip);
+ * prev_stack, out_stack: (n, 4, 84, 84) uint8, must not alias;
+ * reset: (n,) uint8 or NULL -- 1 = episode start: [0, 0, 0, new]. */
+int arl_phi_stack(const uint8_t* rgb_pairs, const uint8_t* prev_stack, const uint8_t* reset,
+                  uint8_t* out_stack, int64_t n, int resize_mode, void* stream);
+
+/* dqn_phi.py:4-17 dqn_phi, batched: (n, 4, 84, 84) uint8 -> float32 / 255. */
+int arl_dqn_phi(const uint8_t* stack_u8, float* out, int64_t n, void* stream);
+
+/* ------------------------------------------------------------------ net */
+typedef struct arl_net arl_net;
+
+/* Describe an A3C model + lockstep actor-learner over n_envs envs and
+ * t_max-step windows (a3c.py:33-61 A3C.__init__, a3c_ale.py:219-229).
+ * env_offset: global id of this rank's env 0 (RNG stream); seed: Philox key. */
+int arl_net_create(arl_net** out, int arch, int n_actions, int n_envs, int t_max, int env_offset,
+                   uint64_t seed);
+void arl_net_destroy(arl_net* net);
+
+/* Flat parameter layout (Chainer namedparams order, each tensor 64-float
+ * aligned).  The same layout is used for params, grads and RMSProp ms. */
+int64_t arl_net_param_floats(const arl_net* net);
+int arl_net_param_count(const arl_net* net);
+int arl_net_param_info(const arl_net* net, int idx, int64_t* offset, int64_t* numel, char* name, int name_cap);
+
+/* Caller-owned device workspace (activations, frame ring, rollout buffers). */
+int64_t arl_net_workspace_bytes(const arl_net* net);
+int arl_net_buffer(const arl_net* net, const char* name, int64_t* offset, int64_t* bytes);
+
+/* Bind caller-owned device memory: params/grads/ms (param_floats f32 each,
+ * 16-byte aligned; grads must be zeroed once by the caller) and workspace. */
+int arl_net_bind(arl_net* net, float* params, float* grads, float* ms, void* workspace);
+
+/* Reset the control block (step counters) and the frame ring; call once
+ * before the first observation (async). */
+int arl_net_reset(arl_net* net, void* stream);
+
+/* Observation at window step t (0..t_max): phi of the env's frame pair into
+ * the ring + stack bookkeeping + ingest of the reward/done that came with it
+ * (a3c.py:69-75; ale.py:111-139).  Pools hold pool_len steps; the step used
+ * is (control-block step + t) % pool_len.  pair_pool: (pool_len, n, 2, 210,
+ * 160, 3) uint8; reward_pool: (pool_len, n) f32; done_pool: (pool_len, n)
+ * uint8 (1 = the transition into this obs ended the episode, which also
+ * resets the frame stack and LSTM state).  force_reset: treat every env as
+ * starting an episode (first observation). */
+int arl_observe(arl_net* net, int t, const uint8_t* pair_pool, const float* reward_pool,
+                const uint8_t* done_pool, int64_t pool_len, int force_reset, int resize_mode, void* stream);
+
+/* A3C.act forward + sample at window step t (a3c.py:154-164): pi_and_v of
+ * the ring state, softmax policy output, Philox inverse-CDF action.  t ==
+ * t_max is the bootstrap value of the window end (a3c.py:85, pre-update
+ * params, LSTM state kept: a3c_ale.py:57-60); it samples nothing. */
+int arl_act(arl_net* net, int t, void* stream);
+
+/* Window update, gradient part (a3c.py:82-130): n-step returns with R = 0 at
+ * terminals, advantage / entropy / value loss gradient, backward through
+ * heads, [LSTM BPTT], FC, conv2, conv1 -> grads (overwritten). */
+int arl_learn(arl_net* net, double gamma, double beta, double v_loss_coef, int clip_reward, void* stream);
+
+/* GradientClipping(clip) + RMSpropAsync update (a3c_ale.py:224-226,
+ * rmsprop_async.py:23-29) of the bound params / ms from the bound grads.
+ * total_steps > 0 anneals lr on device (a3c_ale.py:111-112) with global_t =
+ * (step + t_max) * n_total; otherwise lr = lr0.  clip <= 0 disables clipping. */
+int arl_optimize(arl_net* net, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
+                 double clip, void* stream);
+
+/* End of window: advance step counters, carry reset flags / LSTM state. */
+int arl_advance(arl_net* net, void* stream);
+
+/* A3CFF.pi_and_v on explicit f32 states (a3c_ale.py:38-40; input from
+ * dqn_phi).  n <= n_envs; outputs in the workspace's bootstrap slot. */
+int arl_forward_states(arl_net* net, const float* states, int64_t n, void* stream);
+
+/* ------------------------------------------------------------------ granular ops */
+
+/* RMSpropAsync.update_one (rmsprop_async.py:23-38) on flat f32 arrays, with
+ * optional Chainer GradientClipping (norm over g, scale if clip/norm < 1).
+ * norm_partials: device f64[1024] scratch (needed when clip > 0). */
+int arl_rmsprop(float* param, float* ms, const float* grad, int64_t n, double lr, double alpha, double eps,
+                double clip, double* norm_partials, void* stream);
+
+/* SoftmaxPolicyOutput (policy_output.py:32-61) + FCSoftmaxPolicy / FCVFunction
+ * heads (policy.py:53-58, v_function.py:29-34) for h: (n, 256) f32.  Samples
+ * with Philox(seed; env_offset + row, step) when sample != 0. */
+int arl_policy(const float* h, int64_t n, const float* W_pi, const float* b_pi, const float* W_v,
+               const float* b_v, int n_actions, uint64_t seed, const int64_t* step_dev, int64_t step_off,
+               int env_offset, int sample, float* logits, float* probs, float* log_probs, float* v,
+               float* entropy, int32_t* actions, float* action_log_probs, void* stream);
+
+/* a3c.py:82-126: returns + loss gradient over a (t_max, n) window. v, probs,
+ * log_probs, actions are (t_max+1, n[, A]) with row t_max = bootstrap. */
+int arl_returns_lossgrad(const float* rewards, const uint8_t* dones, const float* v, const float* probs,
+                         const float* log_probs, const int32_t* actions, int t_max, int64_t n, int n_actions,
+                         double gamma, double beta, double v_loss_coef, int clip_reward, float* dlogits,
+                         float* dv, float* loss, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ASYNCRL_HIP_H */

@@ -1,0 +1,84 @@
+"""CPU baseline: the oracle's restatement of ONE reference actor-learner
+process (a3c_ale.py:92-171 train_loop -> a3c.py:67-167 act), batch 1,
+single-threaded (OMP_NUM_THREADS=1 as at a3c_ale.py:186), timed on the host.
+
+TEST / BASELINE INFRASTRUCTURE ONLY (imported by bench.py's cpu_baseline leg).
+Per env-step: ale.py:59-89 current_screen + deque push, dqn_phi, NIPS-head
+forward + heads (batch 1), softmax / log-softmax / entropy, one draw; every
+t_max steps: bootstrap forward, n-step returns, backward over the window,
+GradientClipping(40), RMSpropAsync over all 677,429 parameters -- the same
+work the reference does per step minus the emulator.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+
+import oracle as O
+
+
+def run(seconds: float = 10.0, t_max: int = 5, n_actions: int = 4, seed: int = 0, pool: int = 16):
+    try:
+        from threadpoolctl import threadpool_limits
+        limiter = threadpool_limits(1)
+    except Exception:  # pragma: no cover
+        limiter = None
+    rng = np.random.default_rng(seed)
+    params = O.init_like_torch(O.ARCH_FF, n_actions, rng)
+    ms = {k: np.zeros_like(v) for k, v in params.items()}
+    frames = rng.integers(0, 256, (pool, 2, 210, 160, 3), dtype=np.uint8)
+    rewards = rng.choice(np.array([-1.0, 0.0, 1.0], np.float32), pool, p=[0.025, 0.95, 0.025])
+    dones = (rng.random(pool) < 1 / 500).astype(np.uint8)
+    names = list(params)
+    stack = O.stack_push(None, O.current_screen(frames[0, 0], frames[0, 1]), True)
+    steps = 0
+    buf = []
+    t0 = time.perf_counter()
+    deadline = t0 + seconds
+    while True:
+        k = steps % pool
+        x = O.PHI_LUT[stack][None]
+        logits, v, acts = O.pi_and_v_ff(params, x)
+        p = O.softmax(logits)
+        lp = O.log_softmax(logits)
+        u = O.sample_uniforms(seed, np.zeros(1, np.uint64), steps)
+        a = O.sample_from_uniform(p, u)
+        buf.append((x, acts, p, lp, v, a))
+        # env transition: next observation (phi), reward, terminal
+        j = (k + 1) % pool
+        scr = O.current_screen(frames[j, 0], frames[j, 1])
+        stack = O.stack_push(stack, scr, bool(dones[j]))
+        steps += 1
+        if steps % t_max == 0:
+            xb = O.PHI_LUT[stack][None]
+            _, vb, _ = O.pi_and_v_ff(params, xb)
+            T = len(buf)
+            r = np.array([[rewards[(steps - T + i + 1) % pool]] for i in range(T)], np.float32)
+            d = np.array([[dones[(steps - T + i + 1) % pool]] for i in range(T)], np.uint8)
+            probs = np.stack([b[2] for b in buf])
+            logp = np.stack([b[3] for b in buf])
+            vals = np.stack([b[4] for b in buf])
+            act = np.stack([b[5] for b in buf])
+            _, _, dl, dv, _, _ = O.returns_and_lossgrad(r, d, vals, vb, probs, logp, act)
+            xs = np.concatenate([b[0] for b in buf])
+            a1 = np.concatenate([b[1][0] for b in buf])
+            a2 = np.concatenate([b[1][1] for b in buf])
+            hh = np.concatenate([b[1][2] for b in buf])
+            g = O.ff_backward(params, xs, (a1, a2, hh), dl.reshape(T, -1), dv.reshape(T))
+            gl, _ = O.clip_grads([g[n] for n in names], 40.0)
+            for n, gn in zip(names, gl):
+                params[n], ms[n] = O.rmsprop_update(params[n], ms[n], gn, 7e-4)
+            buf = []
+            if time.perf_counter() >= deadline:
+                break
+    el = time.perf_counter() - t0
+    if limiter is not None:
+        limiter.unregister() if hasattr(limiter, "unregister") else None
+    return {"value": steps / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{steps} env-steps ({steps // t_max} windows of t_max={t_max}) of one batch-1 "
+                      f"A3C-FF actor-learner (NumPy restatement, 1 thread), {el:.1f} s"}
+
+
+if __name__ == "__main__":
+    print(run(5.0))

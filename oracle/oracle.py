@@ -1,0 +1,602 @@
+"""CPU oracle: a NumPy restatement of the reference A3C hot path.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in the product package (`async-rl_amd/`)
+imports this module.  Only `tests/`, `__graft_entry__.smoke()` and the
+`cpu_baseline` leg of `bench.py` may use it, and only as the checker / the
+timed CPU baseline -- never as the thing measured or shipped.
+
+Every function restates one piece of PeerM/async-rl (reference @ v0) and cites
+the file:line it follows.  Where the arithmetic lives in a third-party library
+that is absent here (Chainer 1.8.1, pinned in README.md:53; OpenCV, unpinned),
+the function restates that library's published algorithm and says so.
+
+Pinning (see DESIGN.md "Oracle"):
+  * luminance / max-pool / frame stack / dqn_phi: pinned bit-exact by golden
+    vectors produced by the reference's own code (tests/golden/gen_golden.py
+    imports /root/reference/dqn_phi.py directly and runs ale.py's
+    current_screen with stub ALE/cv2 modules).
+  * RMSpropAsync.update_one_cpu: pinned by golden vectors from the reference's
+    own rmsprop_async.py run on NumPy arrays through a minimal chainer stub.
+  * OpenCV INTER_LINEAR resize: parity UNPINNED (OpenCV absent, version
+    unpinned); the scalar FixedPtCast path is declared canonical.
+  * Chainer conv/linear/LSTM/softmax/autograd: parity UNPINNED by reference
+    fixtures (Chainer absent); restated from Chainer 1.8.1 semantics and
+    cross-checked against torch-CPU autograd in tests/test_oracle.py.  The
+    trained Breakout checkpoint (tests/golden/breakout_ff.npz) supplies real
+    weights.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+F32 = np.float32
+
+# ----------------------------------------------------------------------------
+# Phi: ale.py:59-89, ale.py:111-161, dqn_phi.py:4-17
+# ----------------------------------------------------------------------------
+
+SRC_H, SRC_W = 210, 160
+DST = 84
+
+
+def max_pool_pair(cur: np.ndarray, prev: np.ndarray) -> np.ndarray:
+    """ale.py:62 -- np.maximum of the two captured RGB frames (uint8)."""
+    return np.maximum(cur, prev)
+
+
+def luminance_u8(rgb: np.ndarray) -> np.ndarray:
+    """ale.py:67-69 -- float64 R*0.2126 + G*0.0722 + B*0.7152 (left to
+    right), then astype(uint8) truncation.  Note G/B weights are swapped
+    relative to Rec.709; reproduced as written."""
+    r = rgb[..., 0] * 0.2126
+    g = rgb[..., 1] * 0.0722
+    b = rgb[..., 2] * 0.7152
+    return ((r + g) + b).astype(np.uint8)
+
+
+def resize_coeffs(ssize: int, dsize: int):
+    """OpenCV (unpinned; restated from the 3.x/4.x generic resize path)
+    INTER_LINEAR fixed-point coefficients for one axis, as called from
+    ale.py:84-85 (cv2.resize(img, (84, 84), INTER_LINEAR)).
+
+    scale = 1/(dsize/ssize) in double; f = (float)((d+0.5)*scale-0.5);
+    s = floor(f); f -= s; clamp at borders; alpha = saturate_cast<short>
+    ((1-f)*2048), (f*2048) with round-half-even (cvRound)."""
+    inv_scale = float(dsize) / float(ssize)
+    scale = 1.0 / inv_scale
+    ofs = np.zeros(dsize, np.int32)
+    alpha = np.zeros((dsize, 2), np.int32)
+    for d in range(dsize):
+        f = F32((d + 0.5) * scale - 0.5)
+        s = int(math.floor(float(f)))
+        f = F32(f - F32(s))
+        if s < 0:
+            f, s = F32(0.0), 0
+        if s >= ssize - 1:
+            f, s = F32(0.0), ssize - 1
+        c0 = F32(F32(1.0) - f)
+        c1 = f
+        a0 = int(np.rint(F32(c0 * F32(2048.0))))
+        a1 = int(np.rint(F32(c1 * F32(2048.0))))
+        ofs[d] = s
+        alpha[d] = (a0, a1)
+    return ofs, alpha
+
+
+_XOFS, _XALPHA = resize_coeffs(SRC_W, DST)
+_YOFS, _YBETA = resize_coeffs(SRC_H, DST)
+
+RESIZE_SCALAR = 0   # FixedPtCast<int,uchar,22>: (b0*r0 + b1*r1 + 2^21) >> 22
+RESIZE_SIMD = 1     # VResizeLinearVec_32s8u: ((r0>>4)*b0>>16)+((r1>>4)*b1>>16)+2 >> 2
+
+
+def resize_linear_u8(img: np.ndarray, mode: int = RESIZE_SCALAR) -> np.ndarray:
+    """cv2.resize(img, (84,84), INTER_LINEAR) for a (..., 210, 160) uint8
+    plane (ale.py:84-85).  Horizontal pass: int row = S[sx]*a0 + S[sx+1]*a1
+    (HResizeLinear, exact); vertical pass per `mode`."""
+    src = img.astype(np.int64)
+    xs = _XOFS
+    xs1 = np.minimum(xs + 1, SRC_W - 1)
+    rows = src[..., :, xs] * _XALPHA[:, 0] + src[..., :, xs1] * _XALPHA[:, 1]
+    ys = _YOFS
+    ys1 = np.minimum(ys + 1, SRC_H - 1)
+    r0 = rows[..., ys, :]
+    r1 = rows[..., ys1, :]
+    b0 = _YBETA[:, 0][:, None]
+    b1 = _YBETA[:, 1][:, None]
+    if mode == RESIZE_SCALAR:
+        out = (b0 * r0 + b1 * r1 + (1 << 21)) >> 22
+    elif mode == RESIZE_SIMD:
+        out = ((((r0 >> 4) * b0) >> 16) + (((r1 >> 4) * b1) >> 16) + 2) >> 2
+    else:
+        raise ValueError("resize mode must be 0 (scalar) or 1 (simd)")
+    return np.clip(out, 0, 255).astype(np.uint8)
+
+
+def current_screen(cur: np.ndarray, prev: np.ndarray,
+                   mode: int = RESIZE_SCALAR) -> np.ndarray:
+    """ale.py:59-89 (crop_or_scale='scale', the default at ale.py:18):
+    max of two frames -> luminance -> uint8 -> 84x84 resize."""
+    assert cur.shape[-3:] == (SRC_H, SRC_W, 3)
+    return resize_linear_u8(luminance_u8(max_pool_pair(cur, prev)), mode)
+
+
+def stack_push(stack: np.ndarray, plane: np.ndarray, reset: bool) -> np.ndarray:
+    """ale.py:155-158 (reset: three zero planes + the new screen) and
+    ale.py:135 (deque(maxlen=4).append).  Oldest plane first."""
+    if reset:
+        out = np.zeros((4, DST, DST), np.uint8)
+        out[3] = plane
+        return out
+    return np.concatenate([stack[1:], plane[None]], axis=0)
+
+
+def dqn_phi(screens) -> np.ndarray:
+    """dqn_phi.py:4-17: asarray(float32) then in-place /= 255.0 (IEEE f32)."""
+    assert len(screens) == 4
+    raw = np.asarray(screens, dtype=np.float32)
+    raw /= F32(255.0)
+    return raw
+
+
+PHI_LUT = (np.arange(256, dtype=np.float32) / F32(255.0)).astype(np.float32)
+
+# ----------------------------------------------------------------------------
+# Model parameters: a3c_ale.py:28-70, dqn_head.py:31-52, policy.py:32-58,
+# v_function.py:10-34, init_like_torch.py:5-22
+# ----------------------------------------------------------------------------
+
+ARCH_FF = 0
+ARCH_LSTM = 1
+
+
+def param_shapes(arch: int, n_actions: int):
+    """Chainer namedparams / HDF5 paths in link order (a3c_ale.py:35,52)."""
+    head = [("0/0/W", (16, 4, 8, 8)), ("0/0/b", (16,)),
+            ("0/1/W", (32, 16, 4, 4)), ("0/1/b", (32,)),
+            ("0/2/W", (256, 2592)), ("0/2/b", (256,))]
+    if arch == ARCH_FF:
+        return head + [("1/0/W", (n_actions, 256)), ("1/0/b", (n_actions,)),
+                       ("2/0/W", (1, 256)), ("2/0/b", (1,))]
+    if arch == ARCH_LSTM:
+        return head + [("1/upward/W", (1024, 256)), ("1/upward/b", (1024,)),
+                       ("1/lateral/W", (1024, 256)),
+                       ("2/0/W", (n_actions, 256)), ("2/0/b", (n_actions,)),
+                       ("3/0/W", (1, 256)), ("3/0/b", (1,))]
+    raise ValueError(arch)
+
+
+def pname(arch: int, role: str) -> str:
+    """Short role names -> namedparam paths."""
+    if arch == ARCH_FF:
+        m = {"c1W": "0/0/W", "c1b": "0/0/b", "c2W": "0/1/W", "c2b": "0/1/b",
+             "fcW": "0/2/W", "fcb": "0/2/b", "piW": "1/0/W", "pib": "1/0/b",
+             "vW": "2/0/W", "vb": "2/0/b"}
+    else:
+        m = {"c1W": "0/0/W", "c1b": "0/0/b", "c2W": "0/1/W", "c2b": "0/1/b",
+             "fcW": "0/2/W", "fcb": "0/2/b", "luW": "1/upward/W",
+             "lub": "1/upward/b", "llW": "1/lateral/W", "piW": "2/0/W",
+             "pib": "2/0/b", "vW": "3/0/W", "vb": "3/0/b"}
+    return m[role]
+
+
+def init_like_torch(arch: int, n_actions: int, rng: np.random.Generator):
+    """init_like_torch.py:5-22: U(-1/sqrt(fan_in), +1/sqrt(fan_in)) for W and
+    b of every Linear / Convolution2D; fan_in = in*kh*kw.  (Same distribution,
+    a seeded Generator instead of the global RNG.)"""
+    params = {}
+    shapes = dict(param_shapes(arch, n_actions))
+    for name, shape in param_shapes(arch, n_actions):
+        wshape = shapes[name.rsplit("/", 1)[0] + "/W"]
+        fan_in = int(np.prod(wshape[1:]))
+        stdv = 1.0 / np.sqrt(fan_in)
+        params[name] = rng.uniform(-stdv, stdv, size=shape).astype(np.float32)
+    return params
+
+
+# ----------------------------------------------------------------------------
+# Forward (Chainer 1.8.1 semantics, restated)
+# ----------------------------------------------------------------------------
+
+def _im2col(x: np.ndarray, k: int, s: int):
+    """Chainer conv.im2col_cpu layout: (N, C, kh, kw, OH, OW) -> we return
+    (N, OH, OW, C*kh*kw) rows (cross-correlation, no padding)."""
+    n, c, h, w = x.shape
+    oh = (h - k) // s + 1
+    ow = (w - k) // s + 1
+    st = x.strides
+    view = np.lib.stride_tricks.as_strided(
+        x, shape=(n, oh, ow, c, k, k),
+        strides=(st[0], st[2] * s, st[3] * s, st[1], st[2], st[3]),
+        writeable=False)
+    return np.ascontiguousarray(view).reshape(n, oh, ow, c * k * k), oh, ow
+
+
+def conv2d(x: np.ndarray, W: np.ndarray, b: np.ndarray, s: int) -> np.ndarray:
+    """L.Convolution2D forward (dqn_head.py:41-42): tensordot(col, W) + b."""
+    oc, ic, k, _ = W.shape
+    cols, oh, ow = _im2col(x, k, s)
+    y = cols.reshape(-1, ic * k * k) @ W.reshape(oc, -1).T
+    y = y.astype(np.float32) + b
+    return y.reshape(x.shape[0], oh, ow, oc).transpose(0, 3, 1, 2).copy()
+
+
+def conv2d_backward(x, W, gy, s, need_dx=True):
+    """Gradient of conv2d w.r.t. W, b and (optionally) x."""
+    oc, ic, k, _ = W.shape
+    n = x.shape[0]
+    cols, oh, ow = _im2col(x, k, s)
+    gyf = gy.transpose(0, 2, 3, 1).reshape(-1, oc)
+    gW = (gyf.T @ cols.reshape(-1, ic * k * k)).reshape(W.shape)
+    gb = gyf.sum(axis=0, dtype=np.float32)
+    gx = None
+    if need_dx:
+        gcol = (gyf @ W.reshape(oc, -1)).reshape(n, oh, ow, ic, k, k)
+        gx = np.zeros_like(x)
+        for ky in range(k):
+            for kx in range(k):
+                gx[:, :, ky:ky + s * oh:s, kx:kx + s * ow:s] += \
+                    gcol[:, :, :, :, ky, kx].transpose(0, 3, 1, 2)
+    return gW.astype(np.float32), gb.astype(np.float32), gx
+
+
+def relu(x):
+    return np.maximum(x, F32(0.0))
+
+
+def linear(x, W, b=None):
+    """L.Linear: y = x.dot(W.T) (+ b)."""
+    y = (x @ W.T).astype(np.float32)
+    if b is not None:
+        y = y + b
+    return y
+
+
+def nips_head(params, arch, x):
+    """NIPSDQNHead.__call__ (dqn_head.py:48-52): conv(8,s4) -> relu ->
+    conv(4,s2) -> relu -> Linear(2592,256) -> relu.  Returns activations."""
+    a1 = relu(conv2d(x, params[pname(arch, "c1W")], params[pname(arch, "c1b")], 4))
+    a2 = relu(conv2d(a1, params[pname(arch, "c2W")], params[pname(arch, "c2b")], 2))
+    h = relu(linear(a2.reshape(a2.shape[0], -1), params[pname(arch, "fcW")],
+                    params[pname(arch, "fcb")]))
+    return a1, a2, h
+
+
+def sigmoid(x):
+    return (F32(1.0) / (F32(1.0) + np.exp(-x))).astype(np.float32)
+
+
+def lstm_cell(params, arch, x, h_prev, c_prev, has_state):
+    """Chainer 1.8.1 L.LSTM.__call__ + F.lstm (a3c_ale.py:50-51,59,62):
+    lstm_in = upward(x) [+ lateral(h) if h is not None]; gates interleaved
+    (reshape(N, 256, 4)): a,i,f,o = [:, :, 0..3]; c = tanh(a)*sig(i) +
+    sig(f)*c_prev; h = sig(o)*tanh(c).  has_state (N,) bool: False = state
+    is None (after reset_state, a3c_ale.py:65-66)."""
+    g = linear(x, params[pname(arch, "luW")], params[pname(arch, "lub")])
+    m = has_state.astype(np.float32)[:, None]
+    g = g + linear(h_prev * m, params[pname(arch, "llW")])
+    a = np.tanh(g[:, 0::4])
+    i = sigmoid(g[:, 1::4])
+    f = sigmoid(g[:, 2::4])
+    o = sigmoid(g[:, 3::4])
+    c = a * i + f * (c_prev * m)
+    h = o * np.tanh(c)
+    return g, c.astype(np.float32), h.astype(np.float32)
+
+
+def softmax(z):
+    """F.softmax (policy_output.py:41-43): max-subtracted exp, normalised."""
+    y = z - z.max(axis=1, keepdims=True)
+    y = np.exp(y)
+    return (y / y.sum(axis=1, keepdims=True)).astype(np.float32)
+
+
+def log_softmax(z):
+    """F.log_softmax (policy_output.py:45-47): x - logsumexp(x)."""
+    m = z.max(axis=1, keepdims=True)
+    s = np.log(np.exp(z - m).sum(axis=1, keepdims=True))
+    return (z - (m + s)).astype(np.float32)
+
+
+def entropy(p, logp):
+    """policy_output.py:59-61: -sum(p * log p)."""
+    return (-(p * logp).sum(axis=-1)).astype(np.float32)
+
+
+def pi_and_v_ff(params, x):
+    """A3CFF.pi_and_v (a3c_ale.py:38-40)."""
+    a1, a2, h = nips_head(params, ARCH_FF, x)
+    logits = linear(h, params["1/0/W"], params["1/0/b"])
+    v = linear(h, params["2/0/W"], params["2/0/b"])[:, 0]
+    return logits, v, (a1, a2, h)
+
+
+# ----------------------------------------------------------------------------
+# Sampling: policy_output.py:12-29 (distributional parity); Philox4x32-10
+# ----------------------------------------------------------------------------
+
+_PM0, _PM1 = 0xD2511F53, 0xCD9E8D57
+_PW0, _PW1 = 0x9E3779B9, 0xBB67AE85
+_M32 = 0xFFFFFFFF
+
+
+def philox4x32(ctr, key, rounds=10):
+    """Philox4x32-10 (Salmon et al. 2011).  ctr: (4, n) uint64 arrays of
+    32-bit words; key: (2,) ints.  Returns (4, n) uint64 of 32-bit words."""
+    c0, c1, c2, c3 = [np.asarray(c, np.uint64) & _M32 for c in ctr]
+    k0 = np.uint64(key[0] & _M32)
+    k1 = np.uint64(key[1] & _M32)
+    for r in range(rounds):
+        p0 = c0 * np.uint64(_PM0)
+        p1 = c2 * np.uint64(_PM1)
+        hi0, lo0 = p0 >> np.uint64(32), p0 & np.uint64(_M32)
+        hi1, lo1 = p1 >> np.uint64(32), p1 & np.uint64(_M32)
+        c0, c1, c2, c3 = (hi1 ^ c1 ^ k0), lo1, (hi0 ^ c3 ^ k1), lo0
+        if r != rounds - 1:
+            k0 = (k0 + np.uint64(_PW0)) & np.uint64(_M32)
+            k1 = (k1 + np.uint64(_PW1)) & np.uint64(_M32)
+    return c0, c1, c2, c3
+
+
+def sample_uniforms(seed: int, env_ids: np.ndarray, step: int) -> np.ndarray:
+    """One U[0,1) f32 per env: Philox(ctr=(env, step_lo, step_hi, 0),
+    key=(seed_lo, seed_hi)), u = (word0 >> 8) * 2^-24."""
+    env_ids = np.asarray(env_ids, np.uint64)
+    n = env_ids.shape[0]
+    ctr = (env_ids, np.full(n, step & _M32, np.uint64),
+           np.full(n, (step >> 32) & _M32, np.uint64), np.zeros(n, np.uint64))
+    w0, _, _, _ = philox4x32(ctr, (seed & _M32, (seed >> 32) & _M32))
+    return ((w0 >> np.uint64(8)).astype(np.float32) * F32(2.0 ** -24)).astype(np.float32)
+
+
+def sample_from_uniform(probs: np.ndarray, u: np.ndarray) -> np.ndarray:
+    """Inverse-CDF draw: first k with u < cumsum_f32(p)[k] (sequential f32
+    adds), else A-1.  Distributionally equal to np.random.multinomial(1, p)
+    at policy_output.py:26-28 (which first subtracts epsneg, :24)."""
+    n, a = probs.shape
+    out = np.full(n, a - 1, np.int32)
+    cdf = np.zeros(n, np.float32)
+    done = np.zeros(n, bool)
+    for k in range(a):
+        cdf = (cdf + probs[:, k]).astype(np.float32)
+        hit = (~done) & (u < cdf)
+        out[hit] = k
+        done |= hit
+    return out
+
+
+# ----------------------------------------------------------------------------
+# n-step return, losses and their gradient: a3c.py:82-126
+# ----------------------------------------------------------------------------
+
+def returns_and_lossgrad(rewards, dones, values, vboot, probs, logp, actions,
+                         gamma=0.99, beta=0.01, v_loss_coef=0.5,
+                         clip_reward=True):
+    """Batched restatement of a3c.py:82-126 over a lockstep window.
+
+    rewards, dones: (T, N) -- reward / terminal of transition t -> t+1
+    values: (T, N) f32 v(s_t); vboot: (N,) f32 v(s_T) (pre-update params)
+    probs, logp: (T, N, A); actions: (T, N).
+    R is accumulated in float64 like the Python float at a3c.py:83-92; each
+    terminal restarts it at 0 (a segment per episode, a3c.py:82-83).
+    Returns R (f32), advantage, dlogits (T,N,A), dv (T,N), pi_loss, v_loss.
+    """
+    T, N = rewards.shape
+    A = probs.shape[2]
+    r = np.asarray(rewards, np.float64)
+    if clip_reward:
+        r = np.clip(r, -1, 1)                     # a3c.py:69-70
+    R = vboot.astype(np.float64).copy()
+    Rs = np.zeros((T, N), np.float32)
+    for t in reversed(range(T)):
+        R = np.where(dones[t] != 0, 0.0, R)       # a3c.py:82-83 (R=0 at terminal)
+        R = R * gamma + r[t]                      # a3c.py:91-92
+        Rs[t] = R.astype(np.float32)
+    adv = (Rs - values).astype(np.float32)        # a3c.py:97 (f32 AddConstant)
+    H = entropy(probs, logp)
+    onehot = np.zeros_like(probs)
+    np.put_along_axis(onehot, actions[..., None].astype(np.int64), 1.0, axis=2)
+    # d/dz of [-logpi(a)*adv - beta*H]  (a3c.py:103,105)
+    dlogits = (-adv[..., None] * (onehot - probs)
+               + F32(beta) * probs * (logp + H[..., None])).astype(np.float32)
+    dv = (F32(v_loss_coef) * (values - Rs)).astype(np.float32)   # a3c.py:108,113-114
+    logp_a = np.take_along_axis(logp, actions[..., None].astype(np.int64), 2)[..., 0]
+    pi_loss = float(-(logp_a * adv).sum() - beta * H.sum())
+    v_loss = float(v_loss_coef * (((values - Rs) ** 2) / 2).sum())
+    return Rs, adv, dlogits, dv, pi_loss, v_loss
+
+
+# ----------------------------------------------------------------------------
+# Backward (total_loss.backward(), a3c.py:129-130), restated by hand
+# ----------------------------------------------------------------------------
+
+def ff_backward(params, x, acts, dlogits, dv):
+    """Gradients of sum_i (dlogits_i . z_i + dv_i * v_i) for the A3CFF graph
+    (a3c_ale.py:38-40) over a batch of samples.  acts = (a1, a2, h)."""
+    a1, a2, h = acts
+    g = {}
+    g["1/0/W"] = (dlogits.T @ h).astype(np.float32)
+    g["1/0/b"] = dlogits.sum(0, dtype=np.float32)
+    g["2/0/W"] = (dv[None, :] @ h).astype(np.float32)
+    g["2/0/b"] = np.array([dv.sum(dtype=np.float32)], np.float32)
+    dh = dlogits @ params["1/0/W"] + dv[:, None] * params["2/0/W"]
+    _head_backward(params, ARCH_FF, x, a1, a2, h, dh.astype(np.float32), g)
+    return g
+
+
+def _head_backward(params, arch, x, a1, a2, h, dh, g):
+    n = x.shape[0]
+    dfc = dh * (h > 0)
+    g[pname(arch, "fcW")] = (dfc.T @ a2.reshape(n, -1)).astype(np.float32)
+    g[pname(arch, "fcb")] = dfc.sum(0, dtype=np.float32)
+    da2 = (dfc @ params[pname(arch, "fcW")]).reshape(a2.shape) * (a2 > 0)
+    gW2, gb2, da1 = conv2d_backward(a1, params[pname(arch, "c2W")],
+                                    da2.astype(np.float32), 2)
+    g[pname(arch, "c2W")], g[pname(arch, "c2b")] = gW2, gb2
+    da1 = (da1 * (a1 > 0)).astype(np.float32)
+    gW1, gb1, _ = conv2d_backward(x, params[pname(arch, "c1W")], da1, 4,
+                                  need_dx=False)
+    g[pname(arch, "c1W")], g[pname(arch, "c1b")] = gW1, gb1
+
+
+# ----------------------------------------------------------------------------
+# GradientClipping(40) (a3c_ale.py:226, Chainer hook) and RMSpropAsync
+# ----------------------------------------------------------------------------
+
+def grad_sqnorm(grads) -> float:
+    """Chainer _sum_sqnorm: per-array f32 dot, summed as Python floats."""
+    return float(sum(float(np.dot(gv.ravel(), gv.ravel())) for gv in grads))
+
+
+def clip_grads(grads, threshold=40.0):
+    """GradientClipping: rate = threshold / norm; if rate < 1: g *= rate
+    (f32 array *= f64 scalar -> f32 multiply by f32(rate))."""
+    norm = math.sqrt(grad_sqnorm(grads))
+    rate = threshold / norm if norm > 0 else float("inf")
+    if rate < 1:
+        r32 = F32(rate)
+        return [(gv * r32).astype(np.float32) for gv in grads], norm
+    return [gv.copy() for gv in grads], norm
+
+
+def rmsprop_update(p, ms, g, lr, alpha=0.99, eps=0.1):
+    """rmsprop_async.py:23-29 (update_one_cpu), f32 rounding of each op:
+    ms *= alpha; ms += (1-alpha)*g*g; p -= lr*g/sqrt(ms+eps)."""
+    p = p.astype(np.float32).copy()
+    ms = ms.astype(np.float32).copy()
+    ms *= F32(alpha)
+    ms += (F32(1 - alpha) * g) * g
+    p -= (F32(lr) * g) / np.sqrt(ms + F32(eps))
+    return p, ms
+
+
+def annealed_lr(lr0, total_steps, global_t):
+    """a3c_ale.py:111-112."""
+    return (total_steps - global_t - 1) / total_steps * lr0
+
+
+# ----------------------------------------------------------------------------
+# Lockstep window (batched A3C): per-env segments at fixed theta
+# ----------------------------------------------------------------------------
+
+def state_from_ring(frames, nvalid, slots):
+    """Build (N,4,84,84) f32 states from ring planes frames[slot] (N,84,84)
+    for the 4 slots oldest->newest, zeroing planes before the last reset
+    (nvalid in 1..4 = number of valid trailing planes)."""
+    n = nvalid.shape[0]
+    x = np.zeros((n, 4, DST, DST), np.float32)
+    for c in range(4):
+        pl = PHI_LUT[frames[slots[c]]]
+        keep = (c >= 4 - nvalid.astype(np.int32))
+        x[:, c] = np.where(keep[:, None, None], pl, F32(0.0))
+    return x
+
+
+@dataclass
+class LSTMState:
+    h: np.ndarray
+    c: np.ndarray
+    has: np.ndarray   # (N,) bool
+
+
+def ff_window_grads(params, states, actions, rewards, dones, boot_state,
+                    gamma=0.99, beta=0.01, v_loss_coef=0.5):
+    """Gradient of one lockstep window for A3CFF at fixed theta.
+
+    states: (T, N, 4, 84, 84) f32; boot_state (N,4,84,84) f32 = s_T.
+    Per env the window splits into segments at terminals; each segment is
+    one a3c.py:77-130 update at fixed theta; gradients are summed."""
+    T, N = actions.shape
+    x = states.reshape(T * N, 4, DST, DST)
+    logits, v, acts = pi_and_v_ff(params, x)
+    p = softmax(logits)
+    lp = log_softmax(logits)
+    _, vb, _ = pi_and_v_ff(params, boot_state)
+    A = logits.shape[1]
+    R, adv, dlog, dv, pil, vl = returns_and_lossgrad(
+        rewards, dones, v.reshape(T, N), vb, p.reshape(T, N, A),
+        lp.reshape(T, N, A), actions, gamma, beta, v_loss_coef)
+    g = ff_backward(params, x, acts, dlog.reshape(T * N, A), dv.reshape(T * N))
+    return g, dict(logits=logits.reshape(T, N, A), v=v.reshape(T, N), vboot=vb,
+                   R=R, adv=adv, dlogits=dlog, dv=dv, pi_loss=pil, v_loss=vl)
+
+
+def lstm_window(params, states, actions, rewards, dones_prev, dones, boot_state,
+                st0: LSTMState, gamma=0.99, beta=0.01, v_loss_coef=0.5):
+    """A3CLSTM window (a3c_ale.py:55-70) at fixed theta with truncated BPTT
+    over the window (unchain_backward, a3c.py:144) and resets at terminals.
+
+    dones_prev: (T, N): reset before step t (done of transition t-1 -> t;
+    row 0 = the flag carried from the previous window)."""
+    T, N = actions.shape
+    arch = ARCH_LSTM
+    A = params["2/0/W"].shape[0]
+    xs = states.reshape(T * N, 4, DST, DST)
+    a1, a2, hh = nips_head(params, arch, xs)
+    hh = hh.reshape(T, N, 256)
+    hs, cs, gs, has_l, hprev_l, cprev_l = [], [], [], [], [], []
+    h, c, has = st0.h, st0.c, st0.has.copy()
+    for t in range(T):
+        has = has & (dones_prev[t] == 0)
+        g, c_new, h_new = lstm_cell(params, arch, hh[t], h, c, has)
+        hprev_l.append(h * has[:, None]); cprev_l.append(c * has[:, None])
+        has_l.append(has.copy()); gs.append(g)
+        h, c = h_new, c_new
+        has = np.ones(N, bool)
+        hs.append(h); cs.append(c)
+    H = np.stack(hs)
+    logits = linear(H.reshape(T * N, 256), params["2/0/W"], params["2/0/b"])
+    v = linear(H.reshape(T * N, 256), params["3/0/W"], params["3/0/b"])[:, 0]
+    p = softmax(logits); lp = log_softmax(logits)
+    # bootstrap with keep_same_state (a3c_ale.py:57-60)
+    _, _, hb = nips_head(params, arch, boot_state)
+    hasb = has & (dones[T - 1] == 0)
+    _, _, hbb = lstm_cell(params, arch, hb, h, c, hasb)
+    vb = linear(hbb, params["3/0/W"], params["3/0/b"])[:, 0]
+    R, adv, dlog, dv, pil, vl = returns_and_lossgrad(
+        rewards, dones, v.reshape(T, N), vb, p.reshape(T, N, A),
+        lp.reshape(T, N, A), actions, gamma, beta, v_loss_coef)
+    dl = dlog.reshape(T * N, A); dvf = dv.reshape(T * N)
+    g = {}
+    Hf = H.reshape(T * N, 256)
+    g["2/0/W"] = (dl.T @ Hf).astype(np.float32)
+    g["2/0/b"] = dl.sum(0, dtype=np.float32)
+    g["3/0/W"] = (dvf[None, :] @ Hf).astype(np.float32)
+    g["3/0/b"] = np.array([dvf.sum(dtype=np.float32)], np.float32)
+    dH = (dl @ params["2/0/W"] + dvf[:, None] * params["3/0/W"]).reshape(T, N, 256)
+    dh_next = np.zeros((N, 256), np.float32)
+    dc_next = np.zeros((N, 256), np.float32)
+    dG = np.zeros((T, N, 1024), np.float32)
+    for t in reversed(range(T)):
+        gt = gs[t]
+        a = np.tanh(gt[:, 0::4]); i = sigmoid(gt[:, 1::4])
+        f = sigmoid(gt[:, 2::4]); o = sigmoid(gt[:, 3::4])
+        ct = cs[t]; tc = np.tanh(ct)
+        dh = dH[t] + dh_next
+        dc = dh * o * (F32(1) - tc * tc) + dc_next
+        dg = np.zeros((N, 1024), np.float32)
+        dg[:, 0::4] = dc * i * (F32(1) - a * a)
+        dg[:, 1::4] = dc * a * i * (F32(1) - i)
+        dg[:, 2::4] = dc * cprev_l[t] * f * (F32(1) - f)
+        dg[:, 3::4] = dh * tc * o * (F32(1) - o)
+        dG[t] = dg
+        m = has_l[t].astype(np.float32)[:, None]
+        dc_next = (dc * f * m).astype(np.float32)
+        dh_next = ((dg @ params["1/lateral/W"]) * m).astype(np.float32)
+    dGf = dG.reshape(T * N, 1024)
+    g["1/upward/W"] = (dGf.T @ hh.reshape(T * N, 256)).astype(np.float32)
+    g["1/upward/b"] = dGf.sum(0, dtype=np.float32)
+    g["1/lateral/W"] = (dGf.T @ np.stack(hprev_l).reshape(T * N, 256)).astype(np.float32)
+    dx = (dGf @ params["1/upward/W"]).astype(np.float32)
+    _head_backward(params, arch, xs, a1, a2, hh.reshape(T * N, 256), dx, g)
+    aux = dict(logits=logits.reshape(T, N, A), v=v.reshape(T, N), vboot=vb,
+               R=R, adv=adv, dlogits=dlog, dv=dv, pi_loss=pil, v_loss=vl,
+               h_last=h, c_last=c, has_last=has)
+    return g, aux
+
+
+def flat_names(arch, n_actions):
+    return [n for n, _ in param_shapes(arch, n_actions)]

@@ -1,0 +1,271 @@
+"""Generate the golden fixtures under tests/golden/ from the reference's OWN code.
+
+Run in the build container only (needs /root/reference, read-only):
+    python tests/golden/gen_golden.py
+
+What runs from the reference (nothing is copied; modules are imported from
+/root/reference at generation time only):
+  * dqn_phi.dqn_phi                -- imported directly (numpy only).
+  * ale.ALE.current_screen / initialize / receive_action / state
+                                   -- imported with two stub modules for
+    absent third-party packages: `ale_python_interface` (a fake emulator that
+    serves seeded synthetic 210x160x3 frames, lives and rewards) and `cv2`
+    (its `resize` records the reference's luminance image and answers with
+    the oracle's OpenCV restatement, so resize parity stays "unpinned").
+  * rmsprop_async.RMSpropAsync.update_one_cpu
+                                   -- imported with a minimal `chainer` stub
+    (`cuda.get_array_module`, `optimizer.GradientMethod`), run on NumPy arrays.
+  * trained_model/breakout_ff/80000000_finish.h5
+                                   -- read with h5py (conda python3.9; plain
+    HDF5 datasets, nothing executed) and saved as breakout_ff.npz.
+
+Outputs are data only (inputs + expected outputs).
+"""
+import os
+import subprocess
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import oracle  # noqa: E402
+
+
+def synth_frames(rng, n, kind):
+    """Synthetic 210x160x3 uint8 frames: uniform, sparse palette
+    blocks on black ("Breakout-shaped"), all-255, all-0."""
+    if kind == "uniform":
+        return rng.integers(0, 256, (n, 210, 160, 3), dtype=np.uint8)
+    if kind == "white":
+        return np.full((n, 210, 160, 3), 255, np.uint8)
+    if kind == "black":
+        return np.zeros((n, 210, 160, 3), np.uint8)
+    if kind == "palette":
+        pal = rng.integers(0, 256, (16, 3), dtype=np.uint8)
+        out = np.zeros((n, 210, 160, 3), np.uint8)
+        for i in range(n):
+            for _ in range(40):
+                y, x = rng.integers(0, 200), rng.integers(0, 150)
+                h, w = rng.integers(2, 10), rng.integers(2, 12)
+                out[i, y:y + h, x:x + w] = pal[rng.integers(0, 16)]
+        return out
+    raise ValueError(kind)
+
+
+# --------------------------------------------------------------------------
+# stubs for absent third-party modules
+# --------------------------------------------------------------------------
+RESIZE_LOG = []
+
+
+def install_cv2_stub():
+    cv2 = types.ModuleType("cv2")
+    cv2.INTER_LINEAR = 1
+
+    def resize(img, dsize, interpolation=None):
+        assert dsize == (84, 84) and interpolation == 1
+        RESIZE_LOG.append(np.array(img, copy=True))
+        return oracle.resize_linear_u8(img, oracle.RESIZE_SCALAR)
+
+    cv2.resize = resize
+    sys.modules["cv2"] = cv2
+
+
+class FakeALE:
+    """Stand-in for ale_python_interface.ALEInterface serving seeded frames.
+    Episode: lives 3, a life lost at frame 22, game over at frame 41."""
+
+    def __init__(self):
+        self.rng = np.random.default_rng(11)
+        self.frame = 0
+        self.start = 0
+        self._lives = 3
+        self._over = False
+        self.served = []
+
+    def setInt(self, *a): pass
+    def setFloat(self, *a): pass
+    def setBool(self, *a): pass
+    def setString(self, *a): pass
+    def loadROM(self, *a): pass
+    def getFrameNumber(self): return 0
+    def getMinimalActionSet(self): return [0, 1, 3, 4]
+
+    def getScreenRGB(self):
+        f = synth_frames(np.random.default_rng(1000 + self.frame), 1, "palette")[0]
+        if self.frame % 7 == 3:
+            f[::2, ::3] = 255
+        return f
+
+    def act(self, a):
+        self.frame += 1
+        if self.frame - self.start == 22:
+            self._lives -= 1
+        if self.frame - self.start >= 41:
+            self._over = True
+        return int(self.frame % 5 == 0)
+
+    def lives(self): return self._lives
+    def game_over(self): return self._over
+
+    def reset_game(self):
+        self.start = self.frame
+        self._over = False
+        self._lives = 3
+
+
+def install_ale_stub():
+    m = types.ModuleType("ale_python_interface")
+    m.ALEInterface = FakeALE
+    sys.modules["ale_python_interface"] = m
+
+
+def install_chainer_stub():
+    ch = types.ModuleType("chainer")
+    cuda = types.ModuleType("chainer.cuda")
+    cuda.get_array_module = lambda *a: np
+    opt = types.ModuleType("chainer.optimizer")
+
+    class GradientMethod(object):
+        pass
+
+    opt.GradientMethod = GradientMethod
+    ch.cuda = cuda
+    ch.optimizer = opt
+    sys.modules["chainer"] = ch
+    sys.modules["chainer.cuda"] = cuda
+    sys.modules["chainer.optimizer"] = opt
+
+
+# --------------------------------------------------------------------------
+def gen_phi():
+    rng = np.random.default_rng(1)
+    cur, prev = [], []
+    for kind, n in (("uniform", 2), ("palette", 2), ("white", 1), ("black", 1)):
+        cur.append(synth_frames(rng, n, kind))
+        prev.append(synth_frames(rng, n, kind))
+    # one pair mixing white and uniform so max() matters
+    cur.append(synth_frames(rng, 1, "white"))
+    prev.append(synth_frames(rng, 1, "uniform"))
+    cur = np.concatenate(cur)
+    prev = np.concatenate(prev)
+
+    install_cv2_stub()
+    install_ale_stub()
+    sys.path.insert(0, REF)
+    import ale  # reference ale.py
+
+    gray = []
+    shots = []
+    for i in range(cur.shape[0]):
+        env = ale.ALE.__new__(ale.ALE)
+        env.crop_or_scale = "scale"
+        env.ale = types.SimpleNamespace(getScreenRGB=lambda i=i: cur[i])
+        env.last_raw_screen = prev[i]
+        RESIZE_LOG.clear()
+        shots.append(env.current_screen())          # ale.py:59-89 verbatim
+        gray.append(RESIZE_LOG[0])
+    gray = np.stack(gray)
+    np.savez_compressed(os.path.join(HERE, "phi_golden.npz"), cur=cur, prev=prev,
+                        gray=gray, screen_scalar=np.stack(shots))
+
+    # ---- episode stack semantics through ALE.initialize / receive_action
+    np.random.seed(5)
+    fake_pairs = []
+    orig_cs = ale.ALE.current_screen
+
+    def logged_cs(self):
+        fake_pairs.append((self.ale.getScreenRGB().copy(), self.last_raw_screen.copy()))
+        return orig_cs(self)
+
+    ale.ALE.current_screen = logged_cs
+    env = ale.ALE("fake.rom", seed=3, max_start_nullops=4)
+    states, terms, pair_idx = [np.array(env.state)], [False], [len(fake_pairs) - 1]
+    resets = [True]
+    for step in range(24):
+        if env.is_terminal:
+            env.initialize()
+            resets.append(True)
+        else:
+            env.receive_action(step % 4)
+            resets.append(False)
+        states.append(np.array(env.state))
+        terms.append(bool(env.is_terminal))
+        pair_idx.append(len(fake_pairs) - 1)
+    ale.ALE.current_screen = orig_cs
+    cur_f = np.stack([p[0] for p in fake_pairs])
+    prev_f = np.stack([p[1] for p in fake_pairs])
+    np.savez_compressed(os.path.join(HERE, "ale_stack_golden.npz"),
+                        pair_cur=cur_f, pair_prev=prev_f,
+                        states=np.stack(states), terminal=np.array(terms),
+                        reset=np.array(resets), pair_idx=np.array(pair_idx))
+    sys.path.remove(REF)
+
+
+def gen_dqn_phi():
+    sys.path.insert(0, REF)
+    import dqn_phi  # reference dqn_phi.py, imported directly
+    rng = np.random.default_rng(2)
+    stacks = rng.integers(0, 256, (3, 4, 84, 84), dtype=np.uint8)
+    stacks[0, 0] = np.arange(84 * 84, dtype=np.int64).reshape(84, 84) % 256
+    stacks[1, 2] = 255
+    out = np.stack([dqn_phi.dqn_phi([s for s in st]) for st in stacks])
+    np.savez_compressed(os.path.join(HERE, "dqn_phi_golden.npz"), stacks=stacks, out=out)
+    sys.path.remove(REF)
+
+
+def gen_rmsprop():
+    install_chainer_stub()
+    sys.path.insert(0, REF)
+    import rmsprop_async  # reference rmsprop_async.py
+    rng = np.random.default_rng(3)
+    n = 4096
+    p = rng.standard_normal(n).astype(np.float32) * 0.05
+    ms = np.abs(rng.standard_normal(n)).astype(np.float32) * 0.01
+    ms[:16] = 0.0
+    g = rng.standard_normal(n).astype(np.float32) * 0.3
+    g[16:32] = 0.0
+    steps = []
+    opt = rmsprop_async.RMSpropAsync(lr=7e-4, eps=1e-1, alpha=0.99)
+    cur_p, cur_ms = p.copy(), ms.copy()
+    for k in range(3):
+        # a3c_ale.py:111-112 anneal, total 8e7 steps, at global_t = 10**6*k
+        opt.lr = (8 * 10 ** 7 - 10 ** 6 * k - 1) / (8 * 10 ** 7) * 7e-4
+        gk = (g * (1.0 + 0.5 * k)).astype(np.float32)
+        param = types.SimpleNamespace(data=cur_p.copy(), grad=gk)
+        state = {"ms": cur_ms.copy()}
+        opt.update_one_cpu(param, state)          # rmsprop_async.py:23-29
+        steps.append((cur_p.copy(), cur_ms.copy(), gk, opt.lr, param.data.copy(),
+                      state["ms"].copy()))
+        cur_p, cur_ms = param.data, state["ms"]
+    np.savez_compressed(
+        os.path.join(HERE, "rmsprop_golden.npz"),
+        p=np.stack([s[0] for s in steps]), ms=np.stack([s[1] for s in steps]),
+        g=np.stack([s[2] for s in steps]), lr=np.array([s[3] for s in steps]),
+        p_out=np.stack([s[4] for s in steps]), ms_out=np.stack([s[5] for s in steps]))
+    sys.path.remove(REF)
+
+
+def gen_checkpoint():
+    src = os.path.join(REF, "trained_model/breakout_ff/80000000_finish.h5")
+    dst = os.path.join(HERE, "breakout_ff.npz")
+    code = ("import h5py, numpy as np, sys\n"
+            "f = h5py.File(sys.argv[1], 'r')\n"
+            "d = {}\n"
+            "f.visititems(lambda n, o: d.__setitem__(n, o[()]) "
+            "if isinstance(o, h5py.Dataset) else None)\n"
+            "np.savez_compressed(sys.argv[2], **{k.replace('/', '|'): v for k, v in d.items()})\n")
+    subprocess.check_call(["/opt/conda/bin/python3.9", "-c", code, src, dst])
+
+
+if __name__ == "__main__":
+    gen_phi()
+    gen_dqn_phi()
+    gen_rmsprop()
+    gen_checkpoint()
+    for f in sorted(os.listdir(HERE)):
+        print(f, os.path.getsize(os.path.join(HERE, f)))

@@ -1,0 +1,58 @@
+"""Test-side helpers: synthetic env pools and the oracle's view of the
+lockstep windows the GPU runs on them (test infrastructure, uses oracle/)."""
+import numpy as np
+
+import oracle as O
+
+
+def make_pools(rng, pool_len, n, kind="uniform", p_done=0.15):
+    """pairs (pool_len, n, 2, 210, 160, 3) uint8 (frame 4, frame 3 of the
+    skip); rewards (pool_len, n) f32 incl. out-of-range values (clip test);
+    dones (pool_len, n) uint8."""
+    if kind == "uniform":
+        pairs = rng.integers(0, 256, (pool_len, n, 2, 210, 160, 3), dtype=np.uint8)
+    else:
+        pairs = np.zeros((pool_len, n, 2, 210, 160, 3), np.uint8)
+        pal = rng.integers(0, 256, (16, 3), dtype=np.uint8)
+        for k in range(pool_len):
+            for e in range(n):
+                for f in range(2):
+                    for _ in range(30):
+                        y, x = rng.integers(0, 200), rng.integers(0, 150)
+                        pairs[k, e, f, y:y + 8, x:x + 10] = pal[rng.integers(0, 16)]
+    rewards = rng.choice(np.array([-2.0, -1.0, 0.0, 0.0, 0.0, 1.0, 3.5], np.float32), (pool_len, n))
+    dones = (rng.random((pool_len, n)) < p_done).astype(np.uint8)
+    return pairs, rewards.astype(np.float32), dones
+
+
+class OracleEnvView:
+    """Frame stacks the GPU's ring holds after observing pool steps 0..k
+    (k = 0 force-reset; afterwards reset = done that came with the obs)."""
+
+    def __init__(self, pairs, dones, mode=O.RESIZE_SCALAR):
+        self.pairs, self.dones, self.mode = pairs, dones, mode
+        self.pool_len, self.n = pairs.shape[0], pairs.shape[1]
+        self.stacks = {}
+        self._stack = None
+        self._k = -1
+
+    def stack(self, k):
+        while self._k < k:
+            self._k += 1
+            j = self._k % self.pool_len
+            scr = np.stack([O.current_screen(self.pairs[j, e, 0], self.pairs[j, e, 1], self.mode)
+                            for e in range(self.n)])
+            out = np.zeros((self.n, 4, 84, 84), np.uint8)
+            for e in range(self.n):
+                reset = self._k == 0 or self.dones[j, e] != 0
+                out[e] = O.stack_push(None if reset else self._stack[e], scr[e], reset)
+            self._stack = out
+            self.stacks[self._k] = out
+        return self.stacks[k]
+
+    def states_f32(self, k0, T):
+        return np.stack([O.PHI_LUT[self.stack(k0 + t)] for t in range(T)]), O.PHI_LUT[self.stack(k0 + T)]
+
+    def window_rd(self, rewards, k0, T):
+        idx = [(k0 + t + 1) % self.pool_len for t in range(T)]
+        return rewards[idx].copy(), self.dones[idx].copy()

@@ -1,0 +1,83 @@
+"""CPU: the C-ABI library loads, exports every symbol include/asyncrl_hip.h
+declares, and its host-side logic (layout, validation) behaves -- no kernel
+launches (no GPU here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "asyncrl_hip.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(arl_\w+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    from asyncrl_amd import _lib
+    syms = declared_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(_lib.lib, s), s
+    # and the ctypes table covers exactly the header
+    assert sorted(_lib.SIGNATURES) == syms
+
+
+def test_abi_version_and_errors():
+    from asyncrl_amd._lib import lib
+    assert lib.arl_abi_version() == 1
+    h = ctypes.c_void_p()
+    rc = lib.arl_net_create(ctypes.byref(h), 7, 4, 16, 5, 0, 0)
+    assert rc == 1 and b"arch" in lib.arl_last_error()
+    rc = lib.arl_net_create(ctypes.byref(h), 0, 0, 16, 5, 0, 0)
+    assert rc == 1
+    # calls on an unbound handle fail cleanly
+    assert lib.arl_net_create(ctypes.byref(h), 0, 4, 16, 5, 0, 0) == 0
+    assert lib.arl_act(h, 0, None) == 3
+    assert lib.arl_act(h, 0, None) == 3 and b"bound" in lib.arl_last_error()
+    lib.arl_net_destroy(h)
+
+
+@pytest.mark.parametrize("arch,A,count", [(0, 4, 677429), (1, 6, 1203255)])
+def test_param_layout_matches_chainer(arch, A, count):
+    from asyncrl_amd._lib import lib
+    from asyncrl_amd.net import param_shapes
+    import numpy as np
+    h = ctypes.c_void_p()
+    assert lib.arl_net_create(ctypes.byref(h), arch, A, 256, 5, 0, 0) == 0
+    shapes = param_shapes(arch, A)
+    assert lib.arl_net_param_count(h) == len(shapes)
+    name = ctypes.create_string_buffer(64)
+    total = 0
+    prev_end = 0
+    for i, (nm, shp) in enumerate(shapes):
+        off, num = ctypes.c_int64(), ctypes.c_int64()
+        assert lib.arl_net_param_info(h, i, ctypes.byref(off), ctypes.byref(num), name, 64) == 0
+        assert name.value.decode() == nm
+        assert num.value == int(np.prod(shp))
+        assert off.value % 64 == 0 and off.value >= prev_end
+        prev_end = off.value + num.value
+        total += num.value
+    assert total == count
+    assert lib.arl_net_param_floats(h) >= total
+    ws = lib.arl_net_workspace_bytes(h)
+    assert 0 < ws < 4 << 30
+    off, nb = ctypes.c_int64(), ctypes.c_int64()
+    assert lib.arl_net_buffer(h, b"frames", ctypes.byref(off), ctypes.byref(nb)) == 0
+    assert nb.value == 9 * 256 * 84 * 84 and off.value % 256 == 0
+    assert lib.arl_net_buffer(h, b"nope", ctypes.byref(off), ctypes.byref(nb)) == 1
+    lib.arl_net_destroy(h)
+
+
+def test_product_path_has_no_oracle_dependency():
+    """The shipped package must never import the CPU oracle."""
+    pkg = os.path.join(ROOT, "async-rl_amd", "asyncrl_amd")
+    for f in os.listdir(pkg):
+        if f.endswith(".py"):
+            src = open(os.path.join(pkg, f)).read()
+            assert "oracle" not in src.replace("no oracle", ""), f

@@ -1,0 +1,308 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the
+reference-generated golden fixtures.
+
+Tolerances (stated per test): integer / byte / index work is bit-exact;
+fp32 contractions |gpu - oracle| <= 1e-5 * max(|oracle|, ||oracle||_inf)
+(norm-scaled); the RMSProp kernel is bit-exact vs the reference."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from conftest import close_normscaled, golden, load_checkpoint
+from sim import OracleEnvView, make_pools
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+def dev(x, gpu):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(gpu)
+
+
+# ------------------------------------------------------------------ phi
+def test_luminance_all_rgb_triples(gpu):
+    from asyncrl_amd import max_luminance
+    trip = np.arange(1 << 24, dtype=np.uint32)
+    rgb = np.stack([(trip >> 16) & 255, (trip >> 8) & 255, trip & 255], -1).astype(np.uint8)
+    zero = np.zeros_like(rgb)
+    g = max_luminance(dev(rgb, gpu), dev(zero, gpu)).cpu().numpy()
+    assert (g == O.luminance_u8(rgb)).all()
+    # max() of the pair: swap roles with a shifted copy
+    other = np.roll(rgb, 12345, axis=0)
+    g2 = max_luminance(dev(other, gpu), dev(rgb, gpu)).cpu().numpy()
+    assert (g2 == O.luminance_u8(np.maximum(rgb, other))).all()
+
+
+def test_current_screen_matches_reference_golden(gpu):
+    from asyncrl_amd import current_screen
+    d = golden("phi_golden.npz")
+    cur, prev = dev(d["cur"], gpu), dev(d["prev"], gpu)
+    out = current_screen(cur, prev, 0).cpu().numpy()
+    assert (out == d["screen_scalar"]).all()
+    simd = current_screen(cur, prev, 1).cpu().numpy()
+    ref = np.stack([O.current_screen(c, p, O.RESIZE_SIMD) for c, p in zip(d["cur"], d["prev"])])
+    assert (simd == ref).all()
+
+
+@pytest.mark.parametrize("kind", ["uniform", "palette"])
+def test_phi_stack_matches_oracle(gpu, kind):
+    from asyncrl_amd import phi_stack
+    rng = np.random.default_rng(11)
+    n = 37
+    pairs, _, _ = make_pools(rng, 1, n, kind)
+    pairs = pairs[0]
+    prev = rng.integers(0, 256, (n, 4, 84, 84), dtype=np.uint8)
+    reset = (rng.random(n) < 0.3).astype(np.uint8)
+    out = phi_stack(dev(pairs, gpu), dev(prev, gpu), dev(reset, gpu)).cpu().numpy()
+    for e in range(n):
+        scr = O.current_screen(pairs[e, 0], pairs[e, 1])
+        assert (out[e] == O.stack_push(prev[e], scr, bool(reset[e]))).all(), e
+
+
+def test_dqn_phi_matches_reference_golden(gpu):
+    from asyncrl_amd import dqn_phi
+    d = golden("dqn_phi_golden.npz")
+    out = dqn_phi(dev(d["stacks"], gpu)).cpu().numpy()
+    assert (out == d["out"]).all()
+    allv = np.tile(np.arange(256, dtype=np.uint8), 4 * 84 * 84 // 256 + 1)[:4 * 84 * 84].reshape(1, 4, 84, 84)
+    assert (dqn_phi(dev(allv, gpu)).cpu().numpy() == O.PHI_LUT[allv]).all()
+
+
+def test_observe_ring_reproduces_reference_stacks(gpu):
+    """arl_observe over 12 steps with resets: the ring + nvalid view equals
+    the ale.py deque semantics (oracle.stack_push) at every step."""
+    from asyncrl_amd import DeviceNet
+    rng = np.random.default_rng(12)
+    N, T, P = 5, 5, 12
+    pairs, rewards, dones = make_pools(rng, P, N, "palette", p_done=0.25)
+    net = DeviceNet(0, 4, N, T)
+    net.reset()
+    view = OracleEnvView(pairs, dones)
+    dp, dr, dd = dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu)
+    frames = net.buffer("frames", torch.uint8, (net.t_max + 4, N, 84, 84))
+    nvalid = net.buffer("nvalid", torch.uint8, (net.t_max + 4, N))
+    R = T + 4
+    rew = net.buffer("rewards", torch.float32, (T, N))
+    dn = net.buffer("dones", torch.uint8, (T, N))
+    for w in range(2):                      # obs steps k = w*T + t
+        for t in range(0 if w == 0 else 1, T + 1):
+            k = w * T + t
+            net.observe(t, dp, dr, dd, P, force_reset=(k == 0))
+            fr, nv = frames.cpu().numpy(), nvalid.cpu().numpy()
+            want = view.stack(k)
+            for e in range(N):
+                got = np.stack([fr[(k - 3 + c) % R, e] if c >= 4 - nv[k % R, e]
+                                else np.zeros((84, 84), np.uint8) for c in range(4)])
+                assert (got == want[e]).all(), (k, e)
+            if t >= 1:   # reward / done of the transition into obs k
+                assert (rew[t - 1].cpu().numpy() == rewards[k % P]).all()
+                assert (dn[t - 1].cpu().numpy() == dones[k % P]).all()
+        net.advance()
+
+
+# ------------------------------------------------------------------ forward / policy
+def test_forward_real_checkpoint_matches_oracle(gpu):
+    from asyncrl_amd import A3CFF, dqn_phi
+    ck = load_checkpoint()
+    n = 24
+    model = A3CFF(4, n_envs=n, t_max=5, init_seed=None)
+    model.net.load_params(ck)
+    rng = np.random.default_rng(13)
+    stacks = rng.integers(0, 256, (n, 4, 84, 84), dtype=np.uint8)
+    stacks[:4, :2] = 0
+    x = dqn_phi(dev(stacks, gpu))
+    pout, v = model.pi_and_v(x)
+    lo, vo, _ = O.pi_and_v_ff(ck, O.PHI_LUT[stacks])
+    for got, want in ((pout.logits, lo), (v, vo), (pout.probs, O.softmax(lo)),
+                      (pout.log_probs, O.log_softmax(lo))):
+        ok, err = close_normscaled(got.cpu().numpy(), want, RTOL)
+        assert ok, err
+    ent = O.entropy(O.softmax(lo), O.log_softmax(lo))
+    assert close_normscaled(pout.entropy.cpu().numpy(), ent, RTOL)[0]
+
+
+# ------------------------------------------------------------------ full windows
+def _grads_match(net, g_oracle, rtol=RTOL):
+    got = net.state_dict(net.grads)
+    for k, want in g_oracle.items():
+        ok, err = close_normscaled(got[k], want, rtol)
+        assert ok, (k, err)
+
+
+def _run_ff(gpu, N, T, A, seed, kind, windows=2, ckpt=False):
+    from asyncrl_amd import A3C, A3CFF, GradientClipping, RMSpropAsync
+    rng = np.random.default_rng(seed)
+    P = 2 * T + 1
+    pairs, rewards, dones = make_pools(rng, P, N, kind)
+    model = A3CFF(A, n_envs=N, t_max=T, seed=99, init_seed=seed)
+    if ckpt:
+        model.net.load_params(load_checkpoint())
+    opt = RMSpropAsync(lr=7e-4, eps=1e-1, alpha=0.99)
+    opt.setup(model)
+    opt.add_hook(GradientClipping(40))
+    agent = A3C(model, opt, T, 0.99, beta=1e-2)
+    net = model.net
+    view = OracleEnvView(pairs, dones)
+    dp, dr, dd = dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu)
+    for w in range(windows):
+        k0 = w * T
+        params = net.state_dict()
+        agent.run_window(dp, dr, dd, P, first=(w == 0), split_update=True)
+        torch.cuda.synchronize()
+        states, boot = view.states_f32(k0, T)
+        r, d = view.window_rd(rewards, k0, T)
+        acts = net.buffer("actions", torch.int32, (T + 1, N))[:T].cpu().numpy()
+        g, aux = O.ff_window_grads(params, states, acts, r, d, boot)
+        logits = net.buffer("logits", torch.float32, (T + 1, N, A))[:T].cpu().numpy()
+        v = net.buffer("v", torch.float32, (T + 1, N)).cpu().numpy()
+        assert close_normscaled(logits, aux["logits"], RTOL)[0]
+        assert close_normscaled(v[:T], aux["v"], RTOL)[0]
+        assert close_normscaled(v[T], aux["vboot"], RTOL)[0]
+        dl = net.buffer("dlogits", torch.float32, (T, N, A)).cpu().numpy()
+        assert close_normscaled(dl, aux["dlogits"], RTOL)[0]
+        # sampling: exact given the GPU's probs and the oracle's Philox uniforms
+        probs = net.buffer("probs", torch.float32, (T + 1, N, A)).cpu().numpy()
+        for t in range(T):
+            u = O.sample_uniforms(99, np.arange(N, dtype=np.uint64), k0 + t)
+            assert (O.sample_from_uniform(probs[t], u) == acts[t]).all()
+        _grads_match(net, g)
+        # optimizer step vs oracle clip + RMSProp (delta-params, 1e-4 derived)
+        ms0 = net.state_dict(net.ms)
+        agent.finish_window()
+        torch.cuda.synchronize()
+        names = list(g)
+        gl, _ = O.clip_grads([g[k] for k in names], 40.0)
+        new = net.state_dict()
+        for k, gk in zip(names, gl):
+            p1, _ = O.rmsprop_update(params[k], ms0[k], gk, 7e-4)
+            ok, err = close_normscaled(new[k] - params[k], p1 - params[k], 1e-4)
+            assert ok, (k, err)
+
+
+def test_ff_windows_match_oracle(gpu):
+    _run_ff(gpu, N=6, T=5, A=4, seed=21, kind="uniform")
+
+
+def test_ff_windows_real_checkpoint_palette_frames(gpu):
+    _run_ff(gpu, N=5, T=5, A=4, seed=22, kind="palette", ckpt=True)
+
+
+def test_ff_wide_action_set(gpu):
+    _run_ff(gpu, N=3, T=3, A=18, seed=23, kind="uniform", windows=1)
+
+
+def test_lstm_windows_match_oracle(gpu):
+    from asyncrl_amd import A3C, A3CLSTM, GradientClipping, RMSpropAsync
+    rng = np.random.default_rng(31)
+    N, T, A = 4, 5, 6
+    P = 2 * T + 1
+    pairs, rewards, dones = make_pools(rng, P, N, "palette", p_done=0.2)
+    model = A3CLSTM(A, n_envs=N, t_max=T, seed=5, init_seed=31)
+    opt = RMSpropAsync(lr=7e-4, eps=1e-1, alpha=0.99).setup(model)
+    opt.add_hook(GradientClipping(40))
+    agent = A3C(model, opt, T, 0.99)
+    net = model.net
+    view = OracleEnvView(pairs, dones)
+    dp, dr, dd = dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu)
+    st = O.LSTMState(h=np.zeros((N, 256), np.float32), c=np.zeros((N, 256), np.float32),
+                     has=np.zeros(N, bool))
+    prev_done = np.ones(N, np.uint8)
+    for w in range(2):
+        k0 = w * T
+        params = net.state_dict()
+        agent.run_window(dp, dr, dd, P, first=(w == 0), split_update=True)
+        torch.cuda.synchronize()
+        states, boot = view.states_f32(k0, T)
+        r, d = view.window_rd(rewards, k0, T)
+        dprev = np.concatenate([prev_done[None], d[:-1]], 0)
+        acts = net.buffer("actions", torch.int32, (T + 1, N))[:T].cpu().numpy()
+        g, aux = O.lstm_window(params, states, acts, r, dprev, d, boot, st)
+        v = net.buffer("v", torch.float32, (T + 1, N)).cpu().numpy()
+        assert close_normscaled(v[:T], aux["v"], RTOL)[0]
+        assert close_normscaled(v[T], aux["vboot"], RTOL)[0]
+        hb = net.buffer("hbuf", torch.float32, (T + 2, N, 256)).cpu().numpy()
+        assert close_normscaled(hb[T], aux["h_last"], RTOL)[0]
+        _grads_match(net, g)
+        agent.finish_window()
+        st = O.LSTMState(h=aux["h_last"], c=aux["c_last"], has=np.ones(N, bool))
+        prev_done = d[-1]
+
+
+def test_rmsprop_kernel_bitexact_vs_reference(gpu):
+    from asyncrl_amd import RMSpropAsync
+    r = golden("rmsprop_golden.npz")
+    for k in range(r["p"].shape[0]):
+        opt = RMSpropAsync(lr=float(r["lr"][k]), alpha=0.99, eps=0.1)
+        p, ms, g = dev(r["p"][k], gpu), dev(r["ms"][k], gpu), dev(r["g"][k], gpu)
+        opt.update_arrays(p, ms, g)
+        assert (p.cpu().numpy() == r["p_out"][k]).all()
+        assert (ms.cpu().numpy() == r["ms_out"][k]).all()
+
+
+def test_rmsprop_clip_matches_oracle(gpu):
+    from asyncrl_amd import GradientClipping, RMSpropAsync
+    rng = np.random.default_rng(41)
+    n = 677429
+    p = rng.standard_normal(n).astype(np.float32)
+    ms = np.abs(rng.standard_normal(n)).astype(np.float32) * 0.01
+    g = rng.standard_normal(n).astype(np.float32)
+    opt = RMSpropAsync(lr=7e-4, alpha=0.99, eps=0.1)
+    opt.add_hook(GradientClipping(40))
+    P, M, G = dev(p, gpu), dev(ms, gpu), dev(g, gpu)
+    opt.update_arrays(P, M, G)
+    (gc,), norm = O.clip_grads([g], 40.0)
+    p1, m1 = O.rmsprop_update(p, ms, gc, 7e-4)
+    assert close_normscaled(P.cpu().numpy() - p, p1 - p, 1e-5)[0]
+    assert close_normscaled(M.cpu().numpy(), m1, 1e-5)[0]
+
+
+def test_graph_replay_equals_eager(gpu):
+    """A captured window replays with advancing device step counters and
+    gives bit-identical parameters to the eager path."""
+    from asyncrl_amd import A3C, A3CFF, GradientClipping, RMSpropAsync
+    rng = np.random.default_rng(51)
+    N, T, P = 8, 5, 7
+    pairs, rewards, dones = make_pools(rng, P, N, "uniform")
+    dp, dr, dd = dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu)
+
+    def mk():
+        m = A3CFF(4, n_envs=N, t_max=T, seed=3, init_seed=4)
+        o = RMSpropAsync(lr=7e-4, eps=0.1, alpha=0.99).setup(m)
+        o.add_hook(GradientClipping(40))
+        o.anneal_total_steps, o.n_total_envs = 10 ** 6, N
+        return A3C(m, o, T, 0.99)
+
+    a, b = mk(), mk()
+    for w in range(4):
+        a.run_window(dp, dr, dd, P, first=(w == 0))
+    b.run_window(dp, dr, dd, P, first=True)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        b.run_window(dp, dr, dd, P, first=False)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(a.net.params, b.net.params)
+    assert torch.equal(a.net.ms, b.net.ms)
+
+
+def test_many_windows_stay_finite(gpu):
+    from asyncrl_amd import A3C, A3CFF, GradientClipping, RMSpropAsync
+    rng = np.random.default_rng(61)
+    N, T, P = 16, 5, 9
+    pairs, rewards, dones = make_pools(rng, P, N, "palette")
+    m = A3CFF(4, n_envs=N, t_max=T, seed=1)
+    o = RMSpropAsync(lr=7e-4, eps=0.1, alpha=0.99).setup(m)
+    o.add_hook(GradientClipping(40))
+    agent = A3C(m, o, T, 0.99)
+    dp, dr, dd = dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu)
+    for w in range(30):
+        agent.run_window(dp, dr, dd, P, first=(w == 0))
+    torch.cuda.synchronize()
+    assert torch.isfinite(m.net.params).all()
+    acts = m.net.buffer("actions", torch.int32, (T + 1, N))[:T]
+    assert int(acts.min()) >= 0 and int(acts.max()) < 4
