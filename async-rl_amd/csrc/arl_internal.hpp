@@ -88,6 +88,12 @@ hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_tot
 hipError_t net_advance(Net& net, hipStream_t s);
 hipError_t net_forward_f32(Net& net, const float* x, int n, float* logits, float* v, hipStream_t s);
 
+hipError_t launch_conv1_fwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int t0,
+                            int nsamples, const float* W, const float* b, float* out, hipStream_t s);
+hipError_t launch_conv1_wgrad(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R,
+                              int S, const float* dY, float* slab, float* gW, float* gb, hipStream_t s);
+int64_t conv1_wgrad_slab_floats(int S);
+
 hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, double alpha, double eps,
                           const double* norm_partials, int norm_blocks, float clip, const int64_t* ctl,
                           int64_t total_steps, int64_t n_total, int t_max, hipStream_t s);

@@ -24,15 +24,18 @@ namespace arl {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int BM, int BN, int BK, int WM, int WN, class AOp, class BOp, class EOp>
+// AKF / BKF: gather the A / B chunk with k fastest across threads (for
+// operands that are contiguous along k, e.g. row-major activations, W[n][k]).
+template <int BM, int BN, int BK, int WM, int WN, class AOp, class BOp, class EOp, bool AKF = false,
+          bool BKF = false>
 __global__ void __launch_bounds__(256)
 gemm_kernel(AOp A, BOp B, EOp E, int M, int N, int K, int k_per_split) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TM = BM / (16 * WM);   // MFMA tiles per wave along m
   constexpr int TN = BN / (16 * WN);   // along n
   static_assert(TM >= 1 && TN >= 1, "tile too small for wave layout");
-  constexpr int LDA = BM + 4;
-  constexpr int LDB = BN + 4;
+  constexpr int LDA = AKF ? BM + 1 : BM + 4;
+  constexpr int LDB = BKF ? BN + 1 : BN + 4;
   constexpr int A_PER = (BM * BK) / 256;   // A elements gathered per thread per chunk
   constexpr int B_PER = (BK * BN) / 256;
   static_assert(A_PER >= 1 && B_PER >= 1, "chunk too small");
@@ -60,20 +63,26 @@ gemm_kernel(AOp A, BOp B, EOp E, int M, int N, int K, int k_per_split) {
 
   float ra[A_PER], rb[B_PER];
 
-  // A chunk: element e = tid + 256*i -> (mm = e % BM, kk = e / BM): m fastest
-  // B chunk: element e -> (nn = e % BN, kk = e / BN): n fastest
+  // A chunk: element e = tid + 256*i -> (mm, kk), m fastest (or k fastest if AKF)
+  // B chunk: element e -> (nn, kk), n fastest (or k fastest if BKF)
+  auto a_mk = [](int e, int& mm, int& kk) {
+    if (AKF) { kk = e % BK; mm = e / BK; } else { mm = e % BM; kk = e / BM; }
+  };
+  auto b_nk = [](int e, int& nn, int& kk) {
+    if (BKF) { kk = e % BK; nn = e / BK; } else { nn = e % BN; kk = e / BN; }
+  };
   auto gather = [&](int kc) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
-      const int e = tid + 256 * i;
-      const int mm = e % BM, kk = e / BM;
+      int mm, kk;
+      a_mk(tid + 256 * i, mm, kk);
       const int m = m0 + mm, k = kc + kk;
       ra[i] = (m < M && k < kend) ? A.load(m, k) : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
-      const int e = tid + 256 * i;
-      const int nn = e % BN, kk = e / BN;
+      int nn, kk;
+      b_nk(tid + 256 * i, nn, kk);
       const int n = n0 + nn, k = kc + kk;
       rb[i] = (n < N && k < kend) ? B.load(k, n) : 0.f;
     }
@@ -81,13 +90,15 @@ gemm_kernel(AOp A, BOp B, EOp E, int M, int N, int K, int k_per_split) {
   auto commit = [&]() {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
-      const int e = tid + 256 * i;
-      As[(e / BM) * LDA + (e % BM)] = ra[i];
+      int mm, kk;
+      a_mk(tid + 256 * i, mm, kk);
+      As[kk * LDA + mm] = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
-      const int e = tid + 256 * i;
-      Bs[(e / BN) * LDB + (e % BN)] = rb[i];
+      int nn, kk;
+      b_nk(tid + 256 * i, nn, kk);
+      Bs[kk * LDB + nn] = rb[i];
     }
   };
 
@@ -131,7 +142,8 @@ gemm_kernel(AOp A, BOp B, EOp E, int M, int N, int K, int k_per_split) {
     }
 }
 
-template <int BM, int BN, int BK, int WM, int WN, class AOp, class BOp, class EOp>
+template <int BM, int BN, int BK, int WM, int WN, bool AKF = false, bool BKF = false, class AOp, class BOp,
+          class EOp>
 inline hipError_t launch_gemm(const AOp& A, const BOp& B, const EOp& E, int M, int N, int K,
                               int splits, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0) return hipSuccess;
@@ -140,7 +152,7 @@ inline hipError_t launch_gemm(const AOp& A, const BOp& B, const EOp& E, int M, i
   kps = ((kps + BK - 1) / BK) * BK;
   splits = (K + kps - 1) / kps;
   dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN, splits);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AOp, BOp, EOp>), grid, dim3(256), 0, s,
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AOp, BOp, EOp, AKF, BKF>), grid, dim3(256), 0, s,
                      A, B, E, M, N, K, kps);
   return hipGetLastError();
 }

@@ -29,32 +29,7 @@ namespace arl {
 
 // ---------------------------------------------------------------- accessors
 
-// conv1 operand from the frame ring.  Sample s (relative to activation step
-// t0) = (t = t0 + s / n, env e = s % n); state = ring slots k-3..k of obs step
-// k = ctl[STEP] + t, planes before the env's last reset are zero.
-struct RingIm2col {
-  const uint8_t* __restrict__ frames;
-  const uint8_t* __restrict__ nvalid;
-  const int64_t* __restrict__ ctl;
-  int n, R, t0;
-  // element (s*400 + p, k): p = oy*20 + ox, k = ic*64 + ky*8 + kx
-  __device__ float at(int s, int p, int k) const {
-    const int t = t0 + s / n, e = s - (s / n) * n;
-    const int64_t ks = ctl[CTL_STEP] + t;
-    const int ic = k >> 6, ky = (k >> 3) & 7, kx = k & 7;
-    const int nv = nvalid[(ks % R) * n + e];
-    if (ic < 4 - nv) return 0.f;
-    const int slot = (int)((ks + R - 3 + ic) % R);
-    const int oy = p / 20, ox = p - oy * 20;
-    const uint8_t v = frames[((int64_t)slot * n + e) * PLANE + (4 * oy + ky) * 84 + 4 * ox + kx];
-    return __fdiv_rn((float)v, 255.f);   // dqn_phi.py:16
-  }
-};
-
-struct Conv1FwdA {      // A(m, k), m = s*400 + p
-  RingIm2col x;
-  __device__ float load(int m, int k) const { const int s = m / C1_P; return x.at(s, m - s * C1_P, k); }
-};
+// (conv1 from the uint8 frame ring has dedicated kernels: conv1.hip)
 struct Conv1F32A {      // same from an f32 (n,4,84,84) state tensor (dqn_phi output)
   const float* __restrict__ x;
   __device__ float load(int m, int k) const {
@@ -109,39 +84,25 @@ struct Conv2GB {        // B(q, kk) = im2col(a1)[q][kk] | 1
   Conv2A a;
   __device__ float load(int q, int kk) const { return kk < 256 ? a.load(q, kk) : 1.f; }
 };
-struct ConvT2A {        // A(m, k) for da1 = conv_transpose(da2, W2); m = s*400 + y*20 + x
+// Stride-2 transposed conv split by output parity class (py, px): rows
+// y = 2i + py, x = 2j + px (i, j in 0..9) only meet taps ky = py + 2 dy,
+// kx = px + 2 dx, so K = 32 oc x 2 x 2 = 128 instead of 512 mostly-zero taps.
+struct ConvT2PA {       // A(m, k): m = s*100 + i*10 + j, k = oc*4 + dy*2 + dx
   const float* __restrict__ da2;
   __device__ float load(int m, int k) const {
-    const int s = m / C1_P, p = m - s * C1_P;
-    const int y = p / 20, x = p - y * 20;
-    const int oc = k >> 4, ky = (k >> 2) & 3, kx = k & 3;
-    const int yy = y - ky, xx = x - kx;
-    if (yy < 0 || xx < 0 || (yy & 1) || (xx & 1)) return 0.f;
-    const int oy = yy >> 1, ox = xx >> 1;
-    if (oy >= 9 || ox >= 9) return 0.f;
+    const int s = m / 100, r = m - s * 100;
+    const int i = r / 10, j = r - i * 10;
+    const int oc = k >> 2, dy = (k >> 1) & 1, dx = k & 1;
+    const int oy = i - dy, ox = j - dx;
+    if (oy < 0 || ox < 0 || oy >= 9 || ox >= 9) return 0.f;
     return da2[(int64_t)s * A2 + oc * C2_P + oy * 9 + ox];
   }
 };
-struct ConvT2B {        // B(k, ic) = W2[oc][ic][ky][kx], k = oc*16 + ky*4 + kx
-  const float* __restrict__ w2;
+struct ConvT2PB {       // B(k, ic) = W2[oc][ic][py + 2 dy][px + 2 dx]
+  const float* __restrict__ w2; int py, px;
   __device__ float load(int k, int ic) const {
-    const int oc = k >> 4, t = k & 15;
-    return w2[(oc * 16 + ic) * 16 + t];
-  }
-};
-struct Conv1GA {        // A(oc, q) = da1[s][oc][p], q = s*400 + p
-  const float* __restrict__ da1;
-  __device__ float load(int oc, int q) const {
-    const int s = q / C1_P;
-    return da1[(int64_t)s * A1 + oc * C1_P + (q - s * C1_P)];
-  }
-};
-struct Conv1GB {        // B(q, kk) = im2col(x)[q][kk] | 1
-  RingIm2col x;
-  __device__ float load(int q, int kk) const {
-    if (kk >= 256) return 1.f;
-    const int s = q / C1_P;
-    return x.at(s, q - s * C1_P, kk);
+    const int oc = k >> 2, dy = (k >> 1) & 1, dx = k & 1;
+    return w2[(oc * 16 + ic) * 16 + (py + 2 * dy) * 4 + (px + 2 * dx)];
   }
 };
 struct LstmWB {         // B(s, j) = [x (256) | 1 | h_prev (256, 0 after reset)]
@@ -178,12 +139,13 @@ struct EpiMask {        // out[m][n] = mask[m][n] > 0 ? v : 0  (ReLU backward)
     out[i] = mask[i] > 0.f ? v : 0.f;
   }
 };
-struct EpiConvMask {    // da1[s][ic][p] masked by a1 > 0; m = s*400 + p, n = ic
-  float* __restrict__ out; const float* __restrict__ mask;
+struct EpiConvTMask {   // da1[s][ic][y][x] masked by a1 > 0; m = s*100 + i*10 + j of class (py, px)
+  float* __restrict__ out; const float* __restrict__ mask; int py, px;
   __device__ void store(int m, int n, float v, int) const {
-    const int s = m / C1_P, p = m - s * C1_P;
-    const int64_t i = ((int64_t)s * C1_OC + n) * C1_P + p;
-    out[i] = mask[i] > 0.f ? v : 0.f;
+    const int s = m / 100, r = m - s * 100;
+    const int i = r / 10, j = r - i * 10;
+    const int64_t idx = ((int64_t)s * C1_OC + n) * C1_P + (2 * i + py) * 20 + 2 * j + px;
+    out[idx] = mask[idx] > 0.f ? v : 0.f;
   }
 };
 struct EpiResetMask {   // out[m][n] = reset[m] ? 0 : v
@@ -221,20 +183,31 @@ struct MapHeads {
   }
 };
 
+// block = 64 consecutive outputs x 4 slice groups; f64 sums combined in a
+// fixed order (deterministic for any slice count)
 template <class Map>
-__global__ void reduce_grad_kernel(const float* __restrict__ slab, int splits, int M, int N, Map map) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(256)
+reduce_grad_kernel(const float* __restrict__ slab, int splits, int M, int N, Map map) {
+  __shared__ double part[4][64];
   const int64_t MN = (int64_t)M * N;
-  if (i >= MN) return;
-  double s = 0.0;
-  for (int z = 0; z < splits; ++z) s += (double)slab[(int64_t)z * MN + i];
-  map.put((int)(i / N), (int)(i % N), (float)s);
+  const int64_t i = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int zg = threadIdx.x >> 6;
+  double t = 0.0;
+  if (i < MN)
+    for (int z = zg; z < splits; z += 4) t += (double)slab[(int64_t)z * MN + i];
+  part[zg][threadIdx.x & 63] = t;
+  __syncthreads();
+  if (zg == 0 && i < MN) {
+    const int l = threadIdx.x;
+    const double v = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
+    map.put((int)(i / N), (int)(i % N), (float)v);
+  }
 }
 
 template <class Map>
 static hipError_t launch_reduce_grad(const float* slab, int splits, int M, int N, const Map& map, hipStream_t s) {
   const int64_t MN = (int64_t)M * N;
-  hipLaunchKernelGGL((reduce_grad_kernel<Map>), dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, s, slab, splits,
+  hipLaunchKernelGGL((reduce_grad_kernel<Map>), dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, s, slab, splits,
                      M, N, map);
   return hipGetLastError();
 }
@@ -324,7 +297,7 @@ static int plan_splits(int tiles, int64_t K, int BK, int target = 1024) {
 }
 
 struct Plans {   // effective split counts (launch_gemm may shrink a request)
-  int fc_fwd, heads_w, fc_w, c2_w, c1_w, lstm_w;
+  int fc_fwd, heads_w, fc_w, c2_w, lstm_w;
 };
 
 static Plans make_plans(const Net& net) {
@@ -335,8 +308,6 @@ static Plans make_plans(const Net& net) {
   p.fc_w = effective_splits<32>(S, plan_splits(ceil_div(HID, 64) * ceil_div(A2 + 1, 64), S, 32));
   p.c2_w = effective_splits<32>((int64_t)S * C2_P, plan_splits(ceil_div(C2_OC, 32) * ceil_div(257, 64),
                                                                (int64_t)S * C2_P, 32));
-  p.c1_w = effective_splits<32>((int64_t)S * C1_P, plan_splits(ceil_div(C1_OC, 16) * ceil_div(257, 64),
-                                                               (int64_t)S * C1_P, 32));
   p.lstm_w = effective_splits<32>(S, plan_splits(ceil_div(GATES, 64) * ceil_div(2 * HID + 1, 64), S, 32));
   return p;
 }
@@ -392,7 +363,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   slab = std::max(slab, (int64_t)pl.heads_w * (A + 1) * (HID + 1));
   slab = std::max(slab, (int64_t)pl.fc_w * HID * (A2 + 1));
   slab = std::max(slab, (int64_t)pl.c2_w * C2_OC * 257);
-  slab = std::max(slab, (int64_t)pl.c1_w * C1_OC * 257);
+  slab = std::max(slab, conv1_wgrad_slab_floats((int)S));
   if (arch == ARCH_LSTM) slab = std::max(slab, (int64_t)pl.lstm_w * GATES * (2 * HID + 1));
   net.slab_floats = slab;
   net.bufs.clear();
@@ -440,32 +411,19 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
 }
 
 // ---------------------------------------------------------------- forward
-static RingIm2col ring_of(const Net& net, int t0) {
-  RingIm2col r;
-  r.frames = net.at<uint8_t>(net.w_frames);
-  r.nvalid = net.at<uint8_t>(net.w_nvalid);
-  r.ctl = net.at<int64_t>(net.w_ctl);
-  r.n = net.N; r.R = net.R; r.t0 = t0;
-  return r;
-}
-
 #define ARL_TRY(x) do { hipError_t _e = (x); if (_e != hipSuccess) return _e; } while (0)
 
-// head (conv1 -> conv2 -> fc) for n rows whose conv1 operand is `c1a`,
-// writing activations at a1/a2/hfc (row-major per sample)
-template <class C1A>
-static hipError_t head_forward(const Net& net, const C1A& c1a, int n, float* a1, float* a2, float* hfc,
-                               hipStream_t s) {
+// head after conv1 (conv2 -> fc) for n rows, activations at a1/a2/hfc
+static hipError_t head_forward_tail(const Net& net, int n, float* a1, float* a2, float* hfc, hipStream_t s) {
   const float* P = net.p;
-  ARL_TRY((launch_gemm<64, 16, 32, 4, 1>(c1a, WeightT{P + net.o_c1W, 256}, EpiConv{a1, P + net.o_c1b, C1_OC, C1_P},
-                                         n * C1_P, C1_OC, 256, 1, s)));
-  ARL_TRY((launch_gemm<32, 32, 32, 2, 2>(Conv2A{a1}, WeightT{P + net.o_c2W, 256}, EpiConv{a2, P + net.o_c2b, C2_OC, C2_P},
-                                         n * C2_P, C2_OC, 256, 1, s)));
+  ARL_TRY((launch_gemm<32, 32, 32, 2, 2, false, true>(Conv2A{a1}, WeightT{P + net.o_c2W, 256},
+                                                      EpiConv{a2, P + net.o_c2b, C2_OC, C2_P}, n * C2_P, C2_OC, 256,
+                                                      1, s)));
   const int req = plan_splits(ceil_div(n, 32) * ceil_div(HID, 64), A2, 32, 256);
   const int sp = effective_splits<32>(A2, req);
   float* slab = net.at<float>(net.w_slab);
-  ARL_TRY((launch_gemm<32, 64, 32, 2, 2>(RowMajor{a2, A2}, WeightT{P + net.o_fcW, A2}, EpiSlab{slab, n, HID},
-                                         n, HID, A2, req, s)));
+  ARL_TRY((launch_gemm<32, 64, 32, 2, 2, true, true>(RowMajor{a2, A2}, WeightT{P + net.o_fcW, A2},
+                                                     EpiSlab{slab, n, HID}, n, HID, A2, req, s)));
   const int64_t MN = (int64_t)n * HID;
   hipLaunchKernelGGL(reduce_bias_relu_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, s, slab, sp, MN, HID,
                      P + net.o_fcb, hfc);
@@ -477,8 +435,10 @@ hipError_t net_act(Net& net, int t, int sample, hipStream_t s) {
   float* a1 = net.at<float>(net.w_a1) + (int64_t)t * n * A1;
   float* a2 = net.at<float>(net.w_a2) + (int64_t)t * n * A2;
   float* hfc = net.at<float>(net.w_hfc) + (int64_t)t * n * HID;
-  ARL_TRY(head_forward(net, Conv1FwdA{ring_of(net, t)}, n, a1, a2, hfc, s));
   const float* P = net.p;
+  ARL_TRY(launch_conv1_fwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl),
+                           n, net.R, t, n, P + net.o_c1W, P + net.o_c1b, a1, s));
+  ARL_TRY(head_forward_tail(net, n, a1, a2, hfc, s));
   const float* hpol = hfc;
   if (net.arch == ARCH_LSTM) {
     float* gates = net.at<float>(net.w_gates) + (int64_t)t * n * GATES;
@@ -487,7 +447,7 @@ hipError_t net_act(Net& net, int t, int sample, hipStream_t s) {
     float* hout = net.at<float>(net.w_hbuf) + (int64_t)(t + 1) * n * HID;
     float* cout = net.at<float>(net.w_cbuf) + (int64_t)(t + 1) * n * HID;
     const uint8_t* rs = net.at<uint8_t>(net.w_reset) + (int64_t)t * n;
-    ARL_TRY((launch_gemm<32, 64, 32, 2, 2>(LstmGateA{hfc, hprev, rs}, LstmGateB{P + net.o_luW, P + net.o_llW},
+    ARL_TRY((launch_gemm<32, 64, 32, 2, 2, true, true>(LstmGateA{hfc, hprev, rs}, LstmGateB{P + net.o_luW, P + net.o_llW},
                                            EpiBias{gates, P + net.o_lub, GATES}, n, GATES, 2 * HID, 1, s)));
     const int64_t cnt = (int64_t)n * HID;
     hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, gates, cprev, rs,
@@ -511,8 +471,11 @@ hipError_t net_forward_f32(Net& net, const float* x, int n, float*, float*, hipS
   float* a1 = net.at<float>(net.w_a1) + (int64_t)T * N * A1;
   float* a2 = net.at<float>(net.w_a2) + (int64_t)T * N * A2;
   float* hfc = net.at<float>(net.w_hfc) + (int64_t)T * N * HID;
-  ARL_TRY(head_forward(net, Conv1F32A{x}, n, a1, a2, hfc, s));
   const float* P = net.p;
+  ARL_TRY((launch_gemm<64, 16, 32, 4, 1, false, true>(Conv1F32A{x}, WeightT{P + net.o_c1W, 256},
+                                                      EpiConv{a1, P + net.o_c1b, C1_OC, C1_P}, n * C1_P, C1_OC, 256,
+                                                      1, s)));
+  ARL_TRY(head_forward_tail(net, n, a1, a2, hfc, s));
   const int64_t o = (int64_t)T * N;
   return launch_policy(hfc, n, P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
                        net.at<int64_t>(net.w_ctl), T, net.env_offset, 0, net.at<float>(net.w_logits) + o * A,
@@ -568,14 +531,14 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
                          dG + o * GATES, t == T - 1 ? 1 : 0, cnt);
       ARL_TRY(hipGetLastError());
       if (t > 0)
-        ARL_TRY((launch_gemm<32, 64, 32, 2, 2>(RowMajor{dG + o * GATES, GATES}, RowMajor{P + net.o_llW, HID},
+        ARL_TRY((launch_gemm<32, 64, 32, 2, 2, true, false>(RowMajor{dG + o * GATES, GATES}, RowMajor{P + net.o_llW, HID},
                                                EpiResetMask{dhn, rs + o, HID}, n, HID, GATES, 1, s)));
     }
     ARL_TRY((launch_gemm<64, 64, 32, 2, 2>(ColMajor{dG, GATES}, LstmWB{hfc, hbuf, rs},
                                            EpiSlab{slab, GATES, 2 * HID + 1}, GATES, 2 * HID + 1, S, pl.lstm_w, s)));
     ARL_TRY(launch_reduce_grad(slab, pl.lstm_w, GATES, 2 * HID + 1,
                                MapDense{G, net.o_luW, net.o_lub, net.o_llW, HID}, s));
-    ARL_TRY((launch_gemm<64, 64, 32, 2, 2>(RowMajor{dG, GATES}, RowMajor{P + net.o_luW, HID}, EpiMask{dfc, hfc, HID},
+    ARL_TRY((launch_gemm<64, 64, 32, 2, 2, true, false>(RowMajor{dG, GATES}, RowMajor{P + net.o_luW, HID}, EpiMask{dfc, hfc, HID},
                                            S, HID, GATES, 1, s)));
   }
   // 4. FC: dW (+ bias via ones column) and da2 = (dfc W) * (a2 > 0)
@@ -586,19 +549,20 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
   ARL_TRY((launch_gemm<64, 64, 32, 2, 2>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab, HID, A2 + 1}, HID,
                                          A2 + 1, S, pl.fc_w, s)));
   ARL_TRY(launch_reduce_grad(slab, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s));
-  ARL_TRY((launch_gemm<64, 64, 32, 2, 2>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2}, EpiMask{da2, a2, A2}, S, A2,
+  ARL_TRY((launch_gemm<64, 64, 32, 2, 2, true, false>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2}, EpiMask{da2, a2, A2}, S, A2,
                                          HID, 1, s)));
   // 5. conv2: dW, db; da1 = conv_transpose(da2, W2) * (a1 > 0)
-  ARL_TRY((launch_gemm<32, 64, 32, 2, 2>(Conv2GA{da2}, Conv2GB{Conv2A{a1}}, EpiSlab{slab, C2_OC, 257}, C2_OC, 257,
+  ARL_TRY((launch_gemm<32, 64, 32, 2, 2, true, false>(Conv2GA{da2}, Conv2GB{Conv2A{a1}}, EpiSlab{slab, C2_OC, 257}, C2_OC, 257,
                                          S * C2_P, pl.c2_w, s)));
   ARL_TRY(launch_reduce_grad(slab, pl.c2_w, C2_OC, 257, MapDense{G, net.o_c2W, net.o_c2b, -1, 256}, s));
-  ARL_TRY((launch_gemm<64, 16, 32, 4, 1>(ConvT2A{da2}, ConvT2B{P + net.o_c2W}, EpiConvMask{da1, a1}, S * C1_P, C1_OC,
-                                         C2_OC * 16, 1, s)));
-  // 6. conv1: dW, db (no dx needed)
-  ARL_TRY((launch_gemm<16, 64, 32, 1, 4>(Conv1GA{da1}, Conv1GB{ring_of(net, 0)}, EpiSlab{slab, C1_OC, 257}, C1_OC,
-                                         257, S * C1_P, pl.c1_w, s)));
-  ARL_TRY(launch_reduce_grad(slab, pl.c1_w, C1_OC, 257, MapDense{G, net.o_c1W, net.o_c1b, -1, 256}, s));
-  return hipSuccess;
+  for (int cls = 0; cls < 4; ++cls) {
+    const int py = cls >> 1, px = cls & 1;
+    ARL_TRY((launch_gemm<64, 16, 32, 4, 1>(ConvT2PA{da2}, ConvT2PB{P + net.o_c2W, py, px},
+                                           EpiConvTMask{da1, a1, py, px}, S * 100, C1_OC, C2_OC * 4, 1, s)));
+  }
+  // 6. conv1: dW, db (no dx needed) straight from the frame ring
+  return launch_conv1_wgrad(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl),
+                            n, net.R, S, da1, slab, G + net.o_c1W, G + net.o_c1b, s);
 }
 
 hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,

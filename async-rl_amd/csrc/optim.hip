@@ -67,7 +67,8 @@ struct RmsConst {
 __device__ inline void rms1(float& p, float& ms, float g, const RmsConst& c) {
   ms = __fmul_rn(ms, c.alpha);                                   // ms *= alpha
   ms = __fadd_rn(ms, __fmul_rn(__fmul_rn(c.one_minus_alpha, g), g));   // ms += (1-a)*g*g
-  p = __fsub_rn(p, __fdiv_rn(__fmul_rn(c.lr, g), __fsqrt_rn(__fadd_rn(ms, c.eps))));  // p -= lr*g/sqrt(ms+eps)
+  // sqrtf (not __fsqrt_rn = native approx sqrt) is the correctly rounded one under hipcc defaults
+  p = __fsub_rn(p, __fdiv_rn(__fmul_rn(c.lr, g), sqrtf(__fadd_rn(ms, c.eps))));  // p -= lr*g/sqrt(ms+eps)
 }
 
 __global__ void __launch_bounds__(256)

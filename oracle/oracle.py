@@ -451,10 +451,15 @@ def grad_sqnorm(grads) -> float:
     return float(sum(float(np.dot(gv.ravel(), gv.ravel())) for gv in grads))
 
 
-def clip_grads(grads, threshold=40.0):
+def clip_grads(grads, threshold=40.0, exact_norm=False):
     """GradientClipping: rate = threshold / norm; if rate < 1: g *= rate
-    (f32 array *= f64 scalar -> f32 multiply by f32(rate))."""
-    norm = math.sqrt(grad_sqnorm(grads))
+    (f32 array *= f64 scalar -> f32 multiply by f32(rate)).  exact_norm:
+    accumulate the squared norm in f64 instead of Chainer's per-array f32
+    dot (whose own rounding is ~sqrt(n) ulp on 677k-element arrays)."""
+    if exact_norm:
+        norm = math.sqrt(sum(float((gv.astype(np.float64) ** 2).sum()) for gv in grads))
+    else:
+        norm = math.sqrt(grad_sqnorm(grads))
     rate = threshold / norm if norm > 0 else float("inf")
     if rate < 1:
         r32 = F32(rate)
