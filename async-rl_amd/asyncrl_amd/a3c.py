@@ -27,9 +27,9 @@ import os
 
 import numpy as np
 import torch
-import torch.distributed as dist
 
 from ._lib import ARCH_FF, ARCH_LSTM, RESIZE_SCALAR
+from .distributed import allreduce_grads, world_info
 from .net import DeviceNet, init_like_torch
 from .policy_output import SoftmaxPolicyOutput
 
@@ -101,7 +101,7 @@ class A3C:
         self.v_loss_coef = v_loss_coef
         self.resize_mode = resize_mode
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.world, self.rank = world_info(process_group)
         self.t = 0          # env-steps taken (per env)
         self.net = model.net
         self.net.reset()
@@ -113,8 +113,7 @@ class A3C:
     def _update(self, stream=None):
         net = self.net
         net.learn(self.gamma, self.beta, self.v_loss_coef, self.clip_reward, stream=stream)
-        if self.world > 1:
-            dist.all_reduce(net.grads, op=dist.ReduceOp.SUM, group=self.pg)
+        allreduce_grads(net.grads, self.pg)
         self.optimizer.update(stream=stream)
         net.advance(stream=stream)
 
@@ -168,8 +167,7 @@ class A3C:
         self.finish_window(stream=stream)
 
     def finish_window(self, stream=None):
-        if self.world > 1:
-            dist.all_reduce(self.net.grads, op=dist.ReduceOp.SUM, group=self.pg)
+        allreduce_grads(self.net.grads, self.pg)
         self.optimizer.update(stream=stream)
         self.net.advance(stream=stream)
         self.t += self.t_max

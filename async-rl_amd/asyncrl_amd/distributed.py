@@ -1,0 +1,55 @@
+"""Env-sharded data parallelism for the lockstep actor-learner.
+
+Replaces async.py:68-90 (fork P Hogwild processes sharing RawArray params)
+with one process per GPU: rank r owns envs [r*n, (r+1)*n) -- frame ring,
+LSTM state, rollout buffers and the Philox stream keyed by the global env id
+-- and the ranks exchange exactly one message per window, the SUM all-reduce
+of the flat fp32 gradient (RCCL over xGMI with backend "nccl"; gloo works for
+CPU tests).  Every rank then applies the same clip + RMSProp to replicated
+parameters, so replicas stay bitwise identical (checked by replica_checksum).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def world_info(group=None):
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
+
+
+def shard_envs(global_envs: int, world: int, rank: int):
+    """(n_local, env_offset) for an even split of global_envs over ranks."""
+    if global_envs % world:
+        raise ValueError(f"{global_envs} envs do not split evenly over {world} ranks")
+    n = global_envs // world
+    return n, rank * n
+
+
+def allreduce_grads(grads: torch.Tensor, group=None) -> None:
+    """Sum the flat gradient over ranks in place (one collective per window:
+    2.71 MB FF / 4.81 MB LSTM -- latency-bound, a single ring all-reduce)."""
+    world, _ = world_info(group)
+    if world > 1:
+        dist.all_reduce(grads, op=dist.ReduceOp.SUM, group=group)
+
+
+def replica_checksum(t: torch.Tensor) -> int:
+    """Order-dependent 64-bit hash of the raw bits (equal iff bitwise equal,
+    up to hash collisions)."""
+    w = t.detach().contiguous().view(torch.int32).to(torch.int64)
+    idx = torch.arange(1, w.numel() + 1, dtype=torch.int64, device=w.device)
+    return int(((w * (idx * 2654435761 % 4294967291)) % 9223372036854775783).sum().item())
+
+
+def replicas_identical(t: torch.Tensor, group=None) -> bool:
+    """True iff every rank holds bitwise-identical `t` (all-gathers one int)."""
+    world, _ = world_info(group)
+    if world == 1:
+        return True
+    c = torch.tensor([replica_checksum(t)], dtype=torch.int64, device=t.device)
+    out = [torch.zeros_like(c) for _ in range(world)]
+    dist.all_gather(out, c, group=group)
+    return all(int(o.item()) == int(c.item()) for o in out)

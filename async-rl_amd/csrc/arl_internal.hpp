@@ -68,7 +68,7 @@ struct Net {
   int64_t ws_bytes;
   int64_t w_ctl, w_frames, w_nvalid, w_reset, w_rewards, w_dones, w_a1, w_a2, w_hfc, w_gates, w_hbuf,
       w_cbuf, w_logits, w_probs, w_logp, w_v, w_ent, w_logpa, w_act, w_dlogits, w_dv, w_dh, w_dfc,
-      w_dG, w_dhn, w_dcn, w_da2, w_da1, w_slab, w_norm, w_loss;
+      w_dG, w_dhn, w_dcn, w_da2, w_slab, w_norm, w_loss;
   int64_t slab_floats;
   int norm_blocks;
   // bound pointers
@@ -90,9 +90,10 @@ hipError_t net_forward_f32(Net& net, const float* x, int n, float* logits, float
 
 hipError_t launch_conv1_fwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int t0,
                             int nsamples, const float* W, const float* b, float* out, hipStream_t s);
-hipError_t launch_conv1_wgrad(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R,
-                              int S, const float* dY, float* slab, float* gW, float* gb, hipStream_t s);
-int64_t conv1_wgrad_slab_floats(int S);
+hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int S,
+                           const float* a1, const float* da2, const float* W2, float* slab, float* gW2, float* gb2,
+                           float* gW1, float* gb1, hipStream_t s);
+int64_t conv_bwd_slab_floats(int S);
 
 hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, double alpha, double eps,
                           const double* norm_partials, int norm_blocks, float clip, const int64_t* ctl,

@@ -73,38 +73,6 @@ struct OnesColB {       // B(s, j) = j < K ? X[s][j] : 1   (bias gradient column
   const float* __restrict__ x; int K;
   __device__ float load(int s, int j) const { return j < K ? x[(int64_t)s * K + j] : 1.f; }
 };
-struct Conv2GA {        // A(oc, q) = da2[s][oc][p], q = s*81 + p
-  const float* __restrict__ da2;
-  __device__ float load(int oc, int q) const {
-    const int s = q / C2_P;
-    return da2[(int64_t)s * A2 + oc * C2_P + (q - s * C2_P)];
-  }
-};
-struct Conv2GB {        // B(q, kk) = im2col(a1)[q][kk] | 1
-  Conv2A a;
-  __device__ float load(int q, int kk) const { return kk < 256 ? a.load(q, kk) : 1.f; }
-};
-// Stride-2 transposed conv split by output parity class (py, px): rows
-// y = 2i + py, x = 2j + px (i, j in 0..9) only meet taps ky = py + 2 dy,
-// kx = px + 2 dx, so K = 32 oc x 2 x 2 = 128 instead of 512 mostly-zero taps.
-struct ConvT2PA {       // A(m, k): m = s*100 + i*10 + j, k = oc*4 + dy*2 + dx
-  const float* __restrict__ da2;
-  __device__ float load(int m, int k) const {
-    const int s = m / 100, r = m - s * 100;
-    const int i = r / 10, j = r - i * 10;
-    const int oc = k >> 2, dy = (k >> 1) & 1, dx = k & 1;
-    const int oy = i - dy, ox = j - dx;
-    if (oy < 0 || ox < 0 || oy >= 9 || ox >= 9) return 0.f;
-    return da2[(int64_t)s * A2 + oc * C2_P + oy * 9 + ox];
-  }
-};
-struct ConvT2PB {       // B(k, ic) = W2[oc][ic][py + 2 dy][px + 2 dx]
-  const float* __restrict__ w2; int py, px;
-  __device__ float load(int k, int ic) const {
-    const int oc = k >> 2, dy = (k >> 1) & 1, dx = k & 1;
-    return w2[(oc * 16 + ic) * 16 + (py + 2 * dy) * 4 + (px + 2 * dx)];
-  }
-};
 struct LstmWB {         // B(s, j) = [x (256) | 1 | h_prev (256, 0 after reset)]
   const float* __restrict__ x; const float* __restrict__ h; const uint8_t* __restrict__ reset;
   __device__ float load(int s, int j) const {
@@ -137,15 +105,6 @@ struct EpiMask {        // out[m][n] = mask[m][n] > 0 ? v : 0  (ReLU backward)
   __device__ void store(int m, int n, float v, int) const {
     const int64_t i = (int64_t)m * ld + n;
     out[i] = mask[i] > 0.f ? v : 0.f;
-  }
-};
-struct EpiConvTMask {   // da1[s][ic][y][x] masked by a1 > 0; m = s*100 + i*10 + j of class (py, px)
-  float* __restrict__ out; const float* __restrict__ mask; int py, px;
-  __device__ void store(int m, int n, float v, int) const {
-    const int s = m / 100, r = m - s * 100;
-    const int i = r / 10, j = r - i * 10;
-    const int64_t idx = ((int64_t)s * C1_OC + n) * C1_P + (2 * i + py) * 20 + 2 * j + px;
-    out[idx] = mask[idx] > 0.f ? v : 0.f;
   }
 };
 struct EpiResetMask {   // out[m][n] = reset[m] ? 0 : v
@@ -297,7 +256,7 @@ static int plan_splits(int tiles, int64_t K, int BK, int target = 1024) {
 }
 
 struct Plans {   // effective split counts (launch_gemm may shrink a request)
-  int fc_fwd, heads_w, fc_w, c2_w, lstm_w;
+  int fc_fwd, heads_w, fc_w, lstm_w;
 };
 
 static Plans make_plans(const Net& net) {
@@ -306,8 +265,6 @@ static Plans make_plans(const Net& net) {
   p.fc_fwd = effective_splits<32>(A2, plan_splits(ceil_div(n, 32) * ceil_div(HID, 64), A2, 32, 256));
   p.heads_w = effective_splits<32>(S, plan_splits(ceil_div(net.A + 1, 16) * ceil_div(HID + 1, 64), S, 32));
   p.fc_w = effective_splits<32>(S, plan_splits(ceil_div(HID, 64) * ceil_div(A2 + 1, 64), S, 32));
-  p.c2_w = effective_splits<32>((int64_t)S * C2_P, plan_splits(ceil_div(C2_OC, 32) * ceil_div(257, 64),
-                                                               (int64_t)S * C2_P, 32));
   p.lstm_w = effective_splits<32>(S, plan_splits(ceil_div(GATES, 64) * ceil_div(2 * HID + 1, 64), S, 32));
   return p;
 }
@@ -362,8 +319,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   slab = std::max(slab, (int64_t)pl.fc_fwd * n * HID);
   slab = std::max(slab, (int64_t)pl.heads_w * (A + 1) * (HID + 1));
   slab = std::max(slab, (int64_t)pl.fc_w * HID * (A2 + 1));
-  slab = std::max(slab, (int64_t)pl.c2_w * C2_OC * 257);
-  slab = std::max(slab, conv1_wgrad_slab_floats((int)S));
+  slab = std::max(slab, conv_bwd_slab_floats((int)S));
   if (arch == ARCH_LSTM) slab = std::max(slab, (int64_t)pl.lstm_w * GATES * (2 * HID + 1));
   net.slab_floats = slab;
   net.bufs.clear();
@@ -402,7 +358,6 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   net.w_dhn = buf("dhn", L ? n * HID * 4 : 0);
   net.w_dcn = buf("dcn", L ? n * HID * 4 : 0);
   net.w_da2 = buf("da2", S * A2 * 4);
-  net.w_da1 = buf("da1", S * A1 * 4);
   net.w_slab = buf("slab", slab * 4);
   net.w_norm = buf("norm_partials", (int64_t)net.norm_blocks * 8);
   net.w_loss = buf("loss", n * 2 * 4);
@@ -545,24 +500,17 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
   const float* a2 = net.at<float>(net.w_a2);
   const float* a1 = net.at<float>(net.w_a1);
   float* da2 = net.at<float>(net.w_da2);
-  float* da1 = net.at<float>(net.w_da1);
   ARL_TRY((launch_gemm<64, 64, 32, 2, 2>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab, HID, A2 + 1}, HID,
                                          A2 + 1, S, pl.fc_w, s)));
   ARL_TRY(launch_reduce_grad(slab, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s));
   ARL_TRY((launch_gemm<64, 64, 32, 2, 2, true, false>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2}, EpiMask{da2, a2, A2}, S, A2,
                                          HID, 1, s)));
-  // 5. conv2: dW, db; da1 = conv_transpose(da2, W2) * (a1 > 0)
-  ARL_TRY((launch_gemm<32, 64, 32, 2, 2, true, false>(Conv2GA{da2}, Conv2GB{Conv2A{a1}}, EpiSlab{slab, C2_OC, 257}, C2_OC, 257,
-                                         S * C2_P, pl.c2_w, s)));
-  ARL_TRY(launch_reduce_grad(slab, pl.c2_w, C2_OC, 257, MapDense{G, net.o_c2W, net.o_c2b, -1, 256}, s));
-  for (int cls = 0; cls < 4; ++cls) {
-    const int py = cls >> 1, px = cls & 1;
-    ARL_TRY((launch_gemm<64, 16, 32, 4, 1>(ConvT2PA{da2}, ConvT2PB{P + net.o_c2W, py, px},
-                                           EpiConvTMask{da1, a1, py, px}, S * 100, C1_OC, C2_OC * 4, 1, s)));
-  }
-  // 6. conv1: dW, db (no dx needed) straight from the frame ring
-  return launch_conv1_wgrad(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl),
-                            n, net.R, S, da1, slab, G + net.o_c1W, G + net.o_c1b, s);
+  // 5. fused conv backward per sample (conv_bwd.hip): conv2 dW/db,
+  //    da1 = conv_transpose(da2, W2) * (a1 > 0) kept in LDS, conv1 dW/db
+  //    straight from the frame ring
+  return launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl), n,
+                         net.R, S, a1, da2, P + net.o_c2W, slab, G + net.o_c2W, G + net.o_c2b, G + net.o_c1W,
+                         G + net.o_c1b, s);
 }
 
 hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
