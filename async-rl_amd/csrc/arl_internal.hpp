@@ -88,8 +88,9 @@ hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_tot
 hipError_t net_advance(Net& net, hipStream_t s);
 hipError_t net_forward_f32(Net& net, const float* x, int n, float* logits, float* v, hipStream_t s);
 
-hipError_t launch_conv1_fwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int t0,
-                            int nsamples, const float* W, const float* b, float* out, hipStream_t s);
+hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int t,
+                           const float* W1, const float* b1, const float* W2, const float* b2, float* a1, float* a2,
+                           hipStream_t s);
 hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int S,
                            const float* a1, const float* da2, const float* W2, float* slab, float* gW2, float* gb2,
                            float* gW1, float* gb1, hipStream_t s);

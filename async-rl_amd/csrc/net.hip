@@ -369,11 +369,8 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
 #define ARL_TRY(x) do { hipError_t _e = (x); if (_e != hipSuccess) return _e; } while (0)
 
 // head after conv1 (conv2 -> fc) for n rows, activations at a1/a2/hfc
-static hipError_t head_forward_tail(const Net& net, int n, float* a1, float* a2, float* hfc, hipStream_t s) {
+static hipError_t fc_forward(const Net& net, int n, const float* a2, float* hfc, hipStream_t s) {
   const float* P = net.p;
-  ARL_TRY((launch_gemm<32, 32, 32, 2, 2, false, true>(Conv2A{a1}, WeightT{P + net.o_c2W, 256},
-                                                      EpiConv{a2, P + net.o_c2b, C2_OC, C2_P}, n * C2_P, C2_OC, 256,
-                                                      1, s)));
   const int req = plan_splits(ceil_div(n, 32) * ceil_div(HID, 64), A2, 32, 256);
   const int sp = effective_splits<32>(A2, req);
   float* slab = net.at<float>(net.w_slab);
@@ -391,9 +388,9 @@ hipError_t net_act(Net& net, int t, int sample, hipStream_t s) {
   float* a2 = net.at<float>(net.w_a2) + (int64_t)t * n * A2;
   float* hfc = net.at<float>(net.w_hfc) + (int64_t)t * n * HID;
   const float* P = net.p;
-  ARL_TRY(launch_conv1_fwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl),
-                           n, net.R, t, n, P + net.o_c1W, P + net.o_c1b, a1, s));
-  ARL_TRY(head_forward_tail(net, n, a1, a2, hfc, s));
+  ARL_TRY(launch_conv_fwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl),
+                          n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W, P + net.o_c2b, a1, a2, s));
+  ARL_TRY(fc_forward(net, n, a2, hfc, s));
   const float* hpol = hfc;
   if (net.arch == ARCH_LSTM) {
     float* gates = net.at<float>(net.w_gates) + (int64_t)t * n * GATES;
@@ -430,7 +427,10 @@ hipError_t net_forward_f32(Net& net, const float* x, int n, float*, float*, hipS
   ARL_TRY((launch_gemm<64, 16, 32, 4, 1, false, true>(Conv1F32A{x}, WeightT{P + net.o_c1W, 256},
                                                       EpiConv{a1, P + net.o_c1b, C1_OC, C1_P}, n * C1_P, C1_OC, 256,
                                                       1, s)));
-  ARL_TRY(head_forward_tail(net, n, a1, a2, hfc, s));
+  ARL_TRY((launch_gemm<32, 32, 32, 2, 2, false, true>(Conv2A{a1}, WeightT{P + net.o_c2W, 256},
+                                                      EpiConv{a2, P + net.o_c2b, C2_OC, C2_P}, n * C2_P, C2_OC, 256,
+                                                      1, s)));
+  ARL_TRY(fc_forward(net, n, a2, hfc, s));
   const int64_t o = (int64_t)T * N;
   return launch_policy(hfc, n, P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
                        net.at<int64_t>(net.w_ctl), T, net.env_offset, 0, net.at<float>(net.w_logits) + o * A,
