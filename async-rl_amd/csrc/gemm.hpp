@@ -24,24 +24,33 @@ namespace arl {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// AKF / BKF: gather the A / B chunk with k fastest across threads (for
-// operands that are contiguous along k, e.g. row-major activations, W[n][k]).
-template <int BM, int BN, int BK, int WM, int WN, class AOp, class BOp, class EOp, bool AKF = false,
-          bool BKF = false>
+// Gather modes for the A / B chunk (template AV, BV):
+//   GS (0): scalar, m (n) fastest across threads -- any accessor;
+//   GK (1): 16-byte vectors of 4 consecutive k via load4(m, k) / load4(k, n)
+//           (k-contiguous operands: row-major activations, W[n][k]);
+//   GM (2): 16-byte vectors of 4 consecutive m (n) via load4m(m, k) /
+//           load4n(k, n) (m / n-contiguous operands: W[k][n], X^T).
+// Vector gathers need 16-byte aligned rows (leading dimension % 4 == 0);
+// partial vectors at the K / M / N edges fall back to scalar loads.
+enum { GS = 0, GK = 1, GM = 2 };
+
+template <int BM, int BN, int BK, int WM, int WN, class AOp, class BOp, class EOp, int AV = GS, int BV = GS>
 __global__ void __launch_bounds__(256)
 gemm_kernel(AOp A, BOp B, EOp E, int M, int N, int K, int k_per_split) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TM = BM / (16 * WM);   // MFMA tiles per wave along m
   constexpr int TN = BN / (16 * WN);   // along n
   static_assert(TM >= 1 && TN >= 1, "tile too small for wave layout");
-  constexpr int LDA = AKF ? BM + 1 : BM + 4;
-  constexpr int LDB = BKF ? BN + 1 : BN + 4;
+  constexpr int LDA = AV == GK ? BM + 1 : BM + 4;
+  constexpr int LDB = BV == GK ? BN + 1 : BN + 4;
   constexpr int A_PER = (BM * BK) / 256;   // A elements gathered per thread per chunk
   constexpr int B_PER = (BK * BN) / 256;
   static_assert(A_PER >= 1 && B_PER >= 1, "chunk too small");
+  static_assert(AV == GS || A_PER % 4 == 0, "vector A gather needs whole 4-vectors per thread");
+  static_assert(BV == GS || B_PER % 4 == 0, "vector B gather needs whole 4-vectors per thread");
 
-  __shared__ float As[BK * LDA];
-  __shared__ float Bs[BK * LDB];
+  __shared__ __attribute__((aligned(16))) float As[BK * LDA];
+  __shared__ __attribute__((aligned(16))) float Bs[BK * LDB];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -63,42 +72,140 @@ gemm_kernel(AOp A, BOp B, EOp E, int M, int N, int K, int k_per_split) {
 
   float ra[A_PER], rb[B_PER];
 
-  // A chunk: element e = tid + 256*i -> (mm, kk), m fastest (or k fastest if AKF)
-  // B chunk: element e -> (nn, kk), n fastest (or k fastest if BKF)
-  auto a_mk = [](int e, int& mm, int& kk) {
-    if (AKF) { kk = e % BK; mm = e / BK; } else { mm = e % BM; kk = e / BM; }
-  };
-  auto b_nk = [](int e, int& nn, int& kk) {
-    if (BKF) { kk = e % BK; nn = e / BK; } else { nn = e % BN; kk = e / BN; }
-  };
   auto gather = [&](int kc) {
+    if constexpr (AV == GK) {
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      int mm, kk;
-      a_mk(tid + 256 * i, mm, kk);
-      const int m = m0 + mm, k = kc + kk;
-      ra[i] = (m < M && k < kend) ? A.load(m, k) : 0.f;
+      for (int i = 0; i < A_PER / 4; ++i) {
+        const int v = tid + 256 * i;
+        const int kq = v % (BK / 4), mm = v / (BK / 4);
+        const int m = m0 + mm, k = kc + 4 * kq;
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m < M) {
+          if (k + 3 < kend) x = A.load4(m, k);
+          else {
+            if (k < kend) x.x = A.load(m, k);
+            if (k + 1 < kend) x.y = A.load(m, k + 1);
+            if (k + 2 < kend) x.z = A.load(m, k + 2);
+          }
+        }
+        ra[4 * i] = x.x; ra[4 * i + 1] = x.y; ra[4 * i + 2] = x.z; ra[4 * i + 3] = x.w;
+      }
+    } else if constexpr (AV == GM) {
+#pragma unroll
+      for (int i = 0; i < A_PER / 4; ++i) {
+        const int v = tid + 256 * i;
+        const int mq = v % (BM / 4), kk = v / (BM / 4);
+        const int m = m0 + 4 * mq, k = kc + kk;
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (k < kend) {
+          if (m + 3 < M) x = A.load4m(m, k);
+          else {
+            if (m < M) x.x = A.load(m, k);
+            if (m + 1 < M) x.y = A.load(m + 1, k);
+            if (m + 2 < M) x.z = A.load(m + 2, k);
+          }
+        }
+        ra[4 * i] = x.x; ra[4 * i + 1] = x.y; ra[4 * i + 2] = x.z; ra[4 * i + 3] = x.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_PER; ++i) {
+        const int e = tid + 256 * i;
+        const int mm = e % BM, kk = e / BM;
+        const int m = m0 + mm, k = kc + kk;
+        ra[i] = (m < M && k < kend) ? A.load(m, k) : 0.f;
+      }
     }
+    if constexpr (BV == GK) {
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-      int nn, kk;
-      b_nk(tid + 256 * i, nn, kk);
-      const int n = n0 + nn, k = kc + kk;
-      rb[i] = (n < N && k < kend) ? B.load(k, n) : 0.f;
+      for (int i = 0; i < B_PER / 4; ++i) {
+        const int v = tid + 256 * i;
+        const int kq = v % (BK / 4), nn = v / (BK / 4);
+        const int n = n0 + nn, k = kc + 4 * kq;
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (n < N) {
+          if (k + 3 < kend) x = B.load4(k, n);
+          else {
+            if (k < kend) x.x = B.load(k, n);
+            if (k + 1 < kend) x.y = B.load(k + 1, n);
+            if (k + 2 < kend) x.z = B.load(k + 2, n);
+          }
+        }
+        rb[4 * i] = x.x; rb[4 * i + 1] = x.y; rb[4 * i + 2] = x.z; rb[4 * i + 3] = x.w;
+      }
+    } else if constexpr (BV == GM) {
+#pragma unroll
+      for (int i = 0; i < B_PER / 4; ++i) {
+        const int v = tid + 256 * i;
+        const int nq = v % (BN / 4), kk = v / (BN / 4);
+        const int n = n0 + 4 * nq, k = kc + kk;
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (k < kend) {
+          if (n + 3 < N) x = B.load4n(k, n);
+          else {
+            if (n < N) x.x = B.load(k, n);
+            if (n + 1 < N) x.y = B.load(k, n + 1);
+            if (n + 2 < N) x.z = B.load(k, n + 2);
+          }
+        }
+        rb[4 * i] = x.x; rb[4 * i + 1] = x.y; rb[4 * i + 2] = x.z; rb[4 * i + 3] = x.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < B_PER; ++i) {
+        const int e = tid + 256 * i;
+        const int nn = e % BN, kk = e / BN;
+        const int n = n0 + nn, k = kc + kk;
+        rb[i] = (n < N && k < kend) ? B.load(k, n) : 0.f;
+      }
     }
   };
   auto commit = [&]() {
+    if constexpr (AV == GK) {
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      int mm, kk;
-      a_mk(tid + 256 * i, mm, kk);
-      As[kk * LDA + mm] = ra[i];
+      for (int i = 0; i < A_PER / 4; ++i) {
+        const int v = tid + 256 * i;
+        const int kq = v % (BK / 4), mm = v / (BK / 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) As[(4 * kq + r) * LDA + mm] = ra[4 * i + r];
+      }
+    } else if constexpr (AV == GM) {
+#pragma unroll
+      for (int i = 0; i < A_PER / 4; ++i) {
+        const int v = tid + 256 * i;
+        const int mq = v % (BM / 4), kk = v / (BM / 4);
+        *reinterpret_cast<float4*>(&As[kk * LDA + 4 * mq]) =
+            make_float4(ra[4 * i], ra[4 * i + 1], ra[4 * i + 2], ra[4 * i + 3]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_PER; ++i) {
+        const int e = tid + 256 * i;
+        As[(e / BM) * LDA + (e % BM)] = ra[i];
+      }
     }
+    if constexpr (BV == GK) {
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-      int nn, kk;
-      b_nk(tid + 256 * i, nn, kk);
-      Bs[kk * LDB + nn] = rb[i];
+      for (int i = 0; i < B_PER / 4; ++i) {
+        const int v = tid + 256 * i;
+        const int kq = v % (BK / 4), nn = v / (BK / 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Bs[(4 * kq + r) * LDB + nn] = rb[4 * i + r];
+      }
+    } else if constexpr (BV == GM) {
+#pragma unroll
+      for (int i = 0; i < B_PER / 4; ++i) {
+        const int v = tid + 256 * i;
+        const int nq = v % (BN / 4), kk = v / (BN / 4);
+        *reinterpret_cast<float4*>(&Bs[kk * LDB + 4 * nq]) =
+            make_float4(rb[4 * i], rb[4 * i + 1], rb[4 * i + 2], rb[4 * i + 3]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < B_PER; ++i) {
+        const int e = tid + 256 * i;
+        Bs[(e / BN) * LDB + (e % BN)] = rb[i];
+      }
     }
   };
 
@@ -142,8 +249,7 @@ gemm_kernel(AOp A, BOp B, EOp E, int M, int N, int K, int k_per_split) {
     }
 }
 
-template <int BM, int BN, int BK, int WM, int WN, bool AKF = false, bool BKF = false, class AOp, class BOp,
-          class EOp>
+template <int BM, int BN, int BK, int WM, int WN, int AV = GS, int BV = GS, class AOp, class BOp, class EOp>
 inline hipError_t launch_gemm(const AOp& A, const BOp& B, const EOp& E, int M, int N, int K,
                               int splits, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0) return hipSuccess;
@@ -152,7 +258,7 @@ inline hipError_t launch_gemm(const AOp& A, const BOp& B, const EOp& E, int M, i
   kps = ((kps + BK - 1) / BK) * BK;
   splits = (K + kps - 1) / kps;
   dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN, splits);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AOp, BOp, EOp, AKF, BKF>), grid, dim3(256), 0, s,
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AOp, BOp, EOp, AV, BV>), grid, dim3(256), 0, s,
                      A, B, E, M, N, K, kps);
   return hipGetLastError();
 }
@@ -170,10 +276,19 @@ inline int effective_splits(int K, int splits) {
 struct RowMajor {            // X[m][k], leading dimension ld
   const float* p; int ld;
   __device__ float load(int m, int k) const { return p[(int64_t)m * ld + k]; }
+  __device__ float4 load4(int m, int k) const {   // k % 4 == 0, ld % 4 == 0
+    return *reinterpret_cast<const float4*>(p + (int64_t)m * ld + k);
+  }
+  __device__ float4 load4n(int k, int n) const {  // as a B operand: 4 consecutive n
+    return *reinterpret_cast<const float4*>(p + (int64_t)k * ld + n);
+  }
 };
 struct ColMajor {            // element (r, c) = X[c][r]  (i.e. X transposed)
   const float* p; int ld;
   __device__ float load(int r, int c) const { return p[(int64_t)c * ld + r]; }
+  __device__ float4 load4m(int r, int c) const {   // 4 consecutive r (A operand)
+    return *reinterpret_cast<const float4*>(p + (int64_t)c * ld + r);
+  }
 };
 
 }  // namespace arl

@@ -51,6 +51,9 @@ struct Conv2A {         // A(m, k) = a1[s][ic][2oy+ky][2ox+kx], m = s*81 + p, k 
 struct WeightT {        // B(k, n) = W[n][k]  (Chainer W is (out, in...))
   const float* __restrict__ w; int K;
   __device__ float load(int k, int n) const { return w[(int64_t)n * K + k]; }
+  __device__ float4 load4(int k, int n) const {
+    return *reinterpret_cast<const float4*>(w + (int64_t)n * K + k);
+  }
 };
 struct LstmGateA {      // A(m, k): [x | h_prev (0 after reset)]
   const float* __restrict__ x; const float* __restrict__ h; const uint8_t* __restrict__ reset;
@@ -58,11 +61,20 @@ struct LstmGateA {      // A(m, k): [x | h_prev (0 after reset)]
     if (k < HID) return x[(int64_t)m * HID + k];
     return reset[m] ? 0.f : h[(int64_t)m * HID + k - HID];
   }
+  __device__ float4 load4(int m, int k) const {   // a 4-vector never straddles k = 256
+    if (k < HID) return *reinterpret_cast<const float4*>(x + (int64_t)m * HID + k);
+    if (reset[m]) return make_float4(0.f, 0.f, 0.f, 0.f);
+    return *reinterpret_cast<const float4*>(h + (int64_t)m * HID + k - HID);
+  }
 };
 struct LstmGateB {      // B(k, j) = [Wu^T ; Wl^T]
   const float* __restrict__ wu; const float* __restrict__ wl;
   __device__ float load(int k, int j) const {
     return k < HID ? wu[(int64_t)j * HID + k] : wl[(int64_t)j * HID + k - HID];
+  }
+  __device__ float4 load4(int k, int j) const {
+    return k < HID ? *reinterpret_cast<const float4*>(wu + (int64_t)j * HID + k)
+                   : *reinterpret_cast<const float4*>(wl + (int64_t)j * HID + k - HID);
   }
 };
 struct HeadsGA {        // A(m, s) = m < A ? dlogits[s][m] : dv[s]
@@ -72,6 +84,10 @@ struct HeadsGA {        // A(m, s) = m < A ? dlogits[s][m] : dv[s]
 struct OnesColB {       // B(s, j) = j < K ? X[s][j] : 1   (bias gradient column)
   const float* __restrict__ x; int K;
   __device__ float load(int s, int j) const { return j < K ? x[(int64_t)s * K + j] : 1.f; }
+  __device__ float4 load4n(int s, int j) const {
+    if (j + 3 < K) return *reinterpret_cast<const float4*>(x + (int64_t)s * K + j);
+    return make_float4(load(s, j), load(s, j + 1), load(s, j + 2), load(s, j + 3));
+  }
 };
 struct LstmWB {         // B(s, j) = [x (256) | 1 | h_prev (256, 0 after reset)]
   const float* __restrict__ x; const float* __restrict__ h; const uint8_t* __restrict__ reset;
@@ -374,7 +390,7 @@ static hipError_t fc_forward(const Net& net, int n, const float* a2, float* hfc,
   const int req = plan_splits(ceil_div(n, 32) * ceil_div(HID, 64), A2, 32, 256);
   const int sp = effective_splits<32>(A2, req);
   float* slab = net.at<float>(net.w_slab);
-  ARL_TRY((launch_gemm<32, 64, 32, 2, 2, true, true>(RowMajor{a2, A2}, WeightT{P + net.o_fcW, A2},
+  ARL_TRY((launch_gemm<32, 64, 32, 2, 2, GK, GK>(RowMajor{a2, A2}, WeightT{P + net.o_fcW, A2},
                                                      EpiSlab{slab, n, HID}, n, HID, A2, req, s)));
   const int64_t MN = (int64_t)n * HID;
   hipLaunchKernelGGL(reduce_bias_relu_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, s, slab, sp, MN, HID,
@@ -399,7 +415,7 @@ hipError_t net_act(Net& net, int t, int sample, hipStream_t s) {
     float* hout = net.at<float>(net.w_hbuf) + (int64_t)(t + 1) * n * HID;
     float* cout = net.at<float>(net.w_cbuf) + (int64_t)(t + 1) * n * HID;
     const uint8_t* rs = net.at<uint8_t>(net.w_reset) + (int64_t)t * n;
-    ARL_TRY((launch_gemm<32, 64, 32, 2, 2, true, true>(LstmGateA{hfc, hprev, rs}, LstmGateB{P + net.o_luW, P + net.o_llW},
+    ARL_TRY((launch_gemm<32, 64, 32, 2, 2, GK, GK>(LstmGateA{hfc, hprev, rs}, LstmGateB{P + net.o_luW, P + net.o_llW},
                                            EpiBias{gates, P + net.o_lub, GATES}, n, GATES, 2 * HID, 1, s)));
     const int64_t cnt = (int64_t)n * HID;
     hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, gates, cprev, rs,
@@ -424,10 +440,10 @@ hipError_t net_forward_f32(Net& net, const float* x, int n, float*, float*, hipS
   float* a2 = net.at<float>(net.w_a2) + (int64_t)T * N * A2;
   float* hfc = net.at<float>(net.w_hfc) + (int64_t)T * N * HID;
   const float* P = net.p;
-  ARL_TRY((launch_gemm<64, 16, 32, 4, 1, false, true>(Conv1F32A{x}, WeightT{P + net.o_c1W, 256},
+  ARL_TRY((launch_gemm<64, 16, 32, 4, 1>(Conv1F32A{x}, WeightT{P + net.o_c1W, 256},
                                                       EpiConv{a1, P + net.o_c1b, C1_OC, C1_P}, n * C1_P, C1_OC, 256,
                                                       1, s)));
-  ARL_TRY((launch_gemm<32, 32, 32, 2, 2, false, true>(Conv2A{a1}, WeightT{P + net.o_c2W, 256},
+  ARL_TRY((launch_gemm<32, 32, 32, 2, 2, GS, GK>(Conv2A{a1}, WeightT{P + net.o_c2W, 256},
                                                       EpiConv{a2, P + net.o_c2b, C2_OC, C2_P}, n * C2_P, C2_OC, 256,
                                                       1, s)));
   ARL_TRY(fc_forward(net, n, a2, hfc, s));
@@ -457,7 +473,7 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
   const float* hheads = L ? net.at<float>(net.w_hbuf) + (int64_t)n * HID : hfc;   // h fed to pi / v
   float* dfc = net.at<float>(net.w_dfc);
   // 2. heads: weight grads (ones column = bias) and dh
-  ARL_TRY((launch_gemm<16, 64, 32, 1, 4>(HeadsGA{dl, dv, A}, OnesColB{hheads, HID}, EpiSlab{slab, A + 1, HID + 1},
+  ARL_TRY((launch_gemm<16, 64, 32, 1, 4, GS, GM>(HeadsGA{dl, dv, A}, OnesColB{hheads, HID}, EpiSlab{slab, A + 1, HID + 1},
                                          A + 1, HID + 1, S, pl.heads_w, s)));
   ARL_TRY(launch_reduce_grad(slab, pl.heads_w, A + 1, HID + 1,
                              MapHeads{G, net.o_piW, net.o_pib, net.o_vW, net.o_vb, A}, s));
@@ -486,24 +502,24 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
                          dG + o * GATES, t == T - 1 ? 1 : 0, cnt);
       ARL_TRY(hipGetLastError());
       if (t > 0)
-        ARL_TRY((launch_gemm<32, 64, 32, 2, 2, true, false>(RowMajor{dG + o * GATES, GATES}, RowMajor{P + net.o_llW, HID},
+        ARL_TRY((launch_gemm<32, 64, 32, 2, 2, GK, GM>(RowMajor{dG + o * GATES, GATES}, RowMajor{P + net.o_llW, HID},
                                                EpiResetMask{dhn, rs + o, HID}, n, HID, GATES, 1, s)));
     }
-    ARL_TRY((launch_gemm<64, 64, 32, 2, 2>(ColMajor{dG, GATES}, LstmWB{hfc, hbuf, rs},
+    ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GM, GS>(ColMajor{dG, GATES}, LstmWB{hfc, hbuf, rs},
                                            EpiSlab{slab, GATES, 2 * HID + 1}, GATES, 2 * HID + 1, S, pl.lstm_w, s)));
     ARL_TRY(launch_reduce_grad(slab, pl.lstm_w, GATES, 2 * HID + 1,
                                MapDense{G, net.o_luW, net.o_lub, net.o_llW, HID}, s));
-    ARL_TRY((launch_gemm<64, 64, 32, 2, 2, true, false>(RowMajor{dG, GATES}, RowMajor{P + net.o_luW, HID}, EpiMask{dfc, hfc, HID},
+    ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GK, GM>(RowMajor{dG, GATES}, RowMajor{P + net.o_luW, HID}, EpiMask{dfc, hfc, HID},
                                            S, HID, GATES, 1, s)));
   }
   // 4. FC: dW (+ bias via ones column) and da2 = (dfc W) * (a2 > 0)
   const float* a2 = net.at<float>(net.w_a2);
   const float* a1 = net.at<float>(net.w_a1);
   float* da2 = net.at<float>(net.w_da2);
-  ARL_TRY((launch_gemm<64, 64, 32, 2, 2>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab, HID, A2 + 1}, HID,
+  ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GM, GM>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab, HID, A2 + 1}, HID,
                                          A2 + 1, S, pl.fc_w, s)));
   ARL_TRY(launch_reduce_grad(slab, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s));
-  ARL_TRY((launch_gemm<64, 64, 32, 2, 2, true, false>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2}, EpiMask{da2, a2, A2}, S, A2,
+  ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GK, GM>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2}, EpiMask{da2, a2, A2}, S, A2,
                                          HID, 1, s)));
   // 5. fused conv backward per sample (conv_bwd.hip): conv2 dW/db,
   //    da1 = conv_transpose(da2, W2) * (a1 > 0) kept in LDS, conv1 dW/db
