@@ -15,7 +15,9 @@ import os
 
 import torch  # noqa: F401  (must precede the CDLL load, see module doc)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libasyncrl_hip.so")
+# ASYNCRL_HIP_LIB: alternative build of the same library (timing ablations only)
+LIB_PATH = os.environ.get("ASYNCRL_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                             "libasyncrl_hip.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

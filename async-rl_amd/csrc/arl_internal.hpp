@@ -68,7 +68,7 @@ struct Net {
   int64_t ws_bytes;
   int64_t w_ctl, w_frames, w_nvalid, w_reset, w_rewards, w_dones, w_a1, w_a2, w_hfc, w_gates, w_hbuf,
       w_cbuf, w_logits, w_probs, w_logp, w_v, w_ent, w_logpa, w_act, w_dlogits, w_dv, w_dh, w_dfc,
-      w_dG, w_dhn, w_dcn, w_da2, w_slab, w_norm, w_loss;
+      w_dG, w_dhn, w_dcn, w_da2, w_slab, w_norm, w_loss, w_tick;
   int64_t slab_floats;
   int norm_blocks;
   // bound pointers
@@ -95,6 +95,11 @@ hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const i
                            const float* a1, const float* da2, const float* W2, float* slab, float* gW2, float* gb2,
                            float* gW1, float* gb1, hipStream_t s);
 int64_t conv_bwd_slab_floats(int S);
+
+constexpr int FC_SPLIT = 8;   // fc forward split-K (one slice per XCD)
+int fc_fwd_tiles(int n);      // tickets needed for n envs
+hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b, float* slab, int* tickets,
+                         float* hfc, hipStream_t s);
 
 hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, double alpha, double eps,
                           const double* norm_partials, int norm_blocks, float clip, const int64_t* ctl,

@@ -29,6 +29,10 @@
 
 #include "arl_internal.hpp"
 
+#ifndef ARL_ABLATE
+#define ARL_ABLATE 0   // timing experiments only (bits: 8 step 1, 16 step 2, 32 step 3, 64 prefetch loads)
+#endif
+
 namespace arl {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -66,6 +70,7 @@ struct Prefetch {
 };
 
 __device__ inline void prefetch_sample(const ConvBwdArgs& a, int s, Prefetch& r) {
+  if (ARL_ABLATE & 64) return;
   const int tid = threadIdx.x;
   const int t = s / a.n, e = s - t * a.n;
   const int64_t ks = a.ctl[CTL_STEP] + t;
@@ -184,7 +189,7 @@ conv_bwd_kernel(ConvBwdArgs a) {
       const float* b0 = a1s + (2 * wave) * A1_LD + (col >> 2) * 20 + (col & 3);
       const float* b1 = b0 + A1_LD;
 #pragma unroll 3
-      for (int ps = 0; ps < 21; ++ps) {
+      for (int ps = 0; ps < ((ARL_ABLATE & 8) ? 0 : 21); ++ps) {
         const int p = 4 * ps + q;
         const bool pv = p < C2_P;
         const int pc = pv ? p : 0;
@@ -221,7 +226,7 @@ conv_bwd_kernel(ConvBwdArgs a) {
         const float* wb = w2t + ((pyB + 2 * dy) * 4 + pxB + 2 * dx) * 16 + col;
         f32x4 cA = {0.f, 0.f, 0.f, 0.f}, cB = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-        for (int ks = 0; ks < 32; ++ks) {
+        for (int ks = 0; ks < ((ARL_ABLATE & 16) ? 0 : 32); ++ks) {
           const float afA = okA ? pa[ks * C2_P] : 0.f;
           const float afB = okB ? pb[ks * C2_P] : 0.f;
           cA = __builtin_amdgcn_mfma_f32_16x16x4f32(afA, wa[ks * 256], cA, 0, 0, 0);
@@ -253,7 +258,7 @@ conv_bwd_kernel(ConvBwdArgs a) {
       b1sum = __fadd_rn(b1sum, t);
     }
 #pragma unroll 2
-    for (int ps = 0; ps < C1_P / 4; ++ps) {
+    for (int ps = 0; ps < ((ARL_ABLATE & 32) ? 0 : C1_P / 4); ++ps) {
       const int p = 4 * ps + q;
       const int oy = p / 20, ox = p - oy * 20;
       const uint32_t w2 = *reinterpret_cast<const uint16_t*>(xs + xoff3 + (4 * oy) * 84 + 4 * ox);

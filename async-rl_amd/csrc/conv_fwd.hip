@@ -21,6 +21,10 @@
 
 #include "arl_internal.hpp"
 
+#ifndef ARL_ABLATE
+#define ARL_ABLATE 0   // timing experiments only (bits: 1 conv1 MFMA, 2 conv2 MFMA, 4 staging loads)
+#endif
+
 namespace arl {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -82,7 +86,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
       const int i = tid + NT * j;
       const int c = i / V, o = i - c * V;
       xv[j] = make_uint4(0, 0, 0, 0);
-      if (i < 4 * V && c >= 4 - nv)
+      if (!(ARL_ABLATE & 4) && i < 4 * V && c >= 4 - nv)
         xv[j] = reinterpret_cast<const uint4*>(a.frames + ((int64_t)slot[c] * a.n + e) * PLANE)[o];
     }
     // W1: thread -> (oc = i & 15, chunk = i >> 4); W2: (oc = i & 31, chunk = i >> 5)
@@ -138,7 +142,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
     const uint8_t* baseB = xs + (4 * oyB) * 84 + 4 * oxB + 4 * (q & 1);
     f32x4 cA = {0.f, 0.f, 0.f, 0.f}, cB = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < ((ARL_ABLATE & 1) ? 0 : 16); ++j) {
       const int u = 2 * j + (q >> 1), ic = u >> 3, ky = u & 7;
       const int off = ic * PLANE + ky * 84;
       const uint32_t wA = *reinterpret_cast<const uint32_t*>(baseA + off);
@@ -178,7 +182,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
     const float* w2B = w2k + q * W2_LD + 16 * ntB + col;
     f32x4 cA = {0.f, 0.f, 0.f, 0.f}, cB = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-    for (int ks = 0; ks < 64; ++ks) {
+    for (int ks = 0; ks < ((ARL_ABLATE & 2) ? 0 : 64); ++ks) {
       // k = 4 ks + q = (ic, ky, kx) = (ks >> 2, ks & 3, q)
       const int aoff = (ks >> 2) * A1_LD + (ks & 3) * 20 + q;
       const float afA = okA ? a1s[aoff + rowA] : 0.f;

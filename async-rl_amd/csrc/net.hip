@@ -131,15 +131,6 @@ struct EpiResetMask {   // out[m][n] = reset[m] ? 0 : v
 };
 
 // ---------------------------------------------------------------- reductions
-__global__ void reduce_bias_relu_kernel(const float* __restrict__ slab, int splits, int64_t MN, int N,
-                                        const float* __restrict__ b, float* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= MN) return;
-  float s = 0.f;
-  for (int z = 0; z < splits; ++z) s = __fadd_rn(s, slab[(int64_t)z * MN + i]);
-  out[i] = fmaxf(__fadd_rn(s, b[i % N]), 0.f);
-}
-
 // dense weight + bias: n < K -> g[oW + m*K + n]; n == K -> g[ob + m];
 // (LSTM) n > K -> g[oL + m*K + n-K-1]
 struct MapDense {
@@ -272,13 +263,12 @@ static int plan_splits(int tiles, int64_t K, int BK, int target = 1024) {
 }
 
 struct Plans {   // effective split counts (launch_gemm may shrink a request)
-  int fc_fwd, heads_w, fc_w, lstm_w;
+  int heads_w, fc_w, lstm_w;
 };
 
 static Plans make_plans(const Net& net) {
-  const int n = net.N, S = net.T * net.N;
+  const int S = net.T * net.N;
   Plans p;
-  p.fc_fwd = effective_splits<32>(A2, plan_splits(ceil_div(n, 32) * ceil_div(HID, 64), A2, 32, 256));
   p.heads_w = effective_splits<32>(S, plan_splits(ceil_div(net.A + 1, 16) * ceil_div(HID + 1, 64), S, 32));
   p.fc_w = effective_splits<32>(S, plan_splits(ceil_div(HID, 64) * ceil_div(A2 + 1, 64), S, 32));
   p.lstm_w = effective_splits<32>(S, plan_splits(ceil_div(GATES, 64) * ceil_div(2 * HID + 1, 64), S, 32));
@@ -332,7 +322,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   net.norm_blocks = 1024;
   Plans pl = make_plans(net);
   int64_t slab = 0;
-  slab = std::max(slab, (int64_t)pl.fc_fwd * n * HID);
+  slab = std::max(slab, (int64_t)FC_SPLIT * n * HID);
   slab = std::max(slab, (int64_t)pl.heads_w * (A + 1) * (HID + 1));
   slab = std::max(slab, (int64_t)pl.fc_w * HID * (A2 + 1));
   slab = std::max(slab, conv_bwd_slab_floats((int)S));
@@ -376,6 +366,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   net.w_da2 = buf("da2", S * A2 * 4);
   net.w_slab = buf("slab", slab * 4);
   net.w_norm = buf("norm_partials", (int64_t)net.norm_blocks * 8);
+  net.w_tick = buf("tickets", (int64_t)fc_fwd_tiles((int)n) * 4);
   net.w_loss = buf("loss", n * 2 * 4);
   net.ws_bytes = wo;
   return true;
@@ -386,16 +377,8 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
 
 // head after conv1 (conv2 -> fc) for n rows, activations at a1/a2/hfc
 static hipError_t fc_forward(const Net& net, int n, const float* a2, float* hfc, hipStream_t s) {
-  const float* P = net.p;
-  const int req = plan_splits(ceil_div(n, 32) * ceil_div(HID, 64), A2, 32, 256);
-  const int sp = effective_splits<32>(A2, req);
-  float* slab = net.at<float>(net.w_slab);
-  ARL_TRY((launch_gemm<32, 64, 32, 2, 2, GK, GK>(RowMajor{a2, A2}, WeightT{P + net.o_fcW, A2},
-                                                     EpiSlab{slab, n, HID}, n, HID, A2, req, s)));
-  const int64_t MN = (int64_t)n * HID;
-  hipLaunchKernelGGL(reduce_bias_relu_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, s, slab, sp, MN, HID,
-                     P + net.o_fcb, hfc);
-  return hipGetLastError();
+  return launch_fc_fwd(a2, n, net.p + net.o_fcW, net.p + net.o_fcb, net.at<float>(net.w_slab),
+                       net.at<int>(net.w_tick), hfc, s);
 }
 
 hipError_t net_act(Net& net, int t, int sample, hipStream_t s) {
