@@ -2,24 +2,31 @@
 // for one env per workgroup, straight from the uint8 frame ring:
 //   a1 = relu(conv(x/255, W1, s4) + b1)   (16 x 20 x 20)  -> LDS + HBM (kept for backward)
 //   a2 = relu(conv(a1, W2, s2) + b2)      (32 x 9 x 9)    -> HBM
-// LDS: the 4 screens (28 KB, planes older than the env's last reset read as
-// 0), W1 (16 KB), W2 (48 KB, k-major, padded) and a1 (25.6 KB) -- one
-// 512-thread workgroup per CU, i.e. two waves per SIMD so one wave's LDS and
-// dependency stalls hide behind the other's MFMAs (rocprof: one wave per SIMD
-// left the MFMA pipe busy only ~26% of the time).
+// Both contractions run on the bf16 matrix cores with exact bf16 splits of
+// the f32 operands (bf16split.hpp): conv1 multiplies the integer pixel values
+// (exact in bf16; 1/255 is applied to the sum) by W1 = h + m + l, 3 MFMAs per
+// k-step; conv2 multiplies a1 = h + m + l by W2 = h + m + l, 6 MFMAs.
 //
-// conv1: C[p][oc], 25 position tiles x K 256, v_mfma_f32_16x16x4_f32 on the
-// integer pixel values (1/255 applied to the sum in the epilogue; dqn_phi.py:16).
-// The K order is permuted so one ds_read_b32 of 4 contiguous pixels feeds 4
-// k-steps: k-step 4j + r, lane quarter q -> (ic, ky) = divmod(2j + (q >> 1), 8),
-// kx = 4 (q & 1) + r; the weights follow the same permutation and live in 64
-// VGPRs.  Two tiles in flight per wave.
-// conv2: C[p][oc] with M = 81 (6 tiles), N = 32 (2 tiles), K = 256 = (ic, ky,
-// kx) read from a1 in LDS: 12 tile jobs over 8 waves.
+// LDS (145.5 KB, one 512-thread workgroup per CU = 2 waves per SIMD):
+//   xb   4 screens as bf16 [ic][y][x]                         56,448 B
+//   R1   W1 split planes [3][oc][k] (rows padded to 528 B),   25,344 B
+//        then (after every wave holds its W1 fragments) the a1 split planes
+//        [3][pixel][ic] with an XOR swizzle of the 16-byte slots  38,400 B
+//   W2p  W2 split planes [3][oc][tap][ic] (rows 528 B)         50,688 B
+//
+// conv1: M = 400 positions (25 tiles), N = 16 oc, K = 256 ordered (ic, ky, kx):
+//   k-step s, lane quarter g -> (ic, ky) = divmod(4 s + g, 8), kx = 0..7, i.e.
+//   8 contiguous bf16 pixels per lane; W1 fragments live in 96 VGPRs.
+// conv2: M = 81 positions (6 tiles), N = 32 oc (2 tiles), K = 256 ordered
+//   (tap = ky*4 + kx, ic): k-step s, quarter g -> tap 2 s + (g >> 1), ic
+//   8 (g & 1) + 0..7 = one 16-byte read of a channel-last a1 pixel.  Wave w
+//   owns n-tile w & 1 (its W2 fragments in 96 VGPRs) and m-tiles w >> 1 and
+//   (w >> 1) + 4: three jobs per SIMD.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "arl_internal.hpp"
+#include "bf16split.hpp"
 
 #ifndef ARL_ABLATE
 #define ARL_ABLATE 0   // timing experiments only (bits: 1 conv1 MFMA, 2 conv2 MFMA, 4 staging loads)
@@ -27,14 +34,25 @@
 
 namespace arl {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
 namespace {
-constexpr int NT = 512;      // threads per workgroup (8 waves)
-constexpr int A1_LD = 401;   // a1 rows (per oc) in LDS, odd stride: lanes reading 16 oc hit 16 banks
-constexpr int W1_LD = 257;   // W1 rows (per oc), odd stride for the same reason
-constexpr int W2_LD = 48;    // W2 stored k-major: w2k[k * 48 + oc]; lanes (q, oc) -> banks 16q + oc
+constexpr int NT = 512;                  // threads per workgroup (8 waves)
+constexpr int XB_ROW = 84 * 2;           // bytes per bf16 screen row
+constexpr int XB_PLANE = PLANE * 2;      // 14,112 bytes per bf16 screen
+constexpr int WROW = 528;                // bytes per oc row of a weight plane (512 + 16: conflict-free b128)
+constexpr int W1P = 16 * WROW;           // 8,448 per W1 plane
+constexpr int W2P = 32 * WROW;           // 16,896 per W2 plane
+constexpr int A1P = C1_P * 32;           // 12,800 per a1 plane: 400 pixels x 16 ic bf16
+constexpr int L_XB = 0;
+constexpr int L_R1 = L_XB + 4 * XB_PLANE;   // 56,448
+constexpr int L_W2 = L_R1 + 3 * A1P;        // 94,848
+constexpr int L_END = L_W2 + 3 * W2P;       // 145,536
+static_assert(3 * W1P <= 3 * A1P, "W1 planes fit the a1 region");
 }  // namespace
+
+// a1 plane byte offset of (pixel P, ic half h): 16-byte slot 2P + h with its
+// low 4 bits XORed by P >> 3, so conv2's 16 lanes (positions 2 pixels apart)
+// spread over the LDS banks
+__device__ inline int a1_slot(int P, int h) { return (((2 * P + h) ^ ((P >> 3) & 15)) << 4); }
 
 struct ConvFwdArgs {
   const uint8_t* frames;
@@ -49,27 +67,14 @@ struct ConvFwdArgs {
   float* a2;            // (n, 32, 81)
 };
 
-__device__ inline float4 relu_scaled(f32x4 c, float bias) {
-  float4 o;
-  o.x = fmaxf(__fadd_rn(__fdiv_rn(c[0], 255.f), bias), 0.f);
-  o.y = fmaxf(__fadd_rn(__fdiv_rn(c[1], 255.f), bias), 0.f);
-  o.z = fmaxf(__fadd_rn(__fdiv_rn(c[2], 255.f), bias), 0.f);
-  o.w = fmaxf(__fadd_rn(__fdiv_rn(c[3], 255.f), bias), 0.f);
-  return o;
-}
-
 __global__ void __launch_bounds__(NT)
 conv_fwd_kernel(ConvFwdArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t xs[4 * PLANE];   // 28,224
-  __shared__ float w1s[16 * W1_LD];                                 // 16,448
-  __shared__ float w2k[256 * W2_LD];                                // 49,152
-  __shared__ float a1s[C1_OC * A1_LD];                              // 25,664
+  __shared__ __attribute__((aligned(16))) uint8_t lds[L_END];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int q = lane >> 4, col = lane & 15;
+  const int g = lane >> 4, col = lane & 15;
   const int e = blockIdx.x;
-  // ---- stage screens + weights: every global load issued before the LDS
-  // writes; the weight writes are laid out so 32 consecutive lanes hit 32 banks
+  // ---- stage: all global loads first, then bf16 conversion / splitting into LDS
   {
     const int64_t ks = a.ctl[CTL_STEP] + a.t;
     const int rs = (int)(ks % a.R);
@@ -77,59 +82,75 @@ conv_fwd_kernel(ConvFwdArgs a) {
     int slot[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) slot[c] = (rs + a.R - 3 + c) % a.R;
-    constexpr int V = PLANE / 16;            // 441 uint4 per screen
+    constexpr int V = PLANE / 16;              // 441 uint4 per screen
     constexpr int NX = (4 * V + NT - 1) / NT;  // 4
     uint4 xv[NX];
-    float4 w1v[2], w2v[4];
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const int i = tid + NT * j;
       const int c = i / V, o = i - c * V;
       xv[j] = make_uint4(0, 0, 0, 0);
-      if (!(ARL_ABLATE & 4) && i < 4 * V && c >= 4 - nv)
+      if (!(ARL_ABLATE & 4) && i < 4 * V && c >= 4 - nv)   // planes older than the last reset read as 0
         xv[j] = reinterpret_cast<const uint4*>(a.frames + ((int64_t)slot[c] * a.n + e) * PLANE)[o];
     }
-    // W1: thread -> (oc = i & 15, chunk = i >> 4); W2: (oc = i & 31, chunk = i >> 5)
+    // W1: thread -> 8 consecutive k of one oc; W2: thread -> (oc, 4 ic, 4 taps)
+    const int w1oc = tid >> 5, w1k = (8 * tid) & 255;
+    const float4 w1a = reinterpret_cast<const float4*>(a.W1)[2 * tid];
+    const float4 w1b = reinterpret_cast<const float4*>(a.W1)[2 * tid + 1];
+    const int w2oc = tid >> 4, ic4 = (tid >> 2) & 3, tg = tid & 3;
+    float4 w2v[4];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int i = tid + NT * j;
-      w1v[j] = reinterpret_cast<const float4*>(a.W1)[(i & 15) * 64 + (i >> 4)];
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = tid + NT * j;
-      w2v[j] = reinterpret_cast<const float4*>(a.W2)[(i & 31) * 64 + (i >> 5)];
-    }
+    for (int ii = 0; ii < 4; ++ii)
+      w2v[ii] = reinterpret_cast<const float4*>(a.W2)[(w2oc * 16 + 4 * ic4 + ii) * 4 + tg];
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const int i = tid + NT * j;
-      if (i < 4 * V) reinterpret_cast<uint4*>(xs)[i] = xv[j];
+      if (i < 4 * V) {
+        const int c = i / V, o = i - c * V;
+        uint4 lo, hi;
+        lo.x = px_pair_bf16(xv[j].x, 0); lo.y = px_pair_bf16(xv[j].x, 1);
+        lo.z = px_pair_bf16(xv[j].y, 0); lo.w = px_pair_bf16(xv[j].y, 1);
+        hi.x = px_pair_bf16(xv[j].z, 0); hi.y = px_pair_bf16(xv[j].z, 1);
+        hi.z = px_pair_bf16(xv[j].w, 0); hi.w = px_pair_bf16(xv[j].w, 1);
+        uint4* d = reinterpret_cast<uint4*>(lds + L_XB + c * XB_PLANE + o * 32);
+        d[0] = lo;
+        d[1] = hi;
+      }
+    }
+    {
+      uint4 ph, pm, pl;
+      split3_pack(w1a.x, w1a.y, ph.x, pm.x, pl.x);
+      split3_pack(w1a.z, w1a.w, ph.y, pm.y, pl.y);
+      split3_pack(w1b.x, w1b.y, ph.z, pm.z, pl.z);
+      split3_pack(w1b.z, w1b.w, ph.w, pm.w, pl.w);
+      uint8_t* d = lds + L_R1 + w1oc * WROW + w1k * 2;
+      *reinterpret_cast<uint4*>(d) = ph;
+      *reinterpret_cast<uint4*>(d + W1P) = pm;
+      *reinterpret_cast<uint4*>(d + 2 * W1P) = pl;
     }
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int i = tid + NT * j;
-      float* d = w1s + (i & 15) * W1_LD + 4 * (i >> 4);
-      d[0] = w1v[j].x; d[1] = w1v[j].y; d[2] = w1v[j].z; d[3] = w1v[j].w;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = tid + NT * j;
-      const int oc = i & 31, k = 4 * (i >> 5);
-      w2k[(k + 0) * W2_LD + oc] = w2v[j].x;
-      w2k[(k + 1) * W2_LD + oc] = w2v[j].y;
-      w2k[(k + 2) * W2_LD + oc] = w2v[j].z;
-      w2k[(k + 3) * W2_LD + oc] = w2v[j].w;
+    for (int tt = 0; tt < 4; ++tt) {
+      const float v0 = w2v[0][tt], v1 = w2v[1][tt], v2 = w2v[2][tt], v3 = w2v[3][tt];
+      uint2 ph, pm, pl;
+      split3_pack(v0, v1, ph.x, pm.x, pl.x);
+      split3_pack(v2, v3, ph.y, pm.y, pl.y);
+      uint8_t* d = lds + L_W2 + w2oc * WROW + ((4 * tg + tt) * 16 + 4 * ic4) * 2;
+      *reinterpret_cast<uint2*>(d) = ph;
+      *reinterpret_cast<uint2*>(d + W2P) = pm;
+      *reinterpret_cast<uint2*>(d + 2 * W2P) = pl;
     }
   }
   __syncthreads();
-  // ---- conv1: permuted weights of this lane (B[k][n = oc = col])
-  float wf[64];
+  // ---- conv1 B fragments: lane (oc = col, g), k-step s -> k = 8 (4 s + g) + 0..7
+  bf16x8 w1h[8], w1m[8], w1l[8];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int u = 2 * j + (q >> 1), ic = u >> 3, ky = u & 7;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) wf[4 * j + r] = w1s[col * W1_LD + ic * 64 + ky * 8 + 4 * (q & 1) + r];
+  for (int s = 0; s < 8; ++s) {
+    const int off = L_R1 + col * WROW + (4 * s + g) * 16;
+    w1h[s] = lds_load<bf16x8>(lds, off);
+    w1m[s] = lds_load<bf16x8>(lds, off + W1P);
+    w1l[s] = lds_load<bf16x8>(lds, off + 2 * W1P);
   }
+  __syncthreads();   // the W1 planes are overwritten by the a1 planes below
   const float bias1 = a.b1[col];
   float* a1g = a.a1 + (int64_t)e * A1;
   // tile pairs (w, w+8), (w+16, w+24): 25 tiles over 8 waves
@@ -138,75 +159,84 @@ conv_fwd_kernel(ConvFwdArgs a) {
     const bool hasB = tB < 25;
     const int pA = tA * 16 + col, pB = (hasB ? tB : tA) * 16 + col;
     const int oyA = pA / 20, oxA = pA - oyA * 20, oyB = pB / 20, oxB = pB - oyB * 20;
-    const uint8_t* baseA = xs + (4 * oyA) * 84 + 4 * oxA + 4 * (q & 1);
-    const uint8_t* baseB = xs + (4 * oyB) * 84 + 4 * oxB + 4 * (q & 1);
-    f32x4 cA = {0.f, 0.f, 0.f, 0.f}, cB = {0.f, 0.f, 0.f, 0.f};
+    const int baseA = L_XB + (4 * oyA) * XB_ROW + 8 * oxA;
+    const int baseB = L_XB + (4 * oyB) * XB_ROW + 8 * oxB;
+    f32x4 bigA = {0.f, 0.f, 0.f, 0.f}, smlA = bigA, bigB = bigA, smlB = bigA;
 #pragma unroll
-    for (int j = 0; j < ((ARL_ABLATE & 1) ? 0 : 16); ++j) {
-      const int u = 2 * j + (q >> 1), ic = u >> 3, ky = u & 7;
-      const int off = ic * PLANE + ky * 84;
-      const uint32_t wA = *reinterpret_cast<const uint32_t*>(baseA + off);
-      const uint32_t wB = *reinterpret_cast<const uint32_t*>(baseB + off);
+    for (int s = 0; s < ((ARL_ABLATE & 1) ? 0 : 8); ++s) {
+      const int u = 4 * s + g, off = (u >> 3) * XB_PLANE + (u & 7) * XB_ROW;
+      const bf16x8 xa = lds_load8_a8(lds, baseA + off);
+      const bf16x8 xb = lds_load8_a8(lds, baseB + off);
+      mfma_x3(xa, w1h[s], w1m[s], w1l[s], bigA, smlA);
+      mfma_x3(xb, w1h[s], w1m[s], w1l[s], bigB, smlB);
+    }
+    // C rows g*4 + r -> positions tile*16 + g*4 + r, col = oc
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      if (pass == 1 && !hasB) break;
+      const f32x4 big = pass ? bigB : bigA, sml = pass ? smlB : smlA;
+      const int p0 = (pass ? tB : tA) * 16 + g * 4;
+      float ov[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        ov[r] = fmaxf(__fadd_rn(__fdiv_rn(__fadd_rn(big[r], sml[r]), 255.f), bias1), 0.f);
+      *reinterpret_cast<float4*>(a1g + col * C1_P + p0) = make_float4(ov[0], ov[1], ov[2], ov[3]);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        cA = __builtin_amdgcn_mfma_f32_16x16x4f32((float)((wA >> (8 * r)) & 0xff), wf[4 * j + r], cA, 0, 0, 0);
-        cB = __builtin_amdgcn_mfma_f32_16x16x4f32((float)((wB >> (8 * r)) & 0xff), wf[4 * j + r], cB, 0, 0, 0);
+        uint32_t h, m, l;
+        split3(ov[r], h, m, l);
+        const int off = L_R1 + a1_slot(p0 + r, col >> 3) + (col & 7) * 2;
+        *reinterpret_cast<uint16_t*>(lds + off) = (uint16_t)h;
+        *reinterpret_cast<uint16_t*>(lds + off + A1P) = (uint16_t)m;
+        *reinterpret_cast<uint16_t*>(lds + off + 2 * A1P) = (uint16_t)l;
       }
-    }
-    // C rows q*4 + r -> positions tile*16 + q*4 + r, col = oc
-    float4 o = relu_scaled(cA, bias1);
-    int p0 = tA * 16 + q * 4;
-    *reinterpret_cast<float4*>(a1g + col * C1_P + p0) = o;
-    float* d = a1s + col * A1_LD + p0;
-    d[0] = o.x; d[1] = o.y; d[2] = o.z; d[3] = o.w;
-    if (hasB) {
-      o = relu_scaled(cB, bias1);
-      p0 = tB * 16 + q * 4;
-      *reinterpret_cast<float4*>(a1g + col * C1_P + p0) = o;
-      d = a1s + col * A1_LD + p0;
-      d[0] = o.x; d[1] = o.y; d[2] = o.z; d[3] = o.w;
     }
   }
   __syncthreads();
-  // ---- conv2: jobs j = wave, wave + 8 (< 12) -> (m-tile j >> 1, n-tile j & 1)
+  // ---- conv2: wave -> n-tile nt = w & 1 (oc = 16 nt + col), m-tiles w >> 1, (w >> 1) + 4
   {
-    const int jA = wave, jB = wave + 8;
-    const bool hasB = jB < 12;
-    const int mtA = jA >> 1, ntA = jA & 1, mtB = hasB ? jB >> 1 : mtA, ntB = hasB ? jB & 1 : ntA;
-    const int posA = 16 * mtA + col, posB = 16 * mtB + col;   // A row of this lane
-    const bool okA = posA < C2_P, okB = posB < C2_P;
-    const int pcA = okA ? posA : 0, pcB = okB ? posB : 0;
-    const int rowA = (2 * (pcA / 9)) * 20 + 2 * (pcA % 9);
-    const int rowB = (2 * (pcB / 9)) * 20 + 2 * (pcB % 9);
-    const float* w2A = w2k + q * W2_LD + 16 * ntA + col;
-    const float* w2B = w2k + q * W2_LD + 16 * ntB + col;
-    f32x4 cA = {0.f, 0.f, 0.f, 0.f}, cB = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int ks = 0; ks < ((ARL_ABLATE & 2) ? 0 : 64); ++ks) {
-      // k = 4 ks + q = (ic, ky, kx) = (ks >> 2, ks & 3, q)
-      const int aoff = (ks >> 2) * A1_LD + (ks & 3) * 20 + q;
-      const float afA = okA ? a1s[aoff + rowA] : 0.f;
-      const float afB = okB ? a1s[aoff + rowB] : 0.f;
-      cA = __builtin_amdgcn_mfma_f32_16x16x4f32(afA, w2A[4 * ks * W2_LD], cA, 0, 0, 0);
-      cB = __builtin_amdgcn_mfma_f32_16x16x4f32(afB, w2B[4 * ks * W2_LD], cB, 0, 0, 0);
-    }
-    float* a2g = a.a2 + (int64_t)e * A2;
-    {
-      const int oc = 16 * ntA + col;
-      const float b = a.b2[oc];
+    const int nt = wave & 1, oc = 16 * nt + col;
+    bf16x8 w2h[8], w2m[8], w2l[8];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int p = 16 * mtA + q * 4 + r;
-        if (p < C2_P) a2g[oc * C2_P + p] = fmaxf(__fadd_rn(cA[r], b), 0.f);
+    for (int s = 0; s < 8; ++s) {
+      const int off = L_W2 + oc * WROW + (2 * s + (g >> 1)) * 32 + (g & 1) * 16;
+      w2h[s] = lds_load<bf16x8>(lds, off);
+      w2m[s] = lds_load<bf16x8>(lds, off + W2P);
+      w2l[s] = lds_load<bf16x8>(lds, off + 2 * W2P);
+    }
+    const int mA = wave >> 1, mB = mA + 4;
+    const bool hasB = mB < 6;
+    const int posA = 16 * mA + col, posB = 16 * (hasB ? mB : mA) + col;   // A row of this lane
+    const int pcA = posA < C2_P ? posA : 0, pcB = posB < C2_P ? posB : 0;
+    const int oyA = pcA / 9, oxA = pcA - oyA * 9, oyB = pcB / 9, oxB = pcB - oyB * 9;
+    const int PA0 = (2 * oyA) * 20 + 2 * oxA, PB0 = (2 * oyB) * 20 + 2 * oxB;
+    f32x4 bigA = {0.f, 0.f, 0.f, 0.f}, smlA = bigA, bigB = bigA, smlB = bigA;
+#pragma unroll
+    for (int s = 0; s < ((ARL_ABLATE & 2) ? 0 : 8); ++s) {
+      const int tap = 2 * s + (g >> 1), dP = (tap >> 2) * 20 + (tap & 3);
+      const int offA = L_R1 + a1_slot(PA0 + dP, g & 1);
+      const bf16x8 ahA = lds_load<bf16x8>(lds, offA), amA = lds_load<bf16x8>(lds, offA + A1P),
+                   alA = lds_load<bf16x8>(lds, offA + 2 * A1P);
+      mfma_x6(ahA, amA, alA, w2h[s], w2m[s], w2l[s], bigA, smlA);
+      if (hasB) {
+        const int offB = L_R1 + a1_slot(PB0 + dP, g & 1);
+        const bf16x8 ahB = lds_load<bf16x8>(lds, offB), amB = lds_load<bf16x8>(lds, offB + A1P),
+                     alB = lds_load<bf16x8>(lds, offB + 2 * A1P);
+        mfma_x6(ahB, amB, alB, w2h[s], w2m[s], w2l[s], bigB, smlB);
       }
     }
+    float* a2g = a.a2 + (int64_t)e * A2;
+    const float b = a.b2[oc];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int p = 16 * mA + g * 4 + r;
+      if (p < C2_P) a2g[oc * C2_P + p] = fmaxf(__fadd_rn(__fadd_rn(bigA[r], smlA[r]), b), 0.f);
+    }
     if (hasB) {
-      const int oc = 16 * ntB + col;
-      const float b = a.b2[oc];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int p = 16 * mtB + q * 4 + r;
-        if (p < C2_P) a2g[oc * C2_P + p] = fmaxf(__fadd_rn(cB[r], b), 0.f);
+        const int p = 16 * mB + g * 4 + r;
+        if (p < C2_P) a2g[oc * C2_P + p] = fmaxf(__fadd_rn(__fadd_rn(bigB[r], smlB[r]), b), 0.f);
       }
     }
   }
