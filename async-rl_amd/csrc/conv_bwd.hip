@@ -3,24 +3,29 @@
 //   (1) dW2 += da2 (x) im2col(a1)           conv2 weight gradient, K = 81 positions
 //   (2) da1  = conv_transpose(da2, W2) * (a1 > 0)        (stride-2 parity classes)
 //   (3) dW1 += im2col(x)^T (x) da1           conv1 weight gradient, K = 400 positions
-// with a1 / da1, da2, the 4 uint8 screens and W2 resident in LDS (~97 KB,
-// one workgroup per CU): da1 never touches HBM and a1 / da2 / x are read once.
+// with every operand of a sample resident in LDS (140 KB, one 512-thread
+// workgroup per CU): da1 never touches HBM and a1 / da2 / x are read once.
 // The next sample's a1 / da2 / screens are loaded into registers while the
-// current one computes (one wave per SIMD leaves the VGPRs for it).
+// current one computes.
 //
 // Reference: a3c.py:129-130 (total_loss.backward through Chainer's
 // Convolution2D backward: im2col + tensordot for gW, col2im for gx).
 //
-// All contractions are v_mfma_f32_16x16x4_f32 (exact f32 products):
-//   (1) M = 32 oc (2 tiles) x N = 256 (ic,ky,kx) (16 tiles) x K = 81 (21 k-steps,
-//       zero padded): each wave owns n-tiles 4w..4w+3 of both m-tiles (8
-//       independent accumulators);
-//   (2) per parity class (py,px): M = 100 positions (7 tiles) x N = 16 ic x
-//       K = 128 (oc, dy, dx): 28 tile jobs, 7 per wave, two in flight; the
-//       masked result overwrites a1 in place (each element has one producer);
-//   (3) M = 256 k x N = 16 oc x K = 400: wave w owns input channel ic = w; its
-//       4 accumulators are kx = 4 (row & 1) + i for i = 0..3, so one
-//       ds_read_b32 of 4 contiguous pixels feeds all four MFMAs.
+// (1) runs on v_mfma_f32_16x16x4_f32 (exact f32): M = 32 oc x N = 256 (ic,
+//     ky, kx) x K = 81; wave w owns n-tiles 2w, 2w+1 of both m-tiles.
+// (2) and (3) run on the bf16 matrix cores with exact bf16 splits of the f32
+//     operands (bf16split.hpp; f32-accurate):
+// (2) per parity class (py, px): M = 100 positions (7 tiles) x N = 16 ic x
+//     K = 128 ordered (dy, dx, oc): A = da2 split planes stored channel-last
+//     on an 11 x 11 grid with a zero border (so the shifted windows need no
+//     bounds checks), B = W2 fragments of the wave's class held in 48 VGPRs;
+//     6 MFMAs per k-step.  The masked result is written as da1 split planes.
+// (3) the stride-4 im2col is made contiguous by splitting each screen row
+//     into its 4 column phases b = x & 3 (X = x >> 2):
+//       dW1[oc][ic][ky][4a + b] = sum_{oy, X} xph[ic][4 oy + ky][b][X + a] da1[oc][oy][X]
+//     M = 256 (ic, ky, a, b) x N = 16 oc x K = 480 (oy, X padded 20 -> 24);
+//     the A fragment is 8 contiguous pixels shifted by a bytes (v_alignbyte),
+//     exact in bf16, so 3 MFMAs per k-step.  Wave w owns m-tiles 2w, 2w+1.
 // Integer pixel values feed (3) and 1/255 is applied in the reduction.
 // Each block sums a contiguous run of samples and writes one partial slab;
 // reduce_conv_bwd_kernel sums the slabs in f64 in a fixed order.
@@ -28,6 +33,7 @@
 #include <stdint.h>
 
 #include "arl_internal.hpp"
+#include "bf16split.hpp"
 
 #ifndef ARL_ABLATE
 #define ARL_ABLATE 0   // timing experiments only (bits: 8 step 1, 16 step 2, 32 step 3, 64 prefetch loads)
@@ -35,21 +41,37 @@
 
 namespace arl {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
 namespace {
 constexpr int NT = 512;                    // threads per workgroup (8 waves, 2 per SIMD)
-constexpr int A1_LD = 401;                 // a1/da1 LDS row stride (odd: conflict-free oc spread)
+constexpr int A1_LD = 401;                 // a1 f32 LDS row stride (odd: conflict-free oc spread)
 constexpr int SLAB_W2 = C2_OC * 256;       // 8192
 constexpr int SLAB_B2 = SLAB_W2;           // +32
 constexpr int SLAB_W1 = SLAB_B2 + C2_OC;   // 8224: D1^T[k][oc], 4096
 constexpr int SLAB_B1 = SLAB_W1 + 256 * 16;
 constexpr int SLAB = SLAB_B1 + 16;         // 12336 floats per block
-constexpr int XV = 4 * PLANE / 16;         // 1764 uint4 of screens per sample
-constexpr int PX = (XV + NT - 1) / NT;     // 4 per thread
+constexpr int XQ = 4 * 84 * 6;             // screen items per sample: (plane, row, quad of 4 dwords)
+constexpr int PX = (XQ + NT - 1) / NT;     // 4 per thread
 constexpr int PA = (A1 / 4 + NT - 1) / NT; // 4 float4 of a1 per thread
 constexpr int PD = (A2 / 4 + NT - 1) / NT; // 2 float4 of da2 per thread
+// LDS map (bytes)
+constexpr int XR = 24;                     // phase row: X = 0..20 (+ pad), uint8
+constexpr int L_XPH = 0;                   // [ic][y][b][XR]                      32,256
+constexpr int D1_ROW = 48;                 // da1 plane row (oy): 24 bf16, X 20..23 stay 0
+constexpr int D1_OC = 20 * D1_ROW + 16;    // 976 = 61 16-byte slots (odd: oc rows spread over banks)
+constexpr int D1P = 16 * D1_OC;            // 15,616 per plane
+constexpr int L_D1 = L_XPH + 4 * 84 * 4 * XR;   // 32,256: 3 planes, 46,848
+constexpr int D2P = 121 * 64;              // 11 x 11 cells x 32 oc bf16: 7,744 per plane
+constexpr int L_D2 = L_D1 + 3 * D1P;       // 79,104: 3 planes, 23,232
+constexpr int L_A1 = L_D2 + 3 * D2P;       // 102,336: a1 f32 [16][401]
+constexpr int L_D2F = L_A1 + C1_OC * A1_LD * 4;   // 128,000: da2 f32 [32][81]
+constexpr int L_RED = L_D2F + A2 * 4;      // 138,368: f32 [NT]
+constexpr int L_END = L_RED + NT * 4;      // 140,416
+static_assert(L_D1 % 16 == 0 && L_D2 % 16 == 0 && L_A1 % 16 == 0 && L_D2F % 16 == 0, "alignment");
 }  // namespace
+
+// da2 plane byte offset of (cell, oc group g = oc >> 3): slot 4 cell + g, low
+// 2 bits XORed by cell >> 2 so runs of consecutive cells spread over banks
+__device__ inline int d2_slot(int cell, int g) { return (((4 * cell + g) ^ ((cell >> 2) & 3)) << 4); }
 
 struct ConvBwdArgs {
   const uint8_t* frames;
@@ -79,14 +101,20 @@ __device__ inline void prefetch_sample(const ConvBwdArgs& a, int s, Prefetch& r)
   int slot[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) slot[c] = (rs + a.R - 3 + c) % a.R;
-  constexpr int V = PLANE / 16;
+  // screens: item (plane c, row y, quad q) = dwords 4q..4q+3 of the row (q = 5: dword 20 only)
 #pragma unroll
   for (int j = 0; j < PX; ++j) {
     const int i = tid + NT * j;
     uint4 v = make_uint4(0, 0, 0, 0);
-    const int c = i / V, o = i - c * V;
-    if (i < XV && c >= 4 - nv)
-      v = reinterpret_cast<const uint4*>(a.frames + ((int64_t)slot[c] * a.n + e) * PLANE)[o];
+    if (i < XQ) {
+      const int c = i / 504, rem = i - c * 504, y = rem / 6, q = rem - y * 6;
+      if (c >= 4 - nv) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.frames + ((int64_t)slot[c] * a.n + e) * PLANE +
+                                                                y * 84) + 4 * q;
+        if (q < 5) { v.x = src[0]; v.y = src[1]; v.z = src[2]; v.w = src[3]; }
+        else v.x = src[0];
+      }
+    }
     r.x[j] = v;
   }
   const float4* g1 = reinterpret_cast<const float4*>(a.a1 + (int64_t)s * A1);
@@ -103,13 +131,28 @@ __device__ inline void prefetch_sample(const ConvBwdArgs& a, int s, Prefetch& r)
   }
 }
 
-__device__ inline void commit_sample(const Prefetch& r, uint8_t* xs, float* a1s, float* d2s) {
+__device__ inline void commit_sample(const Prefetch& r, uint8_t* lds) {
   const int tid = threadIdx.x;
+  // screens -> phase rows: the 4 dwords (X = 4q..4q+3, bytes b = 0..3) are
+  // transposed so each phase b gets one dword of 4 consecutive X
 #pragma unroll
   for (int j = 0; j < PX; ++j) {
     const int i = tid + NT * j;
-    if (i < XV) reinterpret_cast<uint4*>(xs)[i] = r.x[j];
+    if (i < XQ) {
+      const int c = i / 504, rem = i - c * 504, y = rem / 6, q = rem - y * 6;
+      const uint4 v = r.x[j];
+      const uint32_t lo01 = __builtin_amdgcn_perm(v.y, v.x, 0x05010400u);
+      const uint32_t hi01 = __builtin_amdgcn_perm(v.y, v.x, 0x07030602u);
+      const uint32_t lo23 = __builtin_amdgcn_perm(v.w, v.z, 0x05010400u);
+      const uint32_t hi23 = __builtin_amdgcn_perm(v.w, v.z, 0x07030602u);
+      uint8_t* d = lds + L_XPH + (c * 84 + y) * 4 * XR + 4 * q;
+      *reinterpret_cast<uint32_t*>(d) = __builtin_amdgcn_perm(lo23, lo01, 0x05040100u);
+      *reinterpret_cast<uint32_t*>(d + XR) = __builtin_amdgcn_perm(lo23, lo01, 0x07060302u);
+      *reinterpret_cast<uint32_t*>(d + 2 * XR) = __builtin_amdgcn_perm(hi23, hi01, 0x05040100u);
+      *reinterpret_cast<uint32_t*>(d + 3 * XR) = __builtin_amdgcn_perm(hi23, hi01, 0x07060302u);
+    }
   }
+  float* a1s = reinterpret_cast<float*>(lds + L_A1);
 #pragma unroll
   for (int j = 0; j < PA; ++j) {
     const int i = tid + NT * j;
@@ -119,63 +162,95 @@ __device__ inline void commit_sample(const Prefetch& r, uint8_t* xs, float* a1s,
       d[0] = r.a[j].x; d[1] = r.a[j].y; d[2] = r.a[j].z; d[3] = r.a[j].w;
     }
   }
+  float* d2s = reinterpret_cast<float*>(lds + L_D2F);
 #pragma unroll
   for (int j = 0; j < PD; ++j) {
     const int i = tid + NT * j;
-    if (i < A2 / 4) reinterpret_cast<float4*>(d2s)[i] = r.d[j];
+    if (i < A2 / 4) {
+      reinterpret_cast<float4*>(d2s)[i] = r.d[j];
+      const float dv[4] = {r.d[j].x, r.d[j].y, r.d[j].z, r.d[j].w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int f = 4 * i + t, oc = f / C2_P, p = f - oc * C2_P, oy = p / 9, ox = p - oy * 9;
+        uint32_t h, m, l;
+        split3(dv[t], h, m, l);
+        uint8_t* dd = lds + L_D2 + d2_slot((oy + 1) * 11 + ox + 1, oc >> 3) + (oc & 7) * 2;
+        *reinterpret_cast<uint16_t*>(dd) = (uint16_t)h;
+        *reinterpret_cast<uint16_t*>(dd + D2P) = (uint16_t)m;
+        *reinterpret_cast<uint16_t*>(dd + 2 * D2P) = (uint16_t)l;
+      }
+    }
   }
+}
+
+__device__ inline bf16x8 frag_from_pairs(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3) {
+  bf16x8 f;
+  f[0] = (short)(p0 & 0xffff); f[1] = (short)(p0 >> 16);
+  f[2] = (short)(p1 & 0xffff); f[3] = (short)(p1 >> 16);
+  f[4] = (short)(p2 & 0xffff); f[5] = (short)(p2 >> 16);
+  f[6] = (short)(p3 & 0xffff); f[7] = (short)(p3 >> 16);
+  return f;
 }
 
 __global__ void __launch_bounds__(NT)
 conv_bwd_kernel(ConvBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t xs[4 * PLANE];   // 28,224
-  __shared__ float a1s[C1_OC * A1_LD];                              // 25,664
-  __shared__ __attribute__((aligned(16))) float d2s[A2];            // 10,368
-  __shared__ float w2t[C2_OC * 256];   // 32,768: W2 as [oc][tap = ky*4 + kx][ic]
-  __shared__ float red[NT];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[L_END];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int q = lane >> 4, col = lane & 15;
+  const int g = lane >> 4, col = lane & 15;
+  const float* a1s = reinterpret_cast<const float*>(lds + L_A1);
+  const float* d2s = reinterpret_cast<const float*>(lds + L_D2F);
+  float* red = reinterpret_cast<float*>(lds + L_RED);
 
-  {
-    // thread -> (ic = i & 15, oc / tap chunk = i >> 4): reads W2[oc][ic][tap0..tap0+3]
-    // (strided, L2), writes w2t[oc][tap][ic] with 16 consecutive ic per row
-    float4 wv[4];
+  // zero the da1 / da2 split planes once: their padding (X 20..23, the grid
+  // border) is never written and must read as 0
+  for (int i = tid; i < (3 * D1P + 3 * D2P) / 16; i += NT)
+    reinterpret_cast<uint4*>(lds + L_D1)[i] = make_uint4(0, 0, 0, 0);
+
+  // (2) W2 fragments of this wave's parity class: lane (ic = col, g), k-step
+  // ks = (dy, dx), k = oc = 8 g + j -> W2[oc][ic][py + 2 dy][px + 2 dx]
+  const int cls = wave & 3, py = cls >> 1, px = cls & 1;
+  bf16x8 w2h[4], w2m[4], w2l[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = tid + NT * j;
-      const int ic = i & 15, oc = (i >> 4) >> 2, tq = (i >> 4) & 3;
-      wv[j] = reinterpret_cast<const float4*>(a.W2)[(oc * 16 + ic) * 4 + tq];
-    }
+  for (int ks = 0; ks < 4; ++ks) {
+    const int tap = (py + 2 * (ks >> 1)) * 4 + px + 2 * (ks & 1);
+    float v[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = tid + NT * j;
-      const int ic = i & 15, oc = (i >> 4) >> 2, tq = (i >> 4) & 3;
-      float* d = w2t + (oc * 16 + 4 * tq) * 16 + ic;
-      d[0] = wv[j].x; d[16] = wv[j].y; d[32] = wv[j].z; d[48] = wv[j].w;
-    }
+    for (int j = 0; j < 8; ++j) v[j] = a.W2[((8 * g + j) * 16 + col) * 16 + tap];
+    uint32_t h[4], m[4], l[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) split3_pack(v[2 * j], v[2 * j + 1], h[j], m[j], l[j]);
+    w2h[ks] = frag_from_pairs(h[0], h[1], h[2], h[3]);
+    w2m[ks] = frag_from_pairs(m[0], m[1], m[2], m[3]);
+    w2l[ks] = frag_from_pairs(l[0], l[1], l[2], l[3]);
   }
 
-  f32x4 acc2[2][2], acc1[2];
+  f32x4 acc2[2][2], big3[2], sml3[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     acc2[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
     acc2[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    acc1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    big3[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    sml3[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   float b2sum = 0.f, b1sum = 0.f;
 
-  // (3): wave w owns ic = w >> 1 and kx = 4 (row & 1) + 2 (w & 1) + i, i = 0, 1:
-  // A row `col` reads the 2 contiguous pixels at this offset (+ position)
-  const int ic3 = wave >> 1, h3 = wave & 1;
-  const int xoff3 = ic3 * PLANE + (col >> 1) * 84 + 4 * (col & 1) + 2 * h3;
+  // (3): m-tiles mt = 2 w + i -> ic = mt >> 2, ky = 2 (mt & 3) + (col >> 3),
+  // a = (col >> 2) & 1, b = col & 3; A row base of lane (phase row of oy = 0)
+  int xrow3[2];
+  const int sh3 = (col >> 2) & 1;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int mt = 2 * wave + i, ic = mt >> 2, ky = 2 * (mt & 3) + (col >> 3);
+    xrow3[i] = L_XPH + ((ic * 84 + ky) * 4 + (col & 3)) * XR;
+  }
 
   const int s0 = blockIdx.x * a.spb, s1 = min(a.S, s0 + a.spb);
   Prefetch pf;
   if (s0 < s1) prefetch_sample(a, s0, pf);
   for (int s = s0; s < s1; ++s) {
     __syncthreads();                 // previous sample fully consumed
-    commit_sample(pf, xs, a1s, d2s);
+    commit_sample(pf, lds);
     __syncthreads();
     if (s + 1 < s1) prefetch_sample(a, s + 1, pf);   // in flight during compute
     // ---- (1) conv2 weight gradient + bias; wave w: n-tiles (ic) 2w, 2w+1 x both m-tiles
@@ -190,7 +265,7 @@ conv_bwd_kernel(ConvBwdArgs a) {
       const float* b1 = b0 + A1_LD;
 #pragma unroll 3
       for (int ps = 0; ps < ((ARL_ABLATE & 8) ? 0 : 21); ++ps) {
-        const int p = 4 * ps + q;
+        const int p = 4 * ps + g;
         const bool pv = p < C2_P;
         const int pc = pv ? p : 0;
         const int oy = pc / 9, ox = pc - oy * 9;
@@ -204,88 +279,94 @@ conv_bwd_kernel(ConvBwdArgs a) {
         acc2[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(af1, bf1, acc2[1][1], 0, 0, 0);
       }
     }
-    __syncthreads();   // a1s is overwritten by (2)
-    // ---- (2) da1 = convT(da2, W2) * (a1 > 0), in place; job pairs (w, w+8), (w+16, w+24).
-    // k-step ks, lane quarter q: k = 4 ks + q -> oc = ks, dy = q >> 1, dx = q & 1,
-    // so a lane's operand addresses are affine in ks (stride 81 / 256 floats).
-    {
-      const int dy = q >> 1, dx = q & 1;
-      for (int jobA = wave; jobA < 28; jobA += 16) {
-        const int jobB = jobA + 8;
-        const bool hasB = jobB < 28;
-        const int clsA = jobA / 7, ttA = jobA - clsA * 7;
-        const int clsB = hasB ? jobB / 7 : 0, ttB = hasB ? jobB - clsB * 7 : 0;
-        const int pyA = clsA >> 1, pxA = clsA & 1, pyB = clsB >> 1, pxB = clsB & 1;
-        const int rA = 16 * ttA + col, rB = 16 * ttB + col;
-        const int oyA = rA / 10 - dy, oxA = rA % 10 - dx, oyB = rB / 10 - dy, oxB = rB % 10 - dx;
-        const bool okA = rA < 100 && oyA >= 0 && oxA >= 0 && oyA < 9 && oxA < 9;
-        const bool okB = hasB && rB < 100 && oyB >= 0 && oxB >= 0 && oyB < 9 && oxB < 9;
-        const float* pa = d2s + (okA ? oyA * 9 + oxA : 0);
-        const float* pb = d2s + (okB ? oyB * 9 + oxB : 0);
-        const float* wa = w2t + ((pyA + 2 * dy) * 4 + pxA + 2 * dx) * 16 + col;
-        const float* wb = w2t + ((pyB + 2 * dy) * 4 + pxB + 2 * dx) * 16 + col;
-        f32x4 cA = {0.f, 0.f, 0.f, 0.f}, cB = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-        for (int ks = 0; ks < ((ARL_ABLATE & 16) ? 0 : 32); ++ks) {
-          const float afA = okA ? pa[ks * C2_P] : 0.f;
-          const float afB = okB ? pb[ks * C2_P] : 0.f;
-          cA = __builtin_amdgcn_mfma_f32_16x16x4f32(afA, wa[ks * 256], cA, 0, 0, 0);
-          cB = __builtin_amdgcn_mfma_f32_16x16x4f32(afB, wb[ks * 256], cB, 0, 0, 0);
-        }
+    // ---- (2) da1 = convT(da2, W2) * (a1 > 0) -> da1 split planes.
+    // Wave: class cls, m-tiles (w >> 2) + 2 i, two in flight.
+    for (int mA = wave >> 2; mA < 7; mA += 4) {
+      const int mB = mA + 2;
+      const bool hasB = mB < 7;
+      const int rA = 16 * mA + col, rB = 16 * (hasB ? mB : mA) + col;
+      const int cA = rA < 100 ? (rA / 10 + 1) * 11 + rA % 10 + 1 : 0;   // invalid rows read the zero border
+      const int cB = rB < 100 ? (rB / 10 + 1) * 11 + rB % 10 + 1 : 0;
+      f32x4 bigA = {0.f, 0.f, 0.f, 0.f}, smlA = bigA, bigB = bigA, smlB = bigA;
+#pragma unroll
+      for (int ks = 0; ks < ((ARL_ABLATE & 16) ? 0 : 4); ++ks) {
+        const int dcell = (ks >> 1) * 11 + (ks & 1);
+        const int oA = L_D2 + d2_slot(cA ? cA - dcell : 0, g);
+        const int oB = L_D2 + d2_slot(cB ? cB - dcell : 0, g);
+        const bf16x8 ahA = lds_load<bf16x8>(lds, oA), amA = lds_load<bf16x8>(lds, oA + D2P),
+                     alA = lds_load<bf16x8>(lds, oA + 2 * D2P);
+        const bf16x8 ahB = lds_load<bf16x8>(lds, oB), amB = lds_load<bf16x8>(lds, oB + D2P),
+                     alB = lds_load<bf16x8>(lds, oB + 2 * D2P);
+        mfma_x6(ahA, amA, alA, w2h[ks], w2m[ks], w2l[ks], bigA, smlA);
+        mfma_x6(ahB, amB, alB, w2h[ks], w2m[ks], w2l[ks], bigB, smlB);
+      }
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+        if (pass == 1 && !hasB) break;
+        const f32x4 big = pass ? bigB : bigA, sml = pass ? smlB : smlA;
+        const int mt = pass ? mB : mA;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-          const int posA = 16 * ttA + q * 4 + rr;
-          if (posA < 100) {
-            const int i2 = posA / 10, j2 = posA - i2 * 10;
-            float* d = a1s + col * A1_LD + (2 * i2 + pyA) * 20 + 2 * j2 + pxA;
-            *d = *d > 0.f ? cA[rr] : 0.f;
-          }
-          const int posB = 16 * ttB + q * 4 + rr;
-          if (hasB && posB < 100) {
-            const int i2 = posB / 10, j2 = posB - i2 * 10;
-            float* d = a1s + col * A1_LD + (2 * i2 + pyB) * 20 + 2 * j2 + pxB;
-            *d = *d > 0.f ? cB[rr] : 0.f;
+          const int r = 16 * mt + 4 * g + rr;
+          if (r < 100) {
+            const int y2 = r / 10, x2 = r - y2 * 10;
+            const int oy = 2 * y2 + py, ox = 2 * x2 + px;
+            float v = __fadd_rn(big[rr], sml[rr]);
+            if (!(a1s[col * A1_LD + oy * 20 + ox] > 0.f)) v = 0.f;
+            b1sum = __fadd_rn(b1sum, v);
+            uint32_t h, m, l;
+            split3(v, h, m, l);
+            uint8_t* d = lds + L_D1 + col * D1_OC + oy * D1_ROW + ox * 2;
+            *reinterpret_cast<uint16_t*>(d) = (uint16_t)h;
+            *reinterpret_cast<uint16_t*>(d + D1P) = (uint16_t)m;
+            *reinterpret_cast<uint16_t*>(d + 2 * D1P) = (uint16_t)l;
           }
         }
       }
     }
     __syncthreads();
-    // ---- (3) conv1 weight gradient + bias from da1 (in a1s)
-    {
-      const int oc = tid & 15, ch = tid >> 4;   // 32 chunks of <= 13 positions
-      float t = 0.f;
-      for (int p = ch * 13; p < min(C1_P, ch * 13 + 13); ++p) t = __fadd_rn(t, a1s[oc * A1_LD + p]);
-      b1sum = __fadd_rn(b1sum, t);
-    }
-#pragma unroll 2
-    for (int ps = 0; ps < ((ARL_ABLATE & 32) ? 0 : C1_P / 4); ++ps) {
-      const int p = 4 * ps + q;
-      const int oy = p / 20, ox = p - oy * 20;
-      const uint32_t w2 = *reinterpret_cast<const uint16_t*>(xs + xoff3 + (4 * oy) * 84 + 4 * ox);
-      const float bf = a1s[col * A1_LD + p];
-      acc1[0] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)(w2 & 0xff), bf, acc1[0], 0, 0, 0);
-      acc1[1] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)(w2 >> 8), bf, acc1[1], 0, 0, 0);
+    // ---- (3) conv1 weight gradient: k-step ks, quarter g -> group G = 4 ks + g
+    // = (oy, X0 = 8 c): 8 positions (oy, X0..X0+7)
+#pragma unroll 3
+    for (int ks = 0; ks < ((ARL_ABLATE & 32) ? 0 : 15); ++ks) {
+      const int G = 4 * ks + g, oy = G / 3, c = G - 3 * oy;
+      const int ob = L_D1 + col * D1_OC + oy * D1_ROW + 16 * c;
+      const bf16x8 bh = lds_load<bf16x8>(lds, ob), bm = lds_load<bf16x8>(lds, ob + D1P),
+                   bl = lds_load<bf16x8>(lds, ob + 2 * D1P);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int oa = xrow3[i] + oy * 16 * XR + 8 * c;
+        const uint2 lo = lds_load<uint2>(lds, oa);
+        const uint32_t nx = lds_load<uint32_t>(lds, oa + 8);
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(lo.y, lo.x, sh3);
+        const uint32_t w1 = __builtin_amdgcn_alignbyte(nx, lo.y, sh3);
+        const bf16x8 xa = frag_from_pairs(px_pair_bf16(w0, 0), px_pair_bf16(w0, 1), px_pair_bf16(w1, 0),
+                                          px_pair_bf16(w1, 1));
+        mfma_x3(xa, bh, bm, bl, big3[i], sml3[i]);
+      }
     }
   }
   // ---- partial slab of this block
   float* out = a.slab + (int64_t)blockIdx.x * SLAB;
-  // dW2: C map col = kk within n-tile 2w + jn, rows q*4+r -> oc = 16 mt + q*4 + r
+  // dW2: C map col = kk within n-tile 2w + jn, rows g*4+r -> oc = 16 mt + g*4 + r
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
     for (int jn = 0; jn < 2; ++jn)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        out[(16 * mt + q * 4 + r) * 256 + 16 * (2 * wave + jn) + col] = acc2[mt][jn][r];
-  // dW1^T: accumulator i, C row q*4 + r -> k = (ic3, ky = row >> 1, kx = 4 (row & 1) + 2 h3 + i)
+        out[(16 * mt + g * 4 + r) * 256 + 16 * (2 * wave + jn) + col] = acc2[mt][jn][r];
+  // dW1^T: m-tile 2w + i, C row g*4 + r -> (ky low bit, a, b) = (row >> 3, (row >> 2) & 1, row & 3)
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2; ++i) {
+    const int mt = 2 * wave + i, ic = mt >> 2;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int row = q * 4 + r;
-      const int k = ic3 * 64 + (row >> 1) * 8 + 4 * (row & 1) + 2 * h3 + i;
-      out[SLAB_W1 + k * 16 + col] = acc1[i][r];
+      const int row = g * 4 + r;
+      const int ky = 2 * (mt & 3) + (row >> 3), kx = 4 * ((row >> 2) & 1) + (row & 3);
+      out[SLAB_W1 + (ic * 64 + ky * 8 + kx) * 16 + col] = __fadd_rn(big3[i][r], sml3[i][r]);
     }
+  }
   red[tid] = b2sum;
   __syncthreads();
   if (tid < 32) {
@@ -294,7 +375,7 @@ conv_bwd_kernel(ConvBwdArgs a) {
     out[SLAB_B2 + tid] = t;
   }
   __syncthreads();
-  red[tid] = b1sum;
+  red[tid] = b1sum;   // lane's column = ic = tid & 15
   __syncthreads();
   if (tid < 16) {
     float t = 0.f;
