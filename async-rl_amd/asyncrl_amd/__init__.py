@@ -5,5 +5,5 @@ from ._lib import ARCH_FF, ARCH_LSTM, RESIZE_SCALAR, RESIZE_SIMD, ArlError, LIB_
 from .a3c import A3C, A3CFF, A3CLSTM, A3CModel  # noqa: F401
 from .dqn_phi import current_screen, dqn_phi, max_luminance, phi_stack  # noqa: F401
 from .net import DeviceNet, init_like_torch, param_shapes  # noqa: F401
-from .policy_output import SoftmaxPolicyOutput  # noqa: F401
+from .policy_output import SoftmaxPolicyOutput, fc_softmax_policy_and_v  # noqa: F401
 from .rmsprop_async import GradientClipping, RMSpropAsync  # noqa: F401

@@ -47,14 +47,18 @@ class A3CModel:
         if init_seed is not None:
             self.net.load_params(init_like_torch(self.arch, n_actions, np.random.default_rng(init_seed)))
 
-    def pi_and_v(self, state: torch.Tensor, keep_same_state: bool = False):
+    def pi_and_v(self, state: torch.Tensor, keep_same_state: bool = False, deterministic: bool = False):
         """state: (n, 4, 84, 84) f32 (dqn_phi output).  FF only; the LSTM
-        model's recurrent forward runs inside A3C.act."""
-        self.net.forward_states(state.contiguous())
+        model's recurrent forward runs inside A3C.act.  The policy output is
+        computed eagerly: action_indices holds a Philox draw, or, with
+        deterministic=True, most_probable_actions holds the first argmax
+        (the two eval modes of a3c_ale.py:73-89)."""
+        mode = 2 if deterministic else 1
+        self.net.forward_states(state.contiguous(), mode=mode)
         o = self.net.step_outputs(self.net.t_max)
         n = state.shape[0]
         o = {k: v[:n] for k, v in o.items()}
-        return SoftmaxPolicyOutput(o), o["v"]
+        return SoftmaxPolicyOutput(o, greedy=deterministic), o["v"]
 
     def reset_state(self):
         pass

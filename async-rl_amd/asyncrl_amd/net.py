@@ -120,8 +120,9 @@ class DeviceNet:
         check(lib.arl_observe(self._h, t, ptr(pair_pool), ptr(reward_pool), ptr(done_pool), pool_len,
                               int(force_reset), resize_mode, stream_handle(stream)), "arl_observe")
 
-    def act(self, t: int, stream=None):
-        check(lib.arl_act(self._h, t, stream_handle(stream)), "arl_act")
+    def act(self, t: int, mode: int = 1, stream=None):
+        """mode: 0 forward only, 1 sampled action, 2 greedy (first argmax)."""
+        check(lib.arl_act_mode(self._h, t, mode, stream_handle(stream)), "arl_act_mode")
 
     def learn(self, gamma=0.99, beta=1e-2, v_loss_coef=0.5, clip_reward=True, stream=None):
         check(lib.arl_learn(self._h, gamma, beta, v_loss_coef, int(clip_reward), stream_handle(stream)),
@@ -134,9 +135,9 @@ class DeviceNet:
     def advance(self, stream=None):
         check(lib.arl_advance(self._h, stream_handle(stream)), "arl_advance")
 
-    def forward_states(self, states: torch.Tensor, stream=None):
+    def forward_states(self, states: torch.Tensor, mode: int = 0, stream=None):
         n = states.shape[0]
-        check(lib.arl_forward_states(self._h, ptr(states), n, stream_handle(stream)), "arl_forward_states")
+        check(lib.arl_forward_states(self._h, ptr(states), n, mode, stream_handle(stream)), "arl_forward_states")
 
     # ------------------------------------------------------------ outputs
     def step_outputs(self, t: int) -> dict:

@@ -175,6 +175,13 @@ int arl_act(arl_net* h, int t, void* s) {
   return hip_status(arl::net_act(h->net, t, 1, S(s)), "act");
 }
 
+int arl_act_mode(arl_net* h, int t, int mode, void* s) {
+  NEED_BOUND(h);
+  if (t < 0 || t > h->net.T) return fail(ARL_EINVAL, "act: t out of [0, t_max]");
+  if (mode < 0 || mode > 2) return fail(ARL_EINVAL, "act: mode must be 0 (none), 1 (sample) or 2 (greedy)");
+  return hip_status(arl::net_act(h->net, t, mode, S(s)), "act");
+}
+
 int arl_learn(arl_net* h, double gamma, double beta, double vcoef, int clip_reward, void* s) {
   NEED_BOUND(h);
   return hip_status(arl::net_learn(h->net, gamma, (float)beta, (float)vcoef, clip_reward, S(s)), "learn");
@@ -191,11 +198,12 @@ int arl_advance(arl_net* h, void* s) {
   return hip_status(arl::net_advance(h->net, S(s)), "advance");
 }
 
-int arl_forward_states(arl_net* h, const float* x, int64_t n, void* s) {
+int arl_forward_states(arl_net* h, const float* x, int64_t n, int mode, void* s) {
   NEED_BOUND(h);
+  if (mode < 0 || mode > 2) return fail(ARL_EINVAL, "forward_states: mode must be 0, 1 or 2");
   if (h->net.arch != arl::ARCH_FF) return fail(ARL_ESTATE, "forward_states: FF only (LSTM keeps state)");
   if (!x || n < 1 || n > h->net.N) return fail(ARL_EINVAL, "forward_states: need 1 <= n <= n_envs");
-  return hip_status(arl::net_forward_f32(h->net, x, (int)n, nullptr, nullptr, S(s)), "forward_states");
+  return hip_status(arl::net_forward_f32(h->net, x, (int)n, mode, S(s)), "forward_states");
 }
 
 int arl_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, double alpha, double eps, double clip,
@@ -219,7 +227,9 @@ int arl_policy(const float* hh, int64_t n, const float* Wpi, const float* bpi, c
   if (n < 0 || A < 1 || A > arl::MAXA) return fail(ARL_EINVAL, "policy: bad n / n_actions");
   if (n > 0 && (!hh || !Wpi || !bpi || !Wv || !bv || !logits || !probs || !logp || !v || !ent))
     return fail(ARL_EINVAL, "policy: null pointer");
-  if (sample && (!step_dev || !act || !logp_a)) return fail(ARL_EINVAL, "policy: sampling needs step/act/logp_a");
+  if (sample < 0 || sample > 2) return fail(ARL_EINVAL, "policy: sample must be 0, 1 (Philox draw) or 2 (argmax)");
+  if (sample == 1 && !step_dev) return fail(ARL_EINVAL, "policy: sampling needs the device step counter");
+  if (sample && (!act || !logp_a)) return fail(ARL_EINVAL, "policy: sampling needs act/logp_a");
   if (!aligned(hh, 16) || !aligned(Wpi, 16) || !aligned(Wv, 16)) return fail(ARL_EINVAL, "policy: 16-byte alignment");
   return hip_status(arl::launch_policy(hh, n, Wpi, bpi, Wv, bv, A, seed, step_dev, step_off, env_offset, sample,
                                        logits, probs, logp, v, ent, act, logp_a, S(s)),

@@ -81,12 +81,12 @@ struct Net {
 
 bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_offset, uint64_t seed,
               std::string& err);
-hipError_t net_act(Net& net, int t, int sample, hipStream_t s);
+hipError_t net_act(Net& net, int t, int mode, hipStream_t s);   // mode: 0 none, 1 sample, 2 greedy
 hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s);
 hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
                         float clip, hipStream_t s);
 hipError_t net_advance(Net& net, hipStream_t s);
-hipError_t net_forward_f32(Net& net, const float* x, int n, float* logits, float* v, hipStream_t s);
+hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_t s);
 
 hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int t,
                            const float* W1, const float* b1, const float* W2, const float* b2, float* a1, float* a2,
@@ -107,7 +107,7 @@ hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double
 hipError_t launch_grad_sqnorm(const float* g, int64_t n, double* partials, int blocks, hipStream_t s);
 hipError_t launch_policy(const float* h, int64_t n, const float* Wpi, const float* bpi, const float* Wv,
                          const float* bv, int A, uint64_t seed, const int64_t* ctl, int64_t step_off,
-                         int env_offset, int sample, float* logits, float* probs, float* logp, float* v,
+                         int env_offset, int mode, float* logits, float* probs, float* logp, float* v,
                          float* ent, int32_t* act, float* logp_a, hipStream_t s);
 hipError_t launch_returns(const float* rewards, const uint8_t* dones, const float* v, const float* probs,
                           const float* logp, const int32_t* act, int T, int n, int A, double gamma, float beta,

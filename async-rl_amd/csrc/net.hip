@@ -381,7 +381,7 @@ static hipError_t fc_forward(const Net& net, int n, const float* a2, float* hfc,
                        net.at<int>(net.w_tick), hfc, s);
 }
 
-hipError_t net_act(Net& net, int t, int sample, hipStream_t s) {
+hipError_t net_act(Net& net, int t, int mode, hipStream_t s) {
   const int n = net.N, A = net.A;
   float* a1 = net.at<float>(net.w_a1) + (int64_t)t * n * A1;
   float* a2 = net.at<float>(net.w_a2) + (int64_t)t * n * A2;
@@ -408,7 +408,7 @@ hipError_t net_act(Net& net, int t, int sample, hipStream_t s) {
   }
   const int64_t o = (int64_t)t * n;
   return launch_policy(hpol, n, P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
-                       net.at<int64_t>(net.w_ctl), t, net.env_offset, (sample && t < net.T) ? 1 : 0,
+                       net.at<int64_t>(net.w_ctl), t, net.env_offset, t < net.T ? mode : 0,
                        net.at<float>(net.w_logits) + o * A, net.at<float>(net.w_probs) + o * A,
                        net.at<float>(net.w_logp) + o * A, net.at<float>(net.w_v) + o, net.at<float>(net.w_ent) + o,
                        net.at<int32_t>(net.w_act) + o, net.at<float>(net.w_logpa) + o, s);
@@ -416,7 +416,7 @@ hipError_t net_act(Net& net, int t, int sample, hipStream_t s) {
 
 // Drop-in pi_and_v on explicit f32 states (dqn_phi output), FF only; results
 // land in activation slot T (the bootstrap slot) of the workspace.
-hipError_t net_forward_f32(Net& net, const float* x, int n, float*, float*, hipStream_t s) {
+hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_t s) {
   if (net.arch != ARCH_FF || n > net.N) return hipErrorInvalidValue;
   const int T = net.T, A = net.A, N = net.N;
   float* a1 = net.at<float>(net.w_a1) + (int64_t)T * N * A1;
@@ -432,7 +432,7 @@ hipError_t net_forward_f32(Net& net, const float* x, int n, float*, float*, hipS
   ARL_TRY(fc_forward(net, n, a2, hfc, s));
   const int64_t o = (int64_t)T * N;
   return launch_policy(hfc, n, P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
-                       net.at<int64_t>(net.w_ctl), T, net.env_offset, 0, net.at<float>(net.w_logits) + o * A,
+                       net.at<int64_t>(net.w_ctl), T, net.env_offset, mode, net.at<float>(net.w_logits) + o * A,
                        net.at<float>(net.w_probs) + o * A, net.at<float>(net.w_logp) + o * A,
                        net.at<float>(net.w_v) + o, net.at<float>(net.w_ent) + o, net.at<int32_t>(net.w_act) + o,
                        net.at<float>(net.w_logpa) + o, s);

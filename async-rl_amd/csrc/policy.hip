@@ -7,14 +7,19 @@
 // their log-probs), a3c.py:69-70 (reward clip), a3c.py:82-126 (n-step
 // return, advantage, pi/v/entropy losses).
 //
-// policy_kernel: one 64-lane wave per env row.  Lane l holds h[4l..4l+3]
-// (one 16-byte load); each of the A logits and the value is a 256-long dot
-// product reduced across the wave with xor-shuffles; the softmax, the
-// log-softmax and the entropy are then accumulated serially (k = 0..A-1, in
-// the order NumPy uses for small rows) so the sampler's f32 CDF is
-// reproducible by the CPU oracle.  The draw is inverse-CDF on a counter-based
-// Philox4x32-10 uniform keyed by (seed; env id, step), so sampling needs no
-// RNG state and a captured graph replays with fresh numbers.
+// policy_kernel: one 4-wave workgroup per 16 env rows.  The A logits and the
+// value are one small GEMM on the matrix cores: [16 rows x 256] . [256 x
+// (A + 1)] with v_mfma_f32_16x16x4_f32 (exact f32 products; each lane's h and
+// W fragments are 16-byte loads covering 4 k-steps, k permuted identically on
+// both sides); the 4 waves take one K quarter each and the partial tiles are
+// summed in wave order.  The rows go through LDS to one lane
+// per env, which accumulates the softmax, log-softmax and entropy serially
+// (k = 0..A-1, the order NumPy uses for small rows) so the sampler's f32 CDF
+// is reproducible by the CPU oracle.  The draw is inverse-CDF on a
+// counter-based Philox4x32-10 uniform keyed by (seed; env id, step), so
+// sampling needs no RNG state and a captured graph replays with fresh
+// numbers; mode 2 takes the first argmax instead (most_probable_actions,
+// policy_output.py:37-39).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -35,84 +40,102 @@ __device__ inline uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
   return c;
 }
 
-__device__ inline float wave_sum(float x) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) x = __fadd_rn(x, __shfl_xor(x, o));
-  return x;
-}
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __global__ void __launch_bounds__(256)
 policy_kernel(const float* __restrict__ h, int64_t n, const float* __restrict__ Wpi, const float* __restrict__ bpi,
               const float* __restrict__ Wv, const float* __restrict__ bv, int A, uint32_t seed_lo,
-              uint32_t seed_hi, const int64_t* __restrict__ ctl, int64_t step_off, int env_offset, int sample,
+              uint32_t seed_hi, const int64_t* __restrict__ ctl, int64_t step_off, int env_offset, int mode,
               float* __restrict__ logits, float* __restrict__ probs, float* __restrict__ logp,
               float* __restrict__ v, float* __restrict__ ent, int32_t* __restrict__ act,
               float* __restrict__ logp_a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= n) return;
-  const float4 hv = reinterpret_cast<const float4*>(h + row * HID)[lane];
-  auto dot = [&](const float* w) {
-    const float4 wv = reinterpret_cast<const float4*>(w)[lane];
-    float s = __fmul_rn(hv.x, wv.x);
-    s = __fadd_rn(s, __fmul_rn(hv.y, wv.y));
-    s = __fadd_rn(s, __fmul_rn(hv.z, wv.z));
-    s = __fadd_rn(s, __fmul_rn(hv.w, wv.w));
-    return wave_sum(s);
-  };
-  float z = 0.f;     // lane k < A holds logit k
-  for (int k = 0; k < A; ++k) {
-    const float d = __fadd_rn(dot(Wpi + (int64_t)k * HID), bpi[k]);
-    if (lane == k) z = d;
+  // 4 waves split K = 256 into quarters; partial tiles summed in wave order
+  __shared__ float part[4][16][MAXA + 2];
+  __shared__ float zs[16][MAXA + 2];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  const int64_t row0 = (int64_t)blockIdx.x * 16;
+  const int64_t rowc = min(row0 + col, n - 1);   // A row of this lane (rows past n: any valid row, not stored)
+  f32x4 hv[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) hv[s] = *reinterpret_cast<const f32x4*>(h + rowc * HID + 64 * w + 16 * s + 4 * g);
+  for (int nt = 0; 16 * nt <= A; ++nt) {
+    const int j = 16 * nt + col;   // head column: j < A -> pi logit j, j == A -> value
+    const float* wrow = (j < A ? Wpi + (int64_t)j * HID : Wv) + 64 * w;
+    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      f32x4 wv = {0.f, 0.f, 0.f, 0.f};
+      if (j <= A) wv = *reinterpret_cast<const f32x4*>(wrow + 16 * s + 4 * g);
+      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][0], wv[0], c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][1], wv[1], c1, 0, 0, 0);
+      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][2], wv[2], c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][3], wv[3], c1, 0, 0, 0);
+    }
+    if (j <= A) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[w][4 * g + r][j] = __fadd_rn(c0[r], c1[r]);   // C row 4g + r = env
+    }
   }
-  const float vv = __fadd_rn(dot(Wv), bv[0]);
+  __syncthreads();
+  for (int i = tid; i < 16 * (A + 1); i += 256) {
+    const int r = i / (A + 1), j = i - r * (A + 1);
+    float z = __fadd_rn(__fadd_rn(part[0][r][j], part[1][r][j]), __fadd_rn(part[2][r][j], part[3][r][j]));
+    zs[r][j] = __fadd_rn(z, j < A ? bpi[j] : bv[0]);
+  }
+  __syncthreads();
+  const int64_t row = row0 + tid;
+  if (tid >= 16 || row >= n) return;
+  float* z = zs[tid];
+  float* ez = part[0][tid];   // reused: exp(z - max) per action
   // serial max / sum over k (policy_output.py:41-47; Chainer softmax, log_softmax)
-  float m = __shfl(z, 0);
-  for (int k = 1; k < A; ++k) m = fmaxf(m, __shfl(z, k));
-  const float ez = expf(__fsub_rn(z, m));
+  float m = z[0];
+  for (int k = 1; k < A; ++k) m = fmaxf(m, z[k]);
   float se = 0.f;
-  for (int k = 0; k < A; ++k) se = __fadd_rn(se, __shfl(ez, k));
-  const float p = __fdiv_rn(ez, se);                 // softmax: exp(z-m) / sum
-  const float lz = __fsub_rn(z, __fadd_rn(m, logf(se)));   // log_softmax: z - (m + log sum)
-  float H = 0.f;                                     // entropy: -sum p log p
-  for (int k = 0; k < A; ++k) H = __fadd_rn(H, __fmul_rn(__shfl(p, k), __shfl(lz, k)));
-  H = -H;
-  int a = A - 1;
-  if (sample) {
+  for (int k = 0; k < A; ++k) {
+    ez[k] = expf(__fsub_rn(z[k], m));
+    se = __fadd_rn(se, ez[k]);
+  }
+  const float lse = __fadd_rn(m, logf(se));
+  float u = 2.f;   // > any cdf: no draw
+  if (mode == 1) {
     const int64_t step = ctl[CTL_STEP] + step_off;
     const uint4 r = philox4x32_10(make_uint4((uint32_t)(env_offset + row), (uint32_t)step,
                                              (uint32_t)((uint64_t)step >> 32), 0u), seed_lo, seed_hi);
-    const float u = (float)(r.x >> 8) * 5.9604644775390625e-08f;
-    float cdf = 0.f;
-    bool found = false;
-    for (int k = 0; k < A; ++k) {
-      cdf = __fadd_rn(cdf, __shfl(p, k));
-      if (!found && u < cdf) { a = k; found = true; }
+    u = (float)(r.x >> 8) * 5.9604644775390625e-08f;
+  }
+  float H = 0.f, cdf = 0.f, best = -1.f, la = 0.f;
+  int a = A - 1;
+  bool found = false;
+  for (int k = 0; k < A; ++k) {
+    const float p = __fdiv_rn(ez[k], se);                       // softmax: exp(z-m) / sum
+    const float lz = __fsub_rn(z[k], lse);                      // log_softmax: z - (m + log sum)
+    H = __fadd_rn(H, __fmul_rn(p, lz));                         // entropy: -sum p log p
+    logits[row * A + k] = z[k];
+    probs[row * A + k] = p;
+    logp[row * A + k] = lz;
+    if (mode == 1) {
+      cdf = __fadd_rn(cdf, p);
+      if (!found && u < cdf) { a = k; la = lz; found = true; }
+    } else if (mode == 2 && p > best) {
+      best = p; a = k; la = lz;
     }
   }
-  const float la = __shfl(lz, a);
-  if (lane < A) {
-    logits[row * A + lane] = z;
-    probs[row * A + lane] = p;
-    logp[row * A + lane] = lz;
-  }
-  if (lane == 0) {
-    v[row] = vv;
-    ent[row] = H;
-    if (sample) {
-      act[row] = a;
-      logp_a[row] = la;
-    }
+  if (mode == 1 && !found) la = __fsub_rn(z[A - 1], lse);
+  v[row] = z[A];
+  ent[row] = -H;
+  if (mode) {
+    act[row] = a;
+    logp_a[row] = la;
   }
 }
 
 hipError_t launch_policy(const float* h, int64_t n, const float* Wpi, const float* bpi, const float* Wv,
                          const float* bv, int A, uint64_t seed, const int64_t* ctl, int64_t step_off,
-                         int env_offset, int sample, float* logits, float* probs, float* logp, float* v,
+                         int env_offset, int mode, float* logits, float* probs, float* logp, float* v,
                          float* ent, int32_t* act, float* logp_a, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(policy_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, h, n, Wpi, bpi, Wv, bv, A,
-                     (uint32_t)seed, (uint32_t)(seed >> 32), ctl, step_off, env_offset, sample, logits, probs,
+  hipLaunchKernelGGL(policy_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, s, h, n, Wpi, bpi, Wv, bv, A,
+                     (uint32_t)seed, (uint32_t)(seed >> 32), ctl, step_off, env_offset, mode, logits, probs,
                      logp, v, ent, act, logp_a);
   return hipGetLastError();
 }

@@ -103,6 +103,12 @@ int arl_observe(arl_net* net, int t, const uint8_t* pair_pool, const float* rewa
  * params, LSTM state kept: a3c_ale.py:57-60); it samples nothing. */
 int arl_act(arl_net* net, int t, void* stream);
 
+/* arl_act with an explicit action mode: 0 = forward only (no action), 1 =
+ * sample (as arl_act), 2 = greedy, the first argmax of the probabilities
+ * (SoftmaxPolicyOutput.most_probable_actions, policy_output.py:37-39; the
+ * evaluation policy of a3c_ale.py:73-89 / demo_a3c_ale.py:15-30). */
+int arl_act_mode(arl_net* net, int t, int mode, void* stream);
+
 /* Window update, gradient part (a3c.py:82-130): n-step returns with R = 0 at
  * terminals, advantage / entropy / value loss gradient, backward through
  * heads, [LSTM BPTT], FC, conv2, conv1 -> grads (overwritten). */
@@ -119,8 +125,10 @@ int arl_optimize(arl_net* net, double lr0, int64_t total_steps, int64_t n_total,
 int arl_advance(arl_net* net, void* stream);
 
 /* A3CFF.pi_and_v on explicit f32 states (a3c_ale.py:38-40; input from
- * dqn_phi).  n <= n_envs; outputs in the workspace's bootstrap slot. */
-int arl_forward_states(arl_net* net, const float* states, int64_t n, void* stream);
+ * dqn_phi).  n <= n_envs; outputs in the workspace's bootstrap slot.  mode
+ * as arl_act_mode: 0 no action, 1 sampled (action_indices, Philox counter =
+ * step + t_max), 2 greedy (most_probable_actions). */
+int arl_forward_states(arl_net* net, const float* states, int64_t n, int mode, void* stream);
 
 /* ------------------------------------------------------------------ granular ops */
 
@@ -132,7 +140,9 @@ int arl_rmsprop(float* param, float* ms, const float* grad, int64_t n, double lr
 
 /* SoftmaxPolicyOutput (policy_output.py:32-61) + FCSoftmaxPolicy / FCVFunction
  * heads (policy.py:53-58, v_function.py:29-34) for h: (n, 256) f32.  Samples
- * with Philox(seed; env_offset + row, step) when sample != 0. */
+ * with Philox(seed; env_offset + row, step) when sample == 1 (step = *step_dev +
+ * step_off); sample == 2 takes the first argmax (most_probable_actions);
+ * sample == 0 writes no action. */
 int arl_policy(const float* h, int64_t n, const float* W_pi, const float* b_pi, const float* W_v,
                const float* b_v, int n_actions, uint64_t seed, const int64_t* step_dev, int64_t step_off,
                int env_offset, int sample, float* logits, float* probs, float* log_probs, float* v,

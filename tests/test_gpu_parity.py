@@ -123,6 +123,91 @@ def test_forward_real_checkpoint_matches_oracle(gpu):
     assert close_normscaled(pout.entropy.cpu().numpy(), ent, RTOL)[0]
 
 
+def _heads(rng, A):
+    b = 1.0 / np.sqrt(256)
+    W_pi = rng.uniform(-b, b, (A, 256)).astype(np.float32)
+    b_pi = rng.uniform(-b, b, A).astype(np.float32)
+    W_v = rng.uniform(-b, b, (1, 256)).astype(np.float32)
+    b_v = rng.uniform(-b, b, 1).astype(np.float32)
+    return W_pi, b_pi, W_v, b_v
+
+
+@pytest.mark.parametrize("A", [4, 6, 18, 32])
+def test_policy_heads_and_sampling_match_oracle(gpu, A):
+    """arl_policy: logits / probs / log_probs / v / entropy within RTOL of the
+    oracle, and the sampled actions bit-exact given the same Philox uniforms
+    (oracle.sample_uniforms + inverse CDF over the kernel's own probs)."""
+    from asyncrl_amd import fc_softmax_policy_and_v
+    rng = np.random.default_rng(100 + A)
+    n = 333
+    h = np.maximum(rng.normal(0, 1, (n, 256)), 0).astype(np.float32) * 3
+    W_pi, b_pi, W_v, b_v = _heads(rng, A)
+    step = torch.tensor([41], dtype=torch.int64, device=gpu)
+    pout, v = fc_softmax_policy_and_v(dev(h, gpu), dev(W_pi, gpu), dev(b_pi, gpu), dev(W_v, gpu), dev(b_v, gpu),
+                                      seed=7, step=step, step_offset=2, env_offset=1000, mode=1)
+    lo = h @ W_pi.T + b_pi
+    vo = (h @ W_v.T + b_v)[:, 0]
+    p_o, lp_o = O.softmax(lo), O.log_softmax(lo)
+    for got, want in ((pout.logits, lo), (v, vo), (pout.probs, p_o), (pout.log_probs, lp_o),
+                      (pout.entropy, O.entropy(p_o, lp_o))):
+        ok, err = close_normscaled(got.cpu().numpy(), want, RTOL)
+        assert ok, err
+    probs = pout.probs.cpu().numpy()
+    u = O.sample_uniforms(7, np.arange(1000, 1000 + n), 43)
+    want_a = O.sample_from_uniform(probs, u)
+    got_a = pout.action_indices.cpu().numpy()
+    assert (got_a == want_a).all()
+    lpa = pout.sampled_actions_log_probs.cpu().numpy()
+    assert (lpa == pout.log_probs.cpu().numpy()[np.arange(n), got_a]).all()
+
+
+def test_policy_sampling_frequencies_chi2(gpu):
+    """Distributional parity with np.random.multinomial(1, p)
+    (policy_output.py:12-29): 200k draws of one row (independent Philox
+    streams per env id), chi-square goodness of fit against the probs."""
+    from scipy.stats import chisquare
+    from asyncrl_amd import fc_softmax_policy_and_v
+    rng = np.random.default_rng(5)
+    A, n = 6, 200_000
+    h1 = np.maximum(rng.normal(0, 1, 256), 0).astype(np.float32) * 4
+    W_pi, b_pi, W_v, b_v = _heads(rng, A)
+    h = np.broadcast_to(h1, (n, 256)).copy()
+    step = torch.tensor([3], dtype=torch.int64, device=gpu)
+    pout, _ = fc_softmax_policy_and_v(dev(h, gpu), dev(W_pi, gpu), dev(b_pi, gpu), dev(W_v, gpu), dev(b_v, gpu),
+                                      seed=11, step=step, mode=1)
+    p = pout.probs[0].double().cpu().numpy()
+    counts = np.bincount(pout.action_indices.cpu().numpy(), minlength=A)
+    assert counts.sum() == n
+    stat, pval = chisquare(counts, p / p.sum() * n)
+    assert pval > 1e-4, (counts, p * n, pval)
+
+
+def test_policy_greedy_most_probable_actions(gpu):
+    """mode 2 = SoftmaxPolicyOutput.most_probable_actions (policy_output.py:37-39):
+    the first argmax of the kernel's probs, through pi_and_v(deterministic=True)
+    and through the standalone heads."""
+    from asyncrl_amd import A3CFF, dqn_phi, fc_softmax_policy_and_v
+    ck = load_checkpoint()
+    n = 40
+    model = A3CFF(4, n_envs=n, t_max=5, init_seed=None)
+    model.net.load_params(ck)
+    stacks = np.random.default_rng(21).integers(0, 256, (n, 4, 84, 84), dtype=np.uint8)
+    pout, _ = model.pi_and_v(dqn_phi(dev(stacks, gpu)), deterministic=True)
+    probs = pout.probs.cpu().numpy()
+    assert (pout.most_probable_actions.cpu().numpy() == probs.argmax(1)).all()
+    with pytest.raises(RuntimeError):
+        pout.action_indices
+    rng = np.random.default_rng(9)
+    h = np.maximum(rng.normal(0, 1, (64, 256)), 0).astype(np.float32)
+    W_pi, b_pi, W_v, b_v = _heads(rng, 7)
+    W_pi[3] = W_pi[5]   # exact ties: the first index wins, as np.argmax
+    b_pi[3] = b_pi[5]
+    pout, _ = fc_softmax_policy_and_v(dev(h, gpu), dev(W_pi, gpu), dev(b_pi, gpu), dev(W_v, gpu), dev(b_v, gpu),
+                                      mode=2)
+    pr = pout.probs.cpu().numpy()
+    assert (pout.most_probable_actions.cpu().numpy() == pr.argmax(1)).all()
+
+
 # ------------------------------------------------------------------ full windows
 def _grads_match(net, g_oracle, rtol=RTOL):
     got = net.state_dict(net.grads)
