@@ -53,6 +53,7 @@ SIGNATURES = {
     "arl_observe": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int, c_void_p]),
     "arl_act": (c_int, [c_void_p, c_int, c_void_p]),
     "arl_act_mode": (c_int, [c_void_p, c_int, c_int, c_void_p]),
+    "arl_run_stage": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "arl_learn": (c_int, [c_void_p, c_double, c_double, c_double, c_int, c_void_p]),
     "arl_optimize": (c_int, [c_void_p, c_double, c_i64, c_i64, c_double, c_double, c_double, c_void_p]),
     "arl_advance": (c_int, [c_void_p, c_void_p]),

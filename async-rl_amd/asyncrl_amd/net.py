@@ -124,6 +124,12 @@ class DeviceNet:
         """mode: 0 forward only, 1 sampled action, 2 greedy (first argmax)."""
         check(lib.arl_act_mode(self._h, t, mode, stream_handle(stream)), "arl_act_mode")
 
+    STAGES = {"conv_fwd": 1, "fc_fwd": 2, "policy": 3, "fc_bwd": 4, "conv_bwd": 5}
+
+    def run_stage(self, stage: str, t: int = 0, stream=None):
+        """One window stage alone on the current workspace (timing / profiling)."""
+        check(lib.arl_run_stage(self._h, self.STAGES[stage], t, stream_handle(stream)), "arl_run_stage")
+
     def learn(self, gamma=0.99, beta=1e-2, v_loss_coef=0.5, clip_reward=True, stream=None):
         check(lib.arl_learn(self._h, gamma, beta, v_loss_coef, int(clip_reward), stream_handle(stream)),
               "arl_learn")

@@ -182,6 +182,13 @@ int arl_act_mode(arl_net* h, int t, int mode, void* s) {
   return hip_status(arl::net_act(h->net, t, mode, S(s)), "act");
 }
 
+int arl_run_stage(arl_net* h, int stage, int t, void* s) {
+  NEED_BOUND(h);
+  if (stage < ARL_STAGE_CONV_FWD || stage > ARL_STAGE_CONV_BWD) return fail(ARL_EINVAL, "run_stage: unknown stage");
+  if (t < 0 || t > h->net.T) return fail(ARL_EINVAL, "run_stage: t out of [0, t_max]");
+  return hip_status(arl::net_stage(h->net, stage, t, S(s)), "run_stage");
+}
+
 int arl_learn(arl_net* h, double gamma, double beta, double vcoef, int clip_reward, void* s) {
   NEED_BOUND(h);
   return hip_status(arl::net_learn(h->net, gamma, (float)beta, (float)vcoef, clip_reward, S(s)), "learn");

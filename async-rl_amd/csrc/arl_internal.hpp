@@ -86,6 +86,8 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
 hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
                         float clip, hipStream_t s);
 hipError_t net_advance(Net& net, hipStream_t s);
+enum Stage { STAGE_CONV_FWD = 1, STAGE_FC_FWD = 2, STAGE_POLICY = 3, STAGE_FC_BWD = 4, STAGE_CONV_BWD = 5 };
+hipError_t net_stage(Net& net, int stage, int t, hipStream_t s);
 hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_t s);
 
 hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int t,
@@ -93,7 +95,7 @@ hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const i
                            hipStream_t s);
 hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int S,
                            const float* a1, const float* da2, const float* W2, float* slab, float* gW2, float* gb2,
-                           float* gW1, float* gb1, hipStream_t s);
+                           float* gW1, float* gb1, hipStream_t s, bool reduce = true);
 int64_t conv_bwd_slab_floats(int S);
 
 constexpr int FC_SPLIT = 8;   // fc forward split-K (one slice per XCD)

@@ -412,7 +412,7 @@ int64_t conv_bwd_slab_floats(int S) { return (int64_t)conv_bwd_blocks(S) * SLAB;
 
 hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int S,
                            const float* a1, const float* da2, const float* W2, float* slab, float* gW2, float* gb2,
-                           float* gW1, float* gb1, hipStream_t s) {
+                           float* gW1, float* gb1, hipStream_t s, bool reduce) {
   if (S <= 0) return hipSuccess;
   const int G0 = conv_bwd_blocks(S);
   const int spb = (S + G0 - 1) / G0;
@@ -420,7 +420,7 @@ hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const i
   ConvBwdArgs a{frames, nvalid, ctl, n, R, a1, da2, W2, S, spb, slab};
   hipLaunchKernelGGL(conv_bwd_kernel, dim3(G), dim3(NT), 0, s, a);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess || !reduce) return e;
   hipLaunchKernelGGL(reduce_conv_bwd_kernel, dim3((SLAB + 15) / 16), dim3(256), 0, s, slab, G, gW2, gb2, gW1, gb1);
   return hipGetLastError();
 }

@@ -512,6 +512,51 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
                          G + net.o_c1b, s);
 }
 
+// One stage of a window on the current workspace contents (arl_run_stage):
+// the same launches the window makes, isolated for timing.
+hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
+  const int n = net.N, S = net.T * n;
+  const float* P = net.p;
+  float* G = net.g;
+  float* slab = net.at<float>(net.w_slab);
+  float* a2 = net.at<float>(net.w_a2);
+  float* hfc = net.at<float>(net.w_hfc);
+  switch (stage) {
+    case STAGE_CONV_FWD:
+      return launch_conv_fwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
+                             net.at<int64_t>(net.w_ctl), n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W,
+                             P + net.o_c2b, net.at<float>(net.w_a1) + (int64_t)t * n * A1, a2 + (int64_t)t * n * A2,
+                             s);
+    case STAGE_FC_FWD:
+      return fc_forward(net, n, a2 + (int64_t)t * n * A2, hfc + (int64_t)t * n * HID, s);
+    case STAGE_POLICY: {
+      const int64_t o = (int64_t)t * n;
+      const float* h = net.arch == ARCH_LSTM ? net.at<float>(net.w_hbuf) + (o + n) * HID : hfc + o * HID;
+      const int A = net.A;
+      return launch_policy(h, n, P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
+                           net.at<int64_t>(net.w_ctl), t, net.env_offset, 0, net.at<float>(net.w_logits) + o * A,
+                           net.at<float>(net.w_probs) + o * A, net.at<float>(net.w_logp) + o * A,
+                           net.at<float>(net.w_v) + o, net.at<float>(net.w_ent) + o, nullptr, nullptr, s);
+    }
+    case STAGE_FC_BWD: {
+      const Plans pl = make_plans(net);
+      const float* dfc = net.at<float>(net.w_dfc);
+      ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GM, GM>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab, HID, A2 + 1},
+                                                     HID, A2 + 1, S, pl.fc_w, s)));
+      ARL_TRY(launch_reduce_grad(slab, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s));
+      return launch_gemm<64, 64, 32, 2, 2, GK, GM>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2},
+                                                   EpiMask{net.at<float>(net.w_da2), a2, A2}, S, A2, HID, 1, s);
+    }
+    case STAGE_CONV_BWD:
+      return launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
+                             net.at<int64_t>(net.w_ctl), n, net.R, S, net.at<float>(net.w_a1),
+                             net.at<float>(net.w_da2), P + net.o_c2W, slab, G + net.o_c2W, G + net.o_c2b,
+                             G + net.o_c1W, G + net.o_c1b, s, /*reduce=*/false);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
 hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
                         float clip, hipStream_t s) {
   double* parts = net.at<double>(net.w_norm);

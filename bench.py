@@ -34,6 +34,11 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 F32_MFMA_PEAK_TFS = 157.3      # dense fp32 matrix peak (spec)
 PHI_BYTES_PER_ENV_STEP = 201600 + 7056      # pair read + plane write (ring)
 RMSPROP_BYTES_PER_PARAM = 20                # r p,g,ms; w p,ms
+# algorithmic FLOPs (2 per MAC) per env / per sample, NIPS head
+CONV_FWD_FLOP_PER_ENV = 2 * (400 * 16 * 256 + 81 * 32 * 256)             # 4,603,904
+FC_FWD_FLOP_PER_ENV = 2 * 2592 * 256                                     # 1,327,104
+CONV_BWD_FLOP_PER_SAMPLE = 2 * (32 * 256 * 81 + 81 * 32 * 256 + 400 * 16 * 256)   # dW2 + convT + dW1
+HID_BYTES = 256 * 4
 
 
 def parse():
@@ -146,45 +151,73 @@ def main():
     finite = bool(torch.isfinite(model.net.params).all())
 
     # ---------------------------------------------------------------- per-kernel roofline
-    # phi (arl_observe) on the same stream and buffers, HIP events around
-    # kernel-reps back-to-back launches -> average launch duration.
-    roof = None
+    # Every stage of the window is re-launched alone on the same stream and
+    # workspace, kernel-reps times back to back between two HIP events (on
+    # that stream) -> average launch duration.  Algorithmic work per launch
+    # (SURVEY 8(d)); the dominant stage (us x launches per window)
+    # is the "roofline" kernel, the rest are listed under "kernels".
+    roof, kernels = None, None
     if rank == 0:
-        with torch.cuda.stream(stream):
+        net = model.net
+        S = N * T
+
+        def timed(fn):
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            for t in range(3):
-                model.net.observe(1 + t % T, pairs, rewards, dones, P, stream=stream)
+            for i in range(3):
+                fn(i)
             ev0.record(stream)
             for i in range(a.kernel_reps):
-                model.net.observe(1 + i % T, pairs, rewards, dones, P, stream=stream)
+                fn(i)
             ev1.record(stream)
             ev1.synchronize()
-            phi_us = 1e3 * ev0.elapsed_time(ev1) / a.kernel_reps
-            ev0.record(stream)
-            for i in range(a.kernel_reps):
-                model.net.optimize(lr0=1e-12, clip=0.0, stream=stream)
-            ev1.record(stream)
-            ev1.synchronize()
-            rms_us = 1e3 * ev0.elapsed_time(ev1) / a.kernel_reps
-        phi_bytes = N * PHI_BYTES_PER_ENV_STEP
-        phi_gbs = phi_bytes / (phi_us * 1e-6) / 1e9
-        rms_bytes = model.net.n_params * RMSPROP_BYTES_PER_PARAM
+            return 1e3 * ev0.elapsed_time(ev1) / a.kernel_reps
+
+        specs = [  # name, kernel, launch fn, launches per window, bound, algorithmic work per launch
+            ("phi", "phi_ring_kernel",
+             lambda i: net.observe(1 + i % T, pairs, rewards, dones, P, stream=stream), T + 1, "hbm",
+             N * PHI_BYTES_PER_ENV_STEP),
+            ("conv_fwd", "conv_fwd_kernel", lambda i: net.run_stage("conv_fwd", i % T, stream=stream), T + 1,
+             "mfma", N * CONV_FWD_FLOP_PER_ENV),
+            ("fc_fwd", "fc_fwd_kernel", lambda i: net.run_stage("fc_fwd", i % T, stream=stream), T + 1, "mfma",
+             N * FC_FWD_FLOP_PER_ENV),
+            ("policy", "policy_kernel", lambda i: net.run_stage("policy", i % T, stream=stream), T + 1, "hbm",
+             N * (HID_BYTES + 12 * A + 12)),
+            ("fc_bwd", "gemm_kernel x2 + reduce_grad_kernel", lambda i: net.run_stage("fc_bwd", 0, stream=stream),
+             1, "mfma", 2 * FC_FWD_FLOP_PER_ENV * S),
+            ("conv_bwd", "conv_bwd_kernel", lambda i: net.run_stage("conv_bwd", 0, stream=stream), 1, "mfma",
+             S * CONV_BWD_FLOP_PER_SAMPLE),
+            ("rmsprop", "rmsprop_kernel", lambda i: net.optimize(lr0=1e-12, clip=0.0, stream=stream), 1, "hbm",
+             net.n_params * RMSPROP_BYTES_PER_PARAM),
+        ]
+        kernels = {}
+        with torch.cuda.stream(stream):
+            for name, kname, fn, calls, bound, work in specs:
+                us = timed(fn)
+                if bound == "hbm":
+                    ach, peak, unit = work / (us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s"
+                else:
+                    ach, peak, unit = work / (us * 1e-6) / 1e12, F32_MFMA_PEAK_TFS, "TFLOP/s"
+                kernels[name] = {"kernel": kname, "bound": bound, "avg_launch_us": round(us, 2),
+                                 "launches_per_window": calls, "window_share_us": round(us * calls, 1),
+                                 "achieved": round(ach, 2), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
+                                 ("bytes" if bound == "hbm" else "flop") + "_per_launch": int(work)}
+        dom = max((k for k in kernels if k not in ("fc_bwd",)), key=lambda k: kernels[k]["window_share_us"])
+        d = kernels[dom]
         traffic = None
         tf = os.path.join(ROOT, "profiles", "traffic_r01.json")
         if os.path.exists(tf):
             try:
                 with open(tf) as f:
                     tj = json.load(f)
-                if tj.get("envs") == N:
-                    traffic = tj.get("phi_ring_kernel_bytes_per_launch")
+                if tj.get("envs") == N and tj.get("t_max") == T and tj.get("arch") == arch:
+                    traffic = tj.get("kernels", {}).get(d["kernel"])
             except Exception:
                 traffic = None
-        roof = {"bound": "hbm", "kernel": "phi_ring_kernel (arl_observe)", "achieved": round(phi_gbs, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(phi_gbs / HBM_PEAK_GBS, 4),
-                "traffic": traffic, "bytes_per_launch": phi_bytes, "avg_launch_us": round(phi_us, 2),
-                "rmsprop": {"achieved": round(rms_bytes / (rms_us * 1e-6) / 1e9, 1), "unit": "GB/s",
-                            "avg_launch_us": round(rms_us, 2), "bytes_per_launch": rms_bytes,
-                            "note": "sqnorm disabled (clip=0) in this isolated timing"}}
+        roof = {"bound": d["bound"], "kernel": d["kernel"], "achieved": d["achieved"], "peak": d["peak"],
+                "unit": d["unit"], "frac": d["frac"], "traffic": traffic, "avg_launch_us": d["avg_launch_us"],
+                "work_per_launch": d.get("flop_per_launch", d.get("bytes_per_launch")),
+                "peak_note": ("f32-equivalent FLOP/s vs the dense fp32 matrix peak (bf16-split f32 emulation, "
+                              "DESIGN.md)" if d["bound"] == "mfma" else "HBM3E spec peak")}
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
@@ -204,7 +237,7 @@ def main():
                        "envs_per_gpu": N, "global_envs": N * world, "t_max": T, "n_actions": A, "arch": arch,
                        "graph": use_graph, "parallelism": "dp%d" % world,
                        "units_per_step": N * T * world},
-            "roofline": roof, "cpu_baseline": cpu, "params_finite": finite,
+            "roofline": roof, "kernels": kernels, "cpu_baseline": cpu, "params_finite": finite,
         }
         print(json.dumps(out))
     if world > 1:

@@ -121,6 +121,18 @@ int arl_learn(arl_net* net, double gamma, double beta, double v_loss_coef, int c
 int arl_optimize(arl_net* net, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
                  double clip, void* stream);
 
+/* One stage of a window, run alone on the current workspace contents (the
+ * same launches arl_act / arl_learn make), for per-kernel timing and
+ * profiling.  t selects the window step for the forward stages. */
+enum {
+  ARL_STAGE_CONV_FWD = 1,   /* fused conv1 + conv2 forward from the frame ring */
+  ARL_STAGE_FC_FWD = 2,     /* Linear(2592, 256) + relu, in-launch split-K reduce */
+  ARL_STAGE_POLICY = 3,     /* pi / v heads + softmax policy output (no action) */
+  ARL_STAGE_FC_BWD = 4,     /* FC dW / db and da2 GEMMs */
+  ARL_STAGE_CONV_BWD = 5    /* fused conv backward (conv2 dW, convT, conv1 dW) into per-block slabs */
+};
+int arl_run_stage(arl_net* net, int stage, int t, void* stream);
+
 /* End of window: advance step counters, carry reset flags / LSTM state. */
 int arl_advance(arl_net* net, void* stream);
 
