@@ -39,6 +39,10 @@ CONV_FWD_FLOP_PER_ENV = 2 * (400 * 16 * 256 + 81 * 32 * 256)             # 4,603
 FC_FWD_FLOP_PER_ENV = 2 * 2592 * 256                                     # 1,327,104
 CONV_BWD_FLOP_PER_SAMPLE = 2 * (32 * 256 * 81 + 81 * 32 * 256 + 400 * 16 * 256)   # dW2 + convT + dW1
 HID_BYTES = 256 * 4
+PHI_STACK_BYTES_PER_PAIR = 201600 + 3 * 7056 + 4 * 7056   # pair + 3 prior planes + 4-plane stack
+
+# BASELINE.json configs[1..4] -> (arch, envs per GPU, actions)
+WORKLOADS = {"c2": ("ff", 256, 4), "c3": ("lstm", 1024, 6), "c4": ("ff", 512, 4), "c5": ("phi", 16384, 0)}
 
 
 def parse():
@@ -46,9 +50,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--envs-per-gpu", type=int, default=256)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2",
+                    help="BASELINE.json configs: c2 FF 256 envs (default, the metric's config), c3 LSTM 1024 envs "
+                         "A=6, c4 FF 512 envs per GPU (4096 over 8), c5 phi stress 16384 frame pairs")
+    ap.add_argument("--envs-per-gpu", type=int, default=0, help="0: the workload's")
     ap.add_argument("--t-max", type=int, default=5)
-    ap.add_argument("--arch", choices=["ff", "lstm"], default="ff")
+    ap.add_argument("--arch", choices=["ff", "lstm"], default=None, help="default: the workload's")
     ap.add_argument("--actions", type=int, default=0, help="0: 4 for ff (Breakout), 6 for lstm (Space Invaders)")
     ap.add_argument("--pool", type=int, default=8)
     ap.add_argument("--no-graph", action="store_true")
@@ -80,13 +87,85 @@ def synth_pools(n, pool, seed, dev):
     return pairs, torch.from_numpy(rewards).to(dev), torch.from_numpy(dones).to(dev)
 
 
+def bench_phi(a, world, rank, dev, n_default):
+    """configs[4] (c5): dqn_phi preprocessing stress -- one step = one batch of
+    n frame pairs 210x160 RGB -> max -> luminance -> 84x84 -> 4-plane stack
+    (arl_phi_stack, materialised), ping-pong stacks, reset flags from rng(3).
+    Units = frame pairs (= env-steps of the phi stage)."""
+    from asyncrl_amd.dqn_phi import phi_stack
+    n = a.envs_per_gpu or n_default
+    g = torch.Generator(device=dev)
+    g.manual_seed(1 + 1000 * rank)
+    pairs = torch.randint(0, 256, (n, 2, 210, 160, 3), dtype=torch.uint8, device=dev, generator=g)
+    stacks = [torch.zeros((n, 4, 84, 84), dtype=torch.uint8, device=dev) for _ in range(2)]
+    reset = torch.from_numpy((np.random.default_rng(3 + 1000 * rank).random(n) < 1 / 500).astype(np.uint8)).to(dev)
+    stream = torch.cuda.Stream(device=dev)
+    stream.wait_stream(torch.cuda.current_stream())
+    it = [0]
+
+    def step():
+        i = it[0]
+        phi_stack(pairs, stacks[i & 1], reset, out=stacks[(i + 1) & 1], stream=stream)
+        it[0] = i + 1
+
+    with torch.cuda.stream(stream):
+        for _ in range(a.warmup):
+            step()
+    stream.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        ev0.record(stream)
+        for _ in range(a.steps):
+            step()
+        ev1.record(stream)
+    stream.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    us = 1e3 * ev0.elapsed_time(ev1) / a.steps
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        work = n * PHI_STACK_BYTES_PER_PAIR
+        ach = work / (us * 1e-6) / 1e9
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "traffic_r01_c5.json")
+        if os.path.exists(tf):
+            with open(tf) as f:
+                traffic = json.load(f).get("kernels", {}).get("phi_stack_kernel")
+        out = {"metric": "env-steps/sec (phi+forward+sample+update) at 1/2/4/8 MI355X; % roofline",
+               "value": round(n * world * a.steps / elapsed, 1), "unit": "frame pairs/s (phi stage only)",
+               "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+               "ms_per_step": round(1e3 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "u8", "data": "synthetic uniform RGB 210x160 frame pairs",
+               "config": {"workload": "c5: dqn_phi stress, %d frame pairs/batch 210x160 RGB -> 84x84x4 uint8" % n,
+                          "pairs_per_gpu": n, "parallelism": "dp%d" % world},
+               "roofline": {"bound": "hbm", "kernel": "phi_stack_kernel", "achieved": round(ach, 1),
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                            "traffic": traffic, "avg_launch_us": round(us, 2), "work_per_launch": work},
+               "cpu_baseline": None}
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
     world, rank, local = init_dist()
     dev = torch.device("cuda", local)
-    arch = a.arch
-    A = a.actions or (4 if arch == "ff" else 6)
-    N, T = a.envs_per_gpu, a.t_max
+    w_arch, w_envs, w_A = WORKLOADS[a.workload]
+    if w_arch == "phi":
+        return bench_phi(a, world, rank, dev, w_envs)
+    arch = a.arch or w_arch
+    A = a.actions or (w_A if arch == w_arch else (4 if arch == "ff" else 6))
+    N, T = a.envs_per_gpu or w_envs, a.t_max
     Model = A3CFF if arch == "ff" else A3CLSTM
     model = Model(A, n_envs=N, t_max=T, seed=1234, env_offset=rank * N, init_seed=0, device=dev)
     opt = RMSpropAsync(lr=7e-4, eps=1e-1, alpha=0.99).setup(model)
@@ -204,15 +283,12 @@ def main():
         dom = max((k for k in kernels if k not in ("fc_bwd",)), key=lambda k: kernels[k]["window_share_us"])
         d = kernels[dom]
         traffic = None
-        tf = os.path.join(ROOT, "profiles", "traffic_r01.json")
-        if os.path.exists(tf):
-            try:
-                with open(tf) as f:
-                    tj = json.load(f)
-                if tj.get("envs") == N and tj.get("t_max") == T and tj.get("arch") == arch:
-                    traffic = tj.get("kernels", {}).get(d["kernel"])
-            except Exception:
-                traffic = None
+        import glob
+        for tf in sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json"))):
+            with open(tf) as f:
+                tj = json.load(f)
+            if tj.get("envs") == N and tj.get("t_max") == T and tj.get("arch") == arch:
+                traffic = tj.get("kernels", {}).get(d["kernel"], traffic)
         roof = {"bound": d["bound"], "kernel": d["kernel"], "achieved": d["achieved"], "peak": d["peak"],
                 "unit": d["unit"], "frac": d["frac"], "traffic": traffic, "avg_launch_us": d["avg_launch_us"],
                 "work_per_launch": d.get("flop_per_launch", d.get("bytes_per_launch")),
@@ -220,7 +296,7 @@ def main():
                               "DESIGN.md)" if d["bound"] == "mfma" else "HBM3E spec peak")}
 
     cpu = None
-    if rank == 0 and world == 1 and a.cpu_seconds > 0:
+    if rank == 0 and world == 1 and a.cpu_seconds > 0 and arch == "ff":
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import cpu_baseline  # noqa: E402  (oracle/, CPU baseline leg only)
         cpu = cpu_baseline.run(seconds=a.cpu_seconds, t_max=T, n_actions=4)
@@ -232,8 +308,8 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (uniform RGB 210x160 frame pairs, rewards P(!=0)=0.05, terminals p=1/500)",
-            "config": {"workload": ("A3C %s NIPS-DQN head, %d envs x t_max=%d per GPU (phi + conv head + sampling "
-                                    "+ n-step returns + backward + clip + RMSProp)") % (arch.upper(), N, T),
+            "config": {"workload": ("%s: A3C %s NIPS-DQN head, %d envs x t_max=%d per GPU (phi + conv head + sampling "
+                                    "+ n-step returns + backward + clip + RMSProp)") % (a.workload, arch.upper(), N, T),
                        "envs_per_gpu": N, "global_envs": N * world, "t_max": T, "n_actions": A, "arch": arch,
                        "graph": use_graph, "parallelism": "dp%d" % world,
                        "units_per_step": N * T * world},
