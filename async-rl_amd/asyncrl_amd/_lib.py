@@ -75,6 +75,7 @@ for _name, (_res, _args) in SIGNATURES.items():
 
 ARCH_FF = 0
 ARCH_LSTM = 1
+ARCH_FF_NATURE = 2   # A3CFF with NatureDQNHead (dqn_head.py:6-28)
 RESIZE_SCALAR = 0
 RESIZE_SIMD = 1
 

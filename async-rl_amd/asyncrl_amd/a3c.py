@@ -28,7 +28,7 @@ import os
 import numpy as np
 import torch
 
-from ._lib import ARCH_FF, ARCH_LSTM, RESIZE_SCALAR
+from ._lib import ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, RESIZE_SCALAR
 from .distributed import allreduce_grads, world_info
 from .net import DeviceNet, init_like_torch
 from .policy_output import SoftmaxPolicyOutput
@@ -73,6 +73,14 @@ class A3CModel:
 class A3CFF(A3CModel):
     """a3c_ale.py:28-40: NIPSDQNHead -> FCSoftmaxPolicy + FCVFunction."""
     arch = ARCH_FF
+
+
+class A3CFFNature(A3CModel):
+    """A3CFF (a3c_ale.py:28-40) with dqn_head.NatureDQNHead (dqn_head.py:6-28:
+    conv 4->32 k8 s4, 32->64 k4 s2, 64->64 k3 s1, Linear 3136->512) and
+    FCSoftmaxPolicy(512, A) / FCVFunction(512).  Parameters keep the Chainer
+    link paths: 0/0..0/3 (head), 1/0 (policy), 2/0 (value)."""
+    arch = ARCH_FF_NATURE
 
 
 class A3CLSTM(A3CModel):

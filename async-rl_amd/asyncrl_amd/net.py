@@ -14,12 +14,17 @@ import ctypes
 import numpy as np
 import torch
 
-from ._lib import ARCH_FF, ARCH_LSTM, RESIZE_SCALAR, check, lib, ptr, stream_handle
+from ._lib import ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, RESIZE_SCALAR, check, lib, ptr, stream_handle
 
 
 def param_shapes(arch: int, n_actions: int):
     """Chainer parameter shapes in link order (dqn_head.py:40-44,
-    policy.py:49, v_function.py:25, Chainer L.LSTM upward/lateral)."""
+    policy.py:49, v_function.py:25, Chainer L.LSTM upward/lateral; the
+    Nature head dqn_head.py:16-20 with 512-wide policy / value heads)."""
+    if arch == ARCH_FF_NATURE:
+        return [("0/0/W", (32, 4, 8, 8)), ("0/0/b", (32,)), ("0/1/W", (64, 32, 4, 4)), ("0/1/b", (64,)),
+                ("0/2/W", (64, 64, 3, 3)), ("0/2/b", (64,)), ("0/3/W", (512, 3136)), ("0/3/b", (512,)),
+                ("1/0/W", (n_actions, 512)), ("1/0/b", (n_actions,)), ("2/0/W", (1, 512)), ("2/0/b", (1,))]
     head = [("0/0/W", (16, 4, 8, 8)), ("0/0/b", (16,)), ("0/1/W", (32, 16, 4, 4)), ("0/1/b", (32,)),
             ("0/2/W", (256, 2592)), ("0/2/b", (256,))]
     if arch == ARCH_FF:

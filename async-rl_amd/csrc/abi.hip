@@ -208,7 +208,7 @@ int arl_advance(arl_net* h, void* s) {
 int arl_forward_states(arl_net* h, const float* x, int64_t n, int mode, void* s) {
   NEED_BOUND(h);
   if (mode < 0 || mode > 2) return fail(ARL_EINVAL, "forward_states: mode must be 0, 1 or 2");
-  if (h->net.arch != arl::ARCH_FF) return fail(ARL_ESTATE, "forward_states: FF only (LSTM keeps state)");
+  if (h->net.arch == arl::ARCH_LSTM) return fail(ARL_ESTATE, "forward_states: FF only (LSTM keeps state)");
   if (!x || n < 1 || n > h->net.N) return fail(ARL_EINVAL, "forward_states: need 1 <= n <= n_envs");
   return hip_status(arl::net_forward_f32(h->net, x, (int)n, mode, S(s)), "forward_states");
 }

@@ -12,7 +12,7 @@ namespace arl {
 // replays with advancing step counters (no frozen kernel arguments)
 enum { CTL_STEP = 0, CTL_WINDOW = 1, CTL_SIZE = 16 };
 
-enum Arch { ARCH_FF = 0, ARCH_LSTM = 1 };
+enum Arch { ARCH_FF = 0, ARCH_LSTM = 1, ARCH_FF_NATURE = 2 };
 
 constexpr int PLANE = 84 * 84;         // 7056 B per screen
 constexpr int PAIR = 2 * 210 * 160 * 3; // 201,600 B per frame pair
@@ -23,6 +23,11 @@ constexpr int A2 = C2_OC * C2_P;       // 2592
 constexpr int HID = 256;
 constexpr int GATES = 4 * HID;
 constexpr int MAXA = 32;               // max actions supported by the policy kernel
+// NatureDQNHead (dqn_head.py:6-28): 4->32 k8 s4 (20x20), 32->64 k4 s2 (9x9),
+// 64->64 k3 s1 (7x7), Linear 3136 -> 512
+constexpr int NC1 = 32, NP1 = 400, NC2 = 64, NP2 = 81, NC3 = 64, NP3 = 49;
+constexpr int NA1 = NC1 * NP1, NA2 = NC2 * NP2, NA3 = NC3 * NP3;   // 12800, 5184, 3136
+constexpr int NHID = 512;
 
 struct RingArgs {
   const uint8_t* pair_pool;   // (pool_len, n, 2, 210, 160, 3)
@@ -56,12 +61,14 @@ struct ParamInfo {
 
 struct Net {
   int arch, A, N, T, R;
+  int hid;                 // width of the layer the heads read (256 NIPS / LSTM, 512 Nature)
   int env_offset;          // global id of env 0 on this rank (RNG stream)
   uint64_t seed;
   std::vector<ParamInfo> params;
   int64_t param_floats;    // padded flat length
   // parameter offsets (floats)
   int64_t o_c1W, o_c1b, o_c2W, o_c2b, o_fcW, o_fcb, o_luW, o_lub, o_llW, o_piW, o_pib, o_vW, o_vb;
+  int64_t o_c3W = -1, o_c3b = -1;   // Nature head only
   // workspace layout (byte offsets)
   struct Buf { const char* name; int64_t off, bytes; };
   std::vector<Buf> bufs;
@@ -69,6 +76,7 @@ struct Net {
   int64_t w_ctl, w_frames, w_nvalid, w_reset, w_rewards, w_dones, w_a1, w_a2, w_hfc, w_gates, w_hbuf,
       w_cbuf, w_logits, w_probs, w_logp, w_v, w_ent, w_logpa, w_act, w_dlogits, w_dv, w_dh, w_dfc,
       w_dG, w_dhn, w_dcn, w_da2, w_slab, w_norm, w_loss, w_tick;
+  int64_t w_a3 = 0, w_da1 = 0, w_da3 = 0;   // Nature head only
   int64_t slab_floats;
   int norm_blocks;
   // bound pointers
@@ -90,6 +98,17 @@ enum Stage { STAGE_CONV_FWD = 1, STAGE_FC_FWD = 2, STAGE_POLICY = 3, STAGE_FC_BW
 hipError_t net_stage(Net& net, int stage, int t, hipStream_t s);
 hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_t s);
 
+// Nature head (nature.hip)
+int64_t nature_slab_floats(const Net& net);
+hipError_t nature_act(Net& net, int t, int mode, hipStream_t s);
+hipError_t nature_forward_f32(Net& net, const float* x, int n, int mode, hipStream_t s);
+hipError_t nature_learn(Net& net, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s);
+hipError_t nature_stage(Net& net, int stage, int t, hipStream_t s);
+
+// shared pieces of the heads' backward (net.hip)
+hipError_t launch_heads_bwd(const float* dl, const float* dv, const float* Wpi, const float* Wv, int A, int H,
+                            const float* mask, float* out, int64_t S, hipStream_t s);
+
 hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int t,
                            const float* W1, const float* b1, const float* W2, const float* b2, float* a1, float* a2,
                            hipStream_t s);
@@ -110,7 +129,7 @@ hipError_t launch_grad_sqnorm(const float* g, int64_t n, double* partials, int b
 hipError_t launch_policy(const float* h, int64_t n, const float* Wpi, const float* bpi, const float* Wv,
                          const float* bv, int A, uint64_t seed, const int64_t* ctl, int64_t step_off,
                          int env_offset, int mode, float* logits, float* probs, float* logp, float* v,
-                         float* ent, int32_t* act, float* logp_a, hipStream_t s);
+                         float* ent, int32_t* act, float* logp_a, hipStream_t s, int hid = HID);
 hipError_t launch_returns(const float* rewards, const uint8_t* dones, const float* v, const float* probs,
                           const float* logp, const int32_t* act, int T, int n, int A, double gamma, float beta,
                           float vcoef, int clip_reward, float* dlogits, float* dv, float* loss, hipStream_t s);

@@ -24,6 +24,7 @@
 
 #include "arl_internal.hpp"
 #include "gemm.hpp"
+#include "layers.hpp"
 
 namespace arl {
 
@@ -48,13 +49,6 @@ struct Conv2A {         // A(m, k) = a1[s][ic][2oy+ky][2ox+kx], m = s*81 + p, k 
     return a1[(int64_t)s * A1 + ic * C1_P + (2 * oy + ky) * 20 + 2 * ox + kx];
   }
 };
-struct WeightT {        // B(k, n) = W[n][k]  (Chainer W is (out, in...))
-  const float* __restrict__ w; int K;
-  __device__ float load(int k, int n) const { return w[(int64_t)n * K + k]; }
-  __device__ float4 load4(int k, int n) const {
-    return *reinterpret_cast<const float4*>(w + (int64_t)n * K + k);
-  }
-};
 struct LstmGateA {      // A(m, k): [x | h_prev (0 after reset)]
   const float* __restrict__ x; const float* __restrict__ h; const uint8_t* __restrict__ reset;
   __device__ float load(int m, int k) const {
@@ -77,18 +71,6 @@ struct LstmGateB {      // B(k, j) = [Wu^T ; Wl^T]
                    : *reinterpret_cast<const float4*>(wl + (int64_t)j * HID + k - HID);
   }
 };
-struct HeadsGA {        // A(m, s) = m < A ? dlogits[s][m] : dv[s]
-  const float* __restrict__ dl; const float* __restrict__ dv; int A;
-  __device__ float load(int m, int s) const { return m < A ? dl[(int64_t)s * A + m] : dv[s]; }
-};
-struct OnesColB {       // B(s, j) = j < K ? X[s][j] : 1   (bias gradient column)
-  const float* __restrict__ x; int K;
-  __device__ float load(int s, int j) const { return j < K ? x[(int64_t)s * K + j] : 1.f; }
-  __device__ float4 load4n(int s, int j) const {
-    if (j + 3 < K) return *reinterpret_cast<const float4*>(x + (int64_t)s * K + j);
-    return make_float4(load(s, j), load(s, j + 1), load(s, j + 2), load(s, j + 3));
-  }
-};
 struct LstmWB {         // B(s, j) = [x (256) | 1 | h_prev (256, 0 after reset)]
   const float* __restrict__ x; const float* __restrict__ h; const uint8_t* __restrict__ reset;
   __device__ float load(int s, int j) const {
@@ -98,85 +80,12 @@ struct LstmWB {         // B(s, j) = [x (256) | 1 | h_prev (256, 0 after reset)]
   }
 };
 
-// ---------------------------------------------------------------- epilogues
-struct EpiConv {        // out[s][n][p] = relu(v + b[n]); m = s*P + p
-  float* __restrict__ out; const float* __restrict__ b; int OC, P;
-  __device__ void store(int m, int n, float v, int) const {
-    const int s = m / P, p = m - s * P;
-    out[((int64_t)s * OC + n) * P + p] = fmaxf(__fadd_rn(v, b[n]), 0.f);
-  }
-};
-struct EpiSlab {
-  float* __restrict__ slab; int M, N;
-  __device__ void store(int m, int n, float v, int z) const {
-    slab[((int64_t)z * M + m) * N + n] = v;
-  }
-};
-struct EpiBias {        // out[m][n] = v + b[n]
-  float* __restrict__ out; const float* __restrict__ b; int ld;
-  __device__ void store(int m, int n, float v, int) const { out[(int64_t)m * ld + n] = __fadd_rn(v, b[n]); }
-};
-struct EpiMask {        // out[m][n] = mask[m][n] > 0 ? v : 0  (ReLU backward)
-  float* __restrict__ out; const float* __restrict__ mask; int ld;
-  __device__ void store(int m, int n, float v, int) const {
-    const int64_t i = (int64_t)m * ld + n;
-    out[i] = mask[i] > 0.f ? v : 0.f;
-  }
-};
 struct EpiResetMask {   // out[m][n] = reset[m] ? 0 : v
   float* __restrict__ out; const uint8_t* __restrict__ reset; int ld;
   __device__ void store(int m, int n, float v, int) const {
     out[(int64_t)m * ld + n] = reset[m] ? 0.f : v;
   }
 };
-
-// ---------------------------------------------------------------- reductions
-// dense weight + bias: n < K -> g[oW + m*K + n]; n == K -> g[ob + m];
-// (LSTM) n > K -> g[oL + m*K + n-K-1]
-struct MapDense {
-  float* g; int64_t oW, ob, oL; int K;
-  __device__ void put(int m, int n, float v) const {
-    if (n < K) g[oW + (int64_t)m * K + n] = v;
-    else if (n == K) g[ob + m] = v;
-    else g[oL + (int64_t)m * K + (n - K - 1)] = v;
-  }
-};
-struct MapHeads {
-  float* g; int64_t oPW, oPB, oVW, oVB; int A;
-  __device__ void put(int m, int n, float v) const {
-    if (m < A) { if (n < HID) g[oPW + (int64_t)m * HID + n] = v; else g[oPB + m] = v; }
-    else { if (n < HID) g[oVW + n] = v; else g[oVB] = v; }
-  }
-};
-
-// block = 64 consecutive outputs x 4 slice groups; f64 sums combined in a
-// fixed order (deterministic for any slice count)
-template <class Map>
-__global__ void __launch_bounds__(256)
-reduce_grad_kernel(const float* __restrict__ slab, int splits, int M, int N, Map map) {
-  __shared__ double part[4][64];
-  const int64_t MN = (int64_t)M * N;
-  const int64_t i = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
-  const int zg = threadIdx.x >> 6;
-  double t = 0.0;
-  if (i < MN)
-    for (int z = zg; z < splits; z += 4) t += (double)slab[(int64_t)z * MN + i];
-  part[zg][threadIdx.x & 63] = t;
-  __syncthreads();
-  if (zg == 0 && i < MN) {
-    const int l = threadIdx.x;
-    const double v = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
-    map.put((int)(i / N), (int)(i % N), (float)v);
-  }
-}
-
-template <class Map>
-static hipError_t launch_reduce_grad(const float* slab, int splits, int M, int N, const Map& map, hipStream_t s) {
-  const int64_t MN = (int64_t)M * N;
-  hipLaunchKernelGGL((reduce_grad_kernel<Map>), dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, s, slab, splits,
-                     M, N, map);
-  return hipGetLastError();
-}
 
 // ---------------------------------------------------------------- elementwise
 __device__ inline float sigm(float x) { return __fdiv_rn(1.f, __fadd_rn(1.f, expf(-x))); }
@@ -225,17 +134,25 @@ __global__ void lstm_cell_bwd_kernel(const float* __restrict__ gates, const floa
 
 // dh[s][j] = sum_k dlogits[s][k] Wpi[k][j] + dv[s] Wv[j]; with mask: * (h > 0)
 __global__ void heads_bwd_kernel(const float* __restrict__ dl, const float* __restrict__ dv,
-                                 const float* __restrict__ Wpi, const float* __restrict__ Wv, int A,
+                                 const float* __restrict__ Wpi, const float* __restrict__ Wv, int A, int H,
                                  const float* __restrict__ mask, float* __restrict__ out, int64_t count) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
-  const int64_t s = i / HID;
-  const int j = (int)(i - s * HID);
+  const int64_t s = i / H;
+  const int j = (int)(i - s * H);
   float acc = 0.f;
-  for (int k = 0; k < A; ++k) acc = __fadd_rn(acc, __fmul_rn(dl[s * A + k], Wpi[k * HID + j]));
+  for (int k = 0; k < A; ++k) acc = __fadd_rn(acc, __fmul_rn(dl[s * A + k], Wpi[k * H + j]));
   acc = __fadd_rn(acc, __fmul_rn(dv[s], Wv[j]));
   if (mask) acc = mask[i] > 0.f ? acc : 0.f;
   out[i] = acc;
+}
+
+hipError_t launch_heads_bwd(const float* dl, const float* dv, const float* Wpi, const float* Wv, int A, int H,
+                            const float* mask, float* out, int64_t S, hipStream_t s) {
+  const int64_t cnt = S * H;
+  hipLaunchKernelGGL(heads_bwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, dl, dv, Wpi, Wv, A, H,
+                     mask, out, cnt);
+  return hipGetLastError();
 }
 
 __global__ void advance_kernel(int64_t* ctl, int T, uint8_t* reset, int n, float* hbuf, float* cbuf) {
@@ -252,16 +169,6 @@ __global__ void advance_kernel(int64_t* ctl, int T, uint8_t* reset, int n, float
 }
 
 // ---------------------------------------------------------------- planning
-static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
-
-// split-K factor: aim at ~1024 workgroups, each slice >= 4 K-chunks
-static int plan_splits(int tiles, int64_t K, int BK, int target = 1024) {
-  int s = std::max(1, target / std::max(1, tiles));
-  const int maxs = std::max(1, ceil_div(K, (int64_t)BK * 4));
-  s = std::min(s, maxs);
-  return s;
-}
-
 struct Plans {   // effective split counts (launch_gemm may shrink a request)
   int heads_w, fc_w, lstm_w;
 };
@@ -279,13 +186,18 @@ static int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
 bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_offset, uint64_t seed,
               std::string& err) {
-  if (arch != ARCH_FF && arch != ARCH_LSTM) { err = "arch must be 0 (FF) or 1 (LSTM)"; return false; }
+  if (arch != ARCH_FF && arch != ARCH_LSTM && arch != ARCH_FF_NATURE) {
+    err = "arch must be 0 (FF), 1 (LSTM) or 2 (FF, Nature head)";
+    return false;
+  }
   if (n_actions < 1 || n_actions > MAXA) { err = "n_actions must be in [1, 32]"; return false; }
   if (n_envs < 1 || n_envs > (1 << 20)) { err = "n_envs out of range"; return false; }
   if (t_max < 1 || t_max > 64) { err = "t_max must be in [1, 64]"; return false; }
   if ((int64_t)t_max * n_envs * C1_P >= (int64_t)1 << 31) { err = "t_max * n_envs too large"; return false; }
   net.arch = arch; net.A = n_actions; net.N = n_envs; net.T = t_max; net.R = t_max + 4;
   net.env_offset = env_offset; net.seed = seed;
+  const bool NAT = arch == ARCH_FF_NATURE;
+  net.hid = NAT ? NHID : HID;
   // ---- parameters, Chainer link order (a3c_ale.py:35,52)
   net.params.clear();
   int64_t off = 0;
@@ -295,19 +207,34 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
     off = align_up(off + numel, 64);
     return pi.offset;
   };
-  net.o_c1W = add("0/0/W", 16 * 4 * 8 * 8);
-  net.o_c1b = add("0/0/b", 16);
-  net.o_c2W = add("0/1/W", 32 * 16 * 4 * 4);
-  net.o_c2b = add("0/1/b", 32);
-  net.o_fcW = add("0/2/W", (int64_t)HID * A2);
-  net.o_fcb = add("0/2/b", HID);
-  net.o_luW = net.o_lub = net.o_llW = -1;
+  net.o_luW = net.o_lub = net.o_llW = net.o_c3W = net.o_c3b = -1;
+  if (NAT) {   // dqn_head.py:16-20, then FCSoftmaxPolicy(512) / FCVFunction(512)
+    net.o_c1W = add("0/0/W", NC1 * 4 * 8 * 8);
+    net.o_c1b = add("0/0/b", NC1);
+    net.o_c2W = add("0/1/W", NC2 * NC1 * 4 * 4);
+    net.o_c2b = add("0/1/b", NC2);
+    net.o_c3W = add("0/2/W", NC3 * NC2 * 3 * 3);
+    net.o_c3b = add("0/2/b", NC3);
+    net.o_fcW = add("0/3/W", (int64_t)NHID * NA3);
+    net.o_fcb = add("0/3/b", NHID);
+    net.o_piW = add("1/0/W", (int64_t)n_actions * NHID);
+    net.o_pib = add("1/0/b", n_actions);
+    net.o_vW = add("2/0/W", NHID);
+    net.o_vb = add("2/0/b", 1);
+  } else {
+    net.o_c1W = add("0/0/W", 16 * 4 * 8 * 8);
+    net.o_c1b = add("0/0/b", 16);
+    net.o_c2W = add("0/1/W", 32 * 16 * 4 * 4);
+    net.o_c2b = add("0/1/b", 32);
+    net.o_fcW = add("0/2/W", (int64_t)HID * A2);
+    net.o_fcb = add("0/2/b", HID);
+  }
   if (arch == ARCH_FF) {
     net.o_piW = add("1/0/W", (int64_t)n_actions * HID);
     net.o_pib = add("1/0/b", n_actions);
     net.o_vW = add("2/0/W", HID);
     net.o_vb = add("2/0/b", 1);
-  } else {
+  } else if (arch == ARCH_LSTM) {
     net.o_luW = add("1/upward/W", (int64_t)GATES * HID);
     net.o_lub = add("1/upward/b", GATES);
     net.o_llW = add("1/lateral/W", (int64_t)GATES * HID);
@@ -327,6 +254,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   slab = std::max(slab, (int64_t)pl.fc_w * HID * (A2 + 1));
   slab = std::max(slab, conv_bwd_slab_floats((int)S));
   if (arch == ARCH_LSTM) slab = std::max(slab, (int64_t)pl.lstm_w * GATES * (2 * HID + 1));
+  if (NAT) slab = nature_slab_floats(net);
   net.slab_floats = slab;
   net.bufs.clear();
   int64_t wo = 0;
@@ -343,9 +271,11 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   net.w_reset = buf("reset", T1 * n);
   net.w_rewards = buf("rewards", S * 4);
   net.w_dones = buf("dones", S);
-  net.w_a1 = buf("a1", T1 * n * A1 * 4);
-  net.w_a2 = buf("a2", T1 * n * A2 * 4);
-  net.w_hfc = buf("hfc", T1 * n * HID * 4);
+  const int64_t H = net.hid, nA1 = NAT ? NA1 : A1, nA2 = NAT ? NA2 : A2;
+  net.w_a1 = buf("a1", T1 * n * nA1 * 4);
+  net.w_a2 = buf("a2", T1 * n * nA2 * 4);
+  net.w_a3 = buf("a3", NAT ? T1 * n * NA3 * 4 : 0);
+  net.w_hfc = buf("hfc", T1 * n * H * 4);
   net.w_gates = buf("gates", L ? T1 * n * GATES * 4 : 0);
   net.w_hbuf = buf("hbuf", L ? (T + 2) * n * HID * 4 : 0);
   net.w_cbuf = buf("cbuf", L ? (T + 2) * n * HID * 4 : 0);
@@ -358,12 +288,14 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   net.w_act = buf("actions", T1 * n * 4);
   net.w_dlogits = buf("dlogits", S * A * 4);
   net.w_dv = buf("dv", S * 4);
-  net.w_dh = buf("dh", S * HID * 4);
-  net.w_dfc = buf("dfc", S * HID * 4);
+  net.w_dh = buf("dh", L ? S * HID * 4 : 0);
+  net.w_dfc = buf("dfc", S * H * 4);
   net.w_dG = buf("dG", L ? S * GATES * 4 : 0);
   net.w_dhn = buf("dhn", L ? n * HID * 4 : 0);
   net.w_dcn = buf("dcn", L ? n * HID * 4 : 0);
-  net.w_da2 = buf("da2", S * A2 * 4);
+  net.w_da2 = buf("da2", S * nA2 * 4);
+  net.w_da1 = buf("da1", NAT ? S * NA1 * 4 : 0);
+  net.w_da3 = buf("da3", NAT ? S * NA3 * 4 : 0);
   net.w_slab = buf("slab", slab * 4);
   net.w_norm = buf("norm_partials", (int64_t)net.norm_blocks * 8);
   net.w_tick = buf("tickets", (int64_t)fc_fwd_tiles((int)n) * 4);
@@ -382,6 +314,7 @@ static hipError_t fc_forward(const Net& net, int n, const float* a2, float* hfc,
 }
 
 hipError_t net_act(Net& net, int t, int mode, hipStream_t s) {
+  if (net.arch == ARCH_FF_NATURE) return nature_act(net, t, mode, s);
   const int n = net.N, A = net.A;
   float* a1 = net.at<float>(net.w_a1) + (int64_t)t * n * A1;
   float* a2 = net.at<float>(net.w_a2) + (int64_t)t * n * A2;
@@ -417,6 +350,7 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s) {
 // Drop-in pi_and_v on explicit f32 states (dqn_phi output), FF only; results
 // land in activation slot T (the bootstrap slot) of the workspace.
 hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_t s) {
+  if (net.arch == ARCH_FF_NATURE) return nature_forward_f32(net, x, n, mode, s);
   if (net.arch != ARCH_FF || n > net.N) return hipErrorInvalidValue;
   const int T = net.T, A = net.A, N = net.N;
   float* a1 = net.at<float>(net.w_a1) + (int64_t)T * N * A1;
@@ -440,6 +374,7 @@ hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_
 
 // ---------------------------------------------------------------- backward
 hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s) {
+  if (net.arch == ARCH_FF_NATURE) return nature_learn(net, gamma, beta, vcoef, clip_reward, s);
   const int n = net.N, T = net.T, A = net.A, S = T * n;
   const float* P = net.p;
   float* G = net.g;
@@ -459,14 +394,9 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
   ARL_TRY((launch_gemm<16, 64, 32, 1, 4, GS, GM>(HeadsGA{dl, dv, A}, OnesColB{hheads, HID}, EpiSlab{slab, A + 1, HID + 1},
                                          A + 1, HID + 1, S, pl.heads_w, s)));
   ARL_TRY(launch_reduce_grad(slab, pl.heads_w, A + 1, HID + 1,
-                             MapHeads{G, net.o_piW, net.o_pib, net.o_vW, net.o_vb, A}, s));
-  {
-    const int64_t cnt = (int64_t)S * HID;
-    float* dst = L ? net.at<float>(net.w_dh) : dfc;
-    hipLaunchKernelGGL(heads_bwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, dl, dv, P + net.o_piW,
-                       P + net.o_vW, A, L ? nullptr : hfc, dst, cnt);
-    ARL_TRY(hipGetLastError());
-  }
+                             MapHeads{G, net.o_piW, net.o_pib, net.o_vW, net.o_vb, A, HID}, s));
+  ARL_TRY(launch_heads_bwd(dl, dv, P + net.o_piW, P + net.o_vW, A, HID, L ? nullptr : hfc,
+                           L ? net.at<float>(net.w_dh) : dfc, S, s));
   // 3. LSTM: truncated BPTT over the window
   if (L) {
     const float* gates = net.at<float>(net.w_gates);
@@ -515,6 +445,7 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
 // One stage of a window on the current workspace contents (arl_run_stage):
 // the same launches the window makes, isolated for timing.
 hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
+  if (net.arch == ARCH_FF_NATURE) return nature_stage(net, stage, t, s);
   const int n = net.N, S = net.T * n;
   const float* P = net.p;
   float* G = net.g;

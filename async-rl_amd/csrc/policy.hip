@@ -42,6 +42,8 @@ __device__ inline uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// HW = hidden width (256: NIPS head / LSTM; 512: Nature head)
+template <int HW>
 __global__ void __launch_bounds__(256)
 policy_kernel(const float* __restrict__ h, int64_t n, const float* __restrict__ Wpi, const float* __restrict__ bpi,
               const float* __restrict__ Wv, const float* __restrict__ bv, int A, uint32_t seed_lo,
@@ -49,21 +51,22 @@ policy_kernel(const float* __restrict__ h, int64_t n, const float* __restrict__ 
               float* __restrict__ logits, float* __restrict__ probs, float* __restrict__ logp,
               float* __restrict__ v, float* __restrict__ ent, int32_t* __restrict__ act,
               float* __restrict__ logp_a) {
-  // 4 waves split K = 256 into quarters; partial tiles summed in wave order
+  // 4 waves split K = H into quarters; partial tiles summed in wave order
+  constexpr int KW = HW / 4, NS = KW / 16;
   __shared__ float part[4][16][MAXA + 2];
   __shared__ float zs[16][MAXA + 2];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int64_t row0 = (int64_t)blockIdx.x * 16;
   const int64_t rowc = min(row0 + col, n - 1);   // A row of this lane (rows past n: any valid row, not stored)
-  f32x4 hv[4];
+  f32x4 hv[NS];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) hv[s] = *reinterpret_cast<const f32x4*>(h + rowc * HID + 64 * w + 16 * s + 4 * g);
+  for (int s = 0; s < NS; ++s) hv[s] = *reinterpret_cast<const f32x4*>(h + rowc * HW + KW * w + 16 * s + 4 * g);
   for (int nt = 0; 16 * nt <= A; ++nt) {
     const int j = 16 * nt + col;   // head column: j < A -> pi logit j, j == A -> value
-    const float* wrow = (j < A ? Wpi + (int64_t)j * HID : Wv) + 64 * w;
+    const float* wrow = (j < A ? Wpi + (int64_t)j * HW : Wv) + KW * w;
     f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < NS; ++s) {
       f32x4 wv = {0.f, 0.f, 0.f, 0.f};
       if (j <= A) wv = *reinterpret_cast<const f32x4*>(wrow + 16 * s + 4 * g);
       c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][0], wv[0], c0, 0, 0, 0);
@@ -132,11 +135,18 @@ policy_kernel(const float* __restrict__ h, int64_t n, const float* __restrict__ 
 hipError_t launch_policy(const float* h, int64_t n, const float* Wpi, const float* bpi, const float* Wv,
                          const float* bv, int A, uint64_t seed, const int64_t* ctl, int64_t step_off,
                          int env_offset, int mode, float* logits, float* probs, float* logp, float* v,
-                         float* ent, int32_t* act, float* logp_a, hipStream_t s) {
+                         float* ent, int32_t* act, float* logp_a, hipStream_t s, int hid) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(policy_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, s, h, n, Wpi, bpi, Wv, bv, A,
-                     (uint32_t)seed, (uint32_t)(seed >> 32), ctl, step_off, env_offset, mode, logits, probs,
-                     logp, v, ent, act, logp_a);
+  if (hid == 512)
+    hipLaunchKernelGGL(policy_kernel<512>, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, s, h, n, Wpi, bpi, Wv, bv,
+                       A, (uint32_t)seed, (uint32_t)(seed >> 32), ctl, step_off, env_offset, mode, logits, probs,
+                       logp, v, ent, act, logp_a);
+  else if (hid == HID)
+    hipLaunchKernelGGL(policy_kernel<HID>, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, s, h, n, Wpi, bpi, Wv, bv,
+                       A, (uint32_t)seed, (uint32_t)(seed >> 32), ctl, step_off, env_offset, mode, logits, probs,
+                       logp, v, ent, act, logp_a);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -27,7 +27,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "async-rl_amd"))
 
-from asyncrl_amd import A3C, A3CFF, A3CLSTM, GradientClipping, RMSpropAsync  # noqa: E402
+from asyncrl_amd import A3C, A3CFF, A3CFFNature, A3CLSTM, GradientClipping, RMSpropAsync  # noqa: E402
 from asyncrl_amd import _lib  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
@@ -39,6 +39,10 @@ CONV_FWD_FLOP_PER_ENV = 2 * (400 * 16 * 256 + 81 * 32 * 256)             # 4,603
 FC_FWD_FLOP_PER_ENV = 2 * 2592 * 256                                     # 1,327,104
 CONV_BWD_FLOP_PER_SAMPLE = 2 * (32 * 256 * 81 + 81 * 32 * 256 + 400 * 16 * 256)   # dW2 + convT + dW1
 HID_BYTES = 256 * 4
+# NatureDQNHead (dqn_head.py:6-28): conv MACs 400*32*256 + 81*64*512 + 49*64*576, FC 3136*512
+NAT_CONV_FWD_FLOP_PER_ENV = 2 * (400 * 32 * 256 + 81 * 64 * 512 + 49 * 64 * 576)      # 15,474,688
+NAT_FC_FWD_FLOP_PER_ENV = 2 * 3136 * 512
+NAT_CONV_BWD_FLOP_PER_SAMPLE = 2 * (2 * 49 * 64 * 576 + 2 * 81 * 64 * 512 + 400 * 32 * 256)
 PHI_STACK_BYTES_PER_PAIR = 201600 + 3 * 7056 + 4 * 7056   # pair + 3 prior planes + 4-plane stack
 
 # BASELINE.json configs[1..4] -> (arch, envs per GPU, actions)
@@ -55,7 +59,8 @@ def parse():
                          "A=6, c4 FF 512 envs per GPU (4096 over 8), c5 phi stress 16384 frame pairs")
     ap.add_argument("--envs-per-gpu", type=int, default=0, help="0: the workload's")
     ap.add_argument("--t-max", type=int, default=5)
-    ap.add_argument("--arch", choices=["ff", "lstm"], default=None, help="default: the workload's")
+    ap.add_argument("--arch", choices=["ff", "lstm", "nature"], default=None,
+                    help="default: the workload's; nature = A3CFF with NatureDQNHead (SURVEY 8(a) a8)")
     ap.add_argument("--actions", type=int, default=0, help="0: 4 for ff (Breakout), 6 for lstm (Space Invaders)")
     ap.add_argument("--pool", type=int, default=8)
     ap.add_argument("--no-graph", action="store_true")
@@ -164,9 +169,14 @@ def main():
     if w_arch == "phi":
         return bench_phi(a, world, rank, dev, w_envs)
     arch = a.arch or w_arch
-    A = a.actions or (w_A if arch == w_arch else (4 if arch == "ff" else 6))
+    A = a.actions or (w_A if arch == w_arch else (6 if arch == "lstm" else 4))
     N, T = a.envs_per_gpu or w_envs, a.t_max
-    Model = A3CFF if arch == "ff" else A3CLSTM
+    Model = {"ff": A3CFF, "lstm": A3CLSTM, "nature": A3CFFNature}[arch]
+    nat = arch == "nature"
+    conv_fwd_flop = NAT_CONV_FWD_FLOP_PER_ENV if nat else CONV_FWD_FLOP_PER_ENV
+    fc_fwd_flop = NAT_FC_FWD_FLOP_PER_ENV if nat else FC_FWD_FLOP_PER_ENV
+    conv_bwd_flop = NAT_CONV_BWD_FLOP_PER_SAMPLE if nat else CONV_BWD_FLOP_PER_SAMPLE
+    hid_bytes = 2 * HID_BYTES if nat else HID_BYTES
     model = Model(A, n_envs=N, t_max=T, seed=1234, env_offset=rank * N, init_seed=0, device=dev)
     opt = RMSpropAsync(lr=7e-4, eps=1e-1, alpha=0.99).setup(model)
     opt.add_hook(GradientClipping(40))
@@ -255,16 +265,16 @@ def main():
             ("phi", "phi_ring_kernel",
              lambda i: net.observe(1 + i % T, pairs, rewards, dones, P, stream=stream), T + 1, "hbm",
              N * PHI_BYTES_PER_ENV_STEP),
-            ("conv_fwd", "conv_fwd_kernel", lambda i: net.run_stage("conv_fwd", i % T, stream=stream), T + 1,
-             "mfma", N * CONV_FWD_FLOP_PER_ENV),
-            ("fc_fwd", "fc_fwd_kernel", lambda i: net.run_stage("fc_fwd", i % T, stream=stream), T + 1, "mfma",
-             N * FC_FWD_FLOP_PER_ENV),
+            ("conv_fwd", "gemm_kernel x3 (implicit-GEMM convs)" if nat else "conv_fwd_kernel",
+             lambda i: net.run_stage("conv_fwd", i % T, stream=stream), T + 1, "mfma", N * conv_fwd_flop),
+            ("fc_fwd", "gemm_kernel + reduce_grad_kernel" if nat else "fc_fwd_kernel",
+             lambda i: net.run_stage("fc_fwd", i % T, stream=stream), T + 1, "mfma", N * fc_fwd_flop),
             ("policy", "policy_kernel", lambda i: net.run_stage("policy", i % T, stream=stream), T + 1, "hbm",
-             N * (HID_BYTES + 12 * A + 12)),
+             N * (hid_bytes + 12 * A + 12)),
             ("fc_bwd", "gemm_kernel x2 + reduce_grad_kernel", lambda i: net.run_stage("fc_bwd", 0, stream=stream),
-             1, "mfma", 2 * FC_FWD_FLOP_PER_ENV * S),
-            ("conv_bwd", "conv_bwd_kernel", lambda i: net.run_stage("conv_bwd", 0, stream=stream), 1, "mfma",
-             S * CONV_BWD_FLOP_PER_SAMPLE),
+             1, "mfma", 2 * fc_fwd_flop * S),
+            ("conv_bwd", "gemm_kernel x9 + reduce_grad_kernel x3" if nat else "conv_bwd_kernel",
+             lambda i: net.run_stage("conv_bwd", 0, stream=stream), 1, "mfma", S * conv_bwd_flop),
             ("rmsprop", "rmsprop_kernel", lambda i: net.optimize(lr0=1e-12, clip=0.0, stream=stream), 1, "hbm",
              net.n_params * RMSPROP_BYTES_PER_PARAM),
         ]
@@ -292,8 +302,9 @@ def main():
         roof = {"bound": d["bound"], "kernel": d["kernel"], "achieved": d["achieved"], "peak": d["peak"],
                 "unit": d["unit"], "frac": d["frac"], "traffic": traffic, "avg_launch_us": d["avg_launch_us"],
                 "work_per_launch": d.get("flop_per_launch", d.get("bytes_per_launch")),
-                "peak_note": ("f32-equivalent FLOP/s vs the dense fp32 matrix peak (bf16-split f32 emulation, "
-                              "DESIGN.md)" if d["bound"] == "mfma" else "HBM3E spec peak")}
+                "peak_note": (("exact f32 MFMA (v_mfma_f32_16x16x4_f32) vs the dense fp32 matrix peak" if nat else
+                               "f32-equivalent FLOP/s vs the dense fp32 matrix peak (bf16-split f32 emulation, "
+                               "DESIGN.md)") if d["bound"] == "mfma" else "HBM3E spec peak")}
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_seconds > 0 and arch == "ff":
@@ -308,7 +319,7 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (uniform RGB 210x160 frame pairs, rewards P(!=0)=0.05, terminals p=1/500)",
-            "config": {"workload": ("%s: A3C %s NIPS-DQN head, %d envs x t_max=%d per GPU (phi + conv head + sampling "
+            "config": {"workload": ("%s: A3C %s " + ("Nature" if nat else "NIPS") + "-DQN head, %d envs x t_max=%d per GPU (phi + conv head + sampling "
                                     "+ n-step returns + backward + clip + RMSProp)") % (a.workload, arch.upper(), N, T),
                        "envs_per_gpu": N, "global_envs": N * world, "t_max": T, "n_actions": A, "arch": arch,
                        "graph": use_graph, "parallelism": "dp%d" % world,

@@ -28,6 +28,7 @@ extern "C" {
 
 #define ARL_ARCH_FF 0     /* A3CFF   (a3c_ale.py:28-40) */
 #define ARL_ARCH_LSTM 1   /* A3CLSTM (a3c_ale.py:43-70) */
+#define ARL_ARCH_FF_NATURE 2  /* A3CFF with NatureDQNHead (dqn_head.py:6-28) instead of NIPSDQNHead */
 
 #define ARL_RESIZE_SCALAR 0  /* OpenCV FixedPtCast vertical pass (canonical) */
 #define ARL_RESIZE_SIMD 1    /* OpenCV VResizeLinearVec_32s8u (mulhi) pass */

@@ -151,6 +151,7 @@ PHI_LUT = (np.arange(256, dtype=np.float32) / F32(255.0)).astype(np.float32)
 
 ARCH_FF = 0
 ARCH_LSTM = 1
+ARCH_FF_NATURE = 2     # A3CFF with NatureDQNHead (dqn_head.py:6-28) instead of NIPSDQNHead
 
 
 def param_shapes(arch: int, n_actions: int):
@@ -161,6 +162,10 @@ def param_shapes(arch: int, n_actions: int):
     if arch == ARCH_FF:
         return head + [("1/0/W", (n_actions, 256)), ("1/0/b", (n_actions,)),
                        ("2/0/W", (1, 256)), ("2/0/b", (1,))]
+    if arch == ARCH_FF_NATURE:   # dqn_head.py:16-20 (4->32 k8s4, 32->64 k4s2, 64->64 k3s1, 3136->512)
+        return [("0/0/W", (32, 4, 8, 8)), ("0/0/b", (32,)), ("0/1/W", (64, 32, 4, 4)), ("0/1/b", (64,)),
+                ("0/2/W", (64, 64, 3, 3)), ("0/2/b", (64,)), ("0/3/W", (512, 3136)), ("0/3/b", (512,)),
+                ("1/0/W", (n_actions, 512)), ("1/0/b", (n_actions,)), ("2/0/W", (1, 512)), ("2/0/b", (1,))]
     if arch == ARCH_LSTM:
         return head + [("1/upward/W", (1024, 256)), ("1/upward/b", (1024,)),
                        ("1/lateral/W", (1024, 256)),
@@ -175,6 +180,10 @@ def pname(arch: int, role: str) -> str:
         m = {"c1W": "0/0/W", "c1b": "0/0/b", "c2W": "0/1/W", "c2b": "0/1/b",
              "fcW": "0/2/W", "fcb": "0/2/b", "piW": "1/0/W", "pib": "1/0/b",
              "vW": "2/0/W", "vb": "2/0/b"}
+    elif arch == ARCH_FF_NATURE:
+        m = {"c1W": "0/0/W", "c1b": "0/0/b", "c2W": "0/1/W", "c2b": "0/1/b",
+             "c3W": "0/2/W", "c3b": "0/2/b", "fcW": "0/3/W", "fcb": "0/3/b",
+             "piW": "1/0/W", "pib": "1/0/b", "vW": "2/0/W", "vb": "2/0/b"}
     else:
         m = {"c1W": "0/0/W", "c1b": "0/0/b", "c2W": "0/1/W", "c2b": "0/1/b",
              "fcW": "0/2/W", "fcb": "0/2/b", "luW": "1/upward/W",
@@ -265,6 +274,19 @@ def nips_head(params, arch, x):
     return a1, a2, h
 
 
+def nature_head(params, x):
+    """NatureDQNHead.__call__ (dqn_head.py:24-28): conv(4->32, 8, s4) -> relu
+    -> conv(32->64, 4, s2) -> relu -> conv(64->64, 3, s1) -> relu ->
+    Linear(3136, 512) -> relu.  Returns the activations (a1, a2, a3, h)."""
+    arch = ARCH_FF_NATURE
+    a1 = relu(conv2d(x, params[pname(arch, "c1W")], params[pname(arch, "c1b")], 4))
+    a2 = relu(conv2d(a1, params[pname(arch, "c2W")], params[pname(arch, "c2b")], 2))
+    a3 = relu(conv2d(a2, params[pname(arch, "c3W")], params[pname(arch, "c3b")], 1))
+    h = relu(linear(a3.reshape(a3.shape[0], -1), params[pname(arch, "fcW")],
+                    params[pname(arch, "fcb")]))
+    return a1, a2, a3, h
+
+
 def sigmoid(x):
     return (F32(1.0) / (F32(1.0) + np.exp(-x))).astype(np.float32)
 
@@ -306,12 +328,14 @@ def entropy(p, logp):
     return (-(p * logp).sum(axis=-1)).astype(np.float32)
 
 
-def pi_and_v_ff(params, x):
-    """A3CFF.pi_and_v (a3c_ale.py:38-40)."""
-    a1, a2, h = nips_head(params, ARCH_FF, x)
+def pi_and_v_ff(params, x, arch=ARCH_FF):
+    """A3CFF.pi_and_v (a3c_ale.py:38-40); arch=ARCH_FF_NATURE swaps in the
+    Nature head (hidden 512)."""
+    acts = nature_head(params, x) if arch == ARCH_FF_NATURE else nips_head(params, ARCH_FF, x)
+    h = acts[-1]
     logits = linear(h, params["1/0/W"], params["1/0/b"])
     v = linear(h, params["2/0/W"], params["2/0/b"])[:, 0]
-    return logits, v, (a1, a2, h)
+    return logits, v, acts
 
 
 # ----------------------------------------------------------------------------
@@ -413,18 +437,42 @@ def returns_and_lossgrad(rewards, dones, values, vboot, probs, logp, actions,
 # Backward (total_loss.backward(), a3c.py:129-130), restated by hand
 # ----------------------------------------------------------------------------
 
-def ff_backward(params, x, acts, dlogits, dv):
+def ff_backward(params, x, acts, dlogits, dv, arch=ARCH_FF):
     """Gradients of sum_i (dlogits_i . z_i + dv_i * v_i) for the A3CFF graph
-    (a3c_ale.py:38-40) over a batch of samples.  acts = (a1, a2, h)."""
-    a1, a2, h = acts
+    (a3c_ale.py:38-40) over a batch of samples.  acts = (a1, a2, h), or
+    (a1, a2, a3, h) for the Nature head."""
+    h = acts[-1]
     g = {}
     g["1/0/W"] = (dlogits.T @ h).astype(np.float32)
     g["1/0/b"] = dlogits.sum(0, dtype=np.float32)
     g["2/0/W"] = (dv[None, :] @ h).astype(np.float32)
     g["2/0/b"] = np.array([dv.sum(dtype=np.float32)], np.float32)
     dh = dlogits @ params["1/0/W"] + dv[:, None] * params["2/0/W"]
-    _head_backward(params, ARCH_FF, x, a1, a2, h, dh.astype(np.float32), g)
+    if arch == ARCH_FF_NATURE:
+        _nature_backward(params, x, acts, dh.astype(np.float32), g)
+    else:
+        a1, a2, _ = acts
+        _head_backward(params, ARCH_FF, x, a1, a2, h, dh.astype(np.float32), g)
     return g
+
+
+def _nature_backward(params, x, acts, dh, g):
+    """Backward of NatureDQNHead (dqn_head.py:24-28) from dL/dh."""
+    arch = ARCH_FF_NATURE
+    a1, a2, a3, h = acts
+    n = x.shape[0]
+    dfc = dh * (h > 0)
+    g[pname(arch, "fcW")] = (dfc.T @ a3.reshape(n, -1)).astype(np.float32)
+    g[pname(arch, "fcb")] = dfc.sum(0, dtype=np.float32)
+    da3 = ((dfc @ params[pname(arch, "fcW")]).reshape(a3.shape) * (a3 > 0)).astype(np.float32)
+    gW3, gb3, da2 = conv2d_backward(a2, params[pname(arch, "c3W")], da3, 1)
+    g[pname(arch, "c3W")], g[pname(arch, "c3b")] = gW3, gb3
+    da2 = (da2 * (a2 > 0)).astype(np.float32)
+    gW2, gb2, da1 = conv2d_backward(a1, params[pname(arch, "c2W")], da2, 2)
+    g[pname(arch, "c2W")], g[pname(arch, "c2b")] = gW2, gb2
+    da1 = (da1 * (a1 > 0)).astype(np.float32)
+    gW1, gb1, _ = conv2d_backward(x, params[pname(arch, "c1W")], da1, 4, need_dx=False)
+    g[pname(arch, "c1W")], g[pname(arch, "c1b")] = gW1, gb1
 
 
 def _head_backward(params, arch, x, a1, a2, h, dh, g):
@@ -508,7 +556,7 @@ class LSTMState:
 
 
 def ff_window_grads(params, states, actions, rewards, dones, boot_state,
-                    gamma=0.99, beta=0.01, v_loss_coef=0.5):
+                    gamma=0.99, beta=0.01, v_loss_coef=0.5, arch=ARCH_FF):
     """Gradient of one lockstep window for A3CFF at fixed theta.
 
     states: (T, N, 4, 84, 84) f32; boot_state (N,4,84,84) f32 = s_T.
@@ -516,15 +564,15 @@ def ff_window_grads(params, states, actions, rewards, dones, boot_state,
     one a3c.py:77-130 update at fixed theta; gradients are summed."""
     T, N = actions.shape
     x = states.reshape(T * N, 4, DST, DST)
-    logits, v, acts = pi_and_v_ff(params, x)
+    logits, v, acts = pi_and_v_ff(params, x, arch)
     p = softmax(logits)
     lp = log_softmax(logits)
-    _, vb, _ = pi_and_v_ff(params, boot_state)
+    _, vb, _ = pi_and_v_ff(params, boot_state, arch)
     A = logits.shape[1]
     R, adv, dlog, dv, pil, vl = returns_and_lossgrad(
         rewards, dones, v.reshape(T, N), vb, p.reshape(T, N, A),
         lp.reshape(T, N, A), actions, gamma, beta, v_loss_coef)
-    g = ff_backward(params, x, acts, dlog.reshape(T * N, A), dv.reshape(T * N))
+    g = ff_backward(params, x, acts, dlog.reshape(T * N, A), dv.reshape(T * N), arch)
     return g, dict(logits=logits.reshape(T, N, A), v=v.reshape(T, N), vboot=vb,
                    R=R, adv=adv, dlogits=dlog, dv=dv, pi_loss=pil, v_loss=vl)
 

@@ -43,7 +43,7 @@ def test_abi_version_and_errors():
     lib.arl_net_destroy(h)
 
 
-@pytest.mark.parametrize("arch,A,count", [(0, 4, 677429), (1, 6, 1203255)])
+@pytest.mark.parametrize("arch,A,count", [(0, 4, 677429), (1, 6, 1203255), (2, 4, 1686693)])
 def test_param_layout_matches_chainer(arch, A, count):
     from asyncrl_amd._lib import lib
     from asyncrl_amd.net import param_shapes
