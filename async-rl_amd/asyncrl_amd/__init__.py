@@ -7,3 +7,5 @@ from .dqn_phi import current_screen, dqn_phi, max_luminance, phi_stack  # noqa: 
 from .net import DeviceNet, init_like_torch, param_shapes  # noqa: F401
 from .policy_output import SoftmaxPolicyOutput, fc_softmax_policy_and_v  # noqa: F401
 from .rmsprop_async import GradientClipping, RMSpropAsync  # noqa: F401
+from . import serializers  # noqa: F401
+from .hdf5 import read_hdf5, write_hdf5  # noqa: F401

@@ -31,6 +31,7 @@ import torch
 from ._lib import ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, RESIZE_SCALAR
 from .distributed import allreduce_grads, world_info
 from .net import DeviceNet, init_like_torch
+from . import serializers
 from .policy_output import SoftmaxPolicyOutput
 
 
@@ -186,19 +187,16 @@ class A3C:
 
     # ------------------------------------------------------------ checkpoints
     def save_model(self, model_filename: str):
-        """a3c.py:181-185: model params + optimizer state ('.opt').  Stored
-        as .npz with the Chainer HDF5 paths as keys ('0/0/W' -> '0|0|W')."""
-        net = self.net
-        np.savez(model_filename, **{k.replace("/", "|"): v for k, v in net.state_dict().items()})
-        np.savez(model_filename + ".opt", **{k.replace("/", "|"): v for k, v in net.state_dict(net.ms).items()})
+        """a3c.py:181-185: the model and the optimizer state ('.opt') as
+        Chainer-layout HDF5 files (serializers.save_hdf5)."""
+        serializers.save_hdf5(model_filename, self.model)
+        serializers.save_hdf5(model_filename + ".opt", self.optimizer)
 
     def load_model(self, model_filename: str):
-        """a3c.py:169-179 (loads the '.opt' state when present)."""
-        net = self.net
-        with np.load(model_filename if model_filename.endswith(".npz") else model_filename + ".npz") as z:
-            net.load_params({k.replace("|", "/"): z[k] for k in z.files})
-        opt = model_filename + ".opt.npz"
+        """a3c.py:169-179: load the model, and the optimizer state when
+        '<file>.opt' exists (copy_param to a shared model is a no-op: the
+        device parameters are shared)."""
+        serializers.load_hdf5(model_filename, self.model)
+        opt = model_filename + ".opt"
         if os.path.exists(opt):
-            with np.load(opt) as z:
-                for k in z.files:
-                    net.view(net.ms, k.replace("|", "/")).copy_(torch.from_numpy(z[k]))
+            serializers.load_hdf5(opt, self.optimizer)

@@ -37,6 +37,8 @@ class RMSpropAsync:
         self.anneal_total_steps = 0   # 0 = use self.lr as given
         self.n_total_envs = 0         # envs over all ranks (global_t per window)
         self._scratch = None
+        self.t = 0                    # Chainer Optimizer.t / epoch (serialized into '.opt')
+        self.epoch = 0
 
     def setup(self, model):
         """Chainer Optimizer.setup: bind the model whose flat params/grads and
@@ -58,6 +60,7 @@ class RMSpropAsync:
         """GradientClipping hook(s) then update_one for every parameter,
         on the bound model's device buffers (a3c.py:139)."""
         net = self.target.net
+        self.t += 1
         net.optimize(lr0=self.lr, total_steps=self.anneal_total_steps, n_total=self.n_total_envs,
                      alpha=self.alpha, eps=self.eps, clip=self.clip_threshold, stream=stream)
 
