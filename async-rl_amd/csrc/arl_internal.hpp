@@ -77,6 +77,12 @@ struct Net {
       w_cbuf, w_logits, w_probs, w_logp, w_v, w_ent, w_logpa, w_act, w_dlogits, w_dv, w_dh, w_dfc,
       w_dG, w_dhn, w_dcn, w_da2, w_slab, w_norm, w_loss, w_tick;
   int64_t w_a3 = 0, w_da1 = 0, w_da3 = 0;   // Nature head only
+  // split-K slabs of the weight-gradient GEMMs that run beside the main
+  // backward chain on side streams (heads, FC, LSTM gates)
+  int64_t w_slab_heads = 0, w_slab_fc = 0, w_slab_lstm = 0;
+  // side streams + fork / join events of the backward (created at bind)
+  hipStream_t side[2] = {nullptr, nullptr};
+  hipEvent_t ev[6] = {};
   int64_t slab_floats;
   int norm_blocks;
   // bound pointers
@@ -89,6 +95,8 @@ struct Net {
 
 bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_offset, uint64_t seed,
               std::string& err);
+hipError_t net_streams_create(Net& net);
+void net_streams_destroy(Net& net);
 hipError_t net_act(Net& net, int t, int mode, hipStream_t s);   // mode: 0 none, 1 sample, 2 greedy
 hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s);
 hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
@@ -117,10 +125,31 @@ hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const i
                            float* gW1, float* gb1, hipStream_t s, bool reduce = true);
 int64_t conv_bwd_slab_floats(int S);
 
+// arguments of the softmax policy / value heads (policy_rows.hpp)
+struct PolicyArgs {
+  const float *Wpi, *bpi, *Wv, *bv;
+  int A;
+  uint32_t seed_lo, seed_hi;
+  const int64_t* ctl;       // step counter (Philox counter = ctl[STEP] + step_off)
+  int64_t step_off;
+  int env_offset, mode;     // mode: 0 none, 1 sample, 2 greedy
+  float *logits, *probs, *logp, *v, *ent;
+  int32_t* act;
+  float* logp_a;
+};
+inline PolicyArgs make_policy_args(const float* Wpi, const float* bpi, const float* Wv, const float* bv, int A,
+                                   uint64_t seed, const int64_t* ctl, int64_t step_off, int env_offset, int mode,
+                                   float* logits, float* probs, float* logp, float* v, float* ent, int32_t* act,
+                                   float* logp_a) {
+  return PolicyArgs{Wpi, bpi, Wv, bv, A, (uint32_t)seed, (uint32_t)(seed >> 32), ctl, step_off, env_offset, mode,
+                    logits, probs, logp, v, ent, act, logp_a};
+}
+
 constexpr int FC_SPLIT = 8;   // fc forward split-K (one slice per XCD)
 int fc_fwd_tiles(int n);      // tickets needed for n envs
 hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b, float* slab, int* tickets,
                          float* hfc, hipStream_t s);
+hipError_t launch_policy_args(const float* h, int64_t n, const PolicyArgs& pa, hipStream_t s, int hid);
 
 hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, double alpha, double eps,
                           const double* norm_partials, int norm_blocks, float clip, const int64_t* ctl,

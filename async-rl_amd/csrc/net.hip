@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "arl_internal.hpp"
 #include "gemm.hpp"
@@ -250,10 +251,8 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   Plans pl = make_plans(net);
   int64_t slab = 0;
   slab = std::max(slab, (int64_t)FC_SPLIT * n * HID);
-  slab = std::max(slab, (int64_t)pl.heads_w * (A + 1) * (HID + 1));
-  slab = std::max(slab, (int64_t)pl.fc_w * HID * (A2 + 1));
+  slab = std::max(slab, (int64_t)pl.fc_w * HID * (A2 + 1));   // run_stage("fc_bwd") timing uses the main slab
   slab = std::max(slab, conv_bwd_slab_floats((int)S));
-  if (arch == ARCH_LSTM) slab = std::max(slab, (int64_t)pl.lstm_w * GATES * (2 * HID + 1));
   if (NAT) slab = nature_slab_floats(net);
   net.slab_floats = slab;
   net.bufs.clear();
@@ -297,6 +296,11 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   net.w_da1 = buf("da1", NAT ? S * NA1 * 4 : 0);
   net.w_da3 = buf("da3", NAT ? S * NA3 * 4 : 0);
   net.w_slab = buf("slab", slab * 4);
+  if (!NAT) {   // the side-stream GEMMs of the backward own their slabs
+    net.w_slab_heads = buf("slab_heads", (int64_t)pl.heads_w * (A + 1) * (HID + 1) * 4);
+    net.w_slab_fc = buf("slab_fc", (int64_t)pl.fc_w * HID * (A2 + 1) * 4);
+    net.w_slab_lstm = buf("slab_lstm", L ? (int64_t)pl.lstm_w * GATES * (2 * HID + 1) * 4 : 0);
+  }
   net.w_norm = buf("norm_partials", (int64_t)net.norm_blocks * 8);
   net.w_tick = buf("tickets", (int64_t)fc_fwd_tiles((int)n) * 4);
   net.w_loss = buf("loss", n * 2 * 4);
@@ -311,6 +315,18 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
 static hipError_t fc_forward(const Net& net, int n, const float* a2, float* hfc, hipStream_t s) {
   return launch_fc_fwd(a2, n, net.p + net.o_fcW, net.p + net.o_fcb, net.at<float>(net.w_slab),
                        net.at<int>(net.w_tick), hfc, s);
+}
+
+// policy / value heads of window slot t (rows n of env 0..n-1) reading h
+static PolicyArgs slot_policy_args(const Net& net, int t, int mode) {
+  const float* P = net.p;
+  const int A = net.A;
+  const int64_t o = (int64_t)t * net.N;
+  return make_policy_args(P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
+                          net.at<int64_t>(net.w_ctl), t, net.env_offset, mode, net.at<float>(net.w_logits) + o * A,
+                          net.at<float>(net.w_probs) + o * A, net.at<float>(net.w_logp) + o * A,
+                          net.at<float>(net.w_v) + o, net.at<float>(net.w_ent) + o, net.at<int32_t>(net.w_act) + o,
+                          net.at<float>(net.w_logpa) + o);
 }
 
 hipError_t net_act(Net& net, int t, int mode, hipStream_t s) {
@@ -352,7 +368,7 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s) {
 hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_t s) {
   if (net.arch == ARCH_FF_NATURE) return nature_forward_f32(net, x, n, mode, s);
   if (net.arch != ARCH_FF || n > net.N) return hipErrorInvalidValue;
-  const int T = net.T, A = net.A, N = net.N;
+  const int T = net.T, N = net.N;
   float* a1 = net.at<float>(net.w_a1) + (int64_t)T * N * A1;
   float* a2 = net.at<float>(net.w_a2) + (int64_t)T * N * A2;
   float* hfc = net.at<float>(net.w_hfc) + (int64_t)T * N * HID;
@@ -364,12 +380,8 @@ hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_
                                                       EpiConv{a2, P + net.o_c2b, C2_OC, C2_P}, n * C2_P, C2_OC, 256,
                                                       1, s)));
   ARL_TRY(fc_forward(net, n, a2, hfc, s));
-  const int64_t o = (int64_t)T * N;
-  return launch_policy(hfc, n, P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
-                       net.at<int64_t>(net.w_ctl), T, net.env_offset, mode, net.at<float>(net.w_logits) + o * A,
-                       net.at<float>(net.w_probs) + o * A, net.at<float>(net.w_logp) + o * A,
-                       net.at<float>(net.w_v) + o, net.at<float>(net.w_ent) + o, net.at<int32_t>(net.w_act) + o,
-                       net.at<float>(net.w_logpa) + o, s);
+  const PolicyArgs pa = slot_policy_args(net, T, mode);
+  return launch_policy_args(hfc, n, pa, s, HID);
 }
 
 // ---------------------------------------------------------------- backward
@@ -390,11 +402,24 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
   const float* hfc = net.at<float>(net.w_hfc);
   const float* hheads = L ? net.at<float>(net.w_hbuf) + (int64_t)n * HID : hfc;   // h fed to pi / v
   float* dfc = net.at<float>(net.w_dfc);
-  // 2. heads: weight grads (ones column = bias) and dh
-  ARL_TRY((launch_gemm<16, 64, 32, 1, 4, GS, GM>(HeadsGA{dl, dv, A}, OnesColB{hheads, HID}, EpiSlab{slab, A + 1, HID + 1},
-                                         A + 1, HID + 1, S, pl.heads_w, s)));
-  ARL_TRY(launch_reduce_grad(slab, pl.heads_w, A + 1, HID + 1,
-                             MapHeads{G, net.o_piW, net.o_pib, net.o_vW, net.o_vb, A, HID}, s));
+  // 2. heads: weight grads (ones column = bias), then dh.  With
+  //    ARL_FORK_BACKWARD=1 the weight-gradient GEMMs (heads, FC, LSTM gates)
+  //    run on side streams beside the main chain (event fork / join, capture
+  //    safe); by default everything is one stream (measured faster).
+  const bool fork = net.side[0] != nullptr;
+  hipStream_t s0 = fork ? net.side[0] : s, s1 = fork ? net.side[1] : s;
+  auto edge = [&](int i, hipStream_t from, hipStream_t to) -> hipError_t {   // to waits for from's work so far
+    if (!fork) return hipSuccess;
+    hipError_t e = hipEventRecord(net.ev[i], from);
+    return e != hipSuccess ? e : hipStreamWaitEvent(to, net.ev[i], 0);
+  };
+  ARL_TRY(edge(0, s, s0));
+  float* slab_h = net.at<float>(net.w_slab_heads);
+  float* slab_f = net.at<float>(net.w_slab_fc);
+  ARL_TRY((launch_gemm<16, 64, 32, 1, 4, GS, GM>(HeadsGA{dl, dv, A}, OnesColB{hheads, HID},
+                                                 EpiSlab{slab_h, A + 1, HID + 1}, A + 1, HID + 1, S, pl.heads_w, s0)));
+  ARL_TRY(launch_reduce_grad(slab_h, pl.heads_w, A + 1, HID + 1,
+                             MapHeads{G, net.o_piW, net.o_pib, net.o_vW, net.o_vb, A, HID}, s0));
   ARL_TRY(launch_heads_bwd(dl, dv, P + net.o_piW, P + net.o_vW, A, HID, L ? nullptr : hfc,
                            L ? net.at<float>(net.w_dh) : dfc, S, s));
   // 3. LSTM: truncated BPTT over the window
@@ -418,28 +443,56 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
         ARL_TRY((launch_gemm<32, 64, 32, 2, 2, GK, GM>(RowMajor{dG + o * GATES, GATES}, RowMajor{P + net.o_llW, HID},
                                                EpiResetMask{dhn, rs + o, HID}, n, HID, GATES, 1, s)));
     }
+    // gate weight grads on side stream 1, dfc on the main stream
+    float* slab_l = net.at<float>(net.w_slab_lstm);
+    ARL_TRY(edge(1, s, s1));
     ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GM, GS>(ColMajor{dG, GATES}, LstmWB{hfc, hbuf, rs},
-                                           EpiSlab{slab, GATES, 2 * HID + 1}, GATES, 2 * HID + 1, S, pl.lstm_w, s)));
-    ARL_TRY(launch_reduce_grad(slab, pl.lstm_w, GATES, 2 * HID + 1,
-                               MapDense{G, net.o_luW, net.o_lub, net.o_llW, HID}, s));
+                                           EpiSlab{slab_l, GATES, 2 * HID + 1}, GATES, 2 * HID + 1, S, pl.lstm_w, s1)));
+    ARL_TRY(launch_reduce_grad(slab_l, pl.lstm_w, GATES, 2 * HID + 1,
+                               MapDense{G, net.o_luW, net.o_lub, net.o_llW, HID}, s1));
     ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GK, GM>(RowMajor{dG, GATES}, RowMajor{P + net.o_luW, HID}, EpiMask{dfc, hfc, HID},
                                            S, HID, GATES, 1, s)));
   }
-  // 4. FC: dW (+ bias via ones column) and da2 = (dfc W) * (a2 > 0)
+  // 4. FC: dW (+ bias via ones column) on side stream 0 (after the heads), and
+  //    da2 = (dfc W) * (a2 > 0) on the main stream
   const float* a2 = net.at<float>(net.w_a2);
   const float* a1 = net.at<float>(net.w_a1);
   float* da2 = net.at<float>(net.w_da2);
-  ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GM, GM>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab, HID, A2 + 1}, HID,
-                                         A2 + 1, S, pl.fc_w, s)));
-  ARL_TRY(launch_reduce_grad(slab, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s));
-  ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GK, GM>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2}, EpiMask{da2, a2, A2}, S, A2,
-                                         HID, 1, s)));
+  ARL_TRY(edge(2, s, s0));
+  ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GM, GM>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab_f, HID, A2 + 1},
+                                                 HID, A2 + 1, S, pl.fc_w, s0)));
+  ARL_TRY(launch_reduce_grad(slab_f, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s0));
+  ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GK, GM>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2},
+                                                 EpiMask{da2, a2, A2}, S, A2, HID, 1, s)));
   // 5. fused conv backward per sample (conv_bwd.hip): conv2 dW/db,
   //    da1 = conv_transpose(da2, W2) * (a1 > 0) kept in LDS, conv1 dW/db
   //    straight from the frame ring
-  return launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl), n,
-                         net.R, S, a1, da2, P + net.o_c2W, slab, G + net.o_c2W, G + net.o_c2b, G + net.o_c1W,
-                         G + net.o_c1b, s);
+  ARL_TRY(launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl), n,
+                          net.R, S, a1, da2, P + net.o_c2W, slab, G + net.o_c2W, G + net.o_c2b, G + net.o_c1W,
+                          G + net.o_c1b, s));
+  // join
+  ARL_TRY(edge(3, s0, s));
+  if (L) ARL_TRY(edge(4, s1, s));
+  return hipSuccess;
+}
+
+hipError_t net_streams_create(Net& net) {
+  // The forked backward measured SLOWER on MI355X (C2 0.454 vs 0.425 ms per
+  // window, C3 1.733 vs 1.705, same box, A/B): the side-stream GEMMs steal CUs
+  // from the critical da2 -> conv_bwd chain and the cross-stream edges add
+  // latency in the graph.  Kept behind ARL_FORK_BACKWARD=1 for experiments.
+  const char* on = getenv("ARL_FORK_BACKWARD");
+  if (on == nullptr || on[0] != '1') return hipSuccess;
+  for (auto& st : net.side) ARL_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  for (auto& e : net.ev) ARL_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return hipSuccess;
+}
+
+void net_streams_destroy(Net& net) {
+  for (auto& st : net.side)
+    if (st) { (void)hipStreamDestroy(st); st = nullptr; }
+  for (auto& e : net.ev)
+    if (e) { (void)hipEventDestroy(e); e = nullptr; }
 }
 
 // One stage of a window on the current workspace contents (arl_run_stage):

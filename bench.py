@@ -280,7 +280,7 @@ def main():
         ]
         kernels = {}
         with torch.cuda.stream(stream):
-            for name, kname, fn, calls, bound, work in specs:
+            for name, kname, fn, calls, bound, work in filter(None, specs):
                 us = timed(fn)
                 if bound == "hbm":
                     ach, peak, unit = work / (us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s"
@@ -298,7 +298,7 @@ def main():
             with open(tf) as f:
                 tj = json.load(f)
             if tj.get("envs") == N and tj.get("t_max") == T and tj.get("arch") == arch:
-                traffic = tj.get("kernels", {}).get(d["kernel"], traffic)
+                traffic = tj.get("kernels", {}).get(d["kernel"].split()[0], traffic)
         roof = {"bound": d["bound"], "kernel": d["kernel"], "achieved": d["achieved"], "peak": d["peak"],
                 "unit": d["unit"], "frac": d["frac"], "traffic": traffic, "avg_launch_us": d["avg_launch_us"],
                 "work_per_launch": d.get("flop_per_launch", d.get("bytes_per_launch")),
