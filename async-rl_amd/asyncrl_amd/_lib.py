@@ -57,6 +57,7 @@ SIGNATURES = {
     "arl_learn": (c_int, [c_void_p, c_double, c_double, c_double, c_int, c_void_p]),
     "arl_optimize": (c_int, [c_void_p, c_double, c_i64, c_i64, c_double, c_double, c_double, c_void_p]),
     "arl_advance": (c_int, [c_void_p, c_void_p]),
+    "arl_optimize_advance": (c_int, [c_void_p, c_double, c_i64, c_i64, c_double, c_double, c_double, c_void_p]),
     "arl_forward_states": (c_int, [c_void_p, c_void_p, c_i64, c_int, c_void_p]),
     "arl_rmsprop": (c_int, [c_void_p, c_void_p, c_void_p, c_i64, c_double, c_double, c_double, c_double,
                             c_void_p, c_void_p]),

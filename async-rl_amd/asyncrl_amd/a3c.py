@@ -127,8 +127,7 @@ class A3C:
         net = self.net
         net.learn(self.gamma, self.beta, self.v_loss_coef, self.clip_reward, stream=stream)
         allreduce_grads(net.grads, self.pg)
-        self.optimizer.update(stream=stream)
-        net.advance(stream=stream)
+        self.optimizer.update(stream=stream, advance_window=True)
 
     def act(self, pairs: torch.Tensor, reward=None, is_state_terminal=None) -> torch.Tensor:
         """a3c.py:67-167, batched.  pairs: (n, 2, 210, 160, 3) uint8 device
@@ -181,8 +180,7 @@ class A3C:
 
     def finish_window(self, stream=None):
         allreduce_grads(self.net.grads, self.pg)
-        self.optimizer.update(stream=stream)
-        self.net.advance(stream=stream)
+        self.optimizer.update(stream=stream, advance_window=True)
         self.t += self.t_max
 
     # ------------------------------------------------------------ checkpoints

@@ -56,13 +56,15 @@ class RMSpropAsync:
                 return h.threshold
         return 0.0
 
-    def update(self, stream=None):
+    def update(self, stream=None, advance_window=False):
         """GradientClipping hook(s) then update_one for every parameter,
-        on the bound model's device buffers (a3c.py:139)."""
+        on the bound model's device buffers (a3c.py:139).  advance_window:
+        also end the lockstep window (arl_optimize_advance)."""
         net = self.target.net
         self.t += 1
         net.optimize(lr0=self.lr, total_steps=self.anneal_total_steps, n_total=self.n_total_envs,
-                     alpha=self.alpha, eps=self.eps, clip=self.clip_threshold, stream=stream)
+                     alpha=self.alpha, eps=self.eps, clip=self.clip_threshold, stream=stream,
+                     advance=advance_window)
 
     def update_arrays(self, param: torch.Tensor, ms: torch.Tensor, grad: torch.Tensor, stream=None):
         """update_one on explicit flat f32 device tensors (the drop-in for

@@ -209,6 +209,13 @@ int arl_optimize(arl_net* h, double lr0, int64_t total_steps, int64_t n_total, d
   return hip_status(arl::net_optimize(h->net, lr0, total_steps, n_total, alpha, eps, (float)clip, S(s)), "optimize");
 }
 
+int arl_optimize_advance(arl_net* h, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
+                         double clip, void* s) {
+  NEED_BOUND(h);
+  return hip_status(arl::net_optimize(h->net, lr0, total_steps, n_total, alpha, eps, (float)clip, S(s), true),
+                    "optimize_advance");
+}
+
 int arl_advance(arl_net* h, void* s) {
   NEED_BOUND(h);
   return hip_status(arl::net_advance(h->net, S(s)), "advance");

@@ -100,7 +100,7 @@ void net_streams_destroy(Net& net);
 hipError_t net_act(Net& net, int t, int mode, hipStream_t s);   // mode: 0 none, 1 sample, 2 greedy
 hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s);
 hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
-                        float clip, hipStream_t s);
+                        float clip, hipStream_t s, bool advance = false);
 hipError_t net_advance(Net& net, hipStream_t s);
 enum Stage { STAGE_CONV_FWD = 1, STAGE_FC_FWD = 2, STAGE_POLICY = 3, STAGE_FC_BWD = 4, STAGE_CONV_BWD = 5 };
 hipError_t net_stage(Net& net, int stage, int t, hipStream_t s);

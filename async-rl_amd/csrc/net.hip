@@ -542,13 +542,17 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
 }
 
 hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
-                        float clip, hipStream_t s) {
+                        float clip, hipStream_t s, bool advance) {
   double* parts = net.at<double>(net.w_norm);
   const bool do_clip = clip > 0.f;
   if (do_clip) ARL_TRY(launch_grad_sqnorm(net.g, net.param_floats, parts, net.norm_blocks, s));
-  return launch_rmsprop(net.p, net.ms, net.g, net.param_floats, lr0, alpha, eps, do_clip ? parts : nullptr,
-                        net.norm_blocks, clip, total_steps > 0 ? net.at<int64_t>(net.w_ctl) : nullptr, total_steps,
-                        n_total, net.T, s);
+  ARL_TRY(launch_rmsprop(net.p, net.ms, net.g, net.param_floats, lr0, alpha, eps, do_clip ? parts : nullptr,
+                         net.norm_blocks, clip, total_steps > 0 ? net.at<int64_t>(net.w_ctl) : nullptr, total_steps,
+                         n_total, net.T, s));
+  // (Folding the advance into the update's last workgroup through a device
+  // ticket was measured: 662 workgroups on one ticket cost the update more
+  // than the 4 us advance launch it saves.  Kept as two launches.)
+  return advance ? net_advance(net, s) : hipSuccess;
 }
 
 hipError_t net_advance(Net& net, hipStream_t s) {

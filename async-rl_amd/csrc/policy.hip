@@ -57,26 +57,37 @@ hipError_t launch_policy(const float* h, int64_t n, const float* Wpi, const floa
                                                    probs, logp, v, ent, act, logp_a), s, hid);
 }
 
-// a3c.py:82-126 over a lockstep window, one thread per env.
+// a3c.py:82-126 over a lockstep window, one thread per (step t, env).
 // rewards/dones (T, n); v/probs/logp/act indexed (T+1, n[, A]) with row T =
 // the bootstrap value v(s_T) computed with the pre-update parameters.
 // R accumulates in float64 (Python float at a3c.py:83-92) and restarts at 0
 // at every terminal, so each episode segment in the window is one a3c update.
-__global__ void returns_kernel(const float* __restrict__ rewards, const uint8_t* __restrict__ dones,
-                               const float* __restrict__ v, const float* __restrict__ probs,
-                               const float* __restrict__ logp, const int32_t* __restrict__ act, int T, int n,
-                               int A, double gamma, float beta, float vcoef, int clip_reward,
-                               float* __restrict__ dlogits, float* __restrict__ dv, float* __restrict__ loss) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  double R = (double)v[(int64_t)T * n + e];
-  float pi_loss = 0.f, v_loss = 0.f;
-  for (int t = T - 1; t >= 0; --t) {
+// Thread (t, e) runs the reverse recurrence R = R*gamma + r from T-1 down to
+// its own t -- the same operations in the same order as a sequential scan, so
+// R_t is bit-identical -- with every reward / done of its env loaded up front
+// (no dependent loads in the chain).  The per-env losses are then summed in
+// the reference's order (t = T-1 .. 0) through LDS.
+// Block = EB envs x T steps (EB = 256 / T), env fastest.
+__global__ void __launch_bounds__(256)
+returns_kernel(const float* __restrict__ rewards, const uint8_t* __restrict__ dones, const float* __restrict__ v,
+               const float* __restrict__ probs, const float* __restrict__ logp, const int32_t* __restrict__ act, int T,
+               int n, int A, double gamma, float beta, float vcoef, int clip_reward, float* __restrict__ dlogits,
+               float* __restrict__ dv, float* __restrict__ loss) {
+  __shared__ float lpi[256], lv[256];
+  const int EB = 256 / T;
+  const int tid = threadIdx.x, t = tid / EB, el = tid - t * EB;
+  const int e = blockIdx.x * EB + el;
+  const bool on = t < T && e < n;
+  if (on) {
+    double R = (double)v[(int64_t)T * n + e];
+    for (int tt = T - 1; tt >= t; --tt) {
+      const int64_t i = (int64_t)tt * n + e;
+      double r = (double)rewards[i];
+      if (clip_reward) r = r < -1.0 ? -1.0 : (r > 1.0 ? 1.0 : r);
+      if (dones[i]) R = 0.0;
+      R = __dadd_rn(__dmul_rn(R, gamma), r);
+    }
     const int64_t i = (int64_t)t * n + e;
-    double r = (double)rewards[i];
-    if (clip_reward) r = r < -1.0 ? -1.0 : (r > 1.0 ? 1.0 : r);
-    if (dones[i]) R = 0.0;
-    R = __dadd_rn(__dmul_rn(R, gamma), r);
     const float Rf = (float)R;
     const float vi = v[i];
     const float adv = __fsub_rn(Rf, vi);
@@ -95,10 +106,17 @@ __global__ void returns_kernel(const float* __restrict__ rewards, const uint8_t*
     }
     const float dvv = __fsub_rn(vi, Rf);
     dv[i] = __fmul_rn(vcoef, dvv);
-    pi_loss = __fsub_rn(pi_loss, __fadd_rn(__fmul_rn(lp[a], adv), __fmul_rn(beta, H)));
-    v_loss = __fadd_rn(v_loss, __fmul_rn(vcoef, __fmul_rn(__fmul_rn(dvv, dvv), 0.5f)));
+    lpi[tid] = __fadd_rn(__fmul_rn(lp[a], adv), __fmul_rn(beta, H));
+    lv[tid] = __fmul_rn(vcoef, __fmul_rn(__fmul_rn(dvv, dvv), 0.5f));
   }
-  if (loss) {
+  if (loss == nullptr) return;
+  __syncthreads();
+  if (t == 0 && on) {
+    float pi_loss = 0.f, v_loss = 0.f;
+    for (int tt = T - 1; tt >= 0; --tt) {
+      pi_loss = __fsub_rn(pi_loss, lpi[tt * EB + el]);
+      v_loss = __fadd_rn(v_loss, lv[tt * EB + el]);
+    }
     loss[2 * e] = pi_loss;
     loss[2 * e + 1] = v_loss;
   }
@@ -108,7 +126,9 @@ hipError_t launch_returns(const float* rewards, const uint8_t* dones, const floa
                           const float* logp, const int32_t* act, int T, int n, int A, double gamma, float beta,
                           float vcoef, int clip_reward, float* dlogits, float* dv, float* loss, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(returns_kernel, dim3((n + 255) / 256), dim3(256), 0, s, rewards, dones, v, probs, logp, act, T,
+  if (T < 1 || T > 256) return hipErrorInvalidValue;
+  const int EB = 256 / T;
+  hipLaunchKernelGGL(returns_kernel, dim3((n + EB - 1) / EB), dim3(256), 0, s, rewards, dones, v, probs, logp, act, T,
                      n, A, gamma, beta, vcoef, clip_reward, dlogits, dv, loss);
   return hipGetLastError();
 }

@@ -137,6 +137,11 @@ int arl_run_stage(arl_net* net, int stage, int t, void* stream);
 /* End of window: advance step counters, carry reset flags / LSTM state. */
 int arl_advance(arl_net* net, void* stream);
 
+/* arl_optimize followed by arl_advance (the end of a3c.py's update,
+ * a3c.py:139-144) in one call. */
+int arl_optimize_advance(arl_net* net, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
+                         double clip, void* stream);
+
 /* A3CFF.pi_and_v on explicit f32 states (a3c_ale.py:38-40; input from
  * dqn_phi).  n <= n_envs; outputs in the workspace's bootstrap slot.  mode
  * as arl_act_mode: 0 no action, 1 sampled (action_indices, Philox counter =
