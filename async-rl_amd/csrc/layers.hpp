@@ -41,6 +41,7 @@ struct EpiConv {        // out[s][n][p] = relu(v + b[n]); m = s*P + p
   }
 };
 struct EpiSlab {
+  static constexpr bool kRow4 = false;
   float* __restrict__ slab; int M, N;
   __device__ void store(int m, int n, float v, int z) const {
     slab[((int64_t)z * M + m) * N + n] = v;
@@ -51,10 +52,29 @@ struct EpiBias {        // out[m][n] = v + b[n]
   __device__ void store(int m, int n, float v, int) const { out[(int64_t)m * ld + n] = __fadd_rn(v, b[n]); }
 };
 struct EpiMask {        // out[m][n] = mask[m][n] > 0 ? v : 0  (ReLU backward)
+  static constexpr bool kRow4 = false;
   float* __restrict__ out; const float* __restrict__ mask; int ld;
   __device__ void store(int m, int n, float v, int) const {
     const int64_t i = (int64_t)m * ld + n;
     out[i] = mask[i] > 0.f ? v : 0.f;
+  }
+};
+
+struct EpiMask4 {       // EpiMask with 16-byte row pieces (gemm_planes row epilogue; ld % 4 == 0)
+  static constexpr bool kRow4 = true;
+  float* __restrict__ out; const float* __restrict__ mask; int ld;
+  __device__ void store4(int m, int n, float4 v, int) const {
+    const int64_t i = (int64_t)m * ld + n;
+    const float4 k = *reinterpret_cast<const float4*>(mask + i);
+    *reinterpret_cast<float4*>(out + i) =
+        make_float4(k.x > 0.f ? v.x : 0.f, k.y > 0.f ? v.y : 0.f, k.z > 0.f ? v.z : 0.f, k.w > 0.f ? v.w : 0.f);
+  }
+};
+struct EpiSlab4 {       // EpiSlab with 16-byte row pieces (N % 4 == 0)
+  static constexpr bool kRow4 = true;
+  float* __restrict__ slab; int M, N;
+  __device__ void store4(int m, int n, float4 v, int z) const {
+    *reinterpret_cast<float4*>(slab + ((int64_t)z * M + m) * N + n) = v;
   }
 };
 

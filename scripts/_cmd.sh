@@ -1,5 +1,4 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-bash scripts/gpu_quick.sh r1 "" "--steps 100 --warmup 10 --cpu-seconds 0 --kernel-reps 20" || exit $?
-timeout -k 10 300 python -u bench.py --workload c3 --steps 40 --warmup 5 --cpu-seconds 0 --kernel-reps 3 > gpurun_out/r1/bench_c3.log 2>&1 || exit $?
-bash scripts/gpu_prof.sh r1 "--steps 10 --warmup 3 --cpu-seconds 0 --kernel-reps 5"
+mkdir -p gpurun_out/gp
+timeout -k 10 120 ./scripts/gemm_planes_bench > gpurun_out/gp/planes.log 2>&1; rc=$?; cat gpurun_out/gp/planes.log; exit $rc

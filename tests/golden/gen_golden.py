@@ -32,28 +32,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference"
 sys.path.insert(0, os.path.join(REPO, "oracle"))
+sys.path.insert(0, os.path.dirname(HERE))
 import oracle  # noqa: E402
-
-
-def synth_frames(rng, n, kind):
-    """Synthetic 210x160x3 uint8 frames: uniform, sparse palette
-    blocks on black ("Breakout-shaped"), all-255, all-0."""
-    if kind == "uniform":
-        return rng.integers(0, 256, (n, 210, 160, 3), dtype=np.uint8)
-    if kind == "white":
-        return np.full((n, 210, 160, 3), 255, np.uint8)
-    if kind == "black":
-        return np.zeros((n, 210, 160, 3), np.uint8)
-    if kind == "palette":
-        pal = rng.integers(0, 256, (16, 3), dtype=np.uint8)
-        out = np.zeros((n, 210, 160, 3), np.uint8)
-        for i in range(n):
-            for _ in range(40):
-                y, x = rng.integers(0, 200), rng.integers(0, 150)
-                h, w = rng.integers(2, 10), rng.integers(2, 12)
-                out[i, y:y + h, x:x + w] = pal[rng.integers(0, 16)]
-        return out
-    raise ValueError(kind)
+from fake_ale import FakeALE, synth_frames  # noqa: E402  (tests/fake_ale.py)
 
 
 # --------------------------------------------------------------------------
@@ -73,49 +54,6 @@ def install_cv2_stub():
 
     cv2.resize = resize
     sys.modules["cv2"] = cv2
-
-
-class FakeALE:
-    """Stand-in for ale_python_interface.ALEInterface serving seeded frames.
-    Episode: lives 3, a life lost at frame 22, game over at frame 41."""
-
-    def __init__(self):
-        self.rng = np.random.default_rng(11)
-        self.frame = 0
-        self.start = 0
-        self._lives = 3
-        self._over = False
-        self.served = []
-
-    def setInt(self, *a): pass
-    def setFloat(self, *a): pass
-    def setBool(self, *a): pass
-    def setString(self, *a): pass
-    def loadROM(self, *a): pass
-    def getFrameNumber(self): return 0
-    def getMinimalActionSet(self): return [0, 1, 3, 4]
-
-    def getScreenRGB(self):
-        f = synth_frames(np.random.default_rng(1000 + self.frame), 1, "palette")[0]
-        if self.frame % 7 == 3:
-            f[::2, ::3] = 255
-        return f
-
-    def act(self, a):
-        self.frame += 1
-        if self.frame - self.start == 22:
-            self._lives -= 1
-        if self.frame - self.start >= 41:
-            self._over = True
-        return int(self.frame % 5 == 0)
-
-    def lives(self): return self._lives
-    def game_over(self): return self._over
-
-    def reset_game(self):
-        self.start = self.frame
-        self._over = False
-        self._lives = 3
 
 
 def install_ale_stub():
@@ -206,6 +144,51 @@ def gen_phi():
     sys.path.remove(REF)
 
 
+def gen_ale_env():
+    """ale.ALE (ale.py:11-161) driven like a3c_ale.py's train loop over an
+    action-sensitive fake emulator: per receive_action the action, reward,
+    terminal flag and the raw frame pair behind the next observation (the
+    pair of the following initialize() when the step was terminal)."""
+    import fake_ale
+    install_cv2_stub()
+    m = types.ModuleType("ale_python_interface")
+    m.ALEInterface = fake_ale.FakeALEActions
+    sys.modules["ale_python_interface"] = m
+    sys.path.insert(0, REF)
+    for k in [k for k in sys.modules if k == "ale"]:
+        del sys.modules[k]
+    import ale  # reference ale.py
+    pairs = []
+    orig_cs = ale.ALE.current_screen
+
+    def logged_cs(self):
+        pairs.append((self.ale.getScreenRGB().copy(), self.last_raw_screen.copy()))
+        return orig_cs(self)
+
+    ale.ALE.current_screen = logged_cs
+    np.random.seed(7)
+    env = ale.ALE("fake.rom", seed=3, max_start_nullops=6)
+    actions = np.random.default_rng(8).integers(0, 4, 48)
+    rewards, dones, idx = [], [], [len(pairs) - 1]
+    for a in actions:
+        r = env.receive_action(int(a))
+        term = bool(env.is_terminal)
+        if term:
+            env.initialize()
+        rewards.append(r)
+        dones.append(term)
+        idx.append(len(pairs) - 1)
+    ale.ALE.current_screen = orig_cs
+    sel = [pairs[i] for i in idx]
+    np.savez_compressed(os.path.join(HERE, "ale_env_golden.npz"), actions=actions,
+                        rewards=np.array(rewards, np.float32), dones=np.array(dones),
+                        pair_cur=np.stack([p[0] for p in sel]), pair_prev=np.stack([p[1] for p in sel]),
+                        emulator_actions=np.array(env.ale.actions))
+    sys.path.remove(REF)
+    del sys.modules["ale"]
+    sys.modules["ale_python_interface"].ALEInterface = FakeALE
+
+
 def gen_dqn_phi():
     sys.path.insert(0, REF)
     import dqn_phi  # reference dqn_phi.py, imported directly
@@ -263,7 +246,12 @@ def gen_checkpoint():
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1:            # e.g. gen_golden.py gen_ale_env
+        for name in sys.argv[1:]:
+            globals()[name]()
+        sys.exit(0)
     gen_phi()
+    gen_ale_env()
     gen_dqn_phi()
     gen_rmsprop()
     gen_checkpoint()
