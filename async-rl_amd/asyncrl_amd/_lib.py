@@ -79,6 +79,7 @@ ARCH_LSTM = 1
 ARCH_FF_NATURE = 2   # A3CFF with NatureDQNHead (dqn_head.py:6-28)
 RESIZE_SCALAR = 0
 RESIZE_SIMD = 1
+RESIZE_CROP = 2      # flag, combine with SCALAR / SIMD: ale.py crop_or_scale='crop'
 
 
 class ArlError(RuntimeError):

@@ -39,7 +39,7 @@ int arl_current_screen(const uint8_t* cur, const uint8_t* prev, uint8_t* out, in
   if (n < 0 || (n > 0 && (!cur || !prev || !out))) return fail(ARL_EINVAL, "current_screen: null pointer / n < 0");
   if (!aligned(cur, 16) || !aligned(prev, 16) || !aligned(out, 4))
     return fail(ARL_EINVAL, "current_screen: frames must be 16-byte aligned, out 4-byte aligned");
-  if (mode != ARL_RESIZE_SCALAR && mode != ARL_RESIZE_SIMD) return fail(ARL_EINVAL, "bad resize_mode");
+  if (mode < 0 || mode > (ARL_RESIZE_SIMD | ARL_RESIZE_CROP)) return fail(ARL_EINVAL, "bad resize_mode");
   if (n > 65535) return fail(ARL_EINVAL, "current_screen: n > 65535 per call");
   return hip_status(arl::launch_current_screen(cur, prev, out, n, mode, S(s)), "current_screen");
 }
@@ -57,7 +57,7 @@ int arl_phi_stack(const uint8_t* pairs, const uint8_t* prev_stack, const uint8_t
   if (!aligned(pairs, 16) || !aligned(prev_stack, 16) || !aligned(out_stack, 16))
     return fail(ARL_EINVAL, "phi_stack: buffers must be 16-byte aligned");
   if (prev_stack == out_stack && n > 0) return fail(ARL_EINVAL, "phi_stack: prev_stack and out_stack alias");
-  if (mode != ARL_RESIZE_SCALAR && mode != ARL_RESIZE_SIMD) return fail(ARL_EINVAL, "bad resize_mode");
+  if (mode < 0 || mode > (ARL_RESIZE_SIMD | ARL_RESIZE_CROP)) return fail(ARL_EINVAL, "bad resize_mode");
   if (n > 65535) return fail(ARL_EINVAL, "phi_stack: n > 65535 per call");
   return hip_status(arl::launch_phi_stack(pairs, prev_stack, reset, out_stack, n, mode, S(s)), "phi_stack");
 }
@@ -157,7 +157,7 @@ int arl_observe(arl_net* h, int t, const uint8_t* pair_pool, const float* reward
   if (t < 0 || t > n.T) return fail(ARL_EINVAL, "observe: t out of [0, t_max]");
   if (!pair_pool || pool_len < 1) return fail(ARL_EINVAL, "observe: need pair_pool and pool_len >= 1");
   if (!aligned(pair_pool, 16)) return fail(ARL_EINVAL, "observe: pair_pool must be 16-byte aligned");
-  if (mode != ARL_RESIZE_SCALAR && mode != ARL_RESIZE_SIMD) return fail(ARL_EINVAL, "bad resize_mode");
+  if (mode < 0 || mode > (ARL_RESIZE_SIMD | ARL_RESIZE_CROP)) return fail(ARL_EINVAL, "bad resize_mode");
   if (n.N > 65535) return fail(ARL_EINVAL, "observe: n_envs > 65535");
   arl::RingArgs a;
   a.pair_pool = pair_pool;

@@ -4,7 +4,10 @@
 // frames, float64 luminance R*0.2126 + G*0.0722 + B*0.7152, astype(uint8),
 // cv2.resize(img, (84, 84), INTER_LINEAR)), ale.py:135 / :155-158 (4-plane
 // deque, reset to three zero planes + the new screen), dqn_phi.py:14-16
-// (f32 /= 255).
+// (f32 /= 255).  Resize mode bits: 1 = SIMD vertical pass, 2 = the 'crop'
+// branch of ale.py:73-82 (resize to 84 x 110, keep rows 18..101: only the
+// vertical coefficients change -- output row dy uses row dy + 18 of a
+// 210 -> 110 resize).
 //
 // One workgroup (256 threads) = one env x one band of 12 output rows (7 bands
 // per 84x84 screen).  Only the source rows the bilinear taps touch are read
@@ -25,6 +28,7 @@ constexpr int SRC_H = 210, SRC_W = 160, DST = 84;
 constexpr int BAND = 12;                   // output rows per workgroup
 constexpr int NBANDS = DST / BAND;         // 7
 constexpr int FRAME_BYTES = SRC_H * SRC_W * 3;   // 100,800
+constexpr int CROP_H = 110, CROP_TOP = (110 - 84) - 8;   // ale.py:75-81: resize to 110 rows, crop 18 .. 101
 
 
 // OpenCV INTER_LINEAR coefficients for one axis (see oracle.resize_coeffs):
@@ -79,7 +83,8 @@ __device__ inline void phi_band(const uint8_t* __restrict__ cur, const uint8_t* 
     sh.xofs[tid] = (int16_t)o; sh.xa0[tid] = (int16_t)a0; sh.xa1[tid] = (int16_t)a1;
   } else if (tid >= 96 && tid < 96 + BAND) {
     int o, b0, b1;
-    resize_coeff(dy0 + tid - 96, SRC_H, DST, o, b0, b1);
+    if (mode & 2) resize_coeff(dy0 + tid - 96 + CROP_TOP, SRC_H, CROP_H, o, b0, b1);
+    else resize_coeff(dy0 + tid - 96, SRC_H, DST, o, b0, b1);
     sh.yofs[tid - 96] = (int16_t)o; sh.yb0[tid - 96] = (int16_t)b0; sh.yb1[tid - 96] = (int16_t)b1;
   }
   __syncthreads();
@@ -123,7 +128,7 @@ __device__ inline void phi_band(const uint8_t* __restrict__ cur, const uint8_t* 
       const int r0 = (int)sh.gray[ly][0][sx] * a0 + (int)sh.gray[ly][0][sx1] * a1;
       const int r1 = (int)sh.gray[ly][1][sx] * a0 + (int)sh.gray[ly][1][sx1] * a1;
       int v;
-      if (mode == 0) {         // FixedPtCast<int, uchar, 22>
+      if ((mode & 1) == 0) {   // FixedPtCast<int, uchar, 22>
         v = (b0 * r0 + b1 * r1 + (1 << 21)) >> 22;
       } else {                 // VResizeLinearVec_32s8u (mulhi form)
         v = ((((r0 >> 4) * b0) >> 16) + (((r1 >> 4) * b1) >> 16) + 2) >> 2;

@@ -32,6 +32,7 @@ extern "C" {
 
 #define ARL_RESIZE_SCALAR 0  /* OpenCV FixedPtCast vertical pass (canonical) */
 #define ARL_RESIZE_SIMD 1    /* OpenCV VResizeLinearVec_32s8u (mulhi) pass */
+#define ARL_RESIZE_CROP 2    /* flag: ale.py:73-82 crop_or_scale='crop' (84x110 resize, rows 18..101) */
 
 int arl_abi_version(void);
 const char* arl_last_error(void);

@@ -91,22 +91,30 @@ _YOFS, _YBETA = resize_coeffs(SRC_H, DST)
 
 RESIZE_SCALAR = 0   # FixedPtCast<int,uchar,22>: (b0*r0 + b1*r1 + 2^21) >> 22
 RESIZE_SIMD = 1     # VResizeLinearVec_32s8u: ((r0>>4)*b0>>16)+((r1>>4)*b1>>16)+2 >> 2
+RESIZE_CROP = 2     # flag: ale.py:73-82 -- cv2.resize(img, (84, 110)), keep rows [18, 102)
+
+_CROP_TOP = (110 - 84) - 8                       # ale.py:78-80: unused_height - bottom_crop
+_YOFS_C, _YBETA_C = (a[_CROP_TOP:_CROP_TOP + DST] for a in resize_coeffs(SRC_H, 110))
 
 
 def resize_linear_u8(img: np.ndarray, mode: int = RESIZE_SCALAR) -> np.ndarray:
     """cv2.resize(img, (84,84), INTER_LINEAR) for a (..., 210, 160) uint8
     plane (ale.py:84-85).  Horizontal pass: int row = S[sx]*a0 + S[sx+1]*a1
-    (HResizeLinear, exact); vertical pass per `mode`."""
+    (HResizeLinear, exact); vertical pass per `mode` (bit 0: SIMD form).
+    mode & RESIZE_CROP: rows 18..101 of cv2.resize(img, (84, 110)) instead
+    (ale.py:73-82) -- the same passes with the 210 -> 110 row coefficients."""
     src = img.astype(np.int64)
     xs = _XOFS
     xs1 = np.minimum(xs + 1, SRC_W - 1)
     rows = src[..., :, xs] * _XALPHA[:, 0] + src[..., :, xs1] * _XALPHA[:, 1]
-    ys = _YOFS
+    yofs, ybeta = (_YOFS_C, _YBETA_C) if mode & RESIZE_CROP else (_YOFS, _YBETA)
+    ys = yofs
     ys1 = np.minimum(ys + 1, SRC_H - 1)
     r0 = rows[..., ys, :]
     r1 = rows[..., ys1, :]
-    b0 = _YBETA[:, 0][:, None]
-    b1 = _YBETA[:, 1][:, None]
+    b0 = ybeta[:, 0][:, None]
+    b1 = ybeta[:, 1][:, None]
+    mode &= ~RESIZE_CROP
     if mode == RESIZE_SCALAR:
         out = (b0 * r0 + b1 * r1 + (1 << 21)) >> 22
     elif mode == RESIZE_SIMD:
@@ -118,8 +126,9 @@ def resize_linear_u8(img: np.ndarray, mode: int = RESIZE_SCALAR) -> np.ndarray:
 
 def current_screen(cur: np.ndarray, prev: np.ndarray,
                    mode: int = RESIZE_SCALAR) -> np.ndarray:
-    """ale.py:59-89 (crop_or_scale='scale', the default at ale.py:18):
-    max of two frames -> luminance -> uint8 -> 84x84 resize."""
+    """ale.py:59-89 (crop_or_scale='scale', the default at ale.py:18; 'crop'
+    with mode | RESIZE_CROP): max of two frames -> luminance -> uint8 ->
+    84x84 resize."""
     assert cur.shape[-3:] == (SRC_H, SRC_W, 3)
     return resize_linear_u8(luminance_u8(max_pool_pair(cur, prev)), mode)
 

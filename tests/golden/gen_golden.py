@@ -43,13 +43,27 @@ from fake_ale import FakeALE, synth_frames  # noqa: E402  (tests/fake_ale.py)
 RESIZE_LOG = []
 
 
+def _resize_rows(img, dst_h):
+    """84-column, dst_h-row restatement of the OpenCV resize (the oracle's
+    passes with the 210 -> dst_h row coefficients) for the cv2 stub."""
+    ys, yb = oracle.resize_coeffs(oracle.SRC_H, dst_h)
+    src = img.astype(np.int64)
+    xs, xa = oracle.resize_coeffs(oracle.SRC_W, oracle.DST)
+    rows = src[:, xs] * xa[:, 0] + src[:, np.minimum(xs + 1, oracle.SRC_W - 1)] * xa[:, 1]
+    r0, r1 = rows[ys, :], rows[np.minimum(ys + 1, oracle.SRC_H - 1), :]
+    out = (yb[:, 0][:, None] * r0 + yb[:, 1][:, None] * r1 + (1 << 21)) >> 22
+    return np.clip(out, 0, 255).astype(np.uint8)
+
+
 def install_cv2_stub():
     cv2 = types.ModuleType("cv2")
     cv2.INTER_LINEAR = 1
 
     def resize(img, dsize, interpolation=None):
-        assert dsize == (84, 84) and interpolation == 1
+        assert dsize in ((84, 84), (84, 110)) and interpolation == 1
         RESIZE_LOG.append(np.array(img, copy=True))
+        if dsize == (84, 110):          # ale.py:75-76, the 'crop' branch
+            return _resize_rows(img, 110)
         return oracle.resize_linear_u8(img, oracle.RESIZE_SCALAR)
 
     cv2.resize = resize
@@ -141,6 +155,26 @@ def gen_phi():
                         pair_cur=cur_f, pair_prev=prev_f,
                         states=np.stack(states), terminal=np.array(terms),
                         reset=np.array(resets), pair_idx=np.array(pair_idx))
+    sys.path.remove(REF)
+
+
+def gen_phi_crop():
+    """ale.py:73-82 (crop_or_scale='crop') run verbatim on the phi_golden
+    frame pairs: pins the crop window (rows 18..101 of the 84 x 110 resize);
+    the resize itself is the stub's restatement (unpinned, as for 'scale')."""
+    install_cv2_stub()
+    install_ale_stub()
+    sys.path.insert(0, REF)
+    import ale  # reference ale.py
+    d = np.load(os.path.join(HERE, "phi_golden.npz"))
+    shots = []
+    for i in range(d["cur"].shape[0]):
+        env = ale.ALE.__new__(ale.ALE)
+        env.crop_or_scale = "crop"
+        env.ale = types.SimpleNamespace(getScreenRGB=lambda i=i: d["cur"][i])
+        env.last_raw_screen = d["prev"][i]
+        shots.append(env.current_screen())
+    np.savez_compressed(os.path.join(HERE, "phi_crop_golden.npz"), screen_crop=np.stack(shots))
     sys.path.remove(REF)
 
 
@@ -251,6 +285,7 @@ if __name__ == "__main__":
             globals()[name]()
         sys.exit(0)
     gen_phi()
+    gen_phi_crop()
     gen_ale_env()
     gen_dqn_phi()
     gen_rmsprop()

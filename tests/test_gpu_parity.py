@@ -44,10 +44,16 @@ def test_current_screen_matches_reference_golden(gpu):
     simd = current_screen(cur, prev, 1).cpu().numpy()
     ref = np.stack([O.current_screen(c, p, O.RESIZE_SIMD) for c, p in zip(d["cur"], d["prev"])])
     assert (simd == ref).all()
+    # ale.py:73-82 crop branch (RESIZE_CROP flag), both vertical-pass forms
+    crop = current_screen(cur, prev, O.RESIZE_CROP).cpu().numpy()
+    assert (crop == golden("phi_crop_golden.npz")["screen_crop"]).all()
+    crop_simd = current_screen(cur, prev, O.RESIZE_CROP | O.RESIZE_SIMD).cpu().numpy()
+    ref = np.stack([O.current_screen(c, p, O.RESIZE_CROP | O.RESIZE_SIMD) for c, p in zip(d["cur"], d["prev"])])
+    assert (crop_simd == ref).all()
 
 
-@pytest.mark.parametrize("kind", ["uniform", "palette"])
-def test_phi_stack_matches_oracle(gpu, kind):
+@pytest.mark.parametrize("kind,mode", [("uniform", 0), ("palette", 0), ("uniform", 2), ("palette", 3)])
+def test_phi_stack_matches_oracle(gpu, kind, mode):
     from asyncrl_amd import phi_stack
     rng = np.random.default_rng(11)
     n = 37
@@ -55,9 +61,9 @@ def test_phi_stack_matches_oracle(gpu, kind):
     pairs = pairs[0]
     prev = rng.integers(0, 256, (n, 4, 84, 84), dtype=np.uint8)
     reset = (rng.random(n) < 0.3).astype(np.uint8)
-    out = phi_stack(dev(pairs, gpu), dev(prev, gpu), dev(reset, gpu)).cpu().numpy()
+    out = phi_stack(dev(pairs, gpu), dev(prev, gpu), dev(reset, gpu), resize_mode=mode).cpu().numpy()
     for e in range(n):
-        scr = O.current_screen(pairs[e, 0], pairs[e, 1])
+        scr = O.current_screen(pairs[e, 0], pairs[e, 1], mode)
         assert (out[e] == O.stack_push(prev[e], scr, bool(reset[e]))).all(), e
 
 
