@@ -142,9 +142,12 @@ class DeviceNet:
     def optimize(self, lr0=7e-4, total_steps=0, n_total=0, alpha=0.99, eps=0.1, clip=40.0, stream=None,
                  advance=False):
         """Clip + RMSProp; advance=True also ends the window (arl_optimize_advance)."""
-        fn = lib.arl_optimize_advance if advance else lib.arl_optimize
-        check(fn(self._h, lr0, int(total_steps), int(n_total), alpha, eps, clip, stream_handle(stream)),
-              "arl_optimize_advance" if advance else "arl_optimize")
+        if advance:
+            check(lib.arl_optimize_advance(self._h, lr0, int(total_steps), int(n_total), alpha, eps, clip,
+                                           stream_handle(stream)), "arl_optimize_advance")
+        else:
+            check(lib.arl_optimize(self._h, lr0, int(total_steps), int(n_total), alpha, eps, clip,
+                                   stream_handle(stream)), "arl_optimize")
 
     def advance(self, stream=None):
         check(lib.arl_advance(self._h, stream_handle(stream)), "arl_advance")

@@ -12,7 +12,6 @@
 struct arl_net {
   arl::Net net;
   bool bound = false;
-  bool streams_made = false;
 };
 
 namespace {
@@ -80,10 +79,7 @@ int arl_net_create(arl_net** out, int arch, int n_actions, int n_envs, int t_max
   return ARL_OK;
 }
 
-void arl_net_destroy(arl_net* h) {
-  if (h) arl::net_streams_destroy(h->net);
-  delete h;
-}
+void arl_net_destroy(arl_net* h) { delete h; }
 
 int64_t arl_net_param_floats(const arl_net* h) { return h ? h->net.param_floats : -1; }
 int arl_net_param_count(const arl_net* h) { return h ? (int)h->net.params.size() : -1; }
@@ -121,11 +117,6 @@ int arl_net_bind(arl_net* h, float* params, float* grads, float* ms, void* ws) {
   h->net.g = grads;
   h->net.ms = ms;
   h->net.ws = reinterpret_cast<char*>(ws);
-  if (!h->streams_made) {
-    h->streams_made = true;
-    const hipError_t e = arl::net_streams_create(h->net);
-    if (e != hipSuccess) return hip_status(e, "net_bind: side streams");
-  }
   h->bound = true;
   return ARL_OK;
 }

@@ -10,7 +10,9 @@ namespace arl {
 
 // control block (device int64[16]), read by kernels so that a captured window
 // replays with advancing step counters (no frozen kernel arguments)
-enum { CTL_STEP = 0, CTL_WINDOW = 1, CTL_SIZE = 16 };
+// CTL_STEP_SNAP: the step counter as the learner saw it (written at learn start),
+// read by the fused optimizer for the lr anneal so it can advance CTL_STEP itself
+enum { CTL_STEP = 0, CTL_WINDOW = 1, CTL_STEP_SNAP = 2, CTL_SIZE = 16 };
 
 enum Arch { ARCH_FF = 0, ARCH_LSTM = 1, ARCH_FF_NATURE = 2 };
 
@@ -77,12 +79,9 @@ struct Net {
       w_cbuf, w_logits, w_probs, w_logp, w_v, w_ent, w_logpa, w_act, w_dlogits, w_dv, w_dh, w_dfc,
       w_dG, w_dhn, w_dcn, w_da2, w_slab, w_norm, w_loss, w_tick;
   int64_t w_a3 = 0, w_da1 = 0, w_da3 = 0;   // Nature head only
-  // split-K slabs of the weight-gradient GEMMs that run beside the main
-  // backward chain on side streams (heads, FC, LSTM gates)
+  // per-job weight-gradient slabs (heads, FC, LSTM gates) of the NIPS learner;
+  // the conv slab is `slab`
   int64_t w_slab_heads = 0, w_slab_fc = 0, w_slab_lstm = 0;
-  // side streams + fork / join events of the backward (created at bind)
-  hipStream_t side[2] = {nullptr, nullptr};
-  hipEvent_t ev[6] = {};
   int64_t slab_floats;
   int norm_blocks;
   // bound pointers
@@ -95,10 +94,10 @@ struct Net {
 
 bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_offset, uint64_t seed,
               std::string& err);
-hipError_t net_streams_create(Net& net);
-void net_streams_destroy(Net& net);
 hipError_t net_act(Net& net, int t, int mode, hipStream_t s);   // mode: 0 none, 1 sample, 2 greedy
 hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s);
+// advance: also end the window, folded into the update kernel (arl_learn
+// snapshots the step counter, so the update's lr anneal does not race it).
 hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
                         float clip, hipStream_t s, bool advance = false);
 hipError_t net_advance(Net& net, hipStream_t s);
@@ -124,6 +123,7 @@ hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const i
                            const float* a1, const float* da2, const float* W2, float* slab, float* gW2, float* gb2,
                            float* gW1, float* gb1, hipStream_t s, bool reduce = true);
 int64_t conv_bwd_slab_floats(int S);
+int conv_bwd_blocks(int S);       // workgroups (= slab slices) of launch_conv_bwd
 
 // arguments of the softmax policy / value heads (policy_rows.hpp)
 struct PolicyArgs {
@@ -151,9 +151,21 @@ hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b,
                          float* hfc, hipStream_t s);
 hipError_t launch_policy_args(const float* h, int64_t n, const PolicyArgs& pa, hipStream_t s, int hid);
 
+// end-of-window advance folded into the update (NIPS learner): the lr reads
+// the learner's snapshot CTL_STEP_SNAP, so no workgroup reads CTL_STEP and one
+// thread can move it without a ticket; reset flags (and the LSTM h / c carry)
+// are copied grid-stride by all workgroups (optim.hip).
+struct AdvanceArgs {
+  int64_t* ctl;             // null: no advance
+  uint8_t* reset;           // (T+1, n): row T -> row 0
+  float* hbuf;              // LSTM: (T+2, n, 256), row T -> row 0 (else null)
+  float* cbuf;
+  int T, n;
+};
 hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, double alpha, double eps,
                           const double* norm_partials, int norm_blocks, float clip, const int64_t* ctl,
-                          int64_t total_steps, int64_t n_total, int t_max, hipStream_t s);
+                          int64_t total_steps, int64_t n_total, int t_max, hipStream_t s,
+                          const AdvanceArgs* adv = nullptr);
 hipError_t launch_grad_sqnorm(const float* g, int64_t n, double* partials, int blocks, hipStream_t s);
 hipError_t launch_policy(const float* h, int64_t n, const float* Wpi, const float* bpi, const float* Wv,
                          const float* bv, int A, uint64_t seed, const int64_t* ctl, int64_t step_off,
@@ -161,6 +173,7 @@ hipError_t launch_policy(const float* h, int64_t n, const float* Wpi, const floa
                          float* ent, int32_t* act, float* logp_a, hipStream_t s, int hid = HID);
 hipError_t launch_returns(const float* rewards, const uint8_t* dones, const float* v, const float* probs,
                           const float* logp, const int32_t* act, int T, int n, int A, double gamma, float beta,
-                          float vcoef, int clip_reward, float* dlogits, float* dv, float* loss, hipStream_t s);
+                          float vcoef, int clip_reward, float* dlogits, float* dv, float* loss, hipStream_t s,
+                          int64_t* ctl_snap = nullptr);
 
 }  // namespace arl

@@ -34,6 +34,7 @@
 
 #include "arl_internal.hpp"
 #include "bf16split.hpp"
+#include "conv_slab.hpp"
 
 #ifndef ARL_ABLATE
 #define ARL_ABLATE 0   // timing experiments only (bits: 8 step 1, 16 step 2, 32 step 3, 64 prefetch loads)
@@ -44,11 +45,6 @@ namespace arl {
 namespace {
 constexpr int NT = 512;                    // threads per workgroup (8 waves, 2 per SIMD)
 constexpr int A1_LD = 401;                 // a1 f32 LDS row stride (odd: conflict-free oc spread)
-constexpr int SLAB_W2 = C2_OC * 256;       // 8192
-constexpr int SLAB_B2 = SLAB_W2;           // +32
-constexpr int SLAB_W1 = SLAB_B2 + C2_OC;   // 8224: D1^T[k][oc], 4096
-constexpr int SLAB_B1 = SLAB_W1 + 256 * 16;
-constexpr int SLAB = SLAB_B1 + 16;         // 12336 floats per block
 constexpr int XQ = 4 * 84 * 6;             // screen items per sample: (plane, row, quad of 4 dwords)
 constexpr int PX = (XQ + NT - 1) / NT;     // 4 per thread
 constexpr int PA = (A1 / 4 + NT - 1) / NT; // 4 float4 of a1 per thread
@@ -398,16 +394,15 @@ reduce_conv_bwd_kernel(const float* __restrict__ slab, int G, float* __restrict_
   if (zg == 0 && o < SLAB) {
     double v = 0.0;
     for (int g = 0; g < 16; ++g) v += part[g][threadIdx.x];
-    if (o < SLAB_B2) gW2[o] = (float)v;                       // [oc][ic*16 + ky*4 + kx]
-    else if (o < SLAB_W1) gb2[o - SLAB_B2] = (float)v;
-    else if (o < SLAB_B1) {
-      const int kk = o - SLAB_W1, k = kk >> 4, oc = kk & 15;
-      gW1[oc * 256 + k] = (float)(v / 255.0);                 // integer pixels -> /255 here
-    } else gb1[o - SLAB_B1] = (float)v;
+    conv_slab_put(o, v, gW2, gb2, gW1, gb1);
   }
 }
 
-int conv_bwd_blocks(int S) { return S < 256 ? S : 256; }
+int conv_bwd_blocks(int S) {   // slices actually launched: G0 <= 256 blocks of spb samples
+  const int G0 = S < 256 ? S : 256;
+  const int spb = (S + G0 - 1) / G0;
+  return (S + spb - 1) / spb;
+}
 int64_t conv_bwd_slab_floats(int S) { return (int64_t)conv_bwd_blocks(S) * SLAB; }
 
 hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int S,

@@ -327,7 +327,8 @@ hipError_t nature_learn(Net& net, double gamma, float beta, float vcoef, int cli
   // n-step returns + loss gradient (a3c.py:82-126)
   ARL_TRY(launch_returns(net.at<float>(net.w_rewards), net.at<uint8_t>(net.w_dones), net.at<float>(net.w_v),
                          net.at<float>(net.w_probs), net.at<float>(net.w_logp), net.at<int32_t>(net.w_act), T, n, A,
-                         gamma, beta, vcoef, clip_reward, dl, dv, net.at<float>(net.w_loss), s));
+                         gamma, beta, vcoef, clip_reward, dl, dv, net.at<float>(net.w_loss), s,
+                         net.at<int64_t>(net.w_ctl)));
   const float* h = net.at<float>(net.w_hfc);
   // heads: weight grads (ones column = bias) and dfc = dh * (h > 0)
   ARL_TRY((launch_gemm<16, 64, 32, 1, 4, GS, GM>(HeadsGA{dl, dv, A}, OnesColB{h, NHID},

@@ -21,7 +21,6 @@
 #include <stdint.h>
 
 #include <algorithm>
-#include <cstdlib>
 
 #include "arl_internal.hpp"
 #include "gemm.hpp"
@@ -296,7 +295,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   net.w_da1 = buf("da1", NAT ? S * NA1 * 4 : 0);
   net.w_da3 = buf("da3", NAT ? S * NA3 * 4 : 0);
   net.w_slab = buf("slab", slab * 4);
-  if (!NAT) {   // the side-stream GEMMs of the backward own their slabs
+  if (!NAT) {   // per-job weight-gradient slabs of the NIPS learner
     net.w_slab_heads = buf("slab_heads", (int64_t)pl.heads_w * (A + 1) * (HID + 1) * 4);
     net.w_slab_fc = buf("slab_fc", (int64_t)pl.fc_w * HID * (A2 + 1) * 4);
     net.w_slab_lstm = buf("slab_lstm", L ? (int64_t)pl.lstm_w * GATES * (2 * HID + 1) * 4 : 0);
@@ -391,38 +390,28 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
   const float* P = net.p;
   float* G = net.g;
   float* slab = net.at<float>(net.w_slab);
+  float* slab_h = net.at<float>(net.w_slab_heads);
+  float* slab_f = net.at<float>(net.w_slab_fc);
   const Plans pl = make_plans(net);
   float* dl = net.at<float>(net.w_dlogits);
   float* dv = net.at<float>(net.w_dv);
-  // 1. n-step returns + loss gradient wrt logits / v  (a3c.py:82-126)
-  ARL_TRY(launch_returns(net.at<float>(net.w_rewards), net.at<uint8_t>(net.w_dones), net.at<float>(net.w_v),
-                         net.at<float>(net.w_probs), net.at<float>(net.w_logp), net.at<int32_t>(net.w_act), T, n, A,
-                         gamma, beta, vcoef, clip_reward, dl, dv, net.at<float>(net.w_loss), s));
   const bool L = net.arch == ARCH_LSTM;
   const float* hfc = net.at<float>(net.w_hfc);
   const float* hheads = L ? net.at<float>(net.w_hbuf) + (int64_t)n * HID : hfc;   // h fed to pi / v
   float* dfc = net.at<float>(net.w_dfc);
-  // 2. heads: weight grads (ones column = bias), then dh.  With
-  //    ARL_FORK_BACKWARD=1 the weight-gradient GEMMs (heads, FC, LSTM gates)
-  //    run on side streams beside the main chain (event fork / join, capture
-  //    safe); by default everything is one stream (measured faster).
-  const bool fork = net.side[0] != nullptr;
-  hipStream_t s0 = fork ? net.side[0] : s, s1 = fork ? net.side[1] : s;
-  auto edge = [&](int i, hipStream_t from, hipStream_t to) -> hipError_t {   // to waits for from's work so far
-    if (!fork) return hipSuccess;
-    hipError_t e = hipEventRecord(net.ev[i], from);
-    return e != hipSuccess ? e : hipStreamWaitEvent(to, net.ev[i], 0);
-  };
-  ARL_TRY(edge(0, s, s0));
-  float* slab_h = net.at<float>(net.w_slab_heads);
-  float* slab_f = net.at<float>(net.w_slab_fc);
+  // 1. n-step returns + loss gradient wrt logits / v (a3c.py:82-126); also
+  //    snapshots the step counter for the optimizer's fused advance
+  ARL_TRY(launch_returns(net.at<float>(net.w_rewards), net.at<uint8_t>(net.w_dones), net.at<float>(net.w_v),
+                         net.at<float>(net.w_probs), net.at<float>(net.w_logp), net.at<int32_t>(net.w_act), T, n, A,
+                         gamma, beta, vcoef, clip_reward, dl, dv, nullptr, s, net.at<int64_t>(net.w_ctl)));
+  // heads: weight grads (ones column = bias) and dh
   ARL_TRY((launch_gemm<16, 64, 32, 1, 4, GS, GM>(HeadsGA{dl, dv, A}, OnesColB{hheads, HID},
-                                                 EpiSlab{slab_h, A + 1, HID + 1}, A + 1, HID + 1, S, pl.heads_w, s0)));
+                                                 EpiSlab{slab_h, A + 1, HID + 1}, A + 1, HID + 1, S, pl.heads_w, s)));
   ARL_TRY(launch_reduce_grad(slab_h, pl.heads_w, A + 1, HID + 1,
-                             MapHeads{G, net.o_piW, net.o_pib, net.o_vW, net.o_vb, A, HID}, s0));
+                             MapHeads{G, net.o_piW, net.o_pib, net.o_vW, net.o_vb, A, HID}, s));
   ARL_TRY(launch_heads_bwd(dl, dv, P + net.o_piW, P + net.o_vW, A, HID, L ? nullptr : hfc,
                            L ? net.at<float>(net.w_dh) : dfc, S, s));
-  // 3. LSTM: truncated BPTT over the window
+  // 2. LSTM: truncated BPTT over the window, gate weight gradients, dfc
   if (L) {
     const float* gates = net.at<float>(net.w_gates);
     const float* cbuf = net.at<float>(net.w_cbuf);
@@ -443,56 +432,29 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
         ARL_TRY((launch_gemm<32, 64, 32, 2, 2, GK, GM>(RowMajor{dG + o * GATES, GATES}, RowMajor{P + net.o_llW, HID},
                                                EpiResetMask{dhn, rs + o, HID}, n, HID, GATES, 1, s)));
     }
-    // gate weight grads on side stream 1, dfc on the main stream
     float* slab_l = net.at<float>(net.w_slab_lstm);
-    ARL_TRY(edge(1, s, s1));
     ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GM, GS>(ColMajor{dG, GATES}, LstmWB{hfc, hbuf, rs},
-                                           EpiSlab{slab_l, GATES, 2 * HID + 1}, GATES, 2 * HID + 1, S, pl.lstm_w, s1)));
+                                           EpiSlab{slab_l, GATES, 2 * HID + 1}, GATES, 2 * HID + 1, S, pl.lstm_w, s)));
     ARL_TRY(launch_reduce_grad(slab_l, pl.lstm_w, GATES, 2 * HID + 1,
-                               MapDense{G, net.o_luW, net.o_lub, net.o_llW, HID}, s1));
+                               MapDense{G, net.o_luW, net.o_lub, net.o_llW, HID}, s));
     ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GK, GM>(RowMajor{dG, GATES}, RowMajor{P + net.o_luW, HID}, EpiMask{dfc, hfc, HID},
                                            S, HID, GATES, 1, s)));
   }
-  // 4. FC: dW (+ bias via ones column) on side stream 0 (after the heads), and
-  //    da2 = (dfc W) * (a2 > 0) on the main stream
+  // 3. FC: dW (+ bias via ones column), da2 = (dfc W) * (a2 > 0)
   const float* a2 = net.at<float>(net.w_a2);
   const float* a1 = net.at<float>(net.w_a1);
   float* da2 = net.at<float>(net.w_da2);
-  ARL_TRY(edge(2, s, s0));
   ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GM, GM>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab_f, HID, A2 + 1},
-                                                 HID, A2 + 1, S, pl.fc_w, s0)));
-  ARL_TRY(launch_reduce_grad(slab_f, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s0));
+                                                 HID, A2 + 1, S, pl.fc_w, s)));
+  ARL_TRY(launch_reduce_grad(slab_f, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s));
   ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GK, GM>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2},
                                                  EpiMask{da2, a2, A2}, S, A2, HID, 1, s)));
-  // 5. fused conv backward per sample (conv_bwd.hip): conv2 dW/db,
+  // 4. fused conv backward per sample (conv_bwd.hip): conv2 dW/db,
   //    da1 = conv_transpose(da2, W2) * (a1 > 0) kept in LDS, conv1 dW/db
   //    straight from the frame ring
-  ARL_TRY(launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl), n,
-                          net.R, S, a1, da2, P + net.o_c2W, slab, G + net.o_c2W, G + net.o_c2b, G + net.o_c1W,
-                          G + net.o_c1b, s));
-  // join
-  ARL_TRY(edge(3, s0, s));
-  if (L) ARL_TRY(edge(4, s1, s));
-  return hipSuccess;
-}
-
-hipError_t net_streams_create(Net& net) {
-  // The forked backward measured SLOWER on MI355X (C2 0.454 vs 0.425 ms per
-  // window, C3 1.733 vs 1.705, same box, A/B): the side-stream GEMMs steal CUs
-  // from the critical da2 -> conv_bwd chain and the cross-stream edges add
-  // latency in the graph.  Kept behind ARL_FORK_BACKWARD=1 for experiments.
-  const char* on = getenv("ARL_FORK_BACKWARD");
-  if (on == nullptr || on[0] != '1') return hipSuccess;
-  for (auto& st : net.side) ARL_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  for (auto& e : net.ev) ARL_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  return hipSuccess;
-}
-
-void net_streams_destroy(Net& net) {
-  for (auto& st : net.side)
-    if (st) { (void)hipStreamDestroy(st); st = nullptr; }
-  for (auto& e : net.ev)
-    if (e) { (void)hipEventDestroy(e); e = nullptr; }
+  return launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl), n,
+                         net.R, S, a1, da2, P + net.o_c2W, slab, G + net.o_c2W, G + net.o_c2b, G + net.o_c1W,
+                         G + net.o_c1b, s);
 }
 
 // One stage of a window on the current workspace contents (arl_run_stage):
@@ -545,14 +507,18 @@ hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_tot
                         float clip, hipStream_t s, bool advance) {
   double* parts = net.at<double>(net.w_norm);
   const bool do_clip = clip > 0.f;
+  // arl_learn left the step snapshot (returns kernel), so the update kernel
+  // can also advance the window
+  const bool fused = advance;
   if (do_clip) ARL_TRY(launch_grad_sqnorm(net.g, net.param_floats, parts, net.norm_blocks, s));
+  const bool L = net.arch == ARCH_LSTM;
+  const AdvanceArgs adv{net.at<int64_t>(net.w_ctl), net.at<uint8_t>(net.w_reset),
+                        L ? net.at<float>(net.w_hbuf) : nullptr, L ? net.at<float>(net.w_cbuf) : nullptr, net.T,
+                        net.N};
   ARL_TRY(launch_rmsprop(net.p, net.ms, net.g, net.param_floats, lr0, alpha, eps, do_clip ? parts : nullptr,
                          net.norm_blocks, clip, total_steps > 0 ? net.at<int64_t>(net.w_ctl) : nullptr, total_steps,
-                         n_total, net.T, s));
-  // (Folding the advance into the update's last workgroup through a device
-  // ticket was measured: 662 workgroups on one ticket cost the update more
-  // than the 4 us advance launch it saves.  Kept as two launches.)
-  return advance ? net_advance(net, s) : hipSuccess;
+                         n_total, net.T, s, fused ? &adv : nullptr));
+  return advance && !fused ? net_advance(net, s) : hipSuccess;
 }
 
 hipError_t net_advance(Net& net, hipStream_t s) {

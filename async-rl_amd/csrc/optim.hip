@@ -55,14 +55,17 @@ grad_sqnorm_kernel(const float* __restrict__ g, int64_t n, double* __restrict__ 
   if (threadIdx.x == 0) partials[blockIdx.x] = t;
 }
 
-struct RmsConst {
+struct RmsConst {   // (AdvanceArgs is declared in arl_internal.hpp)
   float lr, alpha, one_minus_alpha, eps;
   // optional on-device lr anneal (a3c_ale.py:111-112):
   // lr = (total - global_t - 1) / total * lr0, global_t = (ctl[STEP] + t_max) * n_total
   double lr0;
   int64_t total, n_total, t_max;
   const int64_t* ctl;
+  int ctl_idx;              // CTL_STEP, or CTL_STEP_SNAP when this launch also advances
 };
+
+
 
 __device__ inline void rms1(float& p, float& ms, float g, const RmsConst& c) {
   ms = __fmul_rn(ms, c.alpha);                                   // ms *= alpha
@@ -73,10 +76,10 @@ __device__ inline void rms1(float& p, float& ms, float g, const RmsConst& c) {
 
 __global__ void __launch_bounds__(256)
 rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __restrict__ g, int64_t n, RmsConst c,
-               const double* __restrict__ partials, int nparts, float clip) {
+               const double* __restrict__ partials, int nparts, float clip, AdvanceArgs adv) {
   __shared__ double sh[8];
   if (c.ctl != nullptr && c.total > 0) {
-    const int64_t gt = (c.ctl[CTL_STEP] + c.t_max) * c.n_total;
+    const int64_t gt = (c.ctl[c.ctl_idx] + c.t_max) * c.n_total;
     c.lr = (float)(((double)(c.total - gt - 1) / (double)c.total) * c.lr0);
   }
   float scale = 1.f;
@@ -118,6 +121,18 @@ rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __res
     p[j] = pv;
     ms[j] = mv;
   }
+  if (adv.ctl == nullptr) return;
+  const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, gsz = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = gtid; i < adv.n; i += gsz) adv.reset[i] = adv.reset[(int64_t)adv.T * adv.n + i];
+  if (adv.hbuf != nullptr)
+    for (int64_t i = gtid; i < (int64_t)adv.n * HID; i += gsz) {
+      adv.hbuf[i] = adv.hbuf[(int64_t)adv.T * adv.n * HID + i];
+      adv.cbuf[i] = adv.cbuf[(int64_t)adv.T * adv.n * HID + i];
+    }
+  if (gtid == 0) {
+    adv.ctl[CTL_STEP] += adv.T;
+    adv.ctl[CTL_WINDOW] += 1;
+  }
 }
 
 static int stream_blocks(int64_t n) {
@@ -134,7 +149,7 @@ hipError_t launch_grad_sqnorm(const float* g, int64_t n, double* partials, int b
 
 hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, double alpha, double eps,
                           const double* norm_partials, int norm_blocks, float clip, const int64_t* ctl,
-                          int64_t total_steps, int64_t n_total, int t_max, hipStream_t s) {
+                          int64_t total_steps, int64_t n_total, int t_max, hipStream_t s, const AdvanceArgs* adv) {
   if (n <= 0) return hipSuccess;
   // each Python-float hyperparameter meets the f32 arrays as f32(value)
   RmsConst c;
@@ -147,8 +162,11 @@ hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double
   c.n_total = n_total;
   c.t_max = t_max;
   c.ctl = ctl;
+  c.ctl_idx = adv != nullptr ? CTL_STEP_SNAP : CTL_STEP;
+  AdvanceArgs a{};
+  if (adv != nullptr) a = *adv;
   hipLaunchKernelGGL(rmsprop_kernel, dim3(stream_blocks(n)), dim3(256), 0, s, p, ms, g, n, c, norm_partials,
-                     norm_blocks, clip);
+                     norm_blocks, clip, a);
   return hipGetLastError();
 }
 

@@ -66,14 +66,16 @@ hipError_t launch_policy(const float* h, int64_t n, const float* Wpi, const floa
 // its own t -- the same operations in the same order as a sequential scan, so
 // R_t is bit-identical -- with every reward / done of its env loaded up front
 // (no dependent loads in the chain).  The per-env losses are then summed in
-// the reference's order (t = T-1 .. 0) through LDS.
+// the reference's order (t = T-1 .. 0) through LDS.  ctl != null: also
+// snapshot the step counter (CTL_STEP_SNAP) for the optimizer's fused advance.
 // Block = EB envs x T steps (EB = 256 / T), env fastest.
 __global__ void __launch_bounds__(256)
 returns_kernel(const float* __restrict__ rewards, const uint8_t* __restrict__ dones, const float* __restrict__ v,
                const float* __restrict__ probs, const float* __restrict__ logp, const int32_t* __restrict__ act, int T,
                int n, int A, double gamma, float beta, float vcoef, int clip_reward, float* __restrict__ dlogits,
-               float* __restrict__ dv, float* __restrict__ loss) {
+               float* __restrict__ dv, float* __restrict__ loss, int64_t* __restrict__ ctl) {
   __shared__ float lpi[256], lv[256];
+  if (ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) ctl[CTL_STEP_SNAP] = ctl[CTL_STEP];
   const int EB = 256 / T;
   const int tid = threadIdx.x, t = tid / EB, el = tid - t * EB;
   const int e = blockIdx.x * EB + el;
@@ -124,12 +126,13 @@ returns_kernel(const float* __restrict__ rewards, const uint8_t* __restrict__ do
 
 hipError_t launch_returns(const float* rewards, const uint8_t* dones, const float* v, const float* probs,
                           const float* logp, const int32_t* act, int T, int n, int A, double gamma, float beta,
-                          float vcoef, int clip_reward, float* dlogits, float* dv, float* loss, hipStream_t s) {
+                          float vcoef, int clip_reward, float* dlogits, float* dv, float* loss, hipStream_t s,
+                          int64_t* ctl_snap) {
   if (n <= 0) return hipSuccess;
   if (T < 1 || T > 256) return hipErrorInvalidValue;
   const int EB = 256 / T;
   hipLaunchKernelGGL(returns_kernel, dim3((n + EB - 1) / EB), dim3(256), 0, s, rewards, dones, v, probs, logp, act, T,
-                     n, A, gamma, beta, vcoef, clip_reward, dlogits, dv, loss);
+                     n, A, gamma, beta, vcoef, clip_reward, dlogits, dv, loss, ctl_snap);
   return hipGetLastError();
 }
 

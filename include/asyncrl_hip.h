@@ -139,7 +139,8 @@ int arl_run_stage(arl_net* net, int stage, int t, void* stream);
 int arl_advance(arl_net* net, void* stream);
 
 /* arl_optimize followed by arl_advance (the end of a3c.py's update,
- * a3c.py:139-144) in one call. */
+ * a3c.py:139-144) in one call; for the NIPS models the update kernel also
+ * advances the window (one launch fewer). */
 int arl_optimize_advance(arl_net* net, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
                          double clip, void* stream);
 
