@@ -132,9 +132,11 @@ __device__ inline void gemm_gather(const AOp& A, const BOp& B, int M, int N, int
   }
 }
 
-template <int BM, int BN, int BK, int WM, int WN, class AOp, class BOp, class EOp, int AV = GS, int BV = GS>
-__global__ void __launch_bounds__(256)
-gemm_kernel(AOp A, BOp B, EOp E, int M, int N, int K, int k_per_split) {
+// One BM x BN output tile (split-K slice z) of the implicit GEMM; the body of
+// gemm_kernel and of gemm2_kernel (two independent GEMMs in one launch).
+template <int BM, int BN, int BK, int WM, int WN, int AV, int BV, class AOp, class BOp, class EOp>
+__device__ inline void gemm_tile(const AOp& A, const BOp& B, const EOp& E, int M, int N, int K, int k_per_split,
+                                 int bx, int by, int z) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TM = BM / (16 * WM);   // MFMA tiles per wave along m
   constexpr int TN = BN / (16 * WN);   // along n
@@ -155,9 +157,8 @@ gemm_kernel(AOp A, BOp B, EOp E, int M, int N, int K, int k_per_split) {
   const int wave = tid >> 6;
   const int wm = wave / WN;
   const int wn = wave % WN;
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
-  const int z = blockIdx.z;
+  const int m0 = bx * BM;
+  const int n0 = by * BN;
   const int kbeg = z * k_per_split;
   int kend = kbeg + k_per_split;
   if (kend > K) kend = K;
@@ -258,6 +259,55 @@ gemm_kernel(AOp A, BOp B, EOp E, int M, int N, int K, int k_per_split) {
         if (m < M && n < N) E.store(m, n, acc[i][j][r], z);
       }
     }
+}
+
+template <int BM, int BN, int BK, int WM, int WN, class AOp, class BOp, class EOp, int AV = GS, int BV = GS>
+__global__ void __launch_bounds__(256)
+gemm_kernel(AOp A, BOp B, EOp E, int M, int N, int K, int k_per_split) {
+  gemm_tile<BM, BN, BK, WM, WN, AV, BV>(A, B, E, M, N, K, k_per_split, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// Two independent GEMMs of the same tile shape in one launch: workgroups
+// [0, g1) run the first (tile-major: x fastest, then y, then split z), the rest
+// the second.  Latency-bound GEMMs that would run back to back share the chip.
+template <class AOp, class BOp, class EOp>
+struct GemmJob {
+  AOp A; BOp B; EOp E;
+  int M, N, K, kps, gx, gy, gz;
+};
+
+template <int BM, int BN, int BK, int WM, int WN, int AV1, int BV1, int AV2, int BV2, class J1, class J2>
+__global__ void __launch_bounds__(256)
+gemm2_kernel(J1 j1, J2 j2) {
+  int b = blockIdx.x;
+  const int g1 = j1.gx * j1.gy * j1.gz;
+  if (b < g1) {
+    const int x = b % j1.gx, y = (b / j1.gx) % j1.gy, z = b / (j1.gx * j1.gy);
+    gemm_tile<BM, BN, BK, WM, WN, AV1, BV1>(j1.A, j1.B, j1.E, j1.M, j1.N, j1.K, j1.kps, x, y, z);
+  } else {
+    b -= g1;
+    const int x = b % j2.gx, y = (b / j2.gx) % j2.gy, z = b / (j2.gx * j2.gy);
+    gemm_tile<BM, BN, BK, WM, WN, AV2, BV2>(j2.A, j2.B, j2.E, j2.M, j2.N, j2.K, j2.kps, x, y, z);
+  }
+}
+
+template <int BM, int BK, class AOp, class BOp, class EOp>
+inline GemmJob<AOp, BOp, EOp> gemm_job(const AOp& A, const BOp& B, const EOp& E, int M, int N, int K, int splits,
+                                       int BN) {
+  if (splits < 1) splits = 1;
+  int kps = (K + splits - 1) / splits;
+  kps = ((kps + BK - 1) / BK) * BK;
+  splits = (K + kps - 1) / kps;
+  return GemmJob<AOp, BOp, EOp>{A, B, E, M, N, K, kps, (M + BM - 1) / BM, (N + BN - 1) / BN, splits};
+}
+
+template <int BM, int BN, int BK, int WM, int WN, int AV1, int BV1, int AV2, int BV2, class J1, class J2>
+inline hipError_t launch_gemm2(const J1& j1, const J2& j2, hipStream_t s) {
+  const int g = j1.gx * j1.gy * j1.gz + j2.gx * j2.gy * j2.gz;
+  if (g <= 0) return hipSuccess;
+  hipLaunchKernelGGL((gemm2_kernel<BM, BN, BK, WM, WN, AV1, BV1, AV2, BV2, J1, J2>), dim3(g), dim3(256), 0, s, j1,
+                     j2);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- bf16x6 variant

@@ -80,6 +80,12 @@ struct LstmWB {         // B(s, j) = [x (256) | 1 | h_prev (256, 0 after reset)]
   }
 };
 
+constexpr int BPTT_SPLIT = 4;   // split-K of the BPTT dh GEMM (K = 1024)
+
+struct MapResetMask {   // split-K reduce target: out[m][n] = reset[m] ? 0 : v
+  float* out; const uint8_t* reset; int ld;
+  __device__ void put(int m, int n, float v) const { out[(int64_t)m * ld + n] = reset[m] ? 0.f : v; }
+};
 struct EpiResetMask {   // out[m][n] = reset[m] ? 0 : v
   float* __restrict__ out; const uint8_t* __restrict__ reset; int ld;
   __device__ void store(int m, int n, float v, int) const {
@@ -252,6 +258,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   slab = std::max(slab, (int64_t)FC_SPLIT * n * HID);
   slab = std::max(slab, (int64_t)pl.fc_w * HID * (A2 + 1));   // run_stage("fc_bwd") timing uses the main slab
   slab = std::max(slab, conv_bwd_slab_floats((int)S));
+  if (arch == ARCH_LSTM) slab = std::max(slab, (int64_t)BPTT_SPLIT * HID * n);
   if (NAT) slab = nature_slab_floats(net);
   net.slab_floats = slab;
   net.bufs.clear();
@@ -346,8 +353,9 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s) {
     float* hout = net.at<float>(net.w_hbuf) + (int64_t)(t + 1) * n * HID;
     float* cout = net.at<float>(net.w_cbuf) + (int64_t)(t + 1) * n * HID;
     const uint8_t* rs = net.at<uint8_t>(net.w_reset) + (int64_t)t * n;
+    // gates = [x | h] [Wu ; Wl]^T + b (split-K 2 + a bias reduce measured slower: 28.5 vs 27.7 us)
     ARL_TRY((launch_gemm<32, 64, 32, 2, 2, GK, GK>(LstmGateA{hfc, hprev, rs}, LstmGateB{P + net.o_luW, P + net.o_llW},
-                                           EpiBias{gates, P + net.o_lub, GATES}, n, GATES, 2 * HID, 1, s)));
+                                                   EpiBias{gates, P + net.o_lub, GATES}, n, GATES, 2 * HID, 1, s)));
     const int64_t cnt = (int64_t)n * HID;
     hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, gates, cprev, rs,
                        cout, hout, cnt);
@@ -428,27 +436,34 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
                          gates + o * GATES, cbuf + (o + n) * HID, cbuf + o * HID, rs + o, dH + o * HID, dhn, dcn,
                          dG + o * GATES, t == T - 1 ? 1 : 0, cnt);
       ARL_TRY(hipGetLastError());
-      if (t > 0)
+      if (t > 0) {   // dh_{t-1} = (dG_t Wl) * (no reset): K = 1024 split 4 ways + reduce
         ARL_TRY((launch_gemm<32, 64, 32, 2, 2, GK, GM>(RowMajor{dG + o * GATES, GATES}, RowMajor{P + net.o_llW, HID},
-                                               EpiResetMask{dhn, rs + o, HID}, n, HID, GATES, 1, s)));
+                                                       EpiSlab{slab, n, HID}, n, HID, GATES, BPTT_SPLIT, s)));
+        ARL_TRY(launch_reduce_grad(slab, effective_splits<32>(GATES, BPTT_SPLIT), n, HID,
+                                   MapResetMask{dhn, rs + o, HID}, s));
+      }
     }
+    // gate weight gradients and dfc = (dG Wu) * (hfc > 0): independent, one launch
     float* slab_l = net.at<float>(net.w_slab_lstm);
-    ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GM, GS>(ColMajor{dG, GATES}, LstmWB{hfc, hbuf, rs},
-                                           EpiSlab{slab_l, GATES, 2 * HID + 1}, GATES, 2 * HID + 1, S, pl.lstm_w, s)));
+    ARL_TRY((launch_gemm2<64, 64, 32, 2, 2, GM, GS, GK, GM>(
+        gemm_job<64, 32>(ColMajor{dG, GATES}, LstmWB{hfc, hbuf, rs}, EpiSlab{slab_l, GATES, 2 * HID + 1}, GATES,
+                         2 * HID + 1, S, pl.lstm_w, 64),
+        gemm_job<64, 32>(RowMajor{dG, GATES}, RowMajor{P + net.o_luW, HID}, EpiMask{dfc, hfc, HID}, S, HID, GATES, 1,
+                         64),
+        s)));
     ARL_TRY(launch_reduce_grad(slab_l, pl.lstm_w, GATES, 2 * HID + 1,
                                MapDense{G, net.o_luW, net.o_lub, net.o_llW, HID}, s));
-    ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GK, GM>(RowMajor{dG, GATES}, RowMajor{P + net.o_luW, HID}, EpiMask{dfc, hfc, HID},
-                                           S, HID, GATES, 1, s)));
   }
   // 3. FC: dW (+ bias via ones column), da2 = (dfc W) * (a2 > 0)
   const float* a2 = net.at<float>(net.w_a2);
   const float* a1 = net.at<float>(net.w_a1);
   float* da2 = net.at<float>(net.w_da2);
-  ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GM, GM>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab_f, HID, A2 + 1},
-                                                 HID, A2 + 1, S, pl.fc_w, s)));
+  //    as ONE launch: both are latency-bound and independent, so their
+  //    workgroups share the chip instead of running back to back
+  ARL_TRY((launch_gemm2<64, 64, 32, 2, 2, GM, GM, GK, GM>(
+      gemm_job<64, 32>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab_f, HID, A2 + 1}, HID, A2 + 1, S, pl.fc_w, 64),
+      gemm_job<64, 32>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2}, EpiMask{da2, a2, A2}, S, A2, HID, 1, 64), s)));
   ARL_TRY(launch_reduce_grad(slab_f, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s));
-  ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GK, GM>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2},
-                                                 EpiMask{da2, a2, A2}, S, A2, HID, 1, s)));
   // 4. fused conv backward per sample (conv_bwd.hip): conv2 dW/db,
   //    da1 = conv_transpose(da2, W2) * (a1 > 0) kept in LDS, conv1 dW/db
   //    straight from the frame ring
