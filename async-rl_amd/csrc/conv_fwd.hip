@@ -29,7 +29,8 @@
 #include "bf16split.hpp"
 
 #ifndef ARL_ABLATE
-#define ARL_ABLATE 0   // timing experiments only (bits: 1 conv1 MFMA, 2 conv2 MFMA, 4 staging loads)
+#define ARL_ABLATE 0   // timing experiments only (bits: 1 conv1 MFMA, 2 conv2 MFMA, 4 staging loads,
+                       // 8 weight loads + splits, 16 epilogue /255 as a multiply)
 #endif
 
 namespace arl {
@@ -95,13 +96,15 @@ conv_fwd_kernel(ConvFwdArgs a) {
     }
     // W1: thread -> 8 consecutive k of one oc; W2: thread -> (oc, 4 ic, 4 taps)
     const int w1oc = tid >> 5, w1k = (8 * tid) & 255;
+    const int w2oc = tid >> 4, ic4 = (tid >> 2) & 3, tg = tid & 3;
+#if !(ARL_ABLATE & 8)
     const float4 w1a = reinterpret_cast<const float4*>(a.W1)[2 * tid];
     const float4 w1b = reinterpret_cast<const float4*>(a.W1)[2 * tid + 1];
-    const int w2oc = tid >> 4, ic4 = (tid >> 2) & 3, tg = tid & 3;
     float4 w2v[4];
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii)
       w2v[ii] = reinterpret_cast<const float4*>(a.W2)[(w2oc * 16 + 4 * ic4 + ii) * 4 + tg];
+#endif
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const int i = tid + NT * j;
@@ -117,6 +120,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
         d[1] = hi;
       }
     }
+#if !(ARL_ABLATE & 8)
     {
       uint4 ph, pm, pl;
       split3_pack(w1a.x, w1a.y, ph.x, pm.x, pl.x);
@@ -139,6 +143,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
       *reinterpret_cast<uint2*>(d + W2P) = pm;
       *reinterpret_cast<uint2*>(d + 2 * W2P) = pl;
     }
+#endif
   }
   __syncthreads();
   // ---- conv1 B fragments: lane (oc = col, g), k-step s -> k = 8 (4 s + g) + 0..7
@@ -179,7 +184,8 @@ conv_fwd_kernel(ConvFwdArgs a) {
       float ov[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        ov[r] = fmaxf(__fadd_rn(__fdiv_rn(__fadd_rn(big[r], sml[r]), 255.f), bias1), 0.f);
+        ov[r] = (ARL_ABLATE & 16) ? fmaxf(__fadd_rn(__fmul_rn(__fadd_rn(big[r], sml[r]), 1.f / 255.f), bias1), 0.f)
+                                  : fmaxf(__fadd_rn(__fdiv_rn(__fadd_rn(big[r], sml[r]), 255.f), bias1), 0.f);
       *reinterpret_cast<float4*>(a1g + col * C1_P + p0) = make_float4(ov[0], ov[1], ov[2], ov[3]);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {

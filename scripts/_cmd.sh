@@ -1,7 +1,11 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-bash scripts/gpu_quick.sh f1 "" "--steps 100 --warmup 10 --cpu-seconds 0 --kernel-reps 20" || exit $?
-for i in 1 2; do
-timeout -k 10 300 python -u bench.py --workload c3 --steps 40 --warmup 5 --cpu-seconds 0 --kernel-reps 3 > gpurun_out/f1/bench_c3_$i.log 2>&1 || exit $?
+mkdir -p gpurun_out/abl2
+for b in 0 128 256 512 896; do
+  lib=async-rl_amd/csrc/build_abl$b/libasyncrl_hip.so
+  [ "$b" = 0 ] && lib=async-rl_amd/asyncrl_amd/libasyncrl_hip.so
+  ASYNCRL_HIP_LIB=$PWD/$lib timeout -k 10 200 python bench.py --steps 10 --warmup 3 --cpu-seconds 0 --kernel-reps 30 > gpurun_out/abl2/b$b.log 2>&1 || exit $?
+  python -c "
+import json; d=json.loads(open('gpurun_out/abl2/b$b.log').read().strip().splitlines()[-1]); k=d['kernels']
+print('abl $b', 'conv_fwd', k['conv_fwd']['avg_launch_us'], 'fc_fwd', k['fc_fwd']['avg_launch_us'], 'phi', k['phi']['avg_launch_us'])"
 done
-bash scripts/gpu_prof.sh f1 "--workload c3 --steps 10 --warmup 3 --cpu-seconds 0 --kernel-reps 3"
