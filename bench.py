@@ -25,7 +25,8 @@ import torch
 import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(ROOT, "async-rl_amd"))
+# ASYNCRL_PKG_ROOT: another build of the package (A/B timing, scripts/ab.sh)
+sys.path.insert(0, os.environ.get("ASYNCRL_PKG_ROOT") or os.path.join(ROOT, "async-rl_amd"))
 
 from asyncrl_amd import A3C, A3CFF, A3CFFNature, A3CLSTM, GradientClipping, RMSpropAsync  # noqa: E402
 from asyncrl_amd import _lib  # noqa: E402
