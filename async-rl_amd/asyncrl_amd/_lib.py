@@ -40,6 +40,7 @@ SIGNATURES = {
     "arl_max_luminance": (c_int, [c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
     "arl_phi_stack": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p]),
     "arl_dqn_phi": (c_int, [c_void_p, c_void_p, c_i64, c_void_p]),
+    "arl_rgb_phi": (c_int, [c_void_p, c_i64, c_int, c_int, c_void_p, c_int, c_void_p]),
     "arl_net_create": (c_int, [ctypes.POINTER(c_void_p), c_int, c_int, c_int, c_int, c_int, c_u64]),
     "arl_net_destroy": (None, [c_void_p]),
     "arl_net_param_floats": (c_i64, [c_void_p]),
@@ -51,6 +52,8 @@ SIGNATURES = {
     "arl_net_bind": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "arl_net_reset": (c_int, [c_void_p, c_void_p]),
     "arl_observe": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int, c_void_p]),
+    "arl_observe_rgb": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_i64, c_int, c_int,
+                                c_void_p]),
     "arl_act": (c_int, [c_void_p, c_int, c_void_p]),
     "arl_act_mode": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "arl_run_stage": (c_int, [c_void_p, c_int, c_int, c_void_p]),
@@ -77,6 +80,7 @@ for _name, (_res, _args) in SIGNATURES.items():
 ARCH_FF = 0
 ARCH_LSTM = 1
 ARCH_FF_NATURE = 2   # A3CFF with NatureDQNHead (dqn_head.py:6-28)
+ARCH_RGB = 16        # flag for FF / LSTM: the ViZDoom models (train_a3c_doom.py:25-63), RGB screens
 RESIZE_SCALAR = 0
 RESIZE_SIMD = 1
 RESIZE_CROP = 2      # flag, combine with SCALAR / SIMD: ale.py crop_or_scale='crop'

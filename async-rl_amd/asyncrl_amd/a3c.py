@@ -28,7 +28,7 @@ import os
 import numpy as np
 import torch
 
-from ._lib import ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, RESIZE_SCALAR
+from ._lib import ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, RESIZE_SCALAR
 from .distributed import allreduce_grads, world_info
 from .net import DeviceNet, init_like_torch
 from . import serializers
@@ -92,6 +92,23 @@ class A3CLSTM(A3CModel):
         raise NotImplementedError("A3CLSTM forward runs inside A3C.act (recurrent state is on device)")
 
 
+class DoomA3CFF(A3CModel):
+    """train_a3c_doom.py:25-38 A3CFF: NIPSDQNHead(n_input_channels=3) on the
+    RGB screen (phi = train_a3c_doom.py:21-23, no frame stack) ->
+    FCSoftmaxPolicy + FCVFunction.  pi_and_v takes rgb_phi output
+    (n, 3, 84, 84); A3C.act takes the raw (n, H, W, 3) screens."""
+    arch = ARCH_FF | ARCH_RGB
+
+
+class DoomA3CLSTM(A3CModel):
+    """train_a3c_doom.py:41-63 A3CLSTM: the RGB NIPS head -> L.LSTM(256, 256)
+    -> policy + value; recurrent forward inside A3C.act."""
+    arch = ARCH_LSTM | ARCH_RGB
+
+    def pi_and_v(self, state, keep_same_state=False):
+        raise NotImplementedError("DoomA3CLSTM forward runs inside A3C.act (recurrent state is on device)")
+
+
 class A3C:
     """a3c.py:27-185, lockstep-batched.  One `act` call = one env-step of all
     n_envs envs; every t_max calls it also performs the update."""
@@ -131,7 +148,8 @@ class A3C:
 
     def act(self, pairs: torch.Tensor, reward=None, is_state_terminal=None) -> torch.Tensor:
         """a3c.py:67-167, batched.  pairs: (n, 2, 210, 160, 3) uint8 device
-        tensor (frame 4, frame 3 of the skip); reward: (n,) f32 (clipped to
+        tensor (frame 4, frame 3 of the skip) -- for the Doom models the
+        screens (n, H, W, 3) uint8 instead; reward: (n,) f32 (clipped to
         [-1, 1] as at a3c.py:69-70); is_state_terminal: (n,) uint8/bool, the
         transition into this observation ended the episode.  Returns the
         sampled actions (n,) int32 (device)."""

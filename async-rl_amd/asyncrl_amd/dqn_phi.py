@@ -1,6 +1,7 @@
-"""Frame preprocessing surfaces: dqn_phi.dqn_phi (dqn_phi.py:4-17) and the
+"""Frame preprocessing surfaces: dqn_phi.dqn_phi (dqn_phi.py:4-17), the
 arithmetic of ale.ALE.current_screen (ale.py:59-89) + the 4-frame stack
-(ale.py:135,155-158), batched on the GPU.
+(ale.py:135,155-158), and the ViZDoom phi (train_a3c_doom.py:21-23), batched
+on the GPU.
 
 All inputs are device tensors; the computation is libasyncrl_hip.so.
 """
@@ -64,3 +65,18 @@ def phi_stack(rgb_pairs: torch.Tensor, prev_stack: torch.Tensor, reset: torch.Te
     check(lib.arl_phi_stack(ptr(rgb_pairs), ptr(prev_stack), ptr(reset), ptr(out), n, resize_mode,
                             stream_handle(stream)), "arl_phi_stack")
     return out
+
+
+def rgb_phi(images: torch.Tensor, resize_mode: int = RESIZE_SCALAR, stream=None) -> torch.Tensor:
+    """train_a3c_doom.py:21-23 phi, batched: (n, H, W, 3) uint8 RGB24 screens
+    (doom_env.py:47; W % 16 == 0) -> cv2.resize to 84 x 84 per channel ->
+    transpose(2, 0, 1) -> float32 / 255: (n, 3, 84, 84).  One screen
+    (H, W, 3) -> (3, 84, 84)."""
+    single = images.dim() == 3
+    x = images.unsqueeze(0) if single else images
+    assert x.dtype == torch.uint8 and x.dim() == 4 and x.shape[3] == 3, "rgb_phi: (n, H, W, 3) uint8"
+    x = x.contiguous()
+    n, H, W = x.shape[0], x.shape[1], x.shape[2]
+    out = torch.empty((n, 3, 84, 84), dtype=torch.float32, device=x.device)
+    check(lib.arl_rgb_phi(ptr(x), n, H, W, ptr(out), resize_mode, stream_handle(stream)), "arl_rgb_phi")
+    return out[0] if single else out

@@ -14,18 +14,21 @@ import ctypes
 import numpy as np
 import torch
 
-from ._lib import ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, RESIZE_SCALAR, check, lib, ptr, stream_handle
+from ._lib import ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, RESIZE_SCALAR, check, lib, ptr, stream_handle
 
 
 def param_shapes(arch: int, n_actions: int):
     """Chainer parameter shapes in link order (dqn_head.py:40-44,
     policy.py:49, v_function.py:25, Chainer L.LSTM upward/lateral; the
-    Nature head dqn_head.py:16-20 with 512-wide policy / value heads)."""
+    Nature head dqn_head.py:16-20 with 512-wide policy / value heads; the
+    RGB flag: NIPSDQNHead(n_input_channels=3), train_a3c_doom.py:28,46)."""
+    c_in = 3 if arch & ARCH_RGB else 4
+    arch &= ~ARCH_RGB
     if arch == ARCH_FF_NATURE:
         return [("0/0/W", (32, 4, 8, 8)), ("0/0/b", (32,)), ("0/1/W", (64, 32, 4, 4)), ("0/1/b", (64,)),
                 ("0/2/W", (64, 64, 3, 3)), ("0/2/b", (64,)), ("0/3/W", (512, 3136)), ("0/3/b", (512,)),
                 ("1/0/W", (n_actions, 512)), ("1/0/b", (n_actions,)), ("2/0/W", (1, 512)), ("2/0/b", (1,))]
-    head = [("0/0/W", (16, 4, 8, 8)), ("0/0/b", (16,)), ("0/1/W", (32, 16, 4, 4)), ("0/1/b", (32,)),
+    head = [("0/0/W", (16, c_in, 8, 8)), ("0/0/b", (16,)), ("0/1/W", (32, 16, 4, 4)), ("0/1/b", (32,)),
             ("0/2/W", (256, 2592)), ("0/2/b", (256,))]
     if arch == ARCH_FF:
         return head + [("1/0/W", (n_actions, 256)), ("1/0/b", (n_actions,)), ("2/0/W", (1, 256)),
@@ -54,6 +57,7 @@ class DeviceNet:
                  seed: int = 0, device=None):
         self.device = torch.device(device if device is not None else "cuda")
         self.arch, self.n_actions, self.n_envs, self.t_max = arch, n_actions, n_envs, t_max
+        self.rgb = bool(arch & ARCH_RGB)
         self.env_offset, self.seed = env_offset, seed
         h = ctypes.c_void_p()
         check(lib.arl_net_create(ctypes.byref(h), arch, n_actions, n_envs, t_max, env_offset, seed),
@@ -122,6 +126,13 @@ class DeviceNet:
 
     def observe(self, t: int, pair_pool: torch.Tensor, reward_pool=None, done_pool=None, pool_len: int = 1,
                 force_reset: bool = False, resize_mode: int = RESIZE_SCALAR, stream=None):
+        """pair_pool: (pool_len, n, 2, 210, 160, 3) uint8 frame pairs; for an
+        RGB net (arch | ARCH_RGB) the screens (pool_len, n, H, W, 3) instead."""
+        if self.rgb:
+            H, W = pair_pool.shape[-3], pair_pool.shape[-2]
+            check(lib.arl_observe_rgb(self._h, t, ptr(pair_pool), H, W, ptr(reward_pool), ptr(done_pool), pool_len,
+                                      int(force_reset), resize_mode, stream_handle(stream)), "arl_observe_rgb")
+            return
         check(lib.arl_observe(self._h, t, ptr(pair_pool), ptr(reward_pool), ptr(done_pool), pool_len,
                               int(force_reset), resize_mode, stream_handle(stream)), "arl_observe")
 
@@ -154,6 +165,9 @@ class DeviceNet:
 
     def forward_states(self, states: torch.Tensor, mode: int = 0, stream=None):
         n = states.shape[0]
+        c = 3 if self.rgb else 4
+        if states.dtype != torch.float32 or tuple(states.shape[1:]) != (c, 84, 84):
+            raise ValueError(f"forward_states: need (n, {c}, 84, 84) float32 states")
         check(lib.arl_forward_states(self._h, ptr(states), n, mode, stream_handle(stream)), "arl_forward_states")
 
     # ------------------------------------------------------------ outputs

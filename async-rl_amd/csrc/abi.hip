@@ -67,6 +67,21 @@ int arl_dqn_phi(const uint8_t* in, float* out, int64_t n, void* s) {
   return hip_status(arl::launch_dqn_phi(in, out, n * 4 * arl::PLANE, S(s)), "dqn_phi");
 }
 
+static int check_rgb_dims(int H, int W) {
+  if (H < 2 || W < 16 || W % 16 != 0 || W > arl::RGB_MAX_W || H > 65535)
+    return fail(ARL_EINVAL, "rgb: need H >= 2, W % 16 == 0, 16 <= W <= 2048");
+  return ARL_OK;
+}
+
+int arl_rgb_phi(const uint8_t* imgs, int64_t n, int H, int W, float* out, int mode, void* s) {
+  if (n < 0 || (n > 0 && (!imgs || !out))) return fail(ARL_EINVAL, "rgb_phi: null pointer / n < 0");
+  if (int rc = check_rgb_dims(H, W)) return rc;
+  if (n > 65535) return fail(ARL_EINVAL, "rgb_phi: n > 65535");
+  if (!aligned(imgs, 16) || !aligned(out, 16)) return fail(ARL_EINVAL, "rgb_phi: 16-byte alignment");
+  if (mode < 0 || mode > ARL_RESIZE_SIMD) return fail(ARL_EINVAL, "rgb_phi: resize_mode must be 0 or 1");
+  return hip_status(arl::launch_rgb_phi(imgs, n, H, W, out, mode, S(s)), "rgb_phi");
+}
+
 int arl_net_create(arl_net** out, int arch, int n_actions, int n_envs, int t_max, int env_offset, uint64_t seed) {
   if (!out) return fail(ARL_EINVAL, "net_create: out is null");
   arl_net* h = new arl_net();
@@ -141,17 +156,16 @@ int arl_net_reset(arl_net* h, void* s) {
   return hip_status(e, "net_reset");
 }
 
-int arl_observe(arl_net* h, int t, const uint8_t* pair_pool, const float* reward_pool, const uint8_t* done_pool,
-                int64_t pool_len, int force_reset, int mode, void* s) {
-  NEED_BOUND(h);
+static int observe_common(arl_net* h, int t, const uint8_t* pool, const float* reward_pool,
+                          const uint8_t* done_pool, int64_t pool_len, int force_reset, int mode, int H, int W,
+                          void* s) {
   arl::Net& n = h->net;
   if (t < 0 || t > n.T) return fail(ARL_EINVAL, "observe: t out of [0, t_max]");
-  if (!pair_pool || pool_len < 1) return fail(ARL_EINVAL, "observe: need pair_pool and pool_len >= 1");
-  if (!aligned(pair_pool, 16)) return fail(ARL_EINVAL, "observe: pair_pool must be 16-byte aligned");
-  if (mode < 0 || mode > (ARL_RESIZE_SIMD | ARL_RESIZE_CROP)) return fail(ARL_EINVAL, "bad resize_mode");
+  if (!pool || pool_len < 1) return fail(ARL_EINVAL, "observe: need the frame pool and pool_len >= 1");
+  if (!aligned(pool, 16)) return fail(ARL_EINVAL, "observe: the frame pool must be 16-byte aligned");
   if (n.N > 65535) return fail(ARL_EINVAL, "observe: n_envs > 65535");
   arl::RingArgs a;
-  a.pair_pool = pair_pool;
+  a.pair_pool = pool;
   a.reward_pool = reward_pool;
   a.done_pool = done_pool;
   a.pool_len = pool_len;
@@ -166,7 +180,26 @@ int arl_observe(arl_net* h, int t, const uint8_t* pair_pool, const float* reward
   a.t = t;
   a.mode = mode;
   a.force_reset = force_reset ? 1 : 0;
-  return hip_status(arl::launch_phi_ring(a, S(s)), "observe");
+  a.H = H;
+  a.W = W;
+  return hip_status(n.rgb ? arl::launch_rgb_ring(a, S(s)) : arl::launch_phi_ring(a, S(s)), "observe");
+}
+
+int arl_observe(arl_net* h, int t, const uint8_t* pair_pool, const float* reward_pool, const uint8_t* done_pool,
+                int64_t pool_len, int force_reset, int mode, void* s) {
+  NEED_BOUND(h);
+  if (h->net.rgb) return fail(ARL_ESTATE, "observe: RGB net, use arl_observe_rgb");
+  if (mode < 0 || mode > (ARL_RESIZE_SIMD | ARL_RESIZE_CROP)) return fail(ARL_EINVAL, "bad resize_mode");
+  return observe_common(h, t, pair_pool, reward_pool, done_pool, pool_len, force_reset, mode, 0, 0, s);
+}
+
+int arl_observe_rgb(arl_net* h, int t, const uint8_t* img_pool, int H, int W, const float* reward_pool,
+                    const uint8_t* done_pool, int64_t pool_len, int force_reset, int mode, void* s) {
+  NEED_BOUND(h);
+  if (!h->net.rgb) return fail(ARL_ESTATE, "observe_rgb: net was not created with ARL_ARCH_RGB");
+  if (mode < 0 || mode > ARL_RESIZE_SIMD) return fail(ARL_EINVAL, "observe_rgb: resize_mode must be 0 or 1");
+  if (int rc = check_rgb_dims(H, W)) return rc;
+  return observe_common(h, t, img_pool, reward_pool, done_pool, pool_len, force_reset, mode, H, W, s);
 }
 
 int arl_act(arl_net* h, int t, void* s) {

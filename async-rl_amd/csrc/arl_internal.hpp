@@ -15,6 +15,9 @@ namespace arl {
 enum { CTL_STEP = 0, CTL_WINDOW = 1, CTL_STEP_SNAP = 2, CTL_SIZE = 16 };
 
 enum Arch { ARCH_FF = 0, ARCH_LSTM = 1, ARCH_FF_NATURE = 2 };
+// arch flag: RGB (Doom) observations, train_a3c_doom.py:25-63 (NIPSDQNHead(n_input_channels=3)
+// on one RGB screen); conv1 sees [0, R, G, B] so the fused kernels keep K = 256
+constexpr int ARCH_RGB = 16;
 
 constexpr int PLANE = 84 * 84;         // 7056 B per screen
 constexpr int PAIR = 2 * 210 * 160 * 3; // 201,600 B per frame pair
@@ -43,7 +46,13 @@ struct RingArgs {
   uint8_t* dones;             // (T, n)
   const int64_t* ctl;
   int n, R, t, mode, force_reset;
+  int H = 0, W = 0;           // RGB nets: pair_pool is an image pool (pool_len, n, H, W, 3)
 };
+
+// RGB (Doom) observations, train_a3c_doom.py:21-23 / doom_env.py:47
+constexpr int RGB_MAX_W = 2048;   // staged source rows: 24 x W x 3 bytes of LDS
+hipError_t launch_rgb_phi(const uint8_t* imgs, int64_t n, int H, int W, float* out, int mode, hipStream_t s);
+hipError_t launch_rgb_ring(const RingArgs& a, hipStream_t s);
 
 hipError_t launch_current_screen(const uint8_t* cur, const uint8_t* prev, uint8_t* out, int64_t n,
                                  int mode, hipStream_t s);
@@ -63,6 +72,7 @@ struct ParamInfo {
 
 struct Net {
   int arch, A, N, T, R;
+  bool rgb = false;        // ARCH_RGB: 3 planes per obs step in the ring, conv1 W (16, 3, 8, 8)
   int hid;                 // width of the layer the heads read (256 NIPS / LSTM, 512 Nature)
   int env_offset;          // global id of env 0 on this rank (RNG stream)
   uint64_t seed;
@@ -118,10 +128,10 @@ hipError_t launch_heads_bwd(const float* dl, const float* dv, const float* Wpi, 
 
 hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int t,
                            const float* W1, const float* b1, const float* W2, const float* b2, float* a1, float* a2,
-                           hipStream_t s);
+                           hipStream_t s, bool rgb = false);
 hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int S,
                            const float* a1, const float* da2, const float* W2, float* slab, float* gW2, float* gb2,
-                           float* gW1, float* gb1, hipStream_t s, bool reduce = true);
+                           float* gW1, float* gb1, hipStream_t s, bool reduce = true, bool rgb = false);
 int64_t conv_bwd_slab_floats(int S);
 int conv_bwd_blocks(int S);       // workgroups (= slab slices) of launch_conv_bwd
 

@@ -79,6 +79,7 @@ struct ConvBwdArgs {
   const float* W2;     // (32, 16, 4, 4)
   int S, spb;
   float* slab;         // (G, SLAB)
+  int rgb;             // frames (R, n, 3, 84, 84), input planes [0, R, G, B]
 };
 
 struct Prefetch {
@@ -105,8 +106,8 @@ __device__ inline void prefetch_sample(const ConvBwdArgs& a, int s, Prefetch& r)
     if (i < XQ) {
       const int c = i / 504, rem = i - c * 504, y = rem / 6, q = rem - y * 6;
       if (c >= 4 - nv) {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.frames + ((int64_t)slot[c] * a.n + e) * PLANE +
-                                                                y * 84) + 4 * q;
+        const int64_t pl = a.rgb ? ((int64_t)rs * a.n + e) * 3 + (c - 1) : (int64_t)slot[c] * a.n + e;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.frames + pl * PLANE + y * 84) + 4 * q;
         if (q < 5) { v.x = src[0]; v.y = src[1]; v.z = src[2]; v.w = src[3]; }
         else v.x = src[0];
       }
@@ -382,7 +383,7 @@ conv_bwd_kernel(ConvBwdArgs a) {
 
 __global__ void __launch_bounds__(256)
 reduce_conv_bwd_kernel(const float* __restrict__ slab, int G, float* __restrict__ gW2, float* __restrict__ gb2,
-                       float* __restrict__ gW1, float* __restrict__ gb1) {
+                       float* __restrict__ gW1, float* __restrict__ gb1, int rgb) {
   __shared__ double part[16][16];
   const int o = blockIdx.x * 16 + (threadIdx.x & 15);
   const int zg = threadIdx.x >> 4;
@@ -394,7 +395,7 @@ reduce_conv_bwd_kernel(const float* __restrict__ slab, int G, float* __restrict_
   if (zg == 0 && o < SLAB) {
     double v = 0.0;
     for (int g = 0; g < 16; ++g) v += part[g][threadIdx.x];
-    conv_slab_put(o, v, gW2, gb2, gW1, gb1);
+    conv_slab_put(o, v, gW2, gb2, gW1, gb1, rgb);
   }
 }
 
@@ -407,16 +408,17 @@ int64_t conv_bwd_slab_floats(int S) { return (int64_t)conv_bwd_blocks(S) * SLAB;
 
 hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int S,
                            const float* a1, const float* da2, const float* W2, float* slab, float* gW2, float* gb2,
-                           float* gW1, float* gb1, hipStream_t s, bool reduce) {
+                           float* gW1, float* gb1, hipStream_t s, bool reduce, bool rgb) {
   if (S <= 0) return hipSuccess;
   const int G0 = conv_bwd_blocks(S);
   const int spb = (S + G0 - 1) / G0;
   const int G = (S + spb - 1) / spb;
-  ConvBwdArgs a{frames, nvalid, ctl, n, R, a1, da2, W2, S, spb, slab};
+  ConvBwdArgs a{frames, nvalid, ctl, n, R, a1, da2, W2, S, spb, slab, rgb ? 1 : 0};
   hipLaunchKernelGGL(conv_bwd_kernel, dim3(G), dim3(NT), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !reduce) return e;
-  hipLaunchKernelGGL(reduce_conv_bwd_kernel, dim3((SLAB + 15) / 16), dim3(256), 0, s, slab, G, gW2, gb2, gW1, gb1);
+  hipLaunchKernelGGL(reduce_conv_bwd_kernel, dim3((SLAB + 15) / 16), dim3(256), 0, s, slab, G, gW2, gb2, gW1, gb1,
+                     rgb ? 1 : 0);
   return hipGetLastError();
 }
 

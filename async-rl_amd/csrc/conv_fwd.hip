@@ -60,12 +60,13 @@ struct ConvFwdArgs {
   const uint8_t* nvalid;
   const int64_t* ctl;
   int n, R, t;          // obs step = ctl[STEP] + t; env = blockIdx.x
-  const float* W1;      // (16, 4, 8, 8)
+  const float* W1;      // (16, 4, 8, 8); RGB nets (16, 3, 8, 8) for input planes 1..3
   const float* b1;
   const float* W2;      // (32, 16, 4, 4)
   const float* b2;
   float* a1;            // (n, 16, 400)
   float* a2;            // (n, 32, 81)
+  int rgb;              // frames (R, n, 3, 84, 84): planes [0, R, G, B] of slot ks % R
 };
 
 __global__ void __launch_bounds__(NT)
@@ -92,14 +93,19 @@ conv_fwd_kernel(ConvFwdArgs a) {
       const int c = i / V, o = i - c * V;
       xv[j] = make_uint4(0, 0, 0, 0);
       if (!(ARL_ABLATE & 4) && i < 4 * V && c >= 4 - nv)   // planes older than the last reset read as 0
-        xv[j] = reinterpret_cast<const uint4*>(a.frames + ((int64_t)slot[c] * a.n + e) * PLANE)[o];
+        xv[j] = reinterpret_cast<const uint4*>(
+            a.frames + (a.rgb ? ((int64_t)rs * a.n + e) * 3 + (c - 1) : (int64_t)slot[c] * a.n + e) * PLANE)[o];
     }
     // W1: thread -> 8 consecutive k of one oc; W2: thread -> (oc, 4 ic, 4 taps)
     const int w1oc = tid >> 5, w1k = (8 * tid) & 255;
     const int w2oc = tid >> 4, ic4 = (tid >> 2) & 3, tg = tid & 3;
 #if !(ARL_ABLATE & 8)
-    const float4 w1a = reinterpret_cast<const float4*>(a.W1)[2 * tid];
-    const float4 w1b = reinterpret_cast<const float4*>(a.W1)[2 * tid + 1];
+    float4 w1a = make_float4(0.f, 0.f, 0.f, 0.f), w1b = w1a;   // RGB: input plane 0 is the zero pad
+    if (!a.rgb || w1k >= 64) {
+      const float4* w1p = reinterpret_cast<const float4*>(a.rgb ? a.W1 + w1oc * 192 + w1k - 64 : a.W1 + 8 * tid);
+      w1a = w1p[0];
+      w1b = w1p[1];
+    }
     float4 w2v[4];
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii)
@@ -250,9 +256,9 @@ conv_fwd_kernel(ConvFwdArgs a) {
 
 hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int t,
                            const float* W1, const float* b1, const float* W2, const float* b2, float* a1, float* a2,
-                           hipStream_t s) {
+                           hipStream_t s, bool rgb) {
   if (n <= 0) return hipSuccess;
-  ConvFwdArgs a{frames, nvalid, ctl, n, R, t, W1, b1, W2, b2, a1, a2};
+  ConvFwdArgs a{frames, nvalid, ctl, n, R, t, W1, b1, W2, b2, a1, a2, rgb ? 1 : 0};
   hipLaunchKernelGGL(conv_fwd_kernel, dim3(n), dim3(NT), 0, s, a);
   return hipGetLastError();
 }

@@ -31,13 +31,14 @@ namespace arl {
 // ---------------------------------------------------------------- accessors
 
 // (conv1 from the uint8 frame ring has dedicated kernels: conv1.hip)
-struct Conv1F32A {      // same from an f32 (n,4,84,84) state tensor (dqn_phi output)
+struct Conv1F32A {      // same from an f32 (n,C,84,84) state tensor (dqn_phi output; C = 3 for RGB)
   const float* __restrict__ x;
+  int C;
   __device__ float load(int m, int k) const {
     const int s = m / C1_P, p = m - s * C1_P;
     const int ic = k >> 6, ky = (k >> 3) & 7, kx = k & 7;
     const int oy = p / 20, ox = p - oy * 20;
-    return x[((int64_t)s * 4 + ic) * PLANE + (4 * oy + ky) * 84 + 4 * ox + kx];
+    return x[((int64_t)s * C + ic) * PLANE + (4 * oy + ky) * 84 + 4 * ox + kx];
   }
 };
 struct Conv2A {         // A(m, k) = a1[s][ic][2oy+ky][2ox+kx], m = s*81 + p, k = ic*16+ky*4+kx
@@ -192,8 +193,15 @@ static int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
 bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_offset, uint64_t seed,
               std::string& err) {
+  const bool rgb = (arch & ARCH_RGB) != 0;
+  arch &= ~ARCH_RGB;
+  if (rgb && arch == ARCH_FF_NATURE) {
+    err = "ARCH_RGB applies to the NIPS head (FF or LSTM) only (train_a3c_doom.py:25-63)";
+    return false;
+  }
+  net.rgb = rgb;
   if (arch != ARCH_FF && arch != ARCH_LSTM && arch != ARCH_FF_NATURE) {
-    err = "arch must be 0 (FF), 1 (LSTM) or 2 (FF, Nature head)";
+    err = "arch must be 0 (FF), 1 (LSTM) or 2 (FF, Nature head), optionally | 16 (RGB)";
     return false;
   }
   if (n_actions < 1 || n_actions > MAXA) { err = "n_actions must be in [1, 32]"; return false; }
@@ -228,7 +236,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
     net.o_vW = add("2/0/W", NHID);
     net.o_vb = add("2/0/b", 1);
   } else {
-    net.o_c1W = add("0/0/W", 16 * 4 * 8 * 8);
+    net.o_c1W = add("0/0/W", 16 * (rgb ? 3 : 4) * 8 * 8);
     net.o_c1b = add("0/0/b", 16);
     net.o_c2W = add("0/1/W", 32 * 16 * 4 * 4);
     net.o_c2b = add("0/1/b", 32);
@@ -271,7 +279,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   };
   const bool L = arch == ARCH_LSTM;
   net.w_ctl = buf("ctl", CTL_SIZE * 8);
-  net.w_frames = buf("frames", (int64_t)net.R * n * PLANE);
+  net.w_frames = buf("frames", (int64_t)net.R * n * PLANE * (rgb ? 3 : 1));
   net.w_nvalid = buf("nvalid", (int64_t)net.R * n);
   net.w_reset = buf("reset", T1 * n);
   net.w_rewards = buf("rewards", S * 4);
@@ -343,7 +351,8 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s) {
   float* hfc = net.at<float>(net.w_hfc) + (int64_t)t * n * HID;
   const float* P = net.p;
   ARL_TRY(launch_conv_fwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl),
-                          n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W, P + net.o_c2b, a1, a2, s));
+                          n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W, P + net.o_c2b, a1, a2, s,
+                          net.rgb));
   ARL_TRY(fc_forward(net, n, a2, hfc, s));
   const float* hpol = hfc;
   if (net.arch == ARCH_LSTM) {
@@ -380,8 +389,9 @@ hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_
   float* a2 = net.at<float>(net.w_a2) + (int64_t)T * N * A2;
   float* hfc = net.at<float>(net.w_hfc) + (int64_t)T * N * HID;
   const float* P = net.p;
-  ARL_TRY((launch_gemm<64, 16, 32, 4, 1>(Conv1F32A{x}, WeightT{P + net.o_c1W, 256},
-                                                      EpiConv{a1, P + net.o_c1b, C1_OC, C1_P}, n * C1_P, C1_OC, 256,
+  const int K1 = (net.rgb ? 3 : 4) * 64;
+  ARL_TRY((launch_gemm<64, 16, 32, 4, 1>(Conv1F32A{x, K1 / 64}, WeightT{P + net.o_c1W, K1},
+                                                      EpiConv{a1, P + net.o_c1b, C1_OC, C1_P}, n * C1_P, C1_OC, K1,
                                                       1, s)));
   ARL_TRY((launch_gemm<32, 32, 32, 2, 2, GS, GK>(Conv2A{a1}, WeightT{P + net.o_c2W, 256},
                                                       EpiConv{a2, P + net.o_c2b, C2_OC, C2_P}, n * C2_P, C2_OC, 256,
@@ -469,7 +479,7 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
   //    straight from the frame ring
   return launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl), n,
                          net.R, S, a1, da2, P + net.o_c2W, slab, G + net.o_c2W, G + net.o_c2b, G + net.o_c1W,
-                         G + net.o_c1b, s);
+                         G + net.o_c1b, s, /*reduce=*/true, net.rgb);
 }
 
 // One stage of a window on the current workspace contents (arl_run_stage):
@@ -487,7 +497,7 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
       return launch_conv_fwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
                              net.at<int64_t>(net.w_ctl), n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W,
                              P + net.o_c2b, net.at<float>(net.w_a1) + (int64_t)t * n * A1, a2 + (int64_t)t * n * A2,
-                             s);
+                             s, net.rgb);
     case STAGE_FC_FWD:
       return fc_forward(net, n, a2 + (int64_t)t * n * A2, hfc + (int64_t)t * n * HID, s);
     case STAGE_POLICY: {
@@ -512,7 +522,7 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
       return launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
                              net.at<int64_t>(net.w_ctl), n, net.R, S, net.at<float>(net.w_a1),
                              net.at<float>(net.w_da2), P + net.o_c2W, slab, G + net.o_c2W, G + net.o_c2b,
-                             G + net.o_c1W, G + net.o_c1b, s, /*reduce=*/false);
+                             G + net.o_c1W, G + net.o_c1b, s, /*reduce=*/false, net.rgb);
     default:
       return hipErrorInvalidValue;
   }

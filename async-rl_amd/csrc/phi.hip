@@ -203,6 +203,116 @@ phi_ring_kernel(RingArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- RGB (Doom)
+// train_a3c_doom.py:21-23: phi(obs) = cv2.resize(obs.image_buffer, (84, 84))
+// .transpose(2, 0, 1).astype(float32) / 255 -- the RGB24 (H, W, 3) screen of
+// doom_env.py:47 resized per channel with the same fixed-point INTER_LINEAR
+// as the ALE path, no max-pool, no luminance, no frame stack.  One workgroup
+// = one env x one band of 12 output rows; the 24 source rows the band's taps
+// touch are staged in (dynamic) LDS, W*3 bytes each, 16 bytes per load.
+struct RgbCoef {
+  int16_t xofs[DST];
+  int16_t xa0[DST], xa1[DST];
+  int16_t yofs[BAND];
+  int16_t yb0[BAND], yb1[BAND];
+};
+
+// out(ch, dy, dx) for dy in [dy0, dy0 + 12): uint8 planes (plane stride
+// `pstride` bytes) or, with OUT_F32, f32 / 255 (plane stride 84*84 floats)
+template <bool OUT_F32>
+__device__ inline void rgb_band(const uint8_t* __restrict__ img, int H, int W, void* __restrict__ out,
+                                int64_t pstride, int dy0, int mode, RgbCoef& cf, uint8_t* rows) {
+  const int tid = threadIdx.x;
+  if (tid < DST) {
+    int o, a0, a1;
+    resize_coeff(tid, W, DST, o, a0, a1);
+    cf.xofs[tid] = (int16_t)o; cf.xa0[tid] = (int16_t)a0; cf.xa1[tid] = (int16_t)a1;
+  } else if (tid >= 96 && tid < 96 + BAND) {
+    int o, b0, b1;
+    resize_coeff(dy0 + tid - 96, H, DST, o, b0, b1);
+    cf.yofs[tid - 96] = (int16_t)o; cf.yb0[tid - 96] = (int16_t)b0; cf.yb1[tid - 96] = (int16_t)b1;
+  }
+  __syncthreads();
+  const int rb = W * 3, chunks = rb / 16;   // W % 16 == 0 (checked by the host)
+  for (int i = tid; i < 2 * BAND * chunks; i += 256) {
+    const int r = i / chunks, c = i - r * chunks;
+    int sy = cf.yofs[r >> 1] + (r & 1);
+    if (sy > H - 1) sy = H - 1;
+    reinterpret_cast<uint4*>(rows + r * rb)[c] = reinterpret_cast<const uint4*>(img + (size_t)sy * rb)[c];
+  }
+  __syncthreads();
+  for (int task = tid; task < 3 * BAND * (DST / 4); task += 256) {
+    const int ch = task / (BAND * (DST / 4)), rem = task - ch * (BAND * (DST / 4));
+    const int ly = rem / (DST / 4), q = rem - ly * (DST / 4);
+    const int b0 = cf.yb0[ly], b1 = cf.yb1[ly];
+    const uint8_t* s0 = rows + (2 * ly) * rb + ch;
+    const uint8_t* s1 = s0 + rb;
+    int v4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int dx = q * 4 + j;
+      const int sx = cf.xofs[dx];
+      const int sx1 = sx + 1 < W ? sx + 1 : W - 1;
+      const int a0 = cf.xa0[dx], a1 = cf.xa1[dx];
+      const int r0 = (int)s0[3 * sx] * a0 + (int)s0[3 * sx1] * a1;
+      const int r1 = (int)s1[3 * sx] * a0 + (int)s1[3 * sx1] * a1;
+      int v;
+      if ((mode & 1) == 0) v = (b0 * r0 + b1 * r1 + (1 << 21)) >> 22;
+      else v = ((((r0 >> 4) * b0) >> 16) + (((r1 >> 4) * b1) >> 16) + 2) >> 2;
+      v4[j] = v < 0 ? 0 : (v > 255 ? 255 : v);
+    }
+    const int dy = dy0 + ly;
+    if (OUT_F32) {
+      float4 o;
+      o.x = __fdiv_rn((float)v4[0], 255.f);
+      o.y = __fdiv_rn((float)v4[1], 255.f);
+      o.z = __fdiv_rn((float)v4[2], 255.f);
+      o.w = __fdiv_rn((float)v4[3], 255.f);
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + ch * PLANE + dy * DST + q * 4) = o;
+    } else {
+      const uint32_t packed = (uint32_t)v4[0] | ((uint32_t)v4[1] << 8) | ((uint32_t)v4[2] << 16) |
+                              ((uint32_t)v4[3] << 24);
+      *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(out) + ch * pstride + dy * DST + q * 4) = packed;
+    }
+  }
+}
+
+// batched train_a3c_doom.phi: imgs (n, H, W, 3) -> out (n, 3, 84, 84) f32
+__global__ void __launch_bounds__(256)
+rgb_phi_kernel(const uint8_t* __restrict__ imgs, int H, int W, float* __restrict__ out, int mode) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t rgb_rows[];
+  __shared__ RgbCoef cf;
+  const int64_t e = blockIdx.y;
+  rgb_band<true>(imgs + e * H * W * 3, H, W, out + e * 3 * PLANE, 0, blockIdx.x * BAND, mode, cf, rgb_rows);
+}
+
+// In-loop ring for RGB nets: the 3 planes of obs step k go to slot k % R
+// (frames (R, n, 3, 84, 84)); nvalid = 3 (conv input = [0, R, G, B]); the
+// reward / done / reset bookkeeping of phi_ring_kernel.
+__global__ void __launch_bounds__(256)
+rgb_ring_kernel(RingArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t rgb_rows[];
+  __shared__ RgbCoef cf;
+  const int e = blockIdx.y;
+  const int64_t k = a.ctl[CTL_STEP] + a.t;
+  const int slot = (int)(k % a.R);
+  const int64_t pidx = k % a.pool_len;
+  const uint8_t* img = a.pair_pool + (pidx * a.n + e) * (int64_t)a.H * a.W * 3;
+  uint8_t* dst = a.frames + ((int64_t)slot * a.n + e) * 3 * PLANE;
+  rgb_band<false>(img, a.H, a.W, dst, PLANE, blockIdx.x * BAND, a.mode, cf, rgb_rows);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint8_t d = a.done_pool ? a.done_pool[pidx * a.n + e] : 0;
+    const bool rs = a.force_reset || d != 0;
+    a.nvalid[(int64_t)slot * a.n + e] = 3;
+    a.reset_flags[(int64_t)a.t * a.n + e] = rs ? 1 : 0;
+    if (a.t >= 1) {
+      float r = a.reward_pool ? a.reward_pool[pidx * a.n + e] : 0.f;
+      a.rewards[(int64_t)(a.t - 1) * a.n + e] = r;
+      a.dones[(int64_t)(a.t - 1) * a.n + e] = d;
+    }
+  }
+}
+
 // dqn_phi.py:14-16: float32(x) / 255.0 (IEEE correctly rounded division).
 __global__ void dqn_phi_kernel(const uint8_t* __restrict__ in, float* __restrict__ out, int64_t count) {
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
@@ -259,6 +369,19 @@ hipError_t launch_phi_stack(const uint8_t* pairs, const uint8_t* prev_stack, con
 
 hipError_t launch_phi_ring(const RingArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(phi_ring_kernel, dim3(NBANDS, (unsigned)a.n), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+static size_t rgb_lds(int W) { return (size_t)2 * BAND * W * 3; }
+
+hipError_t launch_rgb_phi(const uint8_t* imgs, int64_t n, int H, int W, float* out, int mode, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rgb_phi_kernel, dim3(NBANDS, (unsigned)n), dim3(256), rgb_lds(W), s, imgs, H, W, out, mode);
+  return hipGetLastError();
+}
+
+hipError_t launch_rgb_ring(const RingArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(rgb_ring_kernel, dim3(NBANDS, (unsigned)a.n), dim3(256), rgb_lds(a.W), s, a);
   return hipGetLastError();
 }
 

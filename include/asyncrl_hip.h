@@ -29,6 +29,9 @@ extern "C" {
 #define ARL_ARCH_FF 0     /* A3CFF   (a3c_ale.py:28-40) */
 #define ARL_ARCH_LSTM 1   /* A3CLSTM (a3c_ale.py:43-70) */
 #define ARL_ARCH_FF_NATURE 2  /* A3CFF with NatureDQNHead (dqn_head.py:6-28) instead of NIPSDQNHead */
+#define ARL_ARCH_RGB 16   /* flag for FF / LSTM: the ViZDoom models of train_a3c_doom.py:25-63
+                             (NIPSDQNHead(n_input_channels=3) on one RGB screen, no frame stack);
+                             observations come through arl_observe_rgb */
 
 #define ARL_RESIZE_SCALAR 0  /* OpenCV FixedPtCast vertical pass (canonical) */
 #define ARL_RESIZE_SIMD 1    /* OpenCV VResizeLinearVec_32s8u (mulhi) pass */
@@ -59,6 +62,13 @@ int arl_phi_stack(const uint8_t* rgb_pairs, const uint8_t* prev_stack, const uin
 
 /* dqn_phi.py:4-17 dqn_phi, batched: (n, 4, 84, 84) uint8 -> float32 / 255. */
 int arl_dqn_phi(const uint8_t* stack_u8, float* out, int64_t n, void* stream);
+
+/* train_a3c_doom.py:21-23 phi, batched: cv2.resize(image_buffer, (84, 84))
+ * per channel (INTER_LINEAR fixed point, resize_mode as above, no crop),
+ * transpose(2, 0, 1), float32 / 255.  imgs: (n, H, W, 3) uint8 RGB24
+ * (doom_env.py:47), 16-byte aligned, W % 16 == 0, W <= 2048; out: (n, 3,
+ * 84, 84) f32. */
+int arl_rgb_phi(const uint8_t* imgs, int64_t n, int H, int W, float* out, int resize_mode, void* stream);
 
 /* ------------------------------------------------------------------ net */
 typedef struct arl_net arl_net;
@@ -98,6 +108,13 @@ int arl_net_reset(arl_net* net, void* stream);
  * starting an episode (first observation). */
 int arl_observe(arl_net* net, int t, const uint8_t* pair_pool, const float* reward_pool,
                 const uint8_t* done_pool, int64_t pool_len, int force_reset, int resize_mode, void* stream);
+
+/* arl_observe for an ARL_ARCH_RGB net: the observation is the env's RGB
+ * screen, img_pool (pool_len, n, H, W, 3) uint8 (W % 16 == 0, W <= 2048),
+ * resized to 3 planes as arl_rgb_phi; same reward / done / reset handling
+ * (the reset clears the LSTM state; there is no frame stack). */
+int arl_observe_rgb(arl_net* net, int t, const uint8_t* img_pool, int H, int W, const float* reward_pool,
+                    const uint8_t* done_pool, int64_t pool_len, int force_reset, int resize_mode, void* stream);
 
 /* A3C.act forward + sample at window step t (a3c.py:154-164): pi_and_v of
  * the ring state, softmax policy output, Philox inverse-CDF action.  t ==

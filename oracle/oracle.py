@@ -124,6 +124,43 @@ def resize_linear_u8(img: np.ndarray, mode: int = RESIZE_SCALAR) -> np.ndarray:
     return np.clip(out, 0, 255).astype(np.uint8)
 
 
+def resize_linear_any_u8(img: np.ndarray, mode: int = RESIZE_SCALAR) -> np.ndarray:
+    """cv2.resize(img, (84, 84), INTER_LINEAR) of a (..., H, W) uint8 plane of
+    any size: the same two fixed-point passes as resize_linear_u8 with the
+    coefficients of H -> 84 and W -> 84 (OpenCV resizes each channel of an
+    8UC3 image with one coefficient set: HResizeLinear indexes sx*cn + k)."""
+    H, W = img.shape[-2:]
+    xs, xa = resize_coeffs(W, DST)
+    ys, yb = resize_coeffs(H, DST)
+    src = img.astype(np.int64)
+    rows = src[..., :, xs] * xa[:, 0] + src[..., :, np.minimum(xs + 1, W - 1)] * xa[:, 1]
+    r0 = rows[..., ys, :]
+    r1 = rows[..., np.minimum(ys + 1, H - 1), :]
+    b0 = yb[:, 0][:, None]
+    b1 = yb[:, 1][:, None]
+    if mode == RESIZE_SCALAR:
+        out = (b0 * r0 + b1 * r1 + (1 << 21)) >> 22
+    elif mode == RESIZE_SIMD:
+        out = ((((r0 >> 4) * b0) >> 16) + (((r1 >> 4) * b1) >> 16) + 2) >> 2
+    else:
+        raise ValueError("resize mode must be 0 (scalar) or 1 (simd)")
+    return np.clip(out, 0, 255).astype(np.uint8)
+
+
+def rgb_screen_u8(img: np.ndarray, mode: int = RESIZE_SCALAR) -> np.ndarray:
+    """train_a3c_doom.py:22-23 up to the uint8 planes: cv2.resize of the
+    (H, W, 3) RGB24 screen (doom_env.py:47) to (84, 84, 3), transposed to
+    (3, 84, 84)."""
+    assert img.ndim == 3 and img.shape[2] == 3
+    return resize_linear_any_u8(np.moveaxis(img, 2, 0), mode)
+
+
+def rgb_phi(img: np.ndarray, mode: int = RESIZE_SCALAR) -> np.ndarray:
+    """train_a3c_doom.py:21-23: phi(obs) = resize -> transpose(2, 0, 1) ->
+    astype(float32) / 255 (f32 true division)."""
+    return rgb_screen_u8(img, mode).astype(np.float32) / F32(255.0)
+
+
 def current_screen(cur: np.ndarray, prev: np.ndarray,
                    mode: int = RESIZE_SCALAR) -> np.ndarray:
     """ale.py:59-89 (crop_or_scale='scale', the default at ale.py:18; 'crop'
@@ -161,11 +198,16 @@ PHI_LUT = (np.arange(256, dtype=np.float32) / F32(255.0)).astype(np.float32)
 ARCH_FF = 0
 ARCH_LSTM = 1
 ARCH_FF_NATURE = 2     # A3CFF with NatureDQNHead (dqn_head.py:6-28) instead of NIPSDQNHead
+ARCH_RGB = 16          # flag (FF / LSTM): the ViZDoom models, train_a3c_doom.py:25-63 --
+                       # NIPSDQNHead(n_input_channels=3) on one RGB screen
 
 
 def param_shapes(arch: int, n_actions: int):
-    """Chainer namedparams / HDF5 paths in link order (a3c_ale.py:35,52)."""
-    head = [("0/0/W", (16, 4, 8, 8)), ("0/0/b", (16,)),
+    """Chainer namedparams / HDF5 paths in link order (a3c_ale.py:35,52;
+    train_a3c_doom.py:28-33,46-53 for the RGB models)."""
+    c_in = 3 if arch & ARCH_RGB else 4
+    arch &= ~ARCH_RGB
+    head = [("0/0/W", (16, c_in, 8, 8)), ("0/0/b", (16,)),
             ("0/1/W", (32, 16, 4, 4)), ("0/1/b", (32,)),
             ("0/2/W", (256, 2592)), ("0/2/b", (256,))]
     if arch == ARCH_FF:
@@ -185,6 +227,7 @@ def param_shapes(arch: int, n_actions: int):
 
 def pname(arch: int, role: str) -> str:
     """Short role names -> namedparam paths."""
+    arch &= ~ARCH_RGB
     if arch == ARCH_FF:
         m = {"c1W": "0/0/W", "c1b": "0/0/b", "c2W": "0/1/W", "c2b": "0/1/b",
              "fcW": "0/2/W", "fcb": "0/2/b", "piW": "1/0/W", "pib": "1/0/b",
@@ -572,7 +615,7 @@ def ff_window_grads(params, states, actions, rewards, dones, boot_state,
     Per env the window splits into segments at terminals; each segment is
     one a3c.py:77-130 update at fixed theta; gradients are summed."""
     T, N = actions.shape
-    x = states.reshape(T * N, 4, DST, DST)
+    x = states.reshape(T * N, states.shape[2], DST, DST)   # 4 planes, or 3 for ARCH_RGB
     logits, v, acts = pi_and_v_ff(params, x, arch)
     p = softmax(logits)
     lp = log_softmax(logits)
@@ -596,7 +639,7 @@ def lstm_window(params, states, actions, rewards, dones_prev, dones, boot_state,
     T, N = actions.shape
     arch = ARCH_LSTM
     A = params["2/0/W"].shape[0]
-    xs = states.reshape(T * N, 4, DST, DST)
+    xs = states.reshape(T * N, states.shape[2], DST, DST)
     a1, a2, hh = nips_head(params, arch, xs)
     hh = hh.reshape(T, N, 256)
     hs, cs, gs, has_l, hprev_l, cprev_l = [], [], [], [], [], []

@@ -56,3 +56,28 @@ class OracleEnvView:
     def window_rd(self, rewards, k0, T):
         idx = [(k0 + t + 1) % self.pool_len for t in range(T)]
         return rewards[idx].copy(), self.dones[idx].copy()
+
+
+def make_rgb_pools(rng, pool_len, n, H=120, W=160, p_done=0.15):
+    """ViZDoom-style pools: screens (pool_len, n, H, W, 3) uint8 RGB24
+    (doom_env.py:47); rewards and dones as make_pools."""
+    imgs = rng.integers(0, 256, (pool_len, n, H, W, 3), dtype=np.uint8)
+    rewards = rng.choice(np.array([-2.0, -1.0, 0.0, 0.0, 0.0, 1.0, 3.5], np.float32), (pool_len, n))
+    dones = (rng.random((pool_len, n)) < p_done).astype(np.uint8)
+    return imgs, rewards.astype(np.float32), dones
+
+
+class OracleRgbView(OracleEnvView):
+    """States of an RGB net: phi of the current screen only
+    (train_a3c_doom.py:21-23), no frame stack."""
+
+    def __init__(self, imgs, dones, mode=O.RESIZE_SCALAR):
+        self.imgs, self.dones, self.mode = imgs, dones, mode
+        self.pool_len, self.n = imgs.shape[0], imgs.shape[1]
+
+    def state(self, k):
+        j = k % self.pool_len
+        return np.stack([O.rgb_phi(self.imgs[j, e], self.mode) for e in range(self.n)])
+
+    def states_f32(self, k0, T):
+        return np.stack([self.state(k0 + t) for t in range(T)]), self.state(k0 + T)

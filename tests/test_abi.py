@@ -36,6 +36,8 @@ def test_abi_version_and_errors():
     assert rc == 1 and b"arch" in lib.arl_last_error()
     rc = lib.arl_net_create(ctypes.byref(h), 0, 0, 16, 5, 0, 0)
     assert rc == 1
+    rc = lib.arl_net_create(ctypes.byref(h), 2 | 16, 4, 16, 5, 0, 0)   # Nature head has no RGB model
+    assert rc == 1 and b"RGB" in lib.arl_last_error()
     # calls on an unbound handle fail cleanly
     assert lib.arl_net_create(ctypes.byref(h), 0, 4, 16, 5, 0, 0) == 0
     assert lib.arl_act(h, 0, None) == 3
@@ -43,7 +45,9 @@ def test_abi_version_and_errors():
     lib.arl_net_destroy(h)
 
 
-@pytest.mark.parametrize("arch,A,count", [(0, 4, 677429), (1, 6, 1203255), (2, 4, 1686693)])
+# 16 / 17: the ViZDoom models (ARL_ARCH_RGB, train_a3c_doom.py:25-63), conv1 W (16, 3, 8, 8)
+@pytest.mark.parametrize("arch,A,count", [(0, 4, 677429), (1, 6, 1203255), (2, 4, 1686693),
+                                          (16, 3, 676148), (17, 3, 1201460)])
 def test_param_layout_matches_chainer(arch, A, count):
     from asyncrl_amd._lib import lib
     from asyncrl_amd.net import param_shapes
@@ -69,7 +73,7 @@ def test_param_layout_matches_chainer(arch, A, count):
     assert 0 < ws < 4 << 30
     off, nb = ctypes.c_int64(), ctypes.c_int64()
     assert lib.arl_net_buffer(h, b"frames", ctypes.byref(off), ctypes.byref(nb)) == 0
-    assert nb.value == 9 * 256 * 84 * 84 and off.value % 256 == 0
+    assert nb.value == 9 * 256 * 84 * 84 * (3 if arch & 16 else 1) and off.value % 256 == 0
     assert lib.arl_net_buffer(h, b"nope", ctypes.byref(off), ctypes.byref(nb)) == 1
     lib.arl_net_destroy(h)
 
