@@ -50,7 +50,7 @@ struct RingArgs {
 };
 
 // RGB (Doom) observations, train_a3c_doom.py:21-23 / doom_env.py:47
-constexpr int RGB_MAX_W = 2048;   // staged source rows: 24 x W x 3 bytes of LDS
+constexpr int RGB_MAX_W = 2048;   // staged source rows: 12 x W x 3 bytes of LDS
 hipError_t launch_rgb_phi(const uint8_t* imgs, int64_t n, int H, int W, float* out, int mode, hipStream_t s);
 hipError_t launch_rgb_ring(const RingArgs& a, hipStream_t s);
 

@@ -208,16 +208,18 @@ phi_ring_kernel(RingArgs a) {
 // .transpose(2, 0, 1).astype(float32) / 255 -- the RGB24 (H, W, 3) screen of
 // doom_env.py:47 resized per channel with the same fixed-point INTER_LINEAR
 // as the ALE path, no max-pool, no luminance, no frame stack.  One workgroup
-// = one env x one band of 12 output rows; the 24 source rows the band's taps
+// = one env x one band of 6 output rows; the 12 source rows the band's taps
 // touch are staged in (dynamic) LDS, W*3 bytes each, 16 bytes per load.
+constexpr int RGB_BAND = 6;                  // output rows per workgroup (12 source rows of LDS)
+constexpr int RGB_NBANDS = DST / RGB_BAND;   // 14
 struct RgbCoef {
   int16_t xofs[DST];
   int16_t xa0[DST], xa1[DST];
-  int16_t yofs[BAND];
-  int16_t yb0[BAND], yb1[BAND];
+  int16_t yofs[RGB_BAND];
+  int16_t yb0[RGB_BAND], yb1[RGB_BAND];
 };
 
-// out(ch, dy, dx) for dy in [dy0, dy0 + 12): uint8 planes (plane stride
+// out(ch, dy, dx) for dy in [dy0, dy0 + 6): uint8 planes (plane stride
 // `pstride` bytes) or, with OUT_F32, f32 / 255 (plane stride 84*84 floats)
 template <bool OUT_F32>
 __device__ inline void rgb_band(const uint8_t* __restrict__ img, int H, int W, void* __restrict__ out,
@@ -227,22 +229,31 @@ __device__ inline void rgb_band(const uint8_t* __restrict__ img, int H, int W, v
     int o, a0, a1;
     resize_coeff(tid, W, DST, o, a0, a1);
     cf.xofs[tid] = (int16_t)o; cf.xa0[tid] = (int16_t)a0; cf.xa1[tid] = (int16_t)a1;
-  } else if (tid >= 96 && tid < 96 + BAND) {
+  } else if (tid >= 96 && tid < 96 + RGB_BAND) {
     int o, b0, b1;
     resize_coeff(dy0 + tid - 96, H, DST, o, b0, b1);
     cf.yofs[tid - 96] = (int16_t)o; cf.yb0[tid - 96] = (int16_t)b0; cf.yb1[tid - 96] = (int16_t)b1;
   }
   __syncthreads();
+  // LDS-DMA (global_load_lds_dwordx4): chunk i = (row r, 16-byte column c)
+  // lands at rows + 16 i, one 1 KB wave instruction at a time, all in flight
+  // before the single wait
   const int rb = W * 3, chunks = rb / 16;   // W % 16 == 0 (checked by the host)
-  for (int i = tid; i < 2 * BAND * chunks; i += 256) {
-    const int r = i / chunks, c = i - r * chunks;
-    int sy = cf.yofs[r >> 1] + (r & 1);
-    if (sy > H - 1) sy = H - 1;
-    reinterpret_cast<uint4*>(rows + r * rb)[c] = reinterpret_cast<const uint4*>(img + (size_t)sy * rb)[c];
+  const int total = 2 * RGB_BAND * chunks, lane = tid & 63;
+  for (int it = tid >> 6; it * 64 < total; it += 4) {
+    const int i = it * 64 + lane;
+    if (i < total) {
+      const int r = i / chunks, c = i - r * chunks;
+      int sy = cf.yofs[r >> 1] + (r & 1);
+      if (sy > H - 1) sy = H - 1;
+      __builtin_amdgcn_global_load_lds(img + (size_t)sy * rb + 16 * c,
+                                       (__attribute__((address_space(3))) void*)(rows + 1024 * it), 16, 0, 0);
+    }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int task = tid; task < 3 * BAND * (DST / 4); task += 256) {
-    const int ch = task / (BAND * (DST / 4)), rem = task - ch * (BAND * (DST / 4));
+  for (int task = tid; task < 3 * RGB_BAND * (DST / 4); task += 256) {
+    const int ch = task / (RGB_BAND * (DST / 4)), rem = task - ch * (RGB_BAND * (DST / 4));
     const int ly = rem / (DST / 4), q = rem - ly * (DST / 4);
     const int b0 = cf.yb0[ly], b1 = cf.yb1[ly];
     const uint8_t* s0 = rows + (2 * ly) * rb + ch;
@@ -283,7 +294,7 @@ rgb_phi_kernel(const uint8_t* __restrict__ imgs, int H, int W, float* __restrict
   extern __shared__ __attribute__((aligned(16))) uint8_t rgb_rows[];
   __shared__ RgbCoef cf;
   const int64_t e = blockIdx.y;
-  rgb_band<true>(imgs + e * H * W * 3, H, W, out + e * 3 * PLANE, 0, blockIdx.x * BAND, mode, cf, rgb_rows);
+  rgb_band<true>(imgs + e * H * W * 3, H, W, out + e * 3 * PLANE, 0, blockIdx.x * RGB_BAND, mode, cf, rgb_rows);
 }
 
 // In-loop ring for RGB nets: the 3 planes of obs step k go to slot k % R
@@ -299,7 +310,7 @@ rgb_ring_kernel(RingArgs a) {
   const int64_t pidx = k % a.pool_len;
   const uint8_t* img = a.pair_pool + (pidx * a.n + e) * (int64_t)a.H * a.W * 3;
   uint8_t* dst = a.frames + ((int64_t)slot * a.n + e) * 3 * PLANE;
-  rgb_band<false>(img, a.H, a.W, dst, PLANE, blockIdx.x * BAND, a.mode, cf, rgb_rows);
+  rgb_band<false>(img, a.H, a.W, dst, PLANE, blockIdx.x * RGB_BAND, a.mode, cf, rgb_rows);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     const uint8_t d = a.done_pool ? a.done_pool[pidx * a.n + e] : 0;
     const bool rs = a.force_reset || d != 0;
@@ -372,16 +383,17 @@ hipError_t launch_phi_ring(const RingArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-static size_t rgb_lds(int W) { return (size_t)2 * BAND * W * 3; }
+static size_t rgb_lds(int W) { return (size_t)2 * RGB_BAND * W * 3; }
 
 hipError_t launch_rgb_phi(const uint8_t* imgs, int64_t n, int H, int W, float* out, int mode, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(rgb_phi_kernel, dim3(NBANDS, (unsigned)n), dim3(256), rgb_lds(W), s, imgs, H, W, out, mode);
+  hipLaunchKernelGGL(rgb_phi_kernel, dim3(RGB_NBANDS, (unsigned)n), dim3(256), rgb_lds(W), s, imgs, H, W, out,
+                     mode);
   return hipGetLastError();
 }
 
 hipError_t launch_rgb_ring(const RingArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(rgb_ring_kernel, dim3(NBANDS, (unsigned)a.n), dim3(256), rgb_lds(a.W), s, a);
+  hipLaunchKernelGGL(rgb_ring_kernel, dim3(RGB_NBANDS, (unsigned)a.n), dim3(256), rgb_lds(a.W), s, a);
   return hipGetLastError();
 }
 

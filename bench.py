@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 # ASYNCRL_PKG_ROOT: another build of the package (A/B timing, scripts/ab.sh)
 sys.path.insert(0, os.environ.get("ASYNCRL_PKG_ROOT") or os.path.join(ROOT, "async-rl_amd"))
 
-from asyncrl_amd import A3C, A3CFF, A3CFFNature, A3CLSTM, GradientClipping, RMSpropAsync  # noqa: E402
+from asyncrl_amd import A3C, A3CFF, A3CFFNature, A3CLSTM, DoomA3CFF, DoomA3CLSTM, GradientClipping, RMSpropAsync  # noqa: E402
 from asyncrl_amd import _lib  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
@@ -40,6 +40,9 @@ CONV_FWD_FLOP_PER_ENV = 2 * (400 * 16 * 256 + 81 * 32 * 256)             # 4,603
 FC_FWD_FLOP_PER_ENV = 2 * 2592 * 256                                     # 1,327,104
 CONV_BWD_FLOP_PER_SAMPLE = 2 * (32 * 256 * 81 + 81 * 32 * 256 + 400 * 16 * 256)   # dW2 + convT + dW1
 HID_BYTES = 256 * 4
+# ViZDoom models (train_a3c_doom.py:28,46): conv1 K = 3 * 64 (the kernels' zero input plane is not counted)
+DOOM_CONV_FWD_FLOP_PER_ENV = 2 * (400 * 16 * 192 + 81 * 32 * 256)
+DOOM_CONV_BWD_FLOP_PER_SAMPLE = 2 * (32 * 256 * 81 + 81 * 32 * 256 + 400 * 16 * 192)
 # NatureDQNHead (dqn_head.py:6-28): conv MACs 400*32*256 + 81*64*512 + 49*64*576, FC 3136*512
 NAT_CONV_FWD_FLOP_PER_ENV = 2 * (400 * 32 * 256 + 81 * 64 * 512 + 49 * 64 * 576)      # 15,474,688
 NAT_FC_FWD_FLOP_PER_ENV = 2 * 3136 * 512
@@ -60,8 +63,11 @@ def parse():
                          "A=6, c4 FF 512 envs per GPU (4096 over 8), c5 phi stress 16384 frame pairs")
     ap.add_argument("--envs-per-gpu", type=int, default=0, help="0: the workload's")
     ap.add_argument("--t-max", type=int, default=5)
-    ap.add_argument("--arch", choices=["ff", "lstm", "nature"], default=None,
-                    help="default: the workload's; nature = A3CFF with NatureDQNHead (SURVEY 8(a) a8)")
+    ap.add_argument("--arch", choices=["ff", "lstm", "nature", "doom_ff", "doom_lstm"], default=None,
+                    help="default: the workload's; nature = A3CFF with NatureDQNHead (SURVEY 8(a) a8); doom_* = "
+                         "the ViZDoom models of train_a3c_doom.py on RGB screens (--doom-width)")
+    ap.add_argument("--doom-width", type=int, choices=[160, 320, 640], default=640,
+                    help="ViZDoom screen resolution (doom_env.py:43-46; 640 = 640x480, the default)")
     ap.add_argument("--actions", type=int, default=0, help="0: 4 for ff (Breakout), 6 for lstm (Space Invaders)")
     ap.add_argument("--pool", type=int, default=8)
     ap.add_argument("--no-graph", action="store_true")
@@ -80,12 +86,36 @@ def init_dist():
     return world, rank, local
 
 
-def synth_pools(n, pool, seed, dev):
+def rgb_phi_bytes(H, W):
+    """Algorithmic bytes of one ViZDoom observation (train_a3c_doom.py:21-23 into
+    the ring): the distinct source rows the bilinear taps touch (OpenCV
+    half-pixel mapping, 2 taps per output row) x W x 3, plus 3 planes written."""
+    rows = set()
+    for d in range(84):
+        f = np.float32((d + 0.5) * (H / 84.0) - 0.5)
+        s = max(0, min(int(np.floor(f)), H - 1))
+        rows.update((s, min(s + 1, H - 1)))
+    return len(rows) * W * 3 + 3 * 84 * 84
+
+
+def synth_rgb_pools(n, pool, seed, dev, H, W):
+    """ViZDoom-shaped synthetic inputs: uniform RGB24 screens (H, W, 3), rewards
+    and terminals as synth_pools."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(1 + 1000 * seed)
+    imgs = torch.randint(0, 256, (pool, n, H, W, 3), dtype=torch.uint8, device=dev, generator=g)
+    _, rewards, dones = synth_pools(n, 1, seed, dev, frames=False, pool_rd=pool)
+    return imgs, rewards, dones
+
+
+def synth_pools(n, pool, seed, dev, frames=True, pool_rd=None):
     """SURVEY 8(d) synthetic inputs: uniform RGB frames (rng 1), rewards in
     {-1,0,+1} with P(!=0)=0.05 (rng 2), terminals Bernoulli(1/500) (rng 3)."""
     g = torch.Generator(device=dev)
     g.manual_seed(1 + 1000 * seed)
-    pairs = torch.randint(0, 256, (pool, n, 2, 210, 160, 3), dtype=torch.uint8, device=dev, generator=g)
+    pairs = torch.randint(0, 256, (pool, n, 2, 210, 160, 3), dtype=torch.uint8, device=dev, generator=g) \
+        if frames else None
+    pool = pool_rd or pool
     r2 = np.random.default_rng(2 + 1000 * seed)
     rewards = r2.choice(np.array([-1.0, 0.0, 1.0], np.float32), (pool, n), p=[0.025, 0.95, 0.025])
     r3 = np.random.default_rng(3 + 1000 * seed)
@@ -172,11 +202,16 @@ def main():
     arch = a.arch or w_arch
     A = a.actions or (w_A if arch == w_arch else (6 if arch == "lstm" else 4))
     N, T = a.envs_per_gpu or w_envs, a.t_max
-    Model = {"ff": A3CFF, "lstm": A3CLSTM, "nature": A3CFFNature}[arch]
+    Model = {"ff": A3CFF, "lstm": A3CLSTM, "nature": A3CFFNature, "doom_ff": DoomA3CFF,
+             "doom_lstm": DoomA3CLSTM}[arch]
     nat = arch == "nature"
-    conv_fwd_flop = NAT_CONV_FWD_FLOP_PER_ENV if nat else CONV_FWD_FLOP_PER_ENV
+    doom = arch.startswith("doom")
+    if doom and not a.actions:
+        A = 3                                          # train_a3c_doom.py:105
+    conv_fwd_flop = NAT_CONV_FWD_FLOP_PER_ENV if nat else DOOM_CONV_FWD_FLOP_PER_ENV if doom else CONV_FWD_FLOP_PER_ENV
     fc_fwd_flop = NAT_FC_FWD_FLOP_PER_ENV if nat else FC_FWD_FLOP_PER_ENV
-    conv_bwd_flop = NAT_CONV_BWD_FLOP_PER_SAMPLE if nat else CONV_BWD_FLOP_PER_SAMPLE
+    conv_bwd_flop = NAT_CONV_BWD_FLOP_PER_SAMPLE if nat else DOOM_CONV_BWD_FLOP_PER_SAMPLE if doom else \
+        CONV_BWD_FLOP_PER_SAMPLE
     hid_bytes = 2 * HID_BYTES if nat else HID_BYTES
     model = Model(A, n_envs=N, t_max=T, seed=1234, env_offset=rank * N, init_seed=0, device=dev)
     opt = RMSpropAsync(lr=7e-4, eps=1e-1, alpha=0.99).setup(model)
@@ -184,7 +219,13 @@ def main():
     opt.anneal_total_steps = 8 * 10 ** 7        # a3c_ale.py:200 --steps default
     opt.n_total_envs = N * world
     agent = A3C(model, opt, T, 0.99, beta=1e-2)
-    pairs, rewards, dones = synth_pools(N, a.pool, rank, dev)
+    if doom:
+        dH, dW = a.doom_width * 3 // 4, a.doom_width
+        pairs, rewards, dones = synth_rgb_pools(N, a.pool, rank, dev, dH, dW)
+        phi_bytes = rgb_phi_bytes(dH, dW)
+    else:
+        pairs, rewards, dones = synth_pools(N, a.pool, rank, dev)
+        phi_bytes = PHI_BYTES_PER_ENV_STEP
     P = a.pool
 
     use_graph = not a.no_graph
@@ -263,9 +304,9 @@ def main():
             return 1e3 * ev0.elapsed_time(ev1) / a.kernel_reps
 
         specs = [  # name, kernel, launch fn, launches per window, bound, algorithmic work per launch
-            ("phi", "phi_ring_kernel",
+            ("phi", "rgb_ring_kernel" if doom else "phi_ring_kernel",
              lambda i: net.observe(1 + i % T, pairs, rewards, dones, P, stream=stream), T + 1, "hbm",
-             N * PHI_BYTES_PER_ENV_STEP),
+             N * phi_bytes),
             ("conv_fwd", "gemm_kernel x3 (implicit-GEMM convs)" if nat else "conv_fwd_kernel",
              lambda i: net.run_stage("conv_fwd", i % T, stream=stream), T + 1, "mfma", N * conv_fwd_flop),
             ("fc_fwd", "gemm_kernel + reduce_grad_kernel" if nat else "fc_fwd_kernel",
@@ -319,8 +360,9 @@ def main():
             "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (uniform RGB 210x160 frame pairs, rewards P(!=0)=0.05, terminals p=1/500)",
-            "config": {"workload": ("%s: A3C %s " + ("Nature" if nat else "NIPS") + "-DQN head, %d envs x t_max=%d per GPU (phi + conv head + sampling "
+            "data": ("synthetic (uniform RGB24 %dx%d ViZDoom-shaped screens" % (dH, dW) if doom else
+                     "synthetic (uniform RGB 210x160 frame pairs") + ", rewards P(!=0)=0.05, terminals p=1/500)",
+            "config": {"workload": ("%s: A3C %s " + ("Nature" if nat else "NIPS (RGB)" if doom else "NIPS") + "-DQN head, %d envs x t_max=%d per GPU (phi + conv head + sampling "
                                     "+ n-step returns + backward + clip + RMSProp)") % (a.workload, arch.upper(), N, T),
                        "envs_per_gpu": N, "global_envs": N * world, "t_max": T, "n_actions": A, "arch": arch,
                        "graph": use_graph, "parallelism": "dp%d" % world,
