@@ -313,6 +313,54 @@ def test_ff_wide_action_set(gpu):
     _run_ff(gpu, N=3, T=3, A=18, seed=23, kind="uniform", windows=1)
 
 
+# ------------------------------------------------------------------ edge cases
+def test_ff_single_env_single_step_windows(gpu):
+    """N = 1, t_max = 1 (every act is a window end: a3c.py:77-78 with
+    t_max = 1), three windows: the smallest grid of every kernel."""
+    _run_ff(gpu, N=1, T=1, A=4, seed=24, kind="uniform", windows=3)
+
+
+def test_ff_ragged_env_count(gpu):
+    """N = 67: one past the 64-env tiles, 3 past the 16-env policy rows and
+    the 32-env FC tiles; two windows with terminals."""
+    _run_ff(gpu, N=67, T=2, A=5, seed=25, kind="palette")
+
+
+def test_ff_every_step_terminal(gpu):
+    """Every observation ends an episode (done = 1 everywhere): every window
+    segment has length 1 with R = 0 (a3c.py:82-83) and the stack resets every
+    step (ale.py:155-158)."""
+    _run_ff(gpu, N=4, T=3, A=4, seed=26, kind="uniform", p_done=1.0)
+
+
+def test_ff_single_action(gpu):
+    """A = 1: softmax = 1, entropy = 0, the sampler must return action 0."""
+    _run_ff(gpu, N=5, T=3, A=1, seed=27, kind="uniform", windows=1)
+
+
+def test_phi_entry_points_accept_empty_batches(gpu):
+    """n = 0 is a no-op on every batched phi entry point (no launch, no error)."""
+    from asyncrl_amd import current_screen, dqn_phi, phi_stack, rgb_phi
+    z = torch.zeros((0, 210, 160, 3), dtype=torch.uint8, device=gpu)
+    assert current_screen(z, z).shape == (0, 84, 84)
+    zp = torch.zeros((0, 2, 210, 160, 3), dtype=torch.uint8, device=gpu)
+    zs = torch.zeros((0, 4, 84, 84), dtype=torch.uint8, device=gpu)
+    assert phi_stack(zp, zs).shape == (0, 4, 84, 84)
+    assert dqn_phi(zs).shape == (0, 4, 84, 84)
+    assert rgb_phi(torch.zeros((0, 480, 640, 3), dtype=torch.uint8, device=gpu)).shape == (0, 3, 84, 84)
+    torch.cuda.synchronize()
+
+
+def test_rgb_phi_rejects_unsupported_widths(gpu):
+    """W must be a multiple of 16 (16-byte row loads) and <= 2048 (LDS);
+    a bad shape fails loudly instead of reading out of bounds."""
+    from asyncrl_amd import ArlError, rgb_phi
+    with pytest.raises(ArlError):
+        rgb_phi(torch.zeros((2, 100, 150, 3), dtype=torch.uint8, device=gpu))
+    with pytest.raises(ArlError):
+        rgb_phi(torch.zeros((1, 8, 4096, 3), dtype=torch.uint8, device=gpu))
+
+
 def test_nature_head_windows_match_oracle(gpu):
     """Row a8: A3CFF with NatureDQNHead (dqn_head.py:6-28), two windows with
     terminals: forward, sampling, returns, every gradient tensor and the
@@ -362,13 +410,13 @@ def test_nature_head_pi_and_v_matches_oracle(gpu):
         assert ok, err
 
 
-@pytest.mark.parametrize("rgb", [False, True])
-def test_lstm_windows_match_oracle(gpu, rgb):
+@pytest.mark.parametrize("rgb,N,T,A", [(False, 4, 5, 6), (True, 4, 5, 6), (False, 37, 2, 6), (False, 1, 1, 3)])
+def test_lstm_windows_match_oracle(gpu, rgb, N, T, A):
     """A3CLSTM (a3c_ale.py:43-70) and, rgb=True, the ViZDoom A3CLSTM
-    (train_a3c_doom.py:41-63) on 120 x 160 RGB screens."""
+    (train_a3c_doom.py:41-63) on 120 x 160 RGB screens; a ragged env count
+    (37) and the N = 1, t_max = 1 corner."""
     from asyncrl_amd import A3C, A3CLSTM, DoomA3CLSTM, GradientClipping, RMSpropAsync
     rng = np.random.default_rng(31)
-    N, T, A = 4, 5, 6
     P = 2 * T + 1
     if rgb:
         pairs, rewards, dones = make_rgb_pools(rng, P, N, p_done=0.2)
