@@ -56,6 +56,9 @@ SIGNATURES = {
                                 c_void_p]),
     "arl_act": (c_int, [c_void_p, c_int, c_void_p]),
     "arl_act_mode": (c_int, [c_void_p, c_int, c_int, c_void_p]),
+    "arl_observe_envs": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_i64,
+                                 c_int, c_int, c_void_p]),
+    "arl_act_envs": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "arl_run_stage": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "arl_learn": (c_int, [c_void_p, c_double, c_double, c_double, c_int, c_void_p]),
     "arl_optimize": (c_int, [c_void_p, c_double, c_i64, c_i64, c_double, c_double, c_double, c_void_p]),
@@ -81,6 +84,9 @@ ARCH_FF = 0
 ARCH_LSTM = 1
 ARCH_FF_NATURE = 2   # A3CFF with NatureDQNHead (dqn_head.py:6-28)
 ARCH_RGB = 16        # flag for FF / LSTM: the ViZDoom models (train_a3c_doom.py:25-63), RGB screens
+ACT_CONV_ONLY = 4      # arl_act_envs mode bits (env-group staggering)
+ACT_AFTER_CONV = 8
+ENV_GROUP_ALIGN = 32   # arl_observe_envs / arl_act_envs: e0 % ENV_GROUP_ALIGN == 0
 RESIZE_SCALAR = 0
 RESIZE_SIMD = 1
 RESIZE_CROP = 2      # flag, combine with SCALAR / SIMD: ale.py crop_or_scale='crop'

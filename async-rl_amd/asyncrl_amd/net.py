@@ -14,7 +14,8 @@ import ctypes
 import numpy as np
 import torch
 
-from ._lib import ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, RESIZE_SCALAR, check, lib, ptr, stream_handle
+from ._lib import (ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, ENV_GROUP_ALIGN, RESIZE_SCALAR, check, lib, ptr,
+                   stream_handle)
 
 
 def param_shapes(arch: int, n_actions: int):
@@ -125,9 +126,17 @@ class DeviceNet:
         check(lib.arl_net_reset(self._h, stream_handle(stream)), "arl_net_reset")
 
     def observe(self, t: int, pair_pool: torch.Tensor, reward_pool=None, done_pool=None, pool_len: int = 1,
-                force_reset: bool = False, resize_mode: int = RESIZE_SCALAR, stream=None):
+                force_reset: bool = False, resize_mode: int = RESIZE_SCALAR, stream=None, envs=None):
         """pair_pool: (pool_len, n, 2, 210, 160, 3) uint8 frame pairs; for an
-        RGB net (arch | ARCH_RGB) the screens (pool_len, n, H, W, 3) instead."""
+        RGB net (arch | ARCH_RGB) the screens (pool_len, n, H, W, 3) instead.
+        envs=(e0, ne): only envs [e0, e0 + ne) (arl_observe_envs)."""
+        if envs is not None:
+            e0, ne = envs
+            H, W = (pair_pool.shape[-3], pair_pool.shape[-2]) if self.rgb else (0, 0)
+            check(lib.arl_observe_envs(self._h, t, e0, ne, ptr(pair_pool), H, W, ptr(reward_pool), ptr(done_pool),
+                                       pool_len, int(force_reset), resize_mode, stream_handle(stream)),
+                  "arl_observe_envs")
+            return
         if self.rgb:
             H, W = pair_pool.shape[-3], pair_pool.shape[-2]
             check(lib.arl_observe_rgb(self._h, t, ptr(pair_pool), H, W, ptr(reward_pool), ptr(done_pool), pool_len,
@@ -136,9 +145,32 @@ class DeviceNet:
         check(lib.arl_observe(self._h, t, ptr(pair_pool), ptr(reward_pool), ptr(done_pool), pool_len,
                               int(force_reset), resize_mode, stream_handle(stream)), "arl_observe")
 
-    def act(self, t: int, mode: int = 1, stream=None):
-        """mode: 0 forward only, 1 sampled action, 2 greedy (first argmax)."""
+    def act(self, t: int, mode: int = 1, stream=None, envs=None):
+        """mode: 0 forward only, 1 sampled action, 2 greedy (first argmax);
+        envs=(e0, ne): only envs [e0, e0 + ne) (arl_act_envs)."""
+        if envs is not None:
+            check(lib.arl_act_envs(self._h, t, envs[0], envs[1], mode, stream_handle(stream)), "arl_act_envs")
+            return
         check(lib.arl_act_mode(self._h, t, mode, stream_handle(stream)), "arl_act_mode")
+
+    def default_env_groups(self) -> int:
+        """Forward chains per window that measured fastest on one MI355X
+        (scripts/groups_ab.sh): 2 from 512 envs up, else 1."""
+        return 2 if self.n_envs >= 512 else 1
+
+    def env_groups(self, groups: int):
+        """Split the envs into <= `groups` contiguous ranges (e0, ne) with e0 a
+        multiple of ENV_GROUP_ALIGN; [(0, n_envs)] when they do not split."""
+        if groups <= 1 or self.arch == ARCH_FF_NATURE:
+            return [(0, self.n_envs)]
+        per = -(-self.n_envs // groups)
+        per = -(-per // ENV_GROUP_ALIGN) * ENV_GROUP_ALIGN
+        out, e0 = [], 0
+        while e0 < self.n_envs:
+            ne = min(per, self.n_envs - e0)
+            out.append((e0, ne))
+            e0 += ne
+        return out
 
     STAGES = {"conv_fwd": 1, "fc_fwd": 2, "policy": 3, "fc_bwd": 4, "conv_bwd": 5}
 

@@ -158,7 +158,7 @@ int arl_net_reset(arl_net* h, void* s) {
 
 static int observe_common(arl_net* h, int t, const uint8_t* pool, const float* reward_pool,
                           const uint8_t* done_pool, int64_t pool_len, int force_reset, int mode, int H, int W,
-                          void* s) {
+                          void* s, int e0 = 0, int ne = -1) {
   arl::Net& n = h->net;
   if (t < 0 || t > n.T) return fail(ARL_EINVAL, "observe: t out of [0, t_max]");
   if (!pool || pool_len < 1) return fail(ARL_EINVAL, "observe: need the frame pool and pool_len >= 1");
@@ -182,6 +182,8 @@ static int observe_common(arl_net* h, int t, const uint8_t* pool, const float* r
   a.force_reset = force_reset ? 1 : 0;
   a.H = H;
   a.W = W;
+  a.e0 = e0;
+  a.ne = ne;
   return hip_status(n.rgb ? arl::launch_rgb_ring(a, S(s)) : arl::launch_phi_ring(a, S(s)), "observe");
 }
 
@@ -213,6 +215,39 @@ int arl_act_mode(arl_net* h, int t, int mode, void* s) {
   if (t < 0 || t > h->net.T) return fail(ARL_EINVAL, "act: t out of [0, t_max]");
   if (mode < 0 || mode > 2) return fail(ARL_EINVAL, "act: mode must be 0 (none), 1 (sample) or 2 (greedy)");
   return hip_status(arl::net_act(h->net, t, mode, S(s)), "act");
+}
+
+static int check_env_range(const arl::Net& n, int e0, int ne) {
+  if (ne < 1 || e0 < 0 || e0 > n.N - ne) return fail(ARL_EINVAL, "env range [e0, e0 + ne) outside [0, n_envs)");
+  if (e0 % ARL_ENV_GROUP_ALIGN) return fail(ARL_EINVAL, "env range: e0 must be a multiple of ARL_ENV_GROUP_ALIGN");
+  if (n.arch == arl::ARCH_FF_NATURE && (e0 != 0 || ne != n.N))
+    return fail(ARL_EINVAL, "env range: the Nature head runs all envs in one launch");
+  return 0;
+}
+
+int arl_observe_envs(arl_net* h, int t, int e0, int ne, const uint8_t* pool, int H, int W, const float* reward_pool,
+                     const uint8_t* done_pool, int64_t pool_len, int force_reset, int mode, void* s) {
+  NEED_BOUND(h);
+  if (int rc = check_env_range(h->net, e0, ne)) return rc;
+  if (h->net.rgb) {
+    if (mode < 0 || mode > ARL_RESIZE_SIMD) return fail(ARL_EINVAL, "observe_rgb: resize_mode must be 0 or 1");
+    if (int rc = check_rgb_dims(H, W)) return rc;
+  } else {
+    if (mode < 0 || mode > (ARL_RESIZE_SIMD | ARL_RESIZE_CROP)) return fail(ARL_EINVAL, "bad resize_mode");
+    H = W = 0;
+  }
+  return observe_common(h, t, pool, reward_pool, done_pool, pool_len, force_reset, mode, H, W, s, e0, ne);
+}
+
+int arl_act_envs(arl_net* h, int t, int e0, int ne, int mode, void* s) {
+  NEED_BOUND(h);
+  if (t < 0 || t > h->net.T) return fail(ARL_EINVAL, "act: t out of [0, t_max]");
+  const int part = mode & ~3;
+  if (mode < 0 || (mode & 3) > 2 || (part != 0 && part != ARL_ACT_CONV_ONLY && part != ARL_ACT_AFTER_CONV))
+    return fail(ARL_EINVAL, "act: mode must be 0 / 1 / 2, optionally | ARL_ACT_CONV_ONLY or ARL_ACT_AFTER_CONV");
+  if (int rc = check_env_range(h->net, e0, ne)) return rc;
+  if (part != 0 && h->net.arch == arl::ARCH_FF_NATURE) return fail(ARL_EINVAL, "act: Nature head has no conv split");
+  return hip_status(arl::net_act(h->net, t, mode, S(s), e0, ne), "act");
 }
 
 int arl_run_stage(arl_net* h, int stage, int t, void* s) {
@@ -259,7 +294,7 @@ int arl_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, doubl
   if (!aligned(p, 16) || !aligned(ms, 16) || !aligned(g, 16)) return fail(ARL_EINVAL, "rmsprop: 16-byte alignment");
   if (clip > 0 && !parts) return fail(ARL_EINVAL, "rmsprop: clip needs norm_partials scratch");
   hipError_t e = hipSuccess;
-  const int blocks = 1024;
+  const int blocks = 256;
   if (clip > 0) e = arl::launch_grad_sqnorm(g, n, parts, blocks, S(s));
   if (e == hipSuccess)
     e = arl::launch_rmsprop(p, ms, g, n, lr, alpha, eps, clip > 0 ? parts : nullptr, blocks, (float)clip, nullptr, 0,

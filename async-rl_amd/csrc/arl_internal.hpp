@@ -47,6 +47,7 @@ struct RingArgs {
   const int64_t* ctl;
   int n, R, t, mode, force_reset;
   int H = 0, W = 0;           // RGB nets: pair_pool is an image pool (pool_len, n, H, W, 3)
+  int e0 = 0, ne = -1;        // env range of this launch: e0 + blockIdx.y, ne envs (-1: all n)
 };
 
 // RGB (Doom) observations, train_a3c_doom.py:21-23 / doom_env.py:47
@@ -104,7 +105,10 @@ struct Net {
 
 bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_offset, uint64_t seed,
               std::string& err);
-hipError_t net_act(Net& net, int t, int mode, hipStream_t s);   // mode: 0 none, 1 sample, 2 greedy
+// mode: 0 none, 1 sample, 2 greedy, | ACT_CONV_ONLY / ACT_AFTER_CONV (env-group staggering:
+// the step split after its conv launch); envs [e0, e0 + ne) (ne < 0: all)
+constexpr int ACT_CONV_ONLY = 4, ACT_AFTER_CONV = 8;
+hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0 = 0, int ne = -1);
 hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s);
 // advance: also end the window, folded into the update kernel (arl_learn
 // snapshots the step counter, so the update's lr anneal does not race it).
@@ -128,7 +132,7 @@ hipError_t launch_heads_bwd(const float* dl, const float* dv, const float* Wpi, 
 
 hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int t,
                            const float* W1, const float* b1, const float* W2, const float* b2, float* a1, float* a2,
-                           hipStream_t s, bool rgb = false);
+                           hipStream_t s, bool rgb = false, int e0 = 0, int ne = -1);
 hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int S,
                            const float* a1, const float* da2, const float* W2, float* slab, float* gW2, float* gb2,
                            float* gW1, float* gb1, hipStream_t s, bool reduce = true, bool rgb = false);

@@ -67,6 +67,7 @@ struct ConvFwdArgs {
   float* a1;            // (n, 16, 400)
   float* a2;            // (n, 32, 81)
   int rgb;              // frames (R, n, 3, 84, 84): planes [0, R, G, B] of slot ks % R
+  int e0;               // first env of this launch (env = e0 + blockIdx.x)
 };
 
 __global__ void __launch_bounds__(NT)
@@ -75,7 +76,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, col = lane & 15;
-  const int e = blockIdx.x;
+  const int e = a.e0 + blockIdx.x;
   // ---- stage: all global loads first, then bf16 conversion / splitting into LDS
   {
     const int64_t ks = a.ctl[CTL_STEP] + a.t;
@@ -256,10 +257,12 @@ conv_fwd_kernel(ConvFwdArgs a) {
 
 hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int t,
                            const float* W1, const float* b1, const float* W2, const float* b2, float* a1, float* a2,
-                           hipStream_t s, bool rgb) {
+                           hipStream_t s, bool rgb, int e0, int ne) {
   if (n <= 0) return hipSuccess;
-  ConvFwdArgs a{frames, nvalid, ctl, n, R, t, W1, b1, W2, b2, a1, a2, rgb ? 1 : 0};
-  hipLaunchKernelGGL(conv_fwd_kernel, dim3(n), dim3(NT), 0, s, a);
+  if (ne < 0) ne = n;
+  if (ne <= 0) return hipSuccess;
+  ConvFwdArgs a{frames, nvalid, ctl, n, R, t, W1, b1, W2, b2, a1, a2, rgb ? 1 : 0, e0};
+  hipLaunchKernelGGL(conv_fwd_kernel, dim3(ne), dim3(NT), 0, s, a);
   return hipGetLastError();
 }
 

@@ -260,7 +260,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   net.param_floats = off;
   // ---- workspace
   const int64_t n = n_envs, T = t_max, T1 = T + 1, S = T * n, A = n_actions;
-  net.norm_blocks = 1024;
+  net.norm_blocks = 256;
   Plans pl = make_plans(net);
   int64_t slab = 0;
   slab = std::max(slab, (int64_t)FC_SPLIT * n * HID);
@@ -343,37 +343,55 @@ static PolicyArgs slot_policy_args(const Net& net, int t, int mode) {
                           net.at<float>(net.w_logpa) + o);
 }
 
-hipError_t net_act(Net& net, int t, int mode, hipStream_t s) {
-  if (net.arch == ARCH_FF_NATURE) return nature_act(net, t, mode, s);
+// One lockstep step (conv -> fc [-> LSTM] -> policy) for envs [e0, e0 + ne)
+// of window slot t.  Disjoint env ranges touch disjoint rows of every buffer
+// (the FC split-K slab and tickets included: e0 is a multiple of the FC's
+// 32-row tile), so ranges can run concurrently on separate streams.
+hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne) {
+  if (ne < 0) {
+    e0 = 0;
+    ne = net.N;
+  }
+  if (net.arch == ARCH_FF_NATURE) {
+    if (e0 != 0 || ne != net.N || mode > 2) return hipErrorInvalidValue;
+    return nature_act(net, t, mode, s);
+  }
   const int n = net.N, A = net.A;
+  const int part = mode & (ACT_CONV_ONLY | ACT_AFTER_CONV);
+  mode &= 3;
   float* a1 = net.at<float>(net.w_a1) + (int64_t)t * n * A1;
   float* a2 = net.at<float>(net.w_a2) + (int64_t)t * n * A2;
-  float* hfc = net.at<float>(net.w_hfc) + (int64_t)t * n * HID;
+  float* hfc = net.at<float>(net.w_hfc) + ((int64_t)t * n + e0) * HID;
   const float* P = net.p;
-  ARL_TRY(launch_conv_fwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl),
-                          n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W, P + net.o_c2b, a1, a2, s,
-                          net.rgb));
-  ARL_TRY(fc_forward(net, n, a2, hfc, s));
+  if (!(part & ACT_AFTER_CONV))
+    ARL_TRY(launch_conv_fwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
+                            net.at<int64_t>(net.w_ctl), n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W,
+                            P + net.o_c2b, a1, a2, s, net.rgb, e0, ne));
+  if (part & ACT_CONV_ONLY) return hipSuccess;
+  ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb,
+                        net.at<float>(net.w_slab) + (int64_t)FC_SPLIT * e0 * HID,
+                        net.at<int>(net.w_tick) + fc_fwd_tiles(e0), hfc, s));
   const float* hpol = hfc;
   if (net.arch == ARCH_LSTM) {
-    float* gates = net.at<float>(net.w_gates) + (int64_t)t * n * GATES;
-    const float* hprev = net.at<float>(net.w_hbuf) + (int64_t)t * n * HID;
-    const float* cprev = net.at<float>(net.w_cbuf) + (int64_t)t * n * HID;
-    float* hout = net.at<float>(net.w_hbuf) + (int64_t)(t + 1) * n * HID;
-    float* cout = net.at<float>(net.w_cbuf) + (int64_t)(t + 1) * n * HID;
-    const uint8_t* rs = net.at<uint8_t>(net.w_reset) + (int64_t)t * n;
+    const int64_t r0 = (int64_t)t * n + e0;
+    float* gates = net.at<float>(net.w_gates) + r0 * GATES;
+    const float* hprev = net.at<float>(net.w_hbuf) + r0 * HID;
+    const float* cprev = net.at<float>(net.w_cbuf) + r0 * HID;
+    float* hout = net.at<float>(net.w_hbuf) + (r0 + n) * HID;
+    float* cout = net.at<float>(net.w_cbuf) + (r0 + n) * HID;
+    const uint8_t* rs = net.at<uint8_t>(net.w_reset) + r0;
     // gates = [x | h] [Wu ; Wl]^T + b (split-K 2 + a bias reduce measured slower: 28.5 vs 27.7 us)
     ARL_TRY((launch_gemm<32, 64, 32, 2, 2, GK, GK>(LstmGateA{hfc, hprev, rs}, LstmGateB{P + net.o_luW, P + net.o_llW},
-                                                   EpiBias{gates, P + net.o_lub, GATES}, n, GATES, 2 * HID, 1, s)));
-    const int64_t cnt = (int64_t)n * HID;
+                                                   EpiBias{gates, P + net.o_lub, GATES}, ne, GATES, 2 * HID, 1, s)));
+    const int64_t cnt = (int64_t)ne * HID;
     hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, gates, cprev, rs,
                        cout, hout, cnt);
     ARL_TRY(hipGetLastError());
     hpol = hout;
   }
-  const int64_t o = (int64_t)t * n;
-  return launch_policy(hpol, n, P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
-                       net.at<int64_t>(net.w_ctl), t, net.env_offset, t < net.T ? mode : 0,
+  const int64_t o = (int64_t)t * n + e0;
+  return launch_policy(hpol, ne, P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
+                       net.at<int64_t>(net.w_ctl), t, net.env_offset + e0, t < net.T ? mode : 0,
                        net.at<float>(net.w_logits) + o * A, net.at<float>(net.w_probs) + o * A,
                        net.at<float>(net.w_logp) + o * A, net.at<float>(net.w_v) + o, net.at<float>(net.w_ent) + o,
                        net.at<int32_t>(net.w_act) + o, net.at<float>(net.w_logpa) + o, s);

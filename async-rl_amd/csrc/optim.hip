@@ -82,6 +82,19 @@ rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __res
     const int64_t gt = (c.ctl[c.ctl_idx] + c.t_max) * c.n_total;
     c.lr = (float)(((double)(c.total - gt - 1) / (double)c.total) * c.lr0);
   }
+  const int64_t n4 = n >> 2;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  float4* m4 = reinterpret_cast<float4*>(ms);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // the first float4 of p / ms / g is in flight while the block reduces the
+  // norm partials (the grid normally covers the buffer in one pass)
+  float4 pv, mv, gv;
+  if (i0 < n4) {
+    pv = p4[i0];
+    mv = m4[i0];
+    gv = g4[i0];
+  }
   float scale = 1.f;
   bool do_clip = false;
   if (partials != nullptr) {
@@ -95,12 +108,12 @@ rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __res
       scale = (float)rate;
     }
   }
-  const int64_t n4 = n >> 2;
-  float4* p4 = reinterpret_cast<float4*>(p);
-  float4* m4 = reinterpret_cast<float4*>(ms);
-  const float4* g4 = reinterpret_cast<const float4*>(g);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    float4 pv = p4[i], mv = m4[i], gv = g4[i];
+  for (int64_t i = i0; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i != i0) {
+      pv = p4[i];
+      mv = m4[i];
+      gv = g4[i];
+    }
     if (do_clip) {
       gv.x = __fmul_rn(gv.x, scale); gv.y = __fmul_rn(gv.y, scale);
       gv.z = __fmul_rn(gv.z, scale); gv.w = __fmul_rn(gv.w, scale);

@@ -181,7 +181,7 @@ phi_stack_kernel(const uint8_t* __restrict__ pairs, const uint8_t* __restrict__ 
 __global__ void __launch_bounds__(256)
 phi_ring_kernel(RingArgs a) {
   __shared__ PhiShared sh;
-  const int e = blockIdx.y;
+  const int e = a.e0 + blockIdx.y;
   const int64_t k = a.ctl[CTL_STEP] + a.t;
   const int slot = (int)(k % a.R);
   const int64_t pidx = k % a.pool_len;
@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(256)
 rgb_ring_kernel(RingArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t rgb_rows[];
   __shared__ RgbCoef cf;
-  const int e = blockIdx.y;
+  const int e = a.e0 + blockIdx.y;
   const int64_t k = a.ctl[CTL_STEP] + a.t;
   const int slot = (int)(k % a.R);
   const int64_t pidx = k % a.pool_len;
@@ -379,7 +379,7 @@ hipError_t launch_phi_stack(const uint8_t* pairs, const uint8_t* prev_stack, con
 }
 
 hipError_t launch_phi_ring(const RingArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(phi_ring_kernel, dim3(NBANDS, (unsigned)a.n), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(phi_ring_kernel, dim3(NBANDS, (unsigned)(a.ne < 0 ? a.n : a.ne)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -393,7 +393,8 @@ hipError_t launch_rgb_phi(const uint8_t* imgs, int64_t n, int H, int W, float* o
 }
 
 hipError_t launch_rgb_ring(const RingArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(rgb_ring_kernel, dim3(RGB_NBANDS, (unsigned)a.n), dim3(256), rgb_lds(a.W), s, a);
+  hipLaunchKernelGGL(rgb_ring_kernel, dim3(RGB_NBANDS, (unsigned)(a.ne < 0 ? a.n : a.ne)), dim3(256), rgb_lds(a.W), s,
+                     a);
   return hipGetLastError();
 }
 

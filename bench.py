@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--actions", type=int, default=0, help="0: 4 for ff (Breakout), 6 for lstm (Space Invaders)")
     ap.add_argument("--pool", type=int, default=8)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--env-groups", type=int, default=0,
+                    help="forward chains on separate streams per window (A3C.run_window env_groups); "
+                         "0: the library default (2 from 512 envs per GPU up, else 1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="0 disables the CPU baseline leg")
     ap.add_argument("--kernel-reps", type=int, default=50)
     return ap.parse_args()
@@ -241,18 +244,19 @@ def main():
             else:
                 agent.t += T
         else:
-            agent.run_window(pairs, rewards, dones, P, first=False, stream=stream)
+            agent.run_window(pairs, rewards, dones, P, first=False, stream=stream, env_groups=(a.env_groups or None))
 
     with torch.cuda.stream(stream):
-        agent.run_window(pairs, rewards, dones, P, first=True, stream=stream)
+        agent.run_window(pairs, rewards, dones, P, first=True, stream=stream, env_groups=(a.env_groups or None))
         for _ in range(max(0, a.warmup - 1)):
-            agent.run_window(pairs, rewards, dones, P, stream=stream)
+            agent.run_window(pairs, rewards, dones, P, stream=stream, env_groups=(a.env_groups or None))
         if use_graph:
             stream.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=stream):
                 # one window; with >1 rank the all-reduce + optimizer stay eager
-                agent.run_window(pairs, rewards, dones, P, stream=stream, split_update=(world > 1))
+                agent.run_window(pairs, rewards, dones, P, stream=stream, split_update=(world > 1),
+                                 env_groups=(a.env_groups or None))
             graph = g
             agent.t -= T if world == 1 else 0
             for _ in range(2):
@@ -365,7 +369,8 @@ def main():
             "config": {"workload": ("%s: A3C %s " + ("Nature" if nat else "NIPS (RGB)" if doom else "NIPS") + "-DQN head, %d envs x t_max=%d per GPU (phi + conv head + sampling "
                                     "+ n-step returns + backward + clip + RMSProp)") % (a.workload, arch.upper(), N, T),
                        "envs_per_gpu": N, "global_envs": N * world, "t_max": T, "n_actions": A, "arch": arch,
-                       "graph": use_graph, "parallelism": "dp%d" % world,
+                       "graph": use_graph, "env_groups": len(model.net.env_groups(a.env_groups or model.net.default_env_groups())),
+                       "parallelism": "dp%d" % world,
                        "units_per_step": N * T * world},
             "roofline": roof, "kernels": kernels, "cpu_baseline": cpu, "params_finite": finite,
         }

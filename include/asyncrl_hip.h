@@ -128,6 +128,27 @@ int arl_act(arl_net* net, int t, void* stream);
  * evaluation policy of a3c_ale.py:73-89 / demo_a3c_ale.py:15-30). */
 int arl_act_mode(arl_net* net, int t, int mode, void* stream);
 
+/* Env groups: arl_observe / arl_observe_rgb and arl_act_mode restricted to
+ * envs [e0, e0 + ne) of the net (no reference counterpart: the batched
+ * form of running a3c.py:67-167 for a subset of the actors).  Disjoint
+ * ranges touch disjoint workspace rows, so ranges issued on different
+ * streams run concurrently (A3C.run_window(env_groups=G) forks one stream
+ * per group for the T + 1 forward steps and joins before arl_learn).
+ * e0 must be a multiple of ARL_ENV_GROUP_ALIGN; H, W are the screen size of
+ * an ARL_ARCH_RGB net (ignored otherwise).  The Nature head accepts only
+ * the full range. */
+#define ARL_ENV_GROUP_ALIGN 32
+int arl_observe_envs(arl_net* net, int t, int e0, int ne, const uint8_t* pool, int H, int W,
+                     const float* reward_pool, const uint8_t* done_pool, int64_t pool_len, int force_reset,
+                     int resize_mode, void* stream);
+/* mode for arl_act_envs: 0 / 1 / 2 as arl_act_mode, optionally | one of
+ * ARL_ACT_CONV_ONLY (launch only the step's conv layers) or
+ * ARL_ACT_AFTER_CONV (the rest of the step): a stream can then record an
+ * event between the two, which is how run_window staggers the groups. */
+#define ARL_ACT_CONV_ONLY 4
+#define ARL_ACT_AFTER_CONV 8
+int arl_act_envs(arl_net* net, int t, int e0, int ne, int mode, void* stream);
+
 /* Window update, gradient part (a3c.py:82-130): n-step returns with R = 0 at
  * terminals, advantage / entropy / value loss gradient, backward through
  * heads, [LSTM BPTT], FC, conv2, conv1 -> grads (overwritten). */

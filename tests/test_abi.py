@@ -85,3 +85,33 @@ def test_product_path_has_no_oracle_dependency():
         if f.endswith(".py"):
             src = open(os.path.join(pkg, f)).read()
             assert "oracle" not in src.replace("no oracle", ""), f
+
+
+def test_env_group_split():
+    """DeviceNet.env_groups: contiguous ranges, e0 a multiple of
+    ENV_GROUP_ALIGN (the FC tile), covering every env exactly once; the
+    Nature head never splits."""
+    from types import SimpleNamespace
+    from asyncrl_amd._lib import ARCH_FF, ARCH_FF_NATURE, ENV_GROUP_ALIGN
+    from asyncrl_amd.net import DeviceNet
+    for n in (1, 31, 32, 96, 100, 256, 1024):
+        for g in (1, 2, 3, 4):
+            rs = DeviceNet.env_groups(SimpleNamespace(n_envs=n, arch=ARCH_FF), g)
+            assert rs[0][0] == 0 and sum(ne for _, ne in rs) == n and len(rs) <= g
+            assert all(e0 % ENV_GROUP_ALIGN == 0 and ne > 0 for e0, ne in rs)
+            assert all(rs[i][0] + rs[i][1] == rs[i + 1][0] for i in range(len(rs) - 1))
+    assert DeviceNet.env_groups(SimpleNamespace(n_envs=256, arch=ARCH_FF), 2) == [(0, 128), (128, 128)]
+    assert DeviceNet.env_groups(SimpleNamespace(n_envs=256, arch=ARCH_FF_NATURE), 2) == [(0, 256)]
+
+
+def test_env_range_validation_without_device():
+    """arl_observe_envs / arl_act_envs reject an unbound handle before any
+    launch (no GPU needed)."""
+    from asyncrl_amd._lib import lib
+    h = ctypes.c_void_p()
+    assert lib.arl_net_create(ctypes.byref(h), 0, 4, 64, 5, 0, 0) == 0
+    try:
+        assert lib.arl_act_envs(h, 0, 0, 32, 1, None) == 3        # ARL_ESTATE: not bound
+        assert lib.arl_observe_envs(h, 0, 0, 32, None, 0, 0, None, None, 1, 0, 0, None) == 3
+    finally:
+        lib.arl_net_destroy(h)

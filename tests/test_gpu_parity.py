@@ -532,3 +532,52 @@ def test_many_windows_stay_finite(gpu):
     assert torch.isfinite(m.net.params).all()
     acts = m.net.buffer("actions", torch.int32, (T + 1, N))[:T]
     assert int(acts.min()) >= 0 and int(acts.max()) < 4
+
+
+@pytest.mark.parametrize("arch,N,groups", [("ff", 96, 3), ("ff", 256, 2), ("lstm", 80, 2), ("doom_ff", 64, 2)])
+def test_env_groups_identical(gpu, arch, N, groups):
+    """run_window(env_groups=G): G forward chains on G streams (staggered by
+    one kernel), eager and graph-captured, give bit-identical actions,
+    values, gradients, parameters and RMSProp state to one chain."""
+    from asyncrl_amd import A3C, A3CFF, A3CLSTM, DoomA3CFF, GradientClipping, RMSpropAsync
+    rng = np.random.default_rng(71)
+    T, P = 5, 7
+    Model = {"ff": A3CFF, "lstm": A3CLSTM, "doom_ff": DoomA3CFF}[arch]
+    A = 3 if arch == "doom_ff" else 4
+    if arch == "doom_ff":
+        pairs = rng.integers(0, 256, size=(P, N, 120, 160, 3), dtype=np.uint8)
+        rewards = rng.choice([-1.0, 0.0, 1.0], p=[0.05, 0.9, 0.05], size=(P, N)).astype(np.float32)
+        dones = (rng.random((P, N)) < 0.1).astype(np.uint8)
+    else:
+        pairs, rewards, dones = make_pools(rng, P, N, "uniform", p_done=0.1)
+    dp, dr, dd = dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu)
+
+    def mk():
+        m = Model(A, n_envs=N, t_max=T, seed=5, init_seed=6)
+        o = RMSpropAsync(lr=7e-4, eps=0.1, alpha=0.99).setup(m)
+        o.add_hook(GradientClipping(40))
+        o.anneal_total_steps, o.n_total_envs = 10 ** 6, N
+        return A3C(m, o, T, 0.99)
+
+    a, b = mk(), mk()
+    assert len(b.net.env_groups(groups)) == groups
+    outs = []
+    for ag, G in ((a, 1), (b, groups)):
+        ag.run_window(dp, dr, dd, P, first=True, env_groups=G)
+        ag.run_window(dp, dr, dd, P, env_groups=G)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            ag.run_window(dp, dr, dd, P, stream=s, env_groups=G)   # creates the side streams before capture
+        s.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            ag.run_window(dp, dr, dd, P, stream=s, env_groups=G, split_update=True)
+        g.replay()
+        torch.cuda.synchronize()
+        net = ag.net
+        outs.append({"actions": net.buffer("actions", torch.int32, (T + 1, N)).clone(),
+                     "v": net.buffer("v", torch.float32, (T + 1, N)).clone(),
+                     "grads": net.grads.clone(), "params": net.params.clone(), "ms": net.ms.clone()})
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
