@@ -61,6 +61,7 @@ SIGNATURES = {
     "arl_act_envs": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "arl_run_stage": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "arl_learn": (c_int, [c_void_p, c_double, c_double, c_double, c_int, c_void_p]),
+    "arl_learn_part": (c_int, [c_void_p, c_int, c_double, c_double, c_double, c_int, c_void_p]),
     "arl_optimize": (c_int, [c_void_p, c_double, c_i64, c_i64, c_double, c_double, c_double, c_void_p]),
     "arl_advance": (c_int, [c_void_p, c_void_p]),
     "arl_optimize_advance": (c_int, [c_void_p, c_double, c_i64, c_i64, c_double, c_double, c_double, c_void_p]),
@@ -87,6 +88,7 @@ ARCH_RGB = 16        # flag for FF / LSTM: the ViZDoom models (train_a3c_doom.py
 ACT_CONV_ONLY = 4      # arl_act_envs mode bits (env-group staggering)
 ACT_AFTER_CONV = 8
 ENV_GROUP_ALIGN = 32   # arl_observe_envs / arl_act_envs: e0 % ENV_GROUP_ALIGN == 0
+LEARN_RETURNS, LEARN_HEADS_DW, LEARN_TRUNK, LEARN_GATES_REDUCE, LEARN_FC_REDUCE, LEARN_CONV = range(6)
 RESIZE_SCALAR = 0
 RESIZE_SIMD = 1
 RESIZE_CROP = 2      # flag, combine with SCALAR / SIMD: ale.py crop_or_scale='crop'

@@ -10,11 +10,13 @@ compute is in libasyncrl_hip.so.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
 
-from ._lib import (ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, ENV_GROUP_ALIGN, RESIZE_SCALAR, check, lib, ptr,
+from ._lib import (ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, ENV_GROUP_ALIGN, LEARN_CONV, LEARN_FC_REDUCE,
+                   LEARN_GATES_REDUCE, LEARN_HEADS_DW, LEARN_RETURNS, LEARN_TRUNK, RESIZE_SCALAR, check, lib, ptr,
                    stream_handle)
 
 
@@ -49,6 +51,13 @@ def init_like_torch(arch: int, n_actions: int, rng: np.random.Generator):
         stdv = 1.0 / np.sqrt(int(np.prod(w[1:])))
         out[name] = rng.uniform(-stdv, stdv, size=shape).astype(np.float32)
     return out
+
+
+# learner side stream for the weight-gradient reduces (ARL_LEARN_FORK=1).  Off by
+# default: measured slower on every config (C2 0.413 -> 0.449 ms, C3 1.543 ->
+# 1.609, C4 0.641 -> 0.676): each cross-stream edge of the window graph costs
+# more on the critical path than the ~19 us of reduces it hides.
+LEARN_FORK = os.environ.get("ARL_LEARN_FORK", "0") == "1"
 
 
 class DeviceNet:
@@ -178,9 +187,36 @@ class DeviceNet:
         """One window stage alone on the current workspace (timing / profiling)."""
         check(lib.arl_run_stage(self._h, self.STAGES[stage], t, stream_handle(stream)), "arl_run_stage")
 
-    def learn(self, gamma=0.99, beta=1e-2, v_loss_coef=0.5, clip_reward=True, stream=None):
-        check(lib.arl_learn(self._h, gamma, beta, v_loss_coef, int(clip_reward), stream_handle(stream)),
-              "arl_learn")
+    def learn(self, gamma=0.99, beta=1e-2, v_loss_coef=0.5, clip_reward=True, stream=None, fork=None):
+        """Gradient of the window (arl_learn).  fork (default: LEARN_FORK)
+        runs the weight-gradient reduces that nothing downstream reads (heads
+        dW, LSTM gate and FC reduces) on a side stream, concurrently with the
+        heads -> FC -> conv backward chain (arl_learn_part); the streams join
+        before this returns, so the result is identical either way."""
+        fork = LEARN_FORK if fork is None else fork
+        if not fork or self.arch == ARCH_FF_NATURE:
+            check(lib.arl_learn(self._h, gamma, beta, v_loss_coef, int(clip_reward), stream_handle(stream)),
+                  "arl_learn")
+            return
+        main = stream if stream is not None else torch.cuda.current_stream(self.device)
+        side = getattr(self, "_learn_side", None)
+        if side is None:
+            side = self._learn_side = torch.cuda.Stream(device=self.device)
+
+        def part(p, s):
+            check(lib.arl_learn_part(self._h, p, gamma, beta, v_loss_coef, int(clip_reward), s.cuda_stream),
+                  "arl_learn_part")
+
+        part(LEARN_RETURNS, main)
+        side.wait_stream(main)
+        part(LEARN_HEADS_DW, side)
+        part(LEARN_TRUNK, main)
+        side.wait_stream(main)
+        if self.arch & ~ARCH_RGB == ARCH_LSTM:
+            part(LEARN_GATES_REDUCE, side)
+        part(LEARN_FC_REDUCE, side)
+        part(LEARN_CONV, main)
+        main.wait_stream(side)
 
     def optimize(self, lr0=7e-4, total_steps=0, n_total=0, alpha=0.99, eps=0.1, clip=40.0, stream=None,
                  advance=False):

@@ -262,6 +262,14 @@ int arl_learn(arl_net* h, double gamma, double beta, double vcoef, int clip_rewa
   return hip_status(arl::net_learn(h->net, gamma, (float)beta, (float)vcoef, clip_reward, S(s)), "learn");
 }
 
+int arl_learn_part(arl_net* h, int part, double gamma, double beta, double vcoef, int clip_reward, void* s) {
+  NEED_BOUND(h);
+  if (part < 0 || part >= arl::LEARN_PARTS) return fail(ARL_EINVAL, "learn_part: part out of range");
+  if (h->net.arch == arl::ARCH_FF_NATURE) return fail(ARL_ESTATE, "learn_part: the Nature learner is one call");
+  return hip_status(arl::net_learn_part(h->net, part, gamma, (float)beta, (float)vcoef, clip_reward, S(s)),
+                    "learn_part");
+}
+
 int arl_optimize(arl_net* h, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps, double clip,
                  void* s) {
   NEED_BOUND(h);

@@ -109,6 +109,9 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
 // the step split after its conv launch); envs [e0, e0 + ne) (ne < 0: all)
 constexpr int ACT_CONV_ONLY = 4, ACT_AFTER_CONV = 8;
 hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0 = 0, int ne = -1);
+// learner parts (net_learn_part); see net.hip for which may run concurrently
+enum { LEARN_RETURNS = 0, LEARN_HEADS_DW, LEARN_TRUNK, LEARN_GATES_REDUCE, LEARN_FC_REDUCE, LEARN_CONV, LEARN_PARTS };
+hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s);
 hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s);
 // advance: also end the window, folded into the update kernel (arl_learn
 // snapshots the step counter, so the update's lr anneal does not race it).

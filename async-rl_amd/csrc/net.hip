@@ -422,6 +422,17 @@ hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_
 // ---------------------------------------------------------------- backward
 hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s) {
   if (net.arch == ARCH_FF_NATURE) return nature_learn(net, gamma, beta, vcoef, clip_reward, s);
+  for (int part = 0; part < LEARN_PARTS; ++part) ARL_TRY(net_learn_part(net, part, gamma, beta, vcoef, clip_reward, s));
+  return hipSuccess;
+}
+
+// One part of the NIPS learner (LEARN_* in arl_internal.hpp).  Parts run in
+// order on one stream give net_learn; LEARN_HEADS_DW may run on a second
+// stream once LEARN_RETURNS is done, and LEARN_GATES_REDUCE / LEARN_FC_REDUCE
+// once LEARN_TRUNK is done, concurrently with the rest: nothing on the
+// critical path (dh -> FC -> conv backward) reads what they write.
+hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s) {
+  if (net.arch == ARCH_FF_NATURE) return hipErrorInvalidValue;
   const int n = net.N, T = net.T, A = net.A, S = T * n;
   const float* P = net.p;
   float* G = net.g;
@@ -437,14 +448,36 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
   float* dfc = net.at<float>(net.w_dfc);
   // 1. n-step returns + loss gradient wrt logits / v (a3c.py:82-126); also
   //    snapshots the step counter for the optimizer's fused advance
-  ARL_TRY(launch_returns(net.at<float>(net.w_rewards), net.at<uint8_t>(net.w_dones), net.at<float>(net.w_v),
-                         net.at<float>(net.w_probs), net.at<float>(net.w_logp), net.at<int32_t>(net.w_act), T, n, A,
-                         gamma, beta, vcoef, clip_reward, dl, dv, nullptr, s, net.at<int64_t>(net.w_ctl)));
+  if (part == LEARN_RETURNS)
+    return launch_returns(net.at<float>(net.w_rewards), net.at<uint8_t>(net.w_dones), net.at<float>(net.w_v),
+                          net.at<float>(net.w_probs), net.at<float>(net.w_logp), net.at<int32_t>(net.w_act), T, n, A,
+                          gamma, beta, vcoef, clip_reward, dl, dv, nullptr, s, net.at<int64_t>(net.w_ctl));
   // heads: weight grads (ones column = bias) and dh
-  ARL_TRY((launch_gemm<16, 64, 32, 1, 4, GS, GM>(HeadsGA{dl, dv, A}, OnesColB{hheads, HID},
-                                                 EpiSlab{slab_h, A + 1, HID + 1}, A + 1, HID + 1, S, pl.heads_w, s)));
-  ARL_TRY(launch_reduce_grad(slab_h, pl.heads_w, A + 1, HID + 1,
-                             MapHeads{G, net.o_piW, net.o_pib, net.o_vW, net.o_vb, A, HID}, s));
+  if (part == LEARN_HEADS_DW) {
+    ARL_TRY((launch_gemm<16, 64, 32, 1, 4, GS, GM>(HeadsGA{dl, dv, A}, OnesColB{hheads, HID},
+                                                   EpiSlab{slab_h, A + 1, HID + 1}, A + 1, HID + 1, S, pl.heads_w,
+                                                   s)));
+    return launch_reduce_grad(slab_h, pl.heads_w, A + 1, HID + 1,
+                              MapHeads{G, net.o_piW, net.o_pib, net.o_vW, net.o_vb, A, HID}, s);
+  }
+  float* slab_l = net.at<float>(net.w_slab_lstm);
+  if (part == LEARN_GATES_REDUCE)
+    return L ? launch_reduce_grad(slab_l, pl.lstm_w, GATES, 2 * HID + 1,
+                                  MapDense{G, net.o_luW, net.o_lub, net.o_llW, HID}, s)
+             : hipSuccess;
+  if (part == LEARN_FC_REDUCE)
+    return launch_reduce_grad(slab_f, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s);
+  const float* a2 = net.at<float>(net.w_a2);
+  const float* a1 = net.at<float>(net.w_a1);
+  float* da2 = net.at<float>(net.w_da2);
+  if (part == LEARN_CONV)
+    // fused conv backward per sample (conv_bwd.hip): conv2 dW/db,
+    // da1 = conv_transpose(da2, W2) * (a1 > 0) kept in LDS, conv1 dW/db
+    // straight from the frame ring
+    return launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
+                           net.at<int64_t>(net.w_ctl), n, net.R, S, a1, da2, P + net.o_c2W, slab, G + net.o_c2W,
+                           G + net.o_c2b, G + net.o_c1W, G + net.o_c1b, s, /*reduce=*/true, net.rgb);
+  if (part != LEARN_TRUNK) return hipErrorInvalidValue;
   ARL_TRY(launch_heads_bwd(dl, dv, P + net.o_piW, P + net.o_vW, A, HID, L ? nullptr : hfc,
                            L ? net.at<float>(net.w_dh) : dfc, S, s));
   // 2. LSTM: truncated BPTT over the window, gate weight gradients, dfc
@@ -472,32 +505,20 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
       }
     }
     // gate weight gradients and dfc = (dG Wu) * (hfc > 0): independent, one launch
-    float* slab_l = net.at<float>(net.w_slab_lstm);
     ARL_TRY((launch_gemm2<64, 64, 32, 2, 2, GM, GS, GK, GM>(
         gemm_job<64, 32>(ColMajor{dG, GATES}, LstmWB{hfc, hbuf, rs}, EpiSlab{slab_l, GATES, 2 * HID + 1}, GATES,
                          2 * HID + 1, S, pl.lstm_w, 64),
         gemm_job<64, 32>(RowMajor{dG, GATES}, RowMajor{P + net.o_luW, HID}, EpiMask{dfc, hfc, HID}, S, HID, GATES, 1,
                          64),
         s)));
-    ARL_TRY(launch_reduce_grad(slab_l, pl.lstm_w, GATES, 2 * HID + 1,
-                               MapDense{G, net.o_luW, net.o_lub, net.o_llW, HID}, s));
   }
   // 3. FC: dW (+ bias via ones column), da2 = (dfc W) * (a2 > 0)
-  const float* a2 = net.at<float>(net.w_a2);
-  const float* a1 = net.at<float>(net.w_a1);
-  float* da2 = net.at<float>(net.w_da2);
   //    as ONE launch: both are latency-bound and independent, so their
   //    workgroups share the chip instead of running back to back
   ARL_TRY((launch_gemm2<64, 64, 32, 2, 2, GM, GM, GK, GM>(
       gemm_job<64, 32>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab_f, HID, A2 + 1}, HID, A2 + 1, S, pl.fc_w, 64),
       gemm_job<64, 32>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2}, EpiMask{da2, a2, A2}, S, A2, HID, 1, 64), s)));
-  ARL_TRY(launch_reduce_grad(slab_f, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s));
-  // 4. fused conv backward per sample (conv_bwd.hip): conv2 dW/db,
-  //    da1 = conv_transpose(da2, W2) * (a1 > 0) kept in LDS, conv1 dW/db
-  //    straight from the frame ring
-  return launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl), n,
-                         net.R, S, a1, da2, P + net.o_c2W, slab, G + net.o_c2W, G + net.o_c2b, G + net.o_c1W,
-                         G + net.o_c1b, s, /*reduce=*/true, net.rgb);
+  return hipSuccess;
 }
 
 // One stage of a window on the current workspace contents (arl_run_stage):

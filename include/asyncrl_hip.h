@@ -154,6 +154,21 @@ int arl_act_envs(arl_net* net, int t, int e0, int ne, int mode, void* stream);
  * heads, [LSTM BPTT], FC, conv2, conv1 -> grads (overwritten). */
 int arl_learn(arl_net* net, double gamma, double beta, double v_loss_coef, int clip_reward, void* stream);
 
+/* arl_learn in parts (NIPS FF / LSTM heads; not the Nature head): calling
+ * parts 0..5 in order on one stream equals arl_learn.  Part 1 (heads weight
+ * gradients) may run on a second stream once part 0 (returns + loss
+ * gradient) is done, and parts 3 (LSTM gate reduce) and 4 (FC reduce) once
+ * part 2 (heads dh, LSTM BPTT, FC dW + da2 GEMMs) is done, concurrently with
+ * part 5 (conv backward); the gradient is complete when both streams are. */
+#define ARL_LEARN_RETURNS 0
+#define ARL_LEARN_HEADS_DW 1
+#define ARL_LEARN_TRUNK 2
+#define ARL_LEARN_GATES_REDUCE 3
+#define ARL_LEARN_FC_REDUCE 4
+#define ARL_LEARN_CONV 5
+int arl_learn_part(arl_net* net, int part, double gamma, double beta, double v_loss_coef, int clip_reward,
+                   void* stream);
+
 /* GradientClipping(clip) + RMSpropAsync update (a3c_ale.py:224-226,
  * rmsprop_async.py:23-29) of the bound params / ms from the bound grads.
  * total_steps > 0 anneals lr on device (a3c_ale.py:111-112) with global_t =

@@ -581,3 +581,29 @@ def test_env_groups_identical(gpu, arch, N, groups):
                      "grads": net.grads.clone(), "params": net.params.clone(), "ms": net.ms.clone()})
     for k in outs[0]:
         assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+@pytest.mark.parametrize("arch", ["ff", "lstm"])
+def test_learn_fork_identical(gpu, arch):
+    """DeviceNet.learn(fork=True) (weight-gradient reduces on a side stream,
+    arl_learn_part) gives the same gradient bits as arl_learn in one call."""
+    from asyncrl_amd import A3C, A3CFF, A3CLSTM, RMSpropAsync
+    rng = np.random.default_rng(81)
+    N, T, P = 48, 5, 7
+    pairs, rewards, dones = make_pools(rng, P, N, "uniform", p_done=0.1)
+    dp, dr, dd = dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu)
+    Model = A3CFF if arch == "ff" else A3CLSTM
+    m = Model(4, n_envs=N, t_max=T, seed=5, init_seed=6)
+    ag = A3C(m, RMSpropAsync(lr=7e-4, eps=0.1, alpha=0.99).setup(m), T, 0.99)
+    ag.run_window(dp, dr, dd, P, first=True, split_update=True)
+    net = ag.net
+    got = []
+    for fork in (False, True, False):
+        net.grads.fill_(1234.5)            # padding between tensors keeps it
+        net.learn(fork=fork)
+        torch.cuda.synchronize()
+        got.append(net.grads.clone())
+    for name in net.layout:               # every tensor was written
+        g = net.view(got[0], name)
+        assert torch.isfinite(g).all() and not (g == 1234.5).any(), name
+    assert torch.equal(got[0], got[1]) and torch.equal(got[0], got[2])
