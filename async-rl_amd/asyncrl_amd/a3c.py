@@ -28,7 +28,8 @@ import os
 import numpy as np
 import torch
 
-from ._lib import ACT_AFTER_CONV, ACT_CONV_ONLY, ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, RESIZE_SCALAR
+from ._lib import (ACT_AFTER_CONV, ACT_CONV_ONLY, ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, LEARN_CONV,
+                   RESIZE_SCALAR)
 from .distributed import allreduce_grads, world_info
 from .net import DeviceNet, init_like_torch
 from . import serializers
@@ -36,6 +37,8 @@ from .policy_output import SoftmaxPolicyOutput
 
 # env groups: chain g starts after chain g-1's first kernel (ARL_GROUP_STAGGER=0: together)
 STAGGER = os.environ.get("ARL_GROUP_STAGGER", "1") != "0"
+# > 1 rank: split the gradient all-reduce around the conv backward (ARL_OVERLAP_ALLREDUCE=0: one call)
+OVERLAP_ALLREDUCE = os.environ.get("ARL_OVERLAP_ALLREDUCE", "1") != "0"
 
 
 class A3CModel:
@@ -143,11 +146,46 @@ class A3C:
         """a3c.py:63-65 -- a no-op: actors read the device parameters."""
 
     # ------------------------------------------------------------ window pieces
-    def _update(self, stream=None):
+    def _overlap_allreduce(self) -> bool:
+        """With > 1 rank (and a learner that runs in parts, i.e. not the
+        Nature head) the gradient all-reduce is split in two: the FC / LSTM /
+        heads section (all but ~12k of the parameters) starts as soon as the
+        FC reduce is done and runs on the collective stream while the conv
+        backward computes; only the conv section waits for it."""
+        return self.world > 1 and OVERLAP_ALLREDUCE and self.net.arch != ARCH_FF_NATURE
+
+    def _learn(self, stream=None):
+        """The gradient part of the window; with the overlapped all-reduce it
+        stops before the conv backward (finish_window runs that part)."""
         net = self.net
-        net.learn(self.gamma, self.beta, self.v_loss_coef, self.clip_reward, stream=stream)
-        allreduce_grads(net.grads, self.pg)
-        self.optimizer.update(stream=stream, advance_window=True)
+        if self._overlap_allreduce():
+            net.learn_parts(range(LEARN_CONV), self.gamma, self.beta, self.v_loss_coef, self.clip_reward,
+                            stream=stream)
+        else:
+            net.learn(self.gamma, self.beta, self.v_loss_coef, self.clip_reward, stream=stream)
+
+    def _reduce_and_step(self, stream=None, conv=None):
+        net = self.net
+        main = stream if stream is not None else torch.cuda.current_stream(net.device)
+        with torch.cuda.stream(main):          # the collectives order against `main`
+            if self._overlap_allreduce():
+                o = net.layout["0/2/W"][0]      # conv1 / conv2 live in [0, o)
+                work = allreduce_grads(net.grads[o:], self.pg, async_op=True)
+                if conv is not None:
+                    conv()                      # e.g. a captured graph of the conv part
+                else:
+                    net.learn_parts([LEARN_CONV], self.gamma, self.beta, self.v_loss_coef, self.clip_reward,
+                                    stream=main)
+                if work is not None:
+                    work.wait()
+                allreduce_grads(net.grads[:o], self.pg)
+            else:
+                allreduce_grads(net.grads, self.pg)
+            self.optimizer.update(stream=main, advance_window=True)
+
+    def _update(self, stream=None):
+        self._learn(stream)
+        self._reduce_and_step(stream)
 
     def act(self, pairs: torch.Tensor, reward=None, is_state_terminal=None) -> torch.Tensor:
         """a3c.py:67-167, batched.  pairs: (n, 2, 210, 160, 3) uint8 device
@@ -211,7 +249,7 @@ class A3C:
             for s in side:
                 main.wait_stream(s)
             stream = main
-        net.learn(self.gamma, self.beta, self.v_loss_coef, self.clip_reward, stream=stream)
+        self._learn(stream)
         if split_update:
             return
         self.finish_window(stream=stream)
@@ -246,9 +284,12 @@ class A3C:
             net.act(t, stream=stream, envs=envs)
         return ev
 
-    def finish_window(self, stream=None):
-        allreduce_grads(self.net.grads, self.pg)
-        self.optimizer.update(stream=stream, advance_window=True)
+    def finish_window(self, stream=None, conv=None):
+        """The rest of a window after run_window(split_update=True): [the conv
+        backward when the all-reduce is overlapped -- `conv`, if given, runs
+        it, e.g. conv_graph.replay], the gradient all-reduce, clip + RMSProp
+        and the window advance."""
+        self._reduce_and_step(stream, conv)
         self.t += self.t_max
 
     # ------------------------------------------------------------ checkpoints

@@ -3,9 +3,10 @@
 Replaces async.py:68-90 (fork P Hogwild processes sharing RawArray params)
 with one process per GPU: rank r owns envs [r*n, (r+1)*n) -- frame ring,
 LSTM state, rollout buffers and the Philox stream keyed by the global env id
--- and the ranks exchange exactly one message per window, the SUM all-reduce
-of the flat fp32 gradient (RCCL over xGMI with backend "nccl"; gloo works for
-CPU tests).  Every rank then applies the same clip + RMSProp to replicated
+-- and the ranks exchange one gradient per window, the SUM all-reduce of the
+flat fp32 gradient (RCCL over xGMI with backend "nccl"; gloo works for CPU
+tests), issued in two sections so the large FC / LSTM / heads part overlaps
+the conv backward (A3C._reduce_and_step).  Every rank then applies the same clip + RMSProp to replicated
 parameters, so replicas stay bitwise identical (checked by replica_checksum).
 """
 from __future__ import annotations
@@ -28,12 +29,15 @@ def shard_envs(global_envs: int, world: int, rank: int):
     return n, rank * n
 
 
-def allreduce_grads(grads: torch.Tensor, group=None) -> None:
-    """Sum the flat gradient over ranks in place (one collective per window:
-    2.71 MB FF / 4.81 MB LSTM -- latency-bound, a single ring all-reduce)."""
+def allreduce_grads(grads: torch.Tensor, group=None, async_op: bool = False):
+    """Sum (a contiguous section of) the flat gradient over ranks in place
+    (2.71 MB FF / 4.81 MB LSTM per window, latency-bound ring all-reduces).
+    async_op: return the work handle (None with one rank); its wait() makes
+    the current stream wait for the collective."""
     world, _ = world_info(group)
     if world > 1:
-        dist.all_reduce(grads, op=dist.ReduceOp.SUM, group=group)
+        return dist.all_reduce(grads, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+    return None
 
 
 def replica_checksum(t: torch.Tensor) -> int:

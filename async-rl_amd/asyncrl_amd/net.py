@@ -218,6 +218,12 @@ class DeviceNet:
         part(LEARN_CONV, main)
         main.wait_stream(side)
 
+    def learn_parts(self, parts, gamma=0.99, beta=1e-2, v_loss_coef=0.5, clip_reward=True, stream=None):
+        """arl_learn_part for each part in order on one stream (NIPS heads)."""
+        h = stream_handle(stream)
+        for p in parts:
+            check(lib.arl_learn_part(self._h, p, gamma, beta, v_loss_coef, int(clip_reward), h), "arl_learn_part")
+
     def optimize(self, lr0=7e-4, total_steps=0, n_total=0, alpha=0.99, eps=0.1, clip=40.0, stream=None,
                  advance=False):
         """Clip + RMSProp; advance=True also ends the window (arl_optimize_advance)."""

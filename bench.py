@@ -30,6 +30,7 @@ sys.path.insert(0, os.environ.get("ASYNCRL_PKG_ROOT") or os.path.join(ROOT, "asy
 
 from asyncrl_amd import A3C, A3CFF, A3CFFNature, A3CLSTM, DoomA3CFF, DoomA3CLSTM, GradientClipping, RMSpropAsync  # noqa: E402
 from asyncrl_amd import _lib  # noqa: E402
+from asyncrl_amd._lib import LEARN_CONV  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 F32_MFMA_PEAK_TFS = 157.3      # dense fp32 matrix peak (spec)
@@ -83,9 +84,17 @@ def init_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N > 1 path on a 1-GPU box: ARL_BENCH_DIST_BACKEND=gloo
+    # ARL_BENCH_SHARE_GPU=1 puts every rank on cuda:0 (RCCL needs one GPU per rank)
+    backend = os.environ.get("ARL_BENCH_DIST_BACKEND", "nccl")
+    if os.environ.get("ARL_BENCH_SHARE_GPU") == "1":
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
 
 
@@ -232,7 +241,7 @@ def main():
     P = a.pool
 
     use_graph = not a.no_graph
-    graph = None
+    graph = conv_graph = None
     stream = torch.cuda.Stream(device=dev)
     stream.wait_stream(torch.cuda.current_stream())
 
@@ -240,7 +249,7 @@ def main():
         if graph is not None:
             graph.replay()
             if world > 1:
-                agent.finish_window(stream=stream)
+                agent.finish_window(stream=stream, conv=conv_graph.replay if conv_graph is not None else None)
             else:
                 agent.t += T
         else:
@@ -254,9 +263,17 @@ def main():
             stream.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=stream):
-                # one window; with >1 rank the all-reduce + optimizer stay eager
+                # one window; with >1 rank the all-reduce + optimizer stay eager, and with the
+                # overlapped all-reduce the conv backward is a second graph replayed while the
+                # FC / heads section of the gradient is on the wire (A3C._reduce_and_step)
                 agent.run_window(pairs, rewards, dones, P, stream=stream, split_update=(world > 1),
                                  env_groups=(a.env_groups or None))
+            if world > 1 and agent._overlap_allreduce():
+                cg = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(cg, stream=stream):
+                    model.net.learn_parts([LEARN_CONV], agent.gamma, agent.beta, agent.v_loss_coef,
+                                          agent.clip_reward, stream=stream)
+                conv_graph = cg
             graph = g
             agent.t -= T if world == 1 else 0
             for _ in range(2):

@@ -83,3 +83,40 @@ def test_shard_envs():
     assert shard_envs(4096, 8, 3) == (512, 1536)
     with pytest.raises(ValueError):
         shard_envs(10, 4, 0)
+
+
+def _sections_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "async-rl_amd"))
+    from asyncrl_amd.distributed import allreduce_grads
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.from_numpy(np.random.default_rng(10 + rank).standard_normal(10_000).astype(np.float32))
+        whole = g.clone()
+        allreduce_grads(whole)
+        o = 1_234                                    # conv section [0, o), the rest overlapped
+        work = allreduce_grads(g[o:], async_op=True)
+        assert work is not None
+        work.wait()
+        assert allreduce_grads(g[:o]) is None        # synchronous form returns nothing
+        q.put((rank, bool(torch.equal(g, whole))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sectioned_allreduce_equals_whole():
+    """A3C._reduce_and_step's split all-reduce (async FC / heads section,
+    then the conv section) sums exactly like one all-reduce of the flat
+    gradient (gloo, world_size 2)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_sections_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    assert all(ok for _, ok in res), res
