@@ -6,10 +6,31 @@ half their bytes on gfx950 -> x2; WRITE_SIZE (KiB) is exact for 16-B stores.
     python scripts/traffic.py gpurun_out/pmc [--envs 256 --t-max 5 --arch ff] > profiles/traffic_r01.json
 """
 import argparse
+import re
 import csv
 import json
 import os
 from collections import defaultdict
+
+
+def kernel_key(name: str) -> str:
+    """'void arl::gemm_kernel<32, 64, ..., arl::EpiSlab, 2, 2>(...)' ->
+    'gemm_kernel<32, 64, ..., EpiSlab, 2, 2>' (template instances stay apart)."""
+    name = name.strip().replace("(anonymous namespace)::", "")
+    if name.startswith("void "):
+        name = name[5:]
+    cut = [i for i in (name.find("<"), name.find("(")) if i >= 0]
+    head = name[:min(cut)] if cut else name
+    base = head.split("::")[-1]
+    if cut and name[min(cut)] == "<":
+        depth, end = 0, len(name)
+        for i in range(min(cut), len(name)):
+            depth += {"<": 1, ">": -1}.get(name[i], 0)
+            if depth == 0:
+                end = i + 1
+                break
+        base += re.sub(r"\b\w+::", "", name[min(cut):end])
+    return base
 
 
 def per_kernel(fn, counter):
@@ -18,7 +39,7 @@ def per_kernel(fn, counter):
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"]
-        short = name.split("(")[0].split("::")[-1].split("<")[0].strip()
+        short = kernel_key(name)
         agg[short].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
