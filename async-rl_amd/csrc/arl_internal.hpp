@@ -167,6 +167,10 @@ int fc_fwd_tiles(int n);      // tickets needed for n envs
 hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b, float* slab, int* tickets,
                          float* hfc, hipStream_t s);
 hipError_t launch_policy_args(const float* h, int64_t n, const PolicyArgs& pa, hipStream_t s, int hid);
+// FC split-K reduce (partials of launch_fc_fwd with tickets == nullptr) + bias
+// + relu -> hfc, then the policy / value heads on the same 16 rows
+hipError_t launch_policy_fc(const float* slab, int n, const float* fc_bias, float* hfc, const PolicyArgs& pa,
+                            hipStream_t s);
 
 // end-of-window advance folded into the update (NIPS learner): the lr reads
 // the learner's snapshot CTL_STEP_SNAP, so no workgroup reads CTL_STEP and one

@@ -15,6 +15,9 @@
 //     ticket) sums the 8 partials in split order 0..7 -- deterministic and
 //     independent of arrival order -- adds the bias, applies relu and writes
 //     hfc, then re-arms the ticket.  No second launch.
+//   * tickets == nullptr (FF act steps): partials only; policy_fc_kernel
+//     (policy.hip) sums them in the same order and runs the heads, so the
+//     ticket round trip and the last-arriver tail leave the step's chain.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -107,7 +110,7 @@ fc_fwd_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, 
                          __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if (ARL_ABLATE & 256) return;
+  if ((ARL_ABLATE & 256) || tickets == nullptr) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0)

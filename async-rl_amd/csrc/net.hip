@@ -368,8 +368,20 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne) {
                             net.at<int64_t>(net.w_ctl), n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W,
                             P + net.o_c2b, a1, a2, s, net.rgb, e0, ne));
   if (part & ACT_CONV_ONLY) return hipSuccess;
-  ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb,
-                        net.at<float>(net.w_slab) + (int64_t)FC_SPLIT * e0 * HID,
+  const int64_t o = (int64_t)t * n + e0;
+  float* fc_slab = net.at<float>(net.w_slab) + (int64_t)FC_SPLIT * e0 * HID;
+  if (net.arch != ARCH_LSTM) {   // FF: split-K partials, reduce + relu + heads in one policy_fc launch
+    ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab, nullptr, nullptr, s));
+    return launch_policy_fc(fc_slab, ne, P + net.o_fcb, hfc,
+                            make_policy_args(P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
+                                             net.at<int64_t>(net.w_ctl), t, net.env_offset + e0, t < net.T ? mode : 0,
+                                             net.at<float>(net.w_logits) + o * A, net.at<float>(net.w_probs) + o * A,
+                                             net.at<float>(net.w_logp) + o * A, net.at<float>(net.w_v) + o,
+                                             net.at<float>(net.w_ent) + o, net.at<int32_t>(net.w_act) + o,
+                                             net.at<float>(net.w_logpa) + o),
+                            s);
+  }
+  ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab,
                         net.at<int>(net.w_tick) + fc_fwd_tiles(e0), hfc, s));
   const float* hpol = hfc;
   if (net.arch == ARCH_LSTM) {
@@ -389,7 +401,6 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne) {
     ARL_TRY(hipGetLastError());
     hpol = hout;
   }
-  const int64_t o = (int64_t)t * n + e0;
   return launch_policy(hpol, ne, P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
                        net.at<int64_t>(net.w_ctl), t, net.env_offset + e0, t < net.T ? mode : 0,
                        net.at<float>(net.w_logits) + o * A, net.at<float>(net.w_probs) + o * A,
@@ -537,10 +548,14 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
                              net.at<int64_t>(net.w_ctl), n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W,
                              P + net.o_c2b, net.at<float>(net.w_a1) + (int64_t)t * n * A1, a2 + (int64_t)t * n * A2,
                              s, net.rgb);
-    case STAGE_FC_FWD:
+    case STAGE_FC_FWD:   // as in net_act: FF runs the partials-only FC, its reduce is in the policy stage
+      if (net.arch != ARCH_LSTM)
+        return launch_fc_fwd(a2 + (int64_t)t * n * A2, n, P + net.o_fcW, P + net.o_fcb, slab, nullptr, nullptr, s);
       return fc_forward(net, n, a2 + (int64_t)t * n * A2, hfc + (int64_t)t * n * HID, s);
     case STAGE_POLICY: {
       const int64_t o = (int64_t)t * n;
+      if (net.arch != ARCH_LSTM)
+        return launch_policy_fc(slab, n, P + net.o_fcb, hfc + o * HID, slot_policy_args(net, t, 0), s);
       const float* h = net.arch == ARCH_LSTM ? net.at<float>(net.w_hbuf) + (o + n) * HID : hfc + o * HID;
       const int A = net.A;
       return launch_policy(h, n, P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,

@@ -48,6 +48,56 @@ hipError_t launch_policy_args(const float* h, int64_t n, const PolicyArgs& pa, h
   return hipGetLastError();
 }
 
+// FF act step: the FC forward's split-K reduce moved here from fc_fwd_kernel's
+// last arriver (fc.hip).  The 8 partial slabs of this group's 16 rows are
+// summed in split order 0..7 from 0.f, then + bias, relu -- the same f32 op
+// sequence as the ticket path, so hfc is bit-identical -- written to hfc (the
+// backward reads it) and to LDS, where the heads read it.
+__global__ void __launch_bounds__(256)
+policy_fc_kernel(const float* __restrict__ slab, int n, const float* __restrict__ fc_bias, float* __restrict__ hfc,
+                 PolicyArgs pa) {
+  __shared__ float part[4][16][MAXA + 2];
+  __shared__ float zs[16][MAXA + 2];
+  __shared__ __attribute__((aligned(16))) float hl[16 * HID];
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * 16;
+  constexpr int V4 = 16 * HID / 4 / 256;   // float4 per thread (4)
+  f32x4v p[V4][FC_SPLIT];
+#pragma unroll
+  for (int z = 0; z < FC_SPLIT; ++z)
+#pragma unroll
+    for (int j = 0; j < V4; ++j) {
+      const int idx = tid + 256 * j, r = idx / (HID / 4), c = 4 * (idx % (HID / 4));
+      const int64_t m = min(row0 + r, (int64_t)n - 1);
+      p[j][z] = *reinterpret_cast<const f32x4v*>(slab + ((int64_t)z * n + m) * HID + c);
+    }
+#pragma unroll
+  for (int j = 0; j < V4; ++j) {
+    const int idx = tid + 256 * j, r = idx / (HID / 4), c = 4 * (idx % (HID / 4));
+    f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int z = 0; z < FC_SPLIT; ++z)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] = __fadd_rn(acc[e], p[j][z][e]);
+    const float4 b = *reinterpret_cast<const float4*>(fc_bias + c);
+    float4 o;
+    o.x = fmaxf(__fadd_rn(acc[0], b.x), 0.f); o.y = fmaxf(__fadd_rn(acc[1], b.y), 0.f);
+    o.z = fmaxf(__fadd_rn(acc[2], b.z), 0.f); o.w = fmaxf(__fadd_rn(acc[3], b.w), 0.f);
+    *reinterpret_cast<float4*>(hl + r * HID + c) = o;
+    if (row0 + r < n) *reinterpret_cast<float4*>(hfc + (row0 + r) * HID + c) = o;
+  }
+  __syncthreads();
+  policy_rows16<HID, false, true>(hl, row0, n, pa, part, zs);
+}
+
+hipError_t launch_policy_fc(const float* slab, int n, const float* fc_bias, float* hfc, const PolicyArgs& pa,
+                            hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(policy_fc_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, s, slab, n, fc_bias, hfc, pa);
+  return hipGetLastError();
+}
+
 hipError_t launch_policy(const float* h, int64_t n, const float* Wpi, const float* bpi, const float* Wv,
                          const float* bv, int A, uint64_t seed, const int64_t* ctl, int64_t step_off,
                          int env_offset, int mode, float* logits, float* probs, float* logp, float* v,

@@ -27,8 +27,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // One group of 16 env rows (row0 .. row0 + 15) of the softmax policy / value
 // heads; part / zs are LDS scratch of the calling workgroup (all 256 threads
 // call).  COH: h was written by other workgroups of the same launch (device
-// scope, sc1) and is read with device-scope loads.
-template <int HW, bool COH>
+// scope, sc1) and is read with device-scope loads.  LOCAL: h holds only the
+// group's 16 rows (row i at h + i * HW, e.g. LDS filled by the caller).
+template <int HW, bool COH, bool LOCAL = false>
 __device__ inline void policy_rows16(const float* __restrict__ h, int64_t row0, int64_t n, const PolicyArgs& pa,
                                      float (*part)[16][MAXA + 2], float (*zs)[MAXA + 2]) {
   // 4 waves split K = HW into quarters; partial tiles summed in wave order
@@ -39,7 +40,7 @@ __device__ inline void policy_rows16(const float* __restrict__ h, int64_t row0, 
   f32x4 hv[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    const float* src = h + rowc * HW + KW * w + 16 * s + 4 * g;
+    const float* src = h + (LOCAL ? rowc - row0 : rowc) * HW + KW * w + 16 * s + 4 * g;
     if constexpr (COH) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) hv[s][e] = __hip_atomic_load(src + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -41,6 +41,7 @@ CONV_FWD_FLOP_PER_ENV = 2 * (400 * 16 * 256 + 81 * 32 * 256)             # 4,603
 FC_FWD_FLOP_PER_ENV = 2 * 2592 * 256                                     # 1,327,104
 CONV_BWD_FLOP_PER_SAMPLE = 2 * (32 * 256 * 81 + 81 * 32 * 256 + 400 * 16 * 256)   # dW2 + convT + dW1
 HID_BYTES = 256 * 4
+FC_SPLIT = 8                                # fc.hip split-K (partial slabs read by policy_fc_kernel)
 # ViZDoom models (train_a3c_doom.py:28,46): conv1 K = 3 * 64 (the kernels' zero input plane is not counted)
 DOOM_CONV_FWD_FLOP_PER_ENV = 2 * (400 * 16 * 192 + 81 * 32 * 256)
 DOOM_CONV_BWD_FLOP_PER_SAMPLE = 2 * (32 * 256 * 81 + 81 * 32 * 256 + 400 * 16 * 192)
@@ -217,6 +218,7 @@ def main():
     Model = {"ff": A3CFF, "lstm": A3CLSTM, "nature": A3CFFNature, "doom_ff": DoomA3CFF,
              "doom_lstm": DoomA3CLSTM}[arch]
     nat = arch == "nature"
+    lstm = arch in ("lstm", "doom_lstm")
     doom = arch.startswith("doom")
     if doom and not a.actions:
         A = 3                                          # train_a3c_doom.py:105
@@ -330,10 +332,14 @@ def main():
              N * phi_bytes),
             ("conv_fwd", "gemm_kernel x3 (implicit-GEMM convs)" if nat else "conv_fwd_kernel",
              lambda i: net.run_stage("conv_fwd", i % T, stream=stream), T + 1, "mfma", N * conv_fwd_flop),
-            ("fc_fwd", "gemm_kernel + reduce_grad_kernel" if nat else "fc_fwd_kernel",
+            ("fc_fwd", "gemm_kernel + reduce_grad_kernel" if nat else "fc_fwd_kernel" if lstm else
+             "fc_fwd_kernel (split-K partials)",
              lambda i: net.run_stage("fc_fwd", i % T, stream=stream), T + 1, "mfma", N * fc_fwd_flop),
-            ("policy", "policy_kernel", lambda i: net.run_stage("policy", i % T, stream=stream), T + 1, "hbm",
-             N * (hid_bytes + 12 * A + 12)),
+            # FF NIPS / Doom FF: the FC split-K reduce + bias + relu runs in the policy launch
+            # (policy_fc_kernel): it also reads the 8 partial slabs and writes h
+            ("policy", "policy_kernel" if (nat or lstm) else "policy_fc_kernel (FC reduce + heads)",
+             lambda i: net.run_stage("policy", i % T, stream=stream), T + 1, "hbm",
+             N * (hid_bytes + 12 * A + 12) + (0 if (nat or lstm) else N * (FC_SPLIT + 1) * hid_bytes)),
             ("fc_bwd", "gemm_kernel x2 + reduce_grad_kernel", lambda i: net.run_stage("fc_bwd", 0, stream=stream),
              1, "mfma", 2 * fc_fwd_flop * S),
             ("conv_bwd", "gemm_kernel x9 + reduce_grad_kernel x3" if nat else "conv_bwd_kernel",
