@@ -49,20 +49,23 @@ hipError_t launch_policy_args(const float* h, int64_t n, const PolicyArgs& pa, h
 }
 
 // FF act step: the FC forward's split-K reduce moved here from fc_fwd_kernel's
-// last arriver (fc.hip).  The 8 partial slabs of this group's 16 rows are
+// last arriver (fc.hip).  The 8 partial slabs of this group's rows are
 // summed in split order 0..7 from 0.f, then + bias, relu -- the same f32 op
 // sequence as the ticket path, so hfc is bit-identical -- written to hfc (the
 // backward reads it) and to LDS, where the heads read it.
+// PF_ROWS env rows per workgroup (4: 64 workgroups at 256 envs, each reading
+// 32 KB of partials; 16 rows per workgroup left the reduce on 16 CUs)
+constexpr int PF_ROWS = 4;
 __global__ void __launch_bounds__(256)
 policy_fc_kernel(const float* __restrict__ slab, int n, const float* __restrict__ fc_bias, float* __restrict__ hfc,
                  PolicyArgs pa) {
   __shared__ float part[4][16][MAXA + 2];
   __shared__ float zs[16][MAXA + 2];
-  __shared__ __attribute__((aligned(16))) float hl[16 * HID];
+  __shared__ __attribute__((aligned(16))) float hl[PF_ROWS * HID];
   typedef float f32x4v __attribute__((ext_vector_type(4)));
   const int tid = threadIdx.x;
-  const int64_t row0 = (int64_t)blockIdx.x * 16;
-  constexpr int V4 = 16 * HID / 4 / 256;   // float4 per thread (4)
+  const int64_t row0 = (int64_t)blockIdx.x * PF_ROWS;
+  constexpr int V4 = PF_ROWS * HID / 4 / 256;   // float4 per thread per slab
   f32x4v p[V4][FC_SPLIT];
 #pragma unroll
   for (int z = 0; z < FC_SPLIT; ++z)
@@ -88,13 +91,13 @@ policy_fc_kernel(const float* __restrict__ slab, int n, const float* __restrict_
     if (row0 + r < n) *reinterpret_cast<float4*>(hfc + (row0 + r) * HID + c) = o;
   }
   __syncthreads();
-  policy_rows16<HID, false, true>(hl, row0, n, pa, part, zs);
+  policy_rows16<HID, false, true, PF_ROWS>(hl, row0, n, pa, part, zs);
 }
 
 hipError_t launch_policy_fc(const float* slab, int n, const float* fc_bias, float* hfc, const PolicyArgs& pa,
                             hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(policy_fc_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, s, slab, n, fc_bias, hfc, pa);
+  hipLaunchKernelGGL(policy_fc_kernel, dim3((unsigned)((n + PF_ROWS - 1) / PF_ROWS)), dim3(256), 0, s, slab, n, fc_bias, hfc, pa);
   return hipGetLastError();
 }
 

@@ -29,14 +29,16 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // call).  COH: h was written by other workgroups of the same launch (device
 // scope, sc1) and is read with device-scope loads.  LOCAL: h holds only the
 // group's 16 rows (row i at h + i * HW, e.g. LDS filled by the caller).
-template <int HW, bool COH, bool LOCAL = false>
+// ROWS < 16: only rows row0 .. row0 + ROWS - 1 are this group's (the other
+// MFMA rows repeat the last one and are not stored).
+template <int HW, bool COH, bool LOCAL = false, int ROWS = 16>
 __device__ inline void policy_rows16(const float* __restrict__ h, int64_t row0, int64_t n, const PolicyArgs& pa,
                                      float (*part)[16][MAXA + 2], float (*zs)[MAXA + 2]) {
   // 4 waves split K = HW into quarters; partial tiles summed in wave order
   constexpr int KW = HW / 4, NS = KW / 16;
   const int A = pa.A;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
-  const int64_t rowc = min(row0 + col, n - 1);   // A row of this lane (rows past n: any valid row, not stored)
+  const int64_t rowc = min(row0 + (col < ROWS ? col : ROWS - 1), n - 1);   // A row of this lane (rows past n: any valid row, not stored)
   f32x4 hv[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
@@ -74,7 +76,7 @@ __device__ inline void policy_rows16(const float* __restrict__ h, int64_t row0, 
   }
   __syncthreads();
   const int64_t row = row0 + tid;
-  if (tid < 16 && row < n) {
+  if (tid < ROWS && row < n) {
     float* z = zs[tid];
     float* ez = part[0][tid];   // reused: exp(z - max) per action
     // serial max / sum over k (policy_output.py:41-47; Chainer softmax, log_softmax)
