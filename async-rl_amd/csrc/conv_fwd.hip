@@ -165,34 +165,44 @@ conv_fwd_kernel(ConvFwdArgs a) {
   __syncthreads();   // the W1 planes are overwritten by the a1 planes below
   const float bias1 = a.b1[col];
   float* a1g = a.a1 + (int64_t)e * A1;
-  // tile pairs (w, w+8), (w+16, w+24): 25 tiles over 8 waves
-  for (int tA = wave; tA < 25; tA += 16) {
-    const int tB = tA + 8;
-    const bool hasB = tB < 25;
-    const int pA = tA * 16 + col, pB = (hasB ? tB : tA) * 16 + col;
-    const int oyA = pA / 20, oxA = pA - oyA * 20, oyB = pB / 20, oxB = pB - oyB * 20;
-    const int baseA = L_XB + (4 * oyA) * XB_ROW + 8 * oxA;
-    const int baseB = L_XB + (4 * oyB) * XB_ROW + 8 * oxB;
-    f32x4 bigA = {0.f, 0.f, 0.f, 0.f}, smlA = bigA, bigB = bigA, smlB = bigA;
+  // tiles w, w + 8, w + 16 (and 24 on wave 0): 25 tiles over 8 waves in one pass,
+  // 3-4 independent accumulator chains per wave (per-tile k order unchanged)
+  {
+    constexpr int TJ = 4;
+    const bool has3 = wave + 24 < 25;   // wave-uniform
+    int baseX[TJ];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int tl = (j < 3 || has3) ? wave + 8 * j : wave;
+      const int p = tl * 16 + col, oy = p / 20, ox = p - oy * 20;
+      baseX[j] = L_XB + (4 * oy) * XB_ROW + 8 * ox;
+    }
+    f32x4 big[TJ], sml[TJ];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) big[j] = sml[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < ((ARL_ABLATE & 1) ? 0 : 8); ++s) {
       const int u = 4 * s + g, off = (u >> 3) * XB_PLANE + (u & 7) * XB_ROW;
-      const bf16x8 xa = lds_load8_a8(lds, baseA + off);
-      const bf16x8 xb = lds_load8_a8(lds, baseB + off);
-      mfma_x3(xa, w1h[s], w1m[s], w1l[s], bigA, smlA);
-      mfma_x3(xb, w1h[s], w1m[s], w1l[s], bigB, smlB);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const bf16x8 xa = lds_load8_a8(lds, baseX[j] + off);
+        mfma_x3(xa, w1h[s], w1m[s], w1l[s], big[j], sml[j]);
+      }
+      if (has3) {
+        const bf16x8 xa = lds_load8_a8(lds, baseX[3] + off);
+        mfma_x3(xa, w1h[s], w1m[s], w1l[s], big[3], sml[3]);
+      }
     }
     // C rows g*4 + r -> positions tile*16 + g*4 + r, col = oc
 #pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      if (pass == 1 && !hasB) break;
-      const f32x4 big = pass ? bigB : bigA, sml = pass ? smlB : smlA;
-      const int p0 = (pass ? tB : tA) * 16 + g * 4;
+    for (int j = 0; j < TJ; ++j) {
+      if (j == 3 && !has3) break;
+      const int p0 = (wave + 8 * j) * 16 + g * 4;
       float ov[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        ov[r] = (ARL_ABLATE & 16) ? fmaxf(__fadd_rn(__fmul_rn(__fadd_rn(big[r], sml[r]), 1.f / 255.f), bias1), 0.f)
-                                  : fmaxf(__fadd_rn(__fdiv_rn(__fadd_rn(big[r], sml[r]), 255.f), bias1), 0.f);
+        ov[r] = (ARL_ABLATE & 16) ? fmaxf(__fadd_rn(__fmul_rn(__fadd_rn(big[j][r], sml[j][r]), 1.f / 255.f), bias1), 0.f)
+                                  : fmaxf(__fadd_rn(__fdiv_rn(__fadd_rn(big[j][r], sml[j][r]), 255.f), bias1), 0.f);
       *reinterpret_cast<float4*>(a1g + col * C1_P + p0) = make_float4(ov[0], ov[1], ov[2], ov[3]);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
