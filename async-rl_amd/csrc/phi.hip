@@ -77,6 +77,24 @@ struct PhiShared {
 __device__ inline void phi_band(const uint8_t* __restrict__ cur, const uint8_t* __restrict__ prev,
                                 uint8_t* __restrict__ out, int dy0, int mode, PhiShared& sh) {
   const int tid = threadIdx.x;
+  // stage: task = (local row r in 0..23 -> (dy, tap), chunk c in 0..9 of 16 px).
+  // Each task derives its own source row, so the loads are issued before the
+  // resize coefficients are tabulated and need no barrier in front of them.
+  const bool stager = tid < 2 * BAND * 10;
+  const int r = tid / 10, c = tid % 10;
+  const int ly = r >> 1, tap = r & 1;
+  uint4 c0, c1, c2, p0, p1, p2;
+  if (stager) {
+    int o, b0, b1;
+    if (mode & 2) resize_coeff(dy0 + ly + CROP_TOP, SRC_H, CROP_H, o, b0, b1);
+    else resize_coeff(dy0 + ly, SRC_H, DST, o, b0, b1);
+    int sy = o + tap;
+    if (sy > SRC_H - 1) sy = SRC_H - 1;
+    const uint4* pc = reinterpret_cast<const uint4*>(cur + (size_t)sy * SRC_W * 3 + c * 48);
+    const uint4* pp = reinterpret_cast<const uint4*>(prev + (size_t)sy * SRC_W * 3 + c * 48);
+    c0 = pc[0]; c1 = pc[1]; c2 = pc[2];
+    p0 = pp[0]; p1 = pp[1]; p2 = pp[2];
+  }
   if (tid < DST) {
     int o, a0, a1;
     resize_coeff(tid, SRC_W, DST, o, a0, a1);
@@ -87,17 +105,7 @@ __device__ inline void phi_band(const uint8_t* __restrict__ cur, const uint8_t* 
     else resize_coeff(dy0 + tid - 96, SRC_H, DST, o, b0, b1);
     sh.yofs[tid - 96] = (int16_t)o; sh.yb0[tid - 96] = (int16_t)b0; sh.yb1[tid - 96] = (int16_t)b1;
   }
-  __syncthreads();
-  // stage: task = (local row r in 0..23 -> (dy, tap), chunk c in 0..9 of 16 px)
-  if (tid < 2 * BAND * 10) {
-    const int r = tid / 10, c = tid % 10;
-    const int ly = r >> 1, tap = r & 1;
-    int sy = sh.yofs[ly] + tap;
-    if (sy > SRC_H - 1) sy = SRC_H - 1;
-    const uint4* pc = reinterpret_cast<const uint4*>(cur + (size_t)sy * SRC_W * 3 + c * 48);
-    const uint4* pp = reinterpret_cast<const uint4*>(prev + (size_t)sy * SRC_W * 3 + c * 48);
-    uint4 c0 = pc[0], c1 = pc[1], c2 = pc[2];
-    uint4 p0 = pp[0], p1 = pp[1], p2 = pp[2];
+  if (stager) {
     uint32_t w[12] = {umax_bytes(c0.x, p0.x), umax_bytes(c0.y, p0.y), umax_bytes(c0.z, p0.z),
                       umax_bytes(c0.w, p0.w), umax_bytes(c1.x, p1.x), umax_bytes(c1.y, p1.y),
                       umax_bytes(c1.z, p1.z), umax_bytes(c1.w, p1.w), umax_bytes(c2.x, p2.x),
