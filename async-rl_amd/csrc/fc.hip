@@ -9,7 +9,7 @@
 //   * 32 x 64 output tile per workgroup; the whole 96 x 324 operand block
 //     (124 KB) is staged by LDS-DMA (global_load_lds_dwordx4) in one burst --
 //     every load in flight at once, one wait, one barrier;
-//   * v_mfma_f32_16x16x4_f32, 2 accumulators per wave, operands read as
+//   * v_mfma_f32_16x16x4_f32, 8 waves with one 16 x 16 sub-tile each, operands read as
 //     ds_read_b128 feeding 4 k-steps each (k permuted identically for A/B);
 //   * partial tiles go to a slab; the last workgroup of each tile (device
 //     ticket) sums the 8 partials in split order 0..7 -- deterministic and
@@ -38,11 +38,13 @@ constexpr int FROWS = FBM + FBN;          // 96 staged rows (32 of a2, 64 of W)
 constexpr int FV = FKS / 4;               // 81 float4 per row
 constexpr int FVEC = FROWS * FV;          // 7776 float4 per workgroup
 constexpr int FINSTR = (FVEC + 63) / 64;  // 122 wave-instructions of LDS-DMA
+constexpr int FT = 512;                   // threads: 8 waves, one 16 x 16 output sub-tile each
+constexpr int FW = FT / 64;
 static_assert(A2 % (4 * FSPLIT) == 0, "K slice must be whole float4s");
 static_assert(HID % FBN == 0, "N tiles");
 }  // namespace
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(FT)
 fc_fwd_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, const float* __restrict__ bias,
               float* __restrict__ slab, int* __restrict__ tickets, float* __restrict__ hfc) {
   __shared__ __attribute__((aligned(16))) float S[FROWS * FKS];   // 124,416 B
@@ -54,7 +56,7 @@ fc_fwd_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, 
 
   // ---- stage: float4 i -> row i / 81, column 4 (i % 81); LDS image is the
   // unpadded [96][324] block, lane-linear per wave-instruction
-  for (int it = wave; it < ((ARL_ABLATE & 128) ? 0 : FINSTR); it += 4) {
+  for (int it = wave; it < ((ARL_ABLATE & 128) ? 0 : FINSTR); it += FW) {
     const int i = it * 64 + lane;
     if (i < FVEC) {
       const int r = i / FV, c = i - r * FV;
@@ -68,29 +70,22 @@ fc_fwd_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // ---- MFMA: wave -> m sub-tile (wave & 1), n sub-tiles 2 (wave >> 1) + {0, 1}
+  // ---- MFMA: wave -> m sub-tile (wave & 1), n sub-tile (wave >> 1)
   const int q = lane >> 4, col = lane & 15;
-  const int ms = wave & 1, ns = 2 * (wave >> 1);
+  const int ms = wave & 1, ns = wave >> 1;
   const float* Ar = S + (ms * 16 + col) * FKS + 4 * q;
   const float* B0 = S + (FBM + ns * 16 + col) * FKS + 4 * q;
-  const float* B1 = B0 + 16 * FKS;
-  f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 c0 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 5
   for (int s = 0; s < ((ARL_ABLATE & 512) ? 0 : FKS / 16); ++s) {   // 20 groups of 16 k: lane quarter q holds k = 16 s + 4 q + r
     const f32x4 av = *reinterpret_cast<const f32x4*>(Ar + 16 * s);
     const f32x4 b0 = *reinterpret_cast<const f32x4*>(B0 + 16 * s);
-    const f32x4 b1 = *reinterpret_cast<const f32x4*>(B1 + 16 * s);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], b0[r], c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], b1[r], c1, 0, 0, 0);
-    }
+    for (int r = 0; r < 4; ++r) c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], b0[r], c0, 0, 0, 0);
   }
   {  // tail k = 320 + q
     constexpr int KT = (FKS / 16) * 16;
-    const float av = Ar[KT - 3 * q], b0 = B0[KT - 3 * q], b1 = B1[KT - 3 * q];
-    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b0, c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b1, c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ar[KT - 3 * q], B0[KT - 3 * q], c0, 0, 0, 0);
   }
   static_assert(FKS - (FKS / 16) * 16 == 4, "one tail k-step");
 
@@ -103,12 +98,9 @@ fc_fwd_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, 
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int m = m0 + ms * 16 + q * 4 + r;
-    if (m < n) {
+    if (m < n)
       __hip_atomic_store(part + (int64_t)m * HID + n0 + ns * 16 + col, c0[r], __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(part + (int64_t)m * HID + n0 + ns * 16 + 16 + col, c1[r], __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
   if ((ARL_ABLATE & 256) || tickets == nullptr) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -117,13 +109,14 @@ fc_fwd_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, 
     is_last = __hip_atomic_fetch_add(&tickets[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == FSPLIT - 1;
   __syncthreads();
   if (!is_last) return;
-  // ---- last arrival: sum splits 0..7 in order, bias, relu (2 float4 per thread,
-  // all 16 device-scope loads in flight before one wait)
-  f32x4 p[2][FSPLIT];
-  int mrow[2], ccol[2];
+  // ---- last arrival: sum splits 0..7 in order, bias, relu (RJ float4 per thread,
+  // all device-scope loads in flight before one wait)
+  constexpr int RJ = FBM * FBN / 4 / FT;
+  f32x4 p[RJ][FSPLIT];
+  int mrow[RJ], ccol[RJ];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int idx = tid + 256 * j;          // 32 rows x 16 float4
+  for (int j = 0; j < RJ; ++j) {
+    const int idx = tid + FT * j;           // 32 rows x 16 float4
     mrow[j] = m0 + (idx >> 4);
     ccol[j] = n0 + 4 * (idx & 15);
   }
@@ -132,12 +125,12 @@ fc_fwd_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, 
     // one descriptor per split slab (wave-uniform base), aux 16 = sc1
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(slab + (int64_t)z * n * HID, 0, n * HID * 4, 0x00020000);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < RJ; ++j)
       p[j][z] = __builtin_bit_cast(
           f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, (min(mrow[j], n - 1) * HID + ccol[j]) * 4, 0, 16));
   }
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < RJ; ++j) {
     if (mrow[j] < n) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -159,7 +152,7 @@ int fc_fwd_tiles(int n) { return ((n + FBM - 1) / FBM) * (HID / FBN); }
 hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b, float* slab, int* tickets,
                          float* hfc, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(fc_fwd_kernel, dim3((unsigned)(fc_fwd_tiles(n) * FSPLIT)), dim3(256), 0, s, a2, n, W, b, slab,
+  hipLaunchKernelGGL(fc_fwd_kernel, dim3((unsigned)(fc_fwd_tiles(n) * FSPLIT)), dim3(FT), 0, s, a2, n, W, b, slab,
                      tickets, hfc);
   return hipGetLastError();
 }
