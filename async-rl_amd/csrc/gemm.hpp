@@ -39,15 +39,15 @@ enum { GS = 0, GK = 1, GM = 2 };
 // Gather one BK-deep K chunk of the A (BM x BK) and B (BK x BN) tiles into
 // registers (ra: A_PER, rb: B_PER values per thread); element order per mode
 // is documented at the commit sites of the two kernels below.
-template <int BM, int BN, int BK, int AV, int BV, class AOp, class BOp>
+template <int BM, int BN, int BK, int AV, int BV, int NTH, class AOp, class BOp>
 __device__ inline void gemm_gather(const AOp& A, const BOp& B, int M, int N, int kend, int m0, int n0, int kc,
                                    int tid, float* ra, float* rb) {
-  constexpr int A_PER = (BM * BK) / 256;
-  constexpr int B_PER = (BK * BN) / 256;
+  constexpr int A_PER = (BM * BK) / NTH;
+  constexpr int B_PER = (BK * BN) / NTH;
   if constexpr (AV == GK) {
 #pragma unroll
     for (int i = 0; i < A_PER / 4; ++i) {
-      const int v = tid + 256 * i;
+      const int v = tid + NTH * i;
       const int kq = v % (BK / 4), mm = v / (BK / 4);
       const int m = m0 + mm, k = kc + 4 * kq;
       float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -64,7 +64,7 @@ __device__ inline void gemm_gather(const AOp& A, const BOp& B, int M, int N, int
   } else if constexpr (AV == GM) {
 #pragma unroll
     for (int i = 0; i < A_PER / 4; ++i) {
-      const int v = tid + 256 * i;
+      const int v = tid + NTH * i;
       const int mq = v % (BM / 4), kk = v / (BM / 4);
       const int m = m0 + 4 * mq, k = kc + kk;
       float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -81,7 +81,7 @@ __device__ inline void gemm_gather(const AOp& A, const BOp& B, int M, int N, int
   } else {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
-      const int e = tid + 256 * i;
+      const int e = tid + NTH * i;
       const int mm = e % BM, kk = e / BM;
       const int m = m0 + mm, k = kc + kk;
       ra[i] = (m < M && k < kend) ? A.load(m, k) : 0.f;
@@ -90,7 +90,7 @@ __device__ inline void gemm_gather(const AOp& A, const BOp& B, int M, int N, int
   if constexpr (BV == GK) {
 #pragma unroll
     for (int i = 0; i < B_PER / 4; ++i) {
-      const int v = tid + 256 * i;
+      const int v = tid + NTH * i;
       const int kq = v % (BK / 4), nn = v / (BK / 4);
       const int n = n0 + nn, k = kc + 4 * kq;
       float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -107,7 +107,7 @@ __device__ inline void gemm_gather(const AOp& A, const BOp& B, int M, int N, int
   } else if constexpr (BV == GM) {
 #pragma unroll
     for (int i = 0; i < B_PER / 4; ++i) {
-      const int v = tid + 256 * i;
+      const int v = tid + NTH * i;
       const int nq = v % (BN / 4), kk = v / (BN / 4);
       const int n = n0 + 4 * nq, k = kc + kk;
       float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -124,7 +124,7 @@ __device__ inline void gemm_gather(const AOp& A, const BOp& B, int M, int N, int
   } else {
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
-      const int e = tid + 256 * i;
+      const int e = tid + NTH * i;
       const int nn = e % BN, kk = e / BN;
       const int n = n0 + nn, k = kc + kk;
       rb[i] = (n < N && k < kend) ? B.load(k, n) : 0.f;
@@ -134,17 +134,17 @@ __device__ inline void gemm_gather(const AOp& A, const BOp& B, int M, int N, int
 
 // One BM x BN output tile (split-K slice z) of the implicit GEMM; the body of
 // gemm_kernel and of gemm2_kernel (two independent GEMMs in one launch).
-template <int BM, int BN, int BK, int WM, int WN, int AV, int BV, class AOp, class BOp, class EOp>
+template <int BM, int BN, int BK, int WM, int WN, int AV, int BV, int NTH, class AOp, class BOp, class EOp>
 __device__ inline void gemm_tile(const AOp& A, const BOp& B, const EOp& E, int M, int N, int K, int k_per_split,
                                  int bx, int by, int z) {
-  static_assert(WM * WN == 4, "4 waves");
+  static_assert(WM * WN == NTH / 64, "one wave per WM x WN slot");
   constexpr int TM = BM / (16 * WM);   // MFMA tiles per wave along m
   constexpr int TN = BN / (16 * WN);   // along n
   static_assert(TM >= 1 && TN >= 1, "tile too small for wave layout");
   constexpr int LDA = AV == GK ? BM + 1 : BM + 4;
   constexpr int LDB = BV == GK ? BN + 1 : BN + 4;
-  constexpr int A_PER = (BM * BK) / 256;   // A elements gathered per thread per chunk
-  constexpr int B_PER = (BK * BN) / 256;
+  constexpr int A_PER = (BM * BK) / NTH;   // A elements gathered per thread per chunk
+  constexpr int B_PER = (BK * BN) / NTH;
   static_assert(A_PER >= 1 && B_PER >= 1, "chunk too small");
   static_assert(AV == GS || A_PER % 4 == 0, "vector A gather needs whole 4-vectors per thread");
   static_assert(BV == GS || B_PER % 4 == 0, "vector B gather needs whole 4-vectors per thread");
@@ -171,12 +171,12 @@ __device__ inline void gemm_tile(const AOp& A, const BOp& B, const EOp& E, int M
 
   float ra[A_PER], rb[B_PER];
 
-  auto gather = [&](int kc) { gemm_gather<BM, BN, BK, AV, BV>(A, B, M, N, kend, m0, n0, kc, tid, ra, rb); };
+  auto gather = [&](int kc) { gemm_gather<BM, BN, BK, AV, BV, NTH>(A, B, M, N, kend, m0, n0, kc, tid, ra, rb); };
   auto commit = [&]() {
     if constexpr (AV == GK) {
 #pragma unroll
       for (int i = 0; i < A_PER / 4; ++i) {
-        const int v = tid + 256 * i;
+        const int v = tid + NTH * i;
         const int kq = v % (BK / 4), mm = v / (BK / 4);
 #pragma unroll
         for (int r = 0; r < 4; ++r) As[(4 * kq + r) * LDA + mm] = ra[4 * i + r];
@@ -184,7 +184,7 @@ __device__ inline void gemm_tile(const AOp& A, const BOp& B, const EOp& E, int M
     } else if constexpr (AV == GM) {
 #pragma unroll
       for (int i = 0; i < A_PER / 4; ++i) {
-        const int v = tid + 256 * i;
+        const int v = tid + NTH * i;
         const int mq = v % (BM / 4), kk = v / (BM / 4);
         *reinterpret_cast<float4*>(&As[kk * LDA + 4 * mq]) =
             make_float4(ra[4 * i], ra[4 * i + 1], ra[4 * i + 2], ra[4 * i + 3]);
@@ -192,14 +192,14 @@ __device__ inline void gemm_tile(const AOp& A, const BOp& B, const EOp& E, int M
     } else {
 #pragma unroll
       for (int i = 0; i < A_PER; ++i) {
-        const int e = tid + 256 * i;
+        const int e = tid + NTH * i;
         As[(e / BM) * LDA + (e % BM)] = ra[i];
       }
     }
     if constexpr (BV == GK) {
 #pragma unroll
       for (int i = 0; i < B_PER / 4; ++i) {
-        const int v = tid + 256 * i;
+        const int v = tid + NTH * i;
         const int kq = v % (BK / 4), nn = v / (BK / 4);
 #pragma unroll
         for (int r = 0; r < 4; ++r) Bs[(4 * kq + r) * LDB + nn] = rb[4 * i + r];
@@ -207,7 +207,7 @@ __device__ inline void gemm_tile(const AOp& A, const BOp& B, const EOp& E, int M
     } else if constexpr (BV == GM) {
 #pragma unroll
       for (int i = 0; i < B_PER / 4; ++i) {
-        const int v = tid + 256 * i;
+        const int v = tid + NTH * i;
         const int nq = v % (BN / 4), kk = v / (BN / 4);
         *reinterpret_cast<float4*>(&Bs[kk * LDB + 4 * nq]) =
             make_float4(rb[4 * i], rb[4 * i + 1], rb[4 * i + 2], rb[4 * i + 3]);
@@ -215,7 +215,7 @@ __device__ inline void gemm_tile(const AOp& A, const BOp& B, const EOp& E, int M
     } else {
 #pragma unroll
       for (int i = 0; i < B_PER; ++i) {
-        const int e = tid + 256 * i;
+        const int e = tid + NTH * i;
         Bs[(e / BN) * LDB + (e % BN)] = rb[i];
       }
     }
@@ -264,7 +264,7 @@ __device__ inline void gemm_tile(const AOp& A, const BOp& B, const EOp& E, int M
 template <int BM, int BN, int BK, int WM, int WN, class AOp, class BOp, class EOp, int AV = GS, int BV = GS>
 __global__ void __launch_bounds__(256)
 gemm_kernel(AOp A, BOp B, EOp E, int M, int N, int K, int k_per_split) {
-  gemm_tile<BM, BN, BK, WM, WN, AV, BV>(A, B, E, M, N, K, k_per_split, blockIdx.x, blockIdx.y, blockIdx.z);
+  gemm_tile<BM, BN, BK, WM, WN, AV, BV, 256>(A, B, E, M, N, K, k_per_split, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 // Two independent GEMMs of the same tile shape in one launch: workgroups
@@ -276,18 +276,18 @@ struct GemmJob {
   int M, N, K, kps, gx, gy, gz;
 };
 
-template <int BM, int BN, int BK, int WM, int WN, int AV1, int BV1, int AV2, int BV2, class J1, class J2>
-__global__ void __launch_bounds__(256)
+template <int BM, int BN, int BK, int WM, int WN, int NTH, int AV1, int BV1, int AV2, int BV2, class J1, class J2>
+__global__ void __launch_bounds__(NTH)
 gemm2_kernel(J1 j1, J2 j2) {
   int b = blockIdx.x;
   const int g1 = j1.gx * j1.gy * j1.gz;
   if (b < g1) {
     const int x = b % j1.gx, y = (b / j1.gx) % j1.gy, z = b / (j1.gx * j1.gy);
-    gemm_tile<BM, BN, BK, WM, WN, AV1, BV1>(j1.A, j1.B, j1.E, j1.M, j1.N, j1.K, j1.kps, x, y, z);
+    gemm_tile<BM, BN, BK, WM, WN, AV1, BV1, NTH>(j1.A, j1.B, j1.E, j1.M, j1.N, j1.K, j1.kps, x, y, z);
   } else {
     b -= g1;
     const int x = b % j2.gx, y = (b / j2.gx) % j2.gy, z = b / (j2.gx * j2.gy);
-    gemm_tile<BM, BN, BK, WM, WN, AV2, BV2>(j2.A, j2.B, j2.E, j2.M, j2.N, j2.K, j2.kps, x, y, z);
+    gemm_tile<BM, BN, BK, WM, WN, AV2, BV2, NTH>(j2.A, j2.B, j2.E, j2.M, j2.N, j2.K, j2.kps, x, y, z);
   }
 }
 
@@ -301,13 +301,19 @@ inline GemmJob<AOp, BOp, EOp> gemm_job(const AOp& A, const BOp& B, const EOp& E,
   return GemmJob<AOp, BOp, EOp>{A, B, E, M, N, K, kps, (M + BM - 1) / BM, (N + BN - 1) / BN, splits};
 }
 
-template <int BM, int BN, int BK, int WM, int WN, int AV1, int BV1, int AV2, int BV2, class J1, class J2>
-inline hipError_t launch_gemm2(const J1& j1, const J2& j2, hipStream_t s) {
+// NTH threads per workgroup (WM x WN = NTH / 64 waves)
+template <int BM, int BN, int BK, int WM, int WN, int NTH, int AV1, int BV1, int AV2, int BV2, class J1, class J2>
+inline hipError_t launch_gemm2_nt(const J1& j1, const J2& j2, hipStream_t s) {
   const int g = j1.gx * j1.gy * j1.gz + j2.gx * j2.gy * j2.gz;
   if (g <= 0) return hipSuccess;
-  hipLaunchKernelGGL((gemm2_kernel<BM, BN, BK, WM, WN, AV1, BV1, AV2, BV2, J1, J2>), dim3(g), dim3(256), 0, s, j1,
-                     j2);
+  hipLaunchKernelGGL((gemm2_kernel<BM, BN, BK, WM, WN, NTH, AV1, BV1, AV2, BV2, J1, J2>), dim3(g), dim3(NTH), 0, s,
+                     j1, j2);
   return hipGetLastError();
+}
+
+template <int BM, int BN, int BK, int WM, int WN, int AV1, int BV1, int AV2, int BV2, class J1, class J2>
+inline hipError_t launch_gemm2(const J1& j1, const J2& j2, hipStream_t s) {
+  return launch_gemm2_nt<BM, BN, BK, WM, WN, 256, AV1, BV1, AV2, BV2>(j1, j2, s);
 }
 
 // ---------------------------------------------------------------- bf16x6 variant

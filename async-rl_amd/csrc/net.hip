@@ -526,7 +526,7 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
   // 3. FC: dW (+ bias via ones column), da2 = (dfc W) * (a2 > 0)
   //    as ONE launch: both are latency-bound and independent, so their
   //    workgroups share the chip instead of running back to back
-  ARL_TRY((launch_gemm2<64, 64, 32, 2, 2, GM, GM, GK, GM>(
+  ARL_TRY((launch_gemm2_nt<64, 64, 32, 2, 4, 512, GM, GM, GK, GM>(   // 8 waves, 2 sub-tiles each
       gemm_job<64, 32>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab_f, HID, A2 + 1}, HID, A2 + 1, S, pl.fc_w, 64),
       gemm_job<64, 32>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2}, EpiMask{da2, a2, A2}, S, A2, HID, 1, 64), s)));
   return hipSuccess;
