@@ -181,8 +181,10 @@ int arl_optimize(arl_net* net, double lr0, int64_t total_steps, int64_t n_total,
  * profiling.  t selects the window step for the forward stages. */
 enum {
   ARL_STAGE_CONV_FWD = 1,   /* fused conv1 + conv2 forward from the frame ring */
-  ARL_STAGE_FC_FWD = 2,     /* Linear(2592, 256) + relu, in-launch split-K reduce */
-  ARL_STAGE_POLICY = 3,     /* pi / v heads + softmax policy output (no action) */
+  ARL_STAGE_FC_FWD = 2,     /* Linear(2592, 256): FF nets write the 8 split-K partials only; LSTM
+                               nets reduce + bias + relu in the same launch */
+  ARL_STAGE_POLICY = 3,     /* pi / v heads + softmax policy output (no action); FF nets first
+                               reduce the FC partials + bias + relu into h (as in a window step) */
   ARL_STAGE_FC_BWD = 4,     /* FC dW / db and da2 GEMMs */
   ARL_STAGE_CONV_BWD = 5    /* fused conv backward (conv2 dW, convT, conv1 dW) into per-block slabs */
 };
