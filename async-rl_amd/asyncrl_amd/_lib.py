@@ -54,6 +54,10 @@ SIGNATURES = {
     "arl_observe": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int, c_void_p]),
     "arl_observe_rgb": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_i64, c_int, c_int,
                                 c_void_p]),
+    "arl_observe_stack": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p]),
+    "arl_truncate_window": (c_int, [c_void_p, c_int, c_void_p]),
+    "arl_net_set_loss": (c_int, [c_void_p, c_double, c_int]),
+    "arl_reset_state": (c_int, [c_void_p, c_i64, c_i64, c_void_p]),
     "arl_act": (c_int, [c_void_p, c_int, c_void_p]),
     "arl_act_mode": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "arl_observe_envs": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_i64,
@@ -72,8 +76,8 @@ SIGNATURES = {
                            c_i64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p]),
     "arl_returns_lossgrad": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_i64,
-                                     c_int, c_double, c_double, c_double, c_int, c_void_p, c_void_p, c_void_p,
-                                     c_void_p]),
+                                     c_int, c_double, c_double, c_double, c_double, c_int, c_int, c_void_p,
+                                     c_void_p, c_void_p, c_void_p]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():
@@ -81,10 +85,16 @@ for _name, (_res, _args) in SIGNATURES.items():
     _fn.restype = _res
     _fn.argtypes = _args
 
+if lib.arl_abi_version() != 2:
+    raise ImportError(f"asyncrl_amd: {LIB_PATH} has ABI {lib.arl_abi_version()}, expected 2 (rebuild it)")
+
 ARCH_FF = 0
 ARCH_LSTM = 1
 ARCH_FF_NATURE = 2   # A3CFF with NatureDQNHead (dqn_head.py:6-28)
 ARCH_RGB = 16        # flag for FF / LSTM: the ViZDoom models (train_a3c_doom.py:25-63), RGB screens
+ARCH_STACK = 32      # flag for FF / LSTM: observations are whole 4-screen stacks (ALE.state, ale.py:91-94)
+FWD_KEEP_STATE = 16  # arl_forward_states mode bit: LSTM keep_same_state (a3c_ale.py:57-60)
+ABI_VERSION = 2
 ACT_CONV_ONLY = 4      # arl_act_envs mode bits (env-group staggering)
 ACT_AFTER_CONV = 8
 ENV_GROUP_ALIGN = 32   # arl_observe_envs / arl_act_envs: e0 % ENV_GROUP_ALIGN == 0

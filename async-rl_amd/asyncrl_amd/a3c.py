@@ -5,21 +5,33 @@ unchain_backward), `A3CFF` / `A3CLSTM` (a3c_ale.py:28-70), `A3C` (a3c.py:27-185:
 __init__ arguments, act(state, reward, is_state_terminal), sync_parameters,
 load_model / save_model).
 
-What changes: the reference runs one env per process and updates
-shared parameters Hogwild-style whenever that env finishes a t_max window or
-an episode.  Here N envs step in lockstep on the GPU; every t_max steps one
-update is made from the sum of all envs' window-segment gradients at fixed
-parameters (a terminal inside a window closes that env's segment with R = 0,
-exactly like a3c.py:82-83), all-reduced over ranks with RCCL when
-torch.distributed is initialised, then clipped (40) and applied by
-RMSpropAsync.  Hogwild races are gone; replicas stay bitwise identical.
+Two ways in, one set of kernels:
 
-`act` takes the raw frame pair of each env (frame 3 and frame 4 of the
-4-frame skip, ale.py:118-119,134-135) -- the phi pre-stage runs on the GPU --
-together with the reward and terminal flag of the transition into it.
-Following batched-env convention, a terminal env's observation is already the
-first frame of its next episode (auto-reset); the reference spends a separate
-act(.., is_state_terminal=True) call on the terminal state instead.
+* `A3C.act(state, reward, is_state_terminal) -> int | None` on a one-env model
+  (the default for n_envs = 1) is the reference's contract call for call
+  (a3c.py:67-167): `state` is ALE.state (4 uint8 84x84 screens, ale.py:91-94)
+  or anything the `phi` plugin maps to dqn_phi's image of such screens; the
+  window restarts at every update (t_start = t, a3c.py:152); a terminal call
+  runs the R = 0 update over the steps since the last one, resets the
+  recurrent state and returns None (a3c.py:77-83,165-167); a full window
+  bootstraps with v(s) at pre-update parameters and acts on s with the
+  post-update ones (a3c.py:85,156); pi_loss_coef, v_loss_coef and
+  keep_loss_scale_same scale the losses as at a3c.py:110-121.  The frames
+  live in an ARCH_STACK ring (one whole stack per slot); the update is the
+  same device learner as the batched path, restricted to the window's steps
+  (arl_truncate_window).
+
+* `A3C.act_batch(pairs, reward, is_state_terminal)` / `run_window(...)` on an
+  n-env model: the envs step in lockstep, phi runs on the GPU
+  from raw frame pairs, and every t_max steps one update is made from the SUM
+  of all envs' window-segment gradients at fixed parameters (a terminal
+  inside a window closes that env's segment with R = 0, exactly like
+  a3c.py:82-83), all-reduced over ranks with RCCL when torch.distributed is
+  initialised, then clipped and applied by RMSpropAsync.  Hogwild races are
+  gone; replicas stay bitwise identical.  batch_loss="mean" divides the
+  summed loss by the envs of all ranks (effective step size).
+  Batched convention: a terminal env's observation is already the first
+  frame of its next episode (auto-reset).
 """
 from __future__ import annotations
 
@@ -28,8 +40,8 @@ import os
 import numpy as np
 import torch
 
-from ._lib import (ACT_AFTER_CONV, ACT_CONV_ONLY, ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, LEARN_CONV,
-                   RESIZE_SCALAR)
+from ._lib import (ACT_AFTER_CONV, ACT_CONV_ONLY, ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, ARCH_STACK,
+                   LEARN_CONV, RESIZE_SCALAR)
 from .distributed import allreduce_grads, world_info
 from .net import DeviceNet, init_like_torch
 from . import serializers
@@ -40,38 +52,69 @@ STAGGER = os.environ.get("ARL_GROUP_STAGGER", "1") != "0"
 # > 1 rank: split the gradient all-reduce around the conv backward (ARL_OVERLAP_ALLREDUCE=0: one call)
 OVERLAP_ALLREDUCE = os.environ.get("ARL_OVERLAP_ALLREDUCE", "1") != "0"
 
+_PHI_LUT = np.arange(256, dtype=np.float32) / np.float32(255.0)   # dqn_phi.py:14-16, per uint8 value
+
+
+def _to_device_f32(state, device) -> torch.Tensor:
+    t = state if torch.is_tensor(state) else torch.from_numpy(np.ascontiguousarray(np.asarray(state, np.float32)))
+    t = t.to(device=device, dtype=torch.float32)
+    if t.dim() == 3:
+        t = t.unsqueeze(0)
+    return t.contiguous()
+
 
 class A3CModel:
-    """a3c.py:15-24."""
+    """a3c.py:15-24.
+
+    frames: "stacks" -- observations are whole ALE.state stacks (the A3C.act
+    drop-in; default for n_envs = 1), or "pairs" -- raw (frame 4, frame 3)
+    pairs whose phi runs on the GPU (the batched hot path; default for
+    n_envs > 1).  RGB (Doom) and Nature models take their own inputs."""
 
     arch = ARCH_FF
 
     def __init__(self, n_actions: int, n_envs: int = 1, t_max: int = 5, seed: int = 0, env_offset: int = 0,
-                 init_seed: int | None = 0, device=None):
+                 init_seed: int | None = 0, device=None, frames: str | None = None):
         self.n_actions = n_actions
-        self.net = DeviceNet(self.arch, n_actions, n_envs, t_max, env_offset=env_offset, seed=seed,
-                             device=device)
+        arch = self.arch
+        stackable = arch in (ARCH_FF, ARCH_LSTM)
+        if frames is None:
+            frames = "stacks" if (n_envs == 1 and stackable) else "pairs"
+        if frames not in ("stacks", "pairs"):
+            raise ValueError("frames must be 'stacks' or 'pairs'")
+        if frames == "stacks":
+            if not stackable:
+                raise ValueError("frames='stacks' applies to the NIPS-head FF / LSTM models")
+            arch |= ARCH_STACK
+        self.frames = frames
+        self.net = DeviceNet(arch, n_actions, n_envs, t_max, env_offset=env_offset, seed=seed, device=device)
         if init_seed is not None:
             self.net.load_params(init_like_torch(self.arch, n_actions, np.random.default_rng(init_seed)))
 
-    def pi_and_v(self, state: torch.Tensor, keep_same_state: bool = False, deterministic: bool = False):
-        """state: (n, 4, 84, 84) f32 (dqn_phi output).  FF only; the LSTM
-        model's recurrent forward runs inside A3C.act.  The policy output is
-        computed eagerly: action_indices holds a Philox draw, or, with
-        deterministic=True, most_probable_actions holds the first argmax
-        (the two eval modes of a3c_ale.py:73-89)."""
+    def pi_and_v(self, state, keep_same_state: bool = False, deterministic: bool = False):
+        """a3c_ale.py:38-40 / 55-63: state (n, C, 84, 84) float32 (dqn_phi
+        output; a device tensor, or host data that is uploaded), n <=
+        n_envs.  The policy output is computed eagerly: action_indices holds
+        a Philox draw (a fresh one per call), or, with deterministic=True,
+        most_probable_actions holds the first argmax (the two eval modes of
+        a3c_ale.py:73-89).  LSTM models carry their pi_and_v recurrent state
+        across calls (reset_state() clears it; keep_same_state=True leaves it
+        as it was, a3c_ale.py:57-60).  The returned tensors are copies."""
+        x = _to_device_f32(state, self.net.device)
         mode = 2 if deterministic else 1
-        self.net.forward_states(state.contiguous(), mode=mode)
-        o = self.net.step_outputs(self.net.t_max)
-        n = state.shape[0]
-        o = {k: v[:n] for k, v in o.items()}
+        self.net.forward_states(x, mode=mode, keep_same_state=keep_same_state)
+        n = x.shape[0]
+        o = {k: v[:n].clone() for k, v in self.net.step_outputs(self.net.t_max).items()}
         return SoftmaxPolicyOutput(o, greedy=deterministic), o["v"]
 
     def reset_state(self):
-        pass
+        """a3c_ale.py:65-66: the pi_and_v recurrent state -> None (LSTM; a
+        no-op for FF).  The lockstep window's state is reset by terminals."""
+        self.net.reset_state()
 
     def unchain_backward(self):
-        pass
+        """a3c_ale.py:68-70: nothing to cut -- the device learner's BPTT is
+        truncated at every window edge by construction."""
 
     def namedparams(self):
         return self.net.state_dict()
@@ -94,39 +137,34 @@ class A3CLSTM(A3CModel):
     """a3c_ale.py:43-70: NIPSDQNHead -> L.LSTM(256, 256) -> policy + value."""
     arch = ARCH_LSTM
 
-    def pi_and_v(self, state, keep_same_state=False):
-        raise NotImplementedError("A3CLSTM forward runs inside A3C.act (recurrent state is on device)")
-
 
 class DoomA3CFF(A3CModel):
     """train_a3c_doom.py:25-38 A3CFF: NIPSDQNHead(n_input_channels=3) on the
     RGB screen (phi = train_a3c_doom.py:21-23, no frame stack) ->
     FCSoftmaxPolicy + FCVFunction.  pi_and_v takes rgb_phi output
-    (n, 3, 84, 84); A3C.act takes the raw (n, H, W, 3) screens."""
+    (n, 3, 84, 84); A3C.act_batch takes the raw (n, H, W, 3) screens."""
     arch = ARCH_FF | ARCH_RGB
 
 
 class DoomA3CLSTM(A3CModel):
     """train_a3c_doom.py:41-63 A3CLSTM: the RGB NIPS head -> L.LSTM(256, 256)
-    -> policy + value; recurrent forward inside A3C.act."""
+    -> policy + value."""
     arch = ARCH_LSTM | ARCH_RGB
-
-    def pi_and_v(self, state, keep_same_state=False):
-        raise NotImplementedError("DoomA3CLSTM forward runs inside A3C.act (recurrent state is on device)")
 
 
 class A3C:
-    """a3c.py:27-185, lockstep-batched.  One `act` call = one env-step of all
-    n_envs envs; every t_max calls it also performs the update."""
+    """a3c.py:27-185.  On a one-env model `act` is the reference's call (one
+    env-step, int | None); on an n-env model one `act_batch` call is one
+    env-step of all envs and every t_max calls also performs the update."""
 
     def __init__(self, model: A3CModel, optimizer, t_max: int, gamma: float, beta: float = 1e-2,
                  process_idx: int = 0, clip_reward: bool = True, phi=None, pi_loss_coef: float = 1.0,
                  v_loss_coef: float = 0.5, keep_loss_scale_same: bool = False, resize_mode: int = RESIZE_SCALAR,
-                 process_group=None):
-        if pi_loss_coef != 1.0 or keep_loss_scale_same:
-            raise NotImplementedError("pi_loss_coef != 1 / keep_loss_scale_same are not supported yet")
+                 process_group=None, batch_loss: str = "sum"):
         if model.net.t_max != t_max:
             raise ValueError("model was built for a different t_max")
+        if batch_loss not in ("sum", "mean"):
+            raise ValueError("batch_loss must be 'sum' or 'mean'")
         self.shared_model = model          # device params are shared by construction
         self.model = model
         self.optimizer = optimizer
@@ -134,13 +172,32 @@ class A3C:
             optimizer.setup(model)
         self.t_max, self.gamma, self.beta = t_max, gamma, beta
         self.process_idx, self.clip_reward = process_idx, clip_reward
-        self.v_loss_coef = v_loss_coef
+        self.phi = phi
+        self.pi_loss_coef, self.v_loss_coef = pi_loss_coef, v_loss_coef
+        self.keep_loss_scale_same = keep_loss_scale_same
         self.resize_mode = resize_mode
         self.pg = process_group
         self.world, self.rank = world_info(process_group)
-        self.t = 0          # env-steps taken (per env)
         self.net = model.net
+        # the loss of the lockstep batch: the sum over envs (and ranks), or its mean
+        scale = 1.0 if batch_loss == "sum" else 1.0 / (self.net.n_envs * self.world)
+        self._vcoef = v_loss_coef * scale
+        self.net.set_loss(pi_loss_coef * scale, keep_loss_scale_same)
+        self.t = 0          # env-steps taken (per env)
+        self.t_start = 0    # a3c.py:56,152 (reference-contract act)
+        self.single = self.net.stack and self.net.n_envs == 1
+        self._episode_start = True
+        self._copied = None
         self.net.reset()
+        if self.single:
+            dev = self.net.device
+            pin = dev.type == "cuda"
+            self._h_stack = torch.empty((1, 4, 84, 84), dtype=torch.uint8, pin_memory=pin)
+            self._h_rd = torch.zeros(2, dtype=torch.float32, pin_memory=pin)
+            self._d_stack = torch.empty((1, 4, 84, 84), dtype=torch.uint8, device=dev)
+            self._d_rd = torch.zeros(2, dtype=torch.float32, device=dev)
+            self._d_done = torch.zeros(2, dtype=torch.uint8, device=dev)   # [0] = 0, [1] = 1
+            self._d_done[1] = 1
 
     def sync_parameters(self):
         """a3c.py:63-65 -- a no-op: actors read the device parameters."""
@@ -159,10 +216,10 @@ class A3C:
         stops before the conv backward (finish_window runs that part)."""
         net = self.net
         if self._overlap_allreduce():
-            net.learn_parts(range(LEARN_CONV), self.gamma, self.beta, self.v_loss_coef, self.clip_reward,
+            net.learn_parts(range(LEARN_CONV), self.gamma, self.beta, self._vcoef, self.clip_reward,
                             stream=stream)
         else:
-            net.learn(self.gamma, self.beta, self.v_loss_coef, self.clip_reward, stream=stream)
+            net.learn(self.gamma, self.beta, self._vcoef, self.clip_reward, stream=stream)
 
     def _reduce_and_step(self, stream=None, conv=None):
         net = self.net
@@ -174,7 +231,7 @@ class A3C:
                 if conv is not None:
                     conv()                      # e.g. a captured graph of the conv part
                 else:
-                    net.learn_parts([LEARN_CONV], self.gamma, self.beta, self.v_loss_coef, self.clip_reward,
+                    net.learn_parts([LEARN_CONV], self.gamma, self.beta, self._vcoef, self.clip_reward,
                                     stream=main)
                 if work is not None:
                     work.wait()
@@ -187,13 +244,83 @@ class A3C:
         self._learn(stream)
         self._reduce_and_step(stream)
 
-    def act(self, pairs: torch.Tensor, reward=None, is_state_terminal=None) -> torch.Tensor:
-        """a3c.py:67-167, batched.  pairs: (n, 2, 210, 160, 3) uint8 device
-        tensor (frame 4, frame 3 of the skip) -- for the Doom models the
-        screens (n, H, W, 3) uint8 instead; reward: (n,) f32 (clipped to
-        [-1, 1] as at a3c.py:69-70); is_state_terminal: (n,) uint8/bool, the
-        transition into this observation ended the episode.  Returns the
-        sampled actions (n,) int32 (device)."""
+    # ------------------------------------------------------------ reference-contract act
+    def act(self, state, reward=None, is_state_terminal=None):
+        """a3c.py:67-167.  One-env model: state = ALE.state (or what `phi`
+        maps to dqn_phi's image of it), reward, is_state_terminal -> the
+        sampled action (int), or None for a terminal state.  n-env models:
+        act_batch."""
+        if not self.single:
+            return self.act_batch(state, reward, is_state_terminal)
+        net, T = self.net, self.t_max
+        terminal = bool(is_state_terminal)
+        r = 0.0 if reward is None else float(np.clip(reward, -1, 1) if self.clip_reward else reward)
+        if self._copied is not None:
+            self._copied.synchronize()                  # the pinned buffers' last upload has landed
+        self._h_rd[0] = r
+        if not terminal:
+            self._h_stack[0].numpy()[...] = self._screens(state)
+            self._d_stack.copy_(self._h_stack, non_blocking=True)
+        self._d_rd.copy_(self._h_rd, non_blocking=True)
+        if net.device.type == "cuda":
+            self._copied = torch.cuda.Event()
+            self._copied.record()
+        rew = self._d_rd[:1]
+        L = self.t - self.t_start
+        update = (terminal and self.t_start < self.t) or L == T          # a3c.py:77-78
+        if update:
+            if terminal:                                # R = 0 over the L steps since the last update
+                net.observe_stack(L, None, rew, self._d_done[1:])
+                net.truncate_window(L)
+            else:                                       # bootstrap v(s) at the pre-update params (a3c.py:85)
+                net.observe_stack(T, self._d_stack, rew, self._d_done[:1])
+                net.act(T, mode=0)
+            self._update()                              # a3c.py:88-144; the window advances (slot T -> 0)
+            self.t_start = self.t                       # a3c.py:152
+        if terminal:                                    # a3c.py:165-167
+            self._episode_start = True
+            return None
+        slot = 0 if update else L
+        if not update:
+            net.observe_stack(slot, self._d_stack, rew, self._d_done[:1], force_reset=self._episode_start)
+        self._episode_start = False
+        net.act(slot, mode=1)                           # a3c.py:154-164, post-update params
+        self.t += 1
+        return int(net.step_outputs(slot)["actions"][0].item())
+
+    def _screens(self, state) -> np.ndarray:
+        """The (4, 84, 84) uint8 screens behind phi(state): the conv kernels
+        read uint8 planes and apply dqn_phi's /255 themselves (bit-exact).
+        phi=None or dqn_phi: `state` is the list of 4 screens (dqn_phi.py:12-13
+        asserts); another phi must return uint8 screens, or float32 values
+        that are exactly dqn_phi's image of uint8 screens."""
+        phi = self.phi
+        if phi is None or getattr(phi, "__name__", "") == "dqn_phi":
+            x = np.asarray(state)
+            if x.shape != (4, 84, 84) or x.dtype != np.uint8:
+                raise ValueError("A3C.act: state must be 4 uint8 84x84 screens (dqn_phi.py:12-13)")
+            return x
+        x = phi(state)
+        x = x.detach().cpu().numpy() if torch.is_tensor(x) else np.asarray(x)
+        x = x.reshape(x.shape[-3:]) if x.ndim == 4 and x.shape[0] == 1 else x
+        if x.shape != (4, 84, 84):
+            raise ValueError(f"A3C.act: phi(state) has shape {x.shape}, need (4, 84, 84)")
+        if x.dtype == np.uint8:
+            return x
+        u = np.clip(np.rint(np.asarray(x, np.float64) * 255.0), 0, 255).astype(np.uint8)
+        if x.dtype != np.float32 or not np.array_equal(_PHI_LUT[u], x):
+            raise ValueError("A3C.act: phi(state) is not dqn_phi's image of uint8 screens; the device "
+                             "learner reads observations as uint8 planes")
+        return u
+
+    def act_batch(self, pairs: torch.Tensor, reward=None, is_state_terminal=None) -> torch.Tensor:
+        """a3c.py:67-167, lockstep-batched.  pairs: (n, 2, 210, 160, 3) uint8
+        device tensor (frame 4, frame 3 of the skip) -- for the Doom models
+        the screens (n, H, W, 3), for frames="stacks" models the (n, 4, 84,
+        84) stacks; reward: (n,) f32 (clipped to [-1, 1] as at a3c.py:69-70);
+        is_state_terminal: (n,) uint8/bool, the transition into this
+        observation ended the episode.  Returns the sampled actions (n,)
+        int32 (a device copy)."""
         net, T = self.net, self.t_max
         r = None if reward is None else torch.as_tensor(reward, dtype=torch.float32, device=net.device).contiguous()
         d = None if is_state_terminal is None else \
@@ -214,7 +341,7 @@ class A3C:
             net.observe(ta, pairs, r, d, 1, resize_mode=self.resize_mode)
             net.act(ta)
         self.t += 1
-        return net.step_outputs(ta)["actions"]
+        return net.step_outputs(ta)["actions"].clone()
 
     def run_window(self, pair_pool, reward_pool, done_pool, pool_len: int, first: bool = False, stream=None,
                    split_update: bool = False, env_groups: int | None = None):

@@ -15,9 +15,9 @@ import os
 import numpy as np
 import torch
 
-from ._lib import (ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, ENV_GROUP_ALIGN, LEARN_CONV, LEARN_FC_REDUCE,
-                   LEARN_GATES_REDUCE, LEARN_HEADS_DW, LEARN_RETURNS, LEARN_TRUNK, RESIZE_SCALAR, check, lib, ptr,
-                   stream_handle)
+from ._lib import (ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, ARCH_STACK, ENV_GROUP_ALIGN, FWD_KEEP_STATE,
+                   LEARN_CONV, LEARN_FC_REDUCE, LEARN_GATES_REDUCE, LEARN_HEADS_DW, LEARN_RETURNS, LEARN_TRUNK,
+                   RESIZE_SCALAR, check, lib, ptr, stream_handle)
 
 
 def param_shapes(arch: int, n_actions: int):
@@ -26,7 +26,7 @@ def param_shapes(arch: int, n_actions: int):
     Nature head dqn_head.py:16-20 with 512-wide policy / value heads; the
     RGB flag: NIPSDQNHead(n_input_channels=3), train_a3c_doom.py:28,46)."""
     c_in = 3 if arch & ARCH_RGB else 4
-    arch &= ~ARCH_RGB
+    arch &= ~(ARCH_RGB | ARCH_STACK)
     if arch == ARCH_FF_NATURE:
         return [("0/0/W", (32, 4, 8, 8)), ("0/0/b", (32,)), ("0/1/W", (64, 32, 4, 4)), ("0/1/b", (64,)),
                 ("0/2/W", (64, 64, 3, 3)), ("0/2/b", (64,)), ("0/3/W", (512, 3136)), ("0/3/b", (512,)),
@@ -68,6 +68,8 @@ class DeviceNet:
         self.device = torch.device(device if device is not None else "cuda")
         self.arch, self.n_actions, self.n_envs, self.t_max = arch, n_actions, n_envs, t_max
         self.rgb = bool(arch & ARCH_RGB)
+        self.stack = bool(arch & ARCH_STACK)
+        self.base_arch = arch & ~(ARCH_RGB | ARCH_STACK)
         self.env_offset, self.seed = env_offset, seed
         h = ctypes.c_void_p()
         check(lib.arl_net_create(ctypes.byref(h), arch, n_actions, n_envs, t_max, env_offset, seed),
@@ -139,6 +141,9 @@ class DeviceNet:
         """pair_pool: (pool_len, n, 2, 210, 160, 3) uint8 frame pairs; for an
         RGB net (arch | ARCH_RGB) the screens (pool_len, n, H, W, 3) instead.
         envs=(e0, ne): only envs [e0, e0 + ne) (arl_observe_envs)."""
+        if self.stack and envs is None:
+            self.observe_stack(t, pair_pool, reward_pool, done_pool, pool_len, force_reset, stream)
+            return
         if envs is not None:
             e0, ne = envs
             H, W = (pair_pool.shape[-3], pair_pool.shape[-2]) if self.rgb else (0, 0)
@@ -153,6 +158,26 @@ class DeviceNet:
             return
         check(lib.arl_observe(self._h, t, ptr(pair_pool), ptr(reward_pool), ptr(done_pool), pool_len,
                               int(force_reset), resize_mode, stream_handle(stream)), "arl_observe")
+
+    def observe_stack(self, t: int, stack_pool=None, reward_pool=None, done_pool=None, pool_len: int = 1,
+                      force_reset: bool = False, stream=None):
+        """ARCH_STACK nets: stack_pool (pool_len, n, 4, 84, 84) uint8 whole
+        frame stacks (arl_observe_stack); None ingests only the reward / done
+        of step t (a terminal observation)."""
+        check(lib.arl_observe_stack(self._h, t, ptr(stack_pool), ptr(reward_pool), ptr(done_pool), pool_len,
+                                    int(force_reset), stream_handle(stream)), "arl_observe_stack")
+
+    def truncate_window(self, t_len: int, stream=None):
+        """Window steps [t_len, t_max) get no loss in the next learn (arl_truncate_window)."""
+        check(lib.arl_truncate_window(self._h, t_len, stream_handle(stream)), "arl_truncate_window")
+
+    def set_loss(self, pi_loss_coef: float = 1.0, keep_loss_scale_same: bool = False):
+        check(lib.arl_net_set_loss(self._h, pi_loss_coef, int(keep_loss_scale_same)), "arl_net_set_loss")
+
+    def reset_state(self, e0: int = 0, n: int | None = None, stream=None):
+        """LSTM: the pi_and_v recurrent state of rows [e0, e0 + n) -> None (arl_reset_state)."""
+        n = self.n_envs - e0 if n is None else n
+        check(lib.arl_reset_state(self._h, e0, n, stream_handle(stream)), "arl_reset_state")
 
     def act(self, t: int, mode: int = 1, stream=None, envs=None):
         """mode: 0 forward only, 1 sampled action, 2 greedy (first argmax);
@@ -212,7 +237,7 @@ class DeviceNet:
         part(LEARN_HEADS_DW, side)
         part(LEARN_TRUNK, main)
         side.wait_stream(main)
-        if self.arch & ~ARCH_RGB == ARCH_LSTM:
+        if self.base_arch == ARCH_LSTM:
             part(LEARN_GATES_REDUCE, side)
         part(LEARN_FC_REDUCE, side)
         part(LEARN_CONV, main)
@@ -237,12 +262,15 @@ class DeviceNet:
     def advance(self, stream=None):
         check(lib.arl_advance(self._h, stream_handle(stream)), "arl_advance")
 
-    def forward_states(self, states: torch.Tensor, mode: int = 0, stream=None):
+    def forward_states(self, states: torch.Tensor, mode: int = 0, stream=None, keep_same_state: bool = False):
+        """pi_and_v on explicit f32 states into slot t_max (arl_forward_states);
+        LSTM: advances the pi_and_v state unless keep_same_state."""
         n = states.shape[0]
         c = 3 if self.rgb else 4
         if states.dtype != torch.float32 or tuple(states.shape[1:]) != (c, 84, 84):
             raise ValueError(f"forward_states: need (n, {c}, 84, 84) float32 states")
-        check(lib.arl_forward_states(self._h, ptr(states), n, mode, stream_handle(stream)), "arl_forward_states")
+        m = mode | (FWD_KEEP_STATE if keep_same_state else 0)
+        check(lib.arl_forward_states(self._h, ptr(states), n, m, stream_handle(stream)), "arl_forward_states")
 
     # ------------------------------------------------------------ outputs
     def step_outputs(self, t: int) -> dict:

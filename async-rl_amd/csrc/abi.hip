@@ -31,7 +31,7 @@ hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 extern "C" {
 
-int arl_abi_version(void) { return 1; }
+int arl_abi_version(void) { return ARL_ABI_VERSION; }
 const char* arl_last_error(void) { return g_err.c_str(); }
 
 int arl_current_screen(const uint8_t* cur, const uint8_t* prev, uint8_t* out, int64_t n, int mode, void* s) {
@@ -152,6 +152,7 @@ int arl_net_reset(arl_net* h, void* s) {
   if (e == hipSuccess && n.arch == arl::ARCH_LSTM) {
     e = hipMemsetAsync(n.ws + n.w_hbuf, 0, (size_t)(n.T + 2) * n.N * arl::HID * 4, S(s));
     if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_cbuf, 0, (size_t)(n.T + 2) * n.N * arl::HID * 4, S(s));
+    if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_eval_reset, 1, (size_t)n.N, S(s));
   }
   return hip_status(e, "net_reset");
 }
@@ -161,7 +162,8 @@ static int observe_common(arl_net* h, int t, const uint8_t* pool, const float* r
                           void* s, int e0 = 0, int ne = -1) {
   arl::Net& n = h->net;
   if (t < 0 || t > n.T) return fail(ARL_EINVAL, "observe: t out of [0, t_max]");
-  if (!pool || pool_len < 1) return fail(ARL_EINVAL, "observe: need the frame pool and pool_len >= 1");
+  if ((!pool && n.layout != arl::FRAMES_STACK) || pool_len < 1)
+    return fail(ARL_EINVAL, "observe: need the frame pool and pool_len >= 1");
   if (!aligned(pool, 16)) return fail(ARL_EINVAL, "observe: the frame pool must be 16-byte aligned");
   if (n.N > 65535) return fail(ARL_EINVAL, "observe: n_envs > 65535");
   arl::RingArgs a;
@@ -184,13 +186,17 @@ static int observe_common(arl_net* h, int t, const uint8_t* pool, const float* r
   a.W = W;
   a.e0 = e0;
   a.ne = ne;
-  return hip_status(n.rgb ? arl::launch_rgb_ring(a, S(s)) : arl::launch_phi_ring(a, S(s)), "observe");
+  return hip_status(n.layout == arl::FRAMES_RGB     ? arl::launch_rgb_ring(a, S(s))
+                    : n.layout == arl::FRAMES_STACK ? arl::launch_stack_ring(a, S(s))
+                                                    : arl::launch_phi_ring(a, S(s)),
+                    "observe");
 }
 
 int arl_observe(arl_net* h, int t, const uint8_t* pair_pool, const float* reward_pool, const uint8_t* done_pool,
                 int64_t pool_len, int force_reset, int mode, void* s) {
   NEED_BOUND(h);
   if (h->net.rgb) return fail(ARL_ESTATE, "observe: RGB net, use arl_observe_rgb");
+  if (h->net.stack) return fail(ARL_ESTATE, "observe: ARL_ARCH_STACK net, use arl_observe_stack");
   if (mode < 0 || mode > (ARL_RESIZE_SIMD | ARL_RESIZE_CROP)) return fail(ARL_EINVAL, "bad resize_mode");
   return observe_common(h, t, pair_pool, reward_pool, done_pool, pool_len, force_reset, mode, 0, 0, s);
 }
@@ -202,6 +208,32 @@ int arl_observe_rgb(arl_net* h, int t, const uint8_t* img_pool, int H, int W, co
   if (mode < 0 || mode > ARL_RESIZE_SIMD) return fail(ARL_EINVAL, "observe_rgb: resize_mode must be 0 or 1");
   if (int rc = check_rgb_dims(H, W)) return rc;
   return observe_common(h, t, img_pool, reward_pool, done_pool, pool_len, force_reset, mode, H, W, s);
+}
+
+int arl_observe_stack(arl_net* h, int t, const uint8_t* stack_pool, const float* reward_pool,
+                      const uint8_t* done_pool, int64_t pool_len, int force_reset, void* s) {
+  NEED_BOUND(h);
+  if (!h->net.stack) return fail(ARL_ESTATE, "observe_stack: net was not created with ARL_ARCH_STACK");
+  if (!stack_pool && t < 1) return fail(ARL_EINVAL, "observe_stack: a frameless observation needs t >= 1");
+  return observe_common(h, t, stack_pool, reward_pool, done_pool, pool_len, force_reset, 0, 0, 0, s);
+}
+
+int arl_truncate_window(arl_net* h, int t_len, void* s) {
+  NEED_BOUND(h);
+  arl::Net& n = h->net;
+  if (t_len < 1 || t_len > n.T) return fail(ARL_EINVAL, "truncate_window: t_len out of [1, t_max]");
+  if (t_len == n.T) return ARL_OK;
+  const size_t rows = (size_t)(n.T - t_len) * n.N;
+  hipError_t e = hipMemsetAsync(n.ws + n.w_dones + (size_t)t_len * n.N, 2, rows, S(s));
+  if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_rewards + (size_t)t_len * n.N * 4, 0, rows * 4, S(s));
+  return hip_status(e, "truncate_window");
+}
+
+int arl_net_set_loss(arl_net* h, double pi_loss_coef, int keep_loss_scale_same) {
+  if (!h) return fail(ARL_EINVAL, "null net");
+  h->net.pi_coef = (float)pi_loss_coef;
+  h->net.keep_scale = keep_loss_scale_same ? 1 : 0;
+  return ARL_OK;
 }
 
 int arl_act(arl_net* h, int t, void* s) {
@@ -232,6 +264,8 @@ int arl_observe_envs(arl_net* h, int t, int e0, int ne, const uint8_t* pool, int
   if (h->net.rgb) {
     if (mode < 0 || mode > ARL_RESIZE_SIMD) return fail(ARL_EINVAL, "observe_rgb: resize_mode must be 0 or 1");
     if (int rc = check_rgb_dims(H, W)) return rc;
+  } else if (h->net.stack) {
+    H = W = mode = 0;
   } else {
     if (mode < 0 || mode > (ARL_RESIZE_SIMD | ARL_RESIZE_CROP)) return fail(ARL_EINVAL, "bad resize_mode");
     H = W = 0;
@@ -290,10 +324,19 @@ int arl_advance(arl_net* h, void* s) {
 
 int arl_forward_states(arl_net* h, const float* x, int64_t n, int mode, void* s) {
   NEED_BOUND(h);
-  if (mode < 0 || mode > 2) return fail(ARL_EINVAL, "forward_states: mode must be 0, 1 or 2");
-  if (h->net.arch == arl::ARCH_LSTM) return fail(ARL_ESTATE, "forward_states: FF only (LSTM keeps state)");
+  const bool keep = (mode & ARL_FWD_KEEP_STATE) != 0;
+  mode &= ~ARL_FWD_KEEP_STATE;
+  if (mode < 0 || mode > 2) return fail(ARL_EINVAL, "forward_states: mode must be 0, 1 or 2 (| ARL_FWD_KEEP_STATE)");
   if (!x || n < 1 || n > h->net.N) return fail(ARL_EINVAL, "forward_states: need 1 <= n <= n_envs");
-  return hip_status(arl::net_forward_f32(h->net, x, (int)n, mode, S(s)), "forward_states");
+  if (!aligned(x, 16)) return fail(ARL_EINVAL, "forward_states: states must be 16-byte aligned");
+  return hip_status(arl::net_forward_f32(h->net, x, (int)n, mode, S(s), keep), "forward_states");
+}
+
+int arl_reset_state(arl_net* h, int64_t e0, int64_t n, void* s) {
+  NEED_BOUND(h);
+  if (e0 < 0 || n < 0 || e0 + n > h->net.N) return fail(ARL_EINVAL, "reset_state: rows outside [0, n_envs)");
+  if (n == 0) return ARL_OK;
+  return hip_status(arl::net_reset_state(h->net, (int)e0, (int)n, S(s)), "reset_state");
 }
 
 int arl_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, double alpha, double eps, double clip,
@@ -328,12 +371,14 @@ int arl_policy(const float* hh, int64_t n, const float* Wpi, const float* bpi, c
 
 int arl_returns_lossgrad(const float* rewards, const uint8_t* dones, const float* v, const float* probs,
                          const float* logp, const int32_t* act, int T, int64_t n, int A, double gamma, double beta,
-                         double vcoef, int clip_reward, float* dlogits, float* dv, float* loss, void* s) {
+                         double pi_loss_coef, double vcoef, int keep_loss_scale_same, int clip_reward, float* dlogits,
+                         float* dv, float* loss, void* s) {
   if (T < 1 || n < 0 || A < 1) return fail(ARL_EINVAL, "returns: bad T / n / A");
   if (n > 0 && (!rewards || !dones || !v || !probs || !logp || !act || !dlogits || !dv))
     return fail(ARL_EINVAL, "returns: null pointer");
   return hip_status(arl::launch_returns(rewards, dones, v, probs, logp, act, T, (int)n, A, gamma, (float)beta,
-                                        (float)vcoef, clip_reward, dlogits, dv, loss, S(s)),
+                                        (float)vcoef, clip_reward, dlogits, dv, loss, S(s), nullptr,
+                                        (float)pi_loss_coef, keep_loss_scale_same ? 1 : 0),
                     "returns");
 }
 

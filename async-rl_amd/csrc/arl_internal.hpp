@@ -12,12 +12,21 @@ namespace arl {
 // replays with advancing step counters (no frozen kernel arguments)
 // CTL_STEP_SNAP: the step counter as the learner saw it (written at learn start),
 // read by the fused optimizer for the lr anneal so it can advance CTL_STEP itself
-enum { CTL_STEP = 0, CTL_WINDOW = 1, CTL_STEP_SNAP = 2, CTL_SIZE = 16 };
+// CTL_ZERO: never written (0 after arl_net_reset); the step base of draws keyed by a host counter
+enum { CTL_STEP = 0, CTL_WINDOW = 1, CTL_STEP_SNAP = 2, CTL_ZERO = 15, CTL_SIZE = 16 };
 
 enum Arch { ARCH_FF = 0, ARCH_LSTM = 1, ARCH_FF_NATURE = 2 };
 // arch flag: RGB (Doom) observations, train_a3c_doom.py:25-63 (NIPSDQNHead(n_input_channels=3)
 // on one RGB screen); conv1 sees [0, R, G, B] so the fused kernels keep K = 256
 constexpr int ARCH_RGB = 16;
+// arch flag: observations are whole 4-screen stacks (ale.py:91-94 ALE.state), one per ring slot
+// (frames (R, n, 4, 84, 84)) -- the layout of the reference-semantics A3C.act drop-in
+constexpr int ARCH_STACK = 32;
+// frame layout of the ring, as the conv kernels read it (conv input plane c of window step t):
+//   FRAMES_RING  one screen per slot, plane c = slot (k - 3 + c) % R   (k = ctl[STEP] + t)
+//   FRAMES_RGB   three planes per slot [0, R, G, B] of slot k % R
+//   FRAMES_STACK four planes per slot, plane c of slot k % R
+enum FrameLayout { FRAMES_RING = 0, FRAMES_RGB = 1, FRAMES_STACK = 2 };
 
 constexpr int PLANE = 84 * 84;         // 7056 B per screen
 constexpr int PAIR = 2 * 210 * 160 * 3; // 201,600 B per frame pair
@@ -54,6 +63,7 @@ struct RingArgs {
 constexpr int RGB_MAX_W = 2048;   // staged source rows: 12 x W x 3 bytes of LDS
 hipError_t launch_rgb_phi(const uint8_t* imgs, int64_t n, int H, int W, float* out, int mode, hipStream_t s);
 hipError_t launch_rgb_ring(const RingArgs& a, hipStream_t s);
+hipError_t launch_stack_ring(const RingArgs& a, hipStream_t s);   // ARCH_STACK nets
 
 hipError_t launch_current_screen(const uint8_t* cur, const uint8_t* prev, uint8_t* out, int64_t n,
                                  int mode, hipStream_t s);
@@ -74,6 +84,12 @@ struct ParamInfo {
 struct Net {
   int arch, A, N, T, R;
   bool rgb = false;        // ARCH_RGB: 3 planes per obs step in the ring, conv1 W (16, 3, 8, 8)
+  bool stack = false;      // ARCH_STACK: 4 planes (a whole stack) per obs step in the ring
+  int layout = FRAMES_RING;
+  // loss options (a3c.py:110-121): pi_loss_coef, keep_loss_scale_same (arl_net_set_loss)
+  float pi_coef = 1.f;
+  int keep_scale = 0;
+  int64_t eval_draws = 0;  // sampling forward_states calls so far (Philox stream 1 counter)
   int hid;                 // width of the layer the heads read (256 NIPS / LSTM, 512 Nature)
   int env_offset;          // global id of env 0 on this rank (RNG stream)
   uint64_t seed;
@@ -90,6 +106,9 @@ struct Net {
       w_cbuf, w_logits, w_probs, w_logp, w_v, w_ent, w_logpa, w_act, w_dlogits, w_dv, w_dh, w_dfc,
       w_dG, w_dhn, w_dcn, w_da2, w_slab, w_norm, w_loss, w_tick;
   int64_t w_a3 = 0, w_da1 = 0, w_da3 = 0;   // Nature head only
+  // LSTM recurrent state of pi_and_v on explicit states (A3CLSTM.pi_and_v, a3c_ale.py:55-63):
+  // h, c (n, 256), the step's outputs hn, cn, and reset flags (1 = state is None)
+  int64_t w_eval_h = 0, w_eval_c = 0, w_eval_hn = 0, w_eval_cn = 0, w_eval_reset = 0;
   // per-job weight-gradient slabs (heads, FC, LSTM gates) of the NIPS learner;
   // the conv slab is `slab`
   int64_t w_slab_heads = 0, w_slab_fc = 0, w_slab_lstm = 0;
@@ -120,7 +139,9 @@ hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_tot
 hipError_t net_advance(Net& net, hipStream_t s);
 enum Stage { STAGE_CONV_FWD = 1, STAGE_FC_FWD = 2, STAGE_POLICY = 3, STAGE_FC_BWD = 4, STAGE_CONV_BWD = 5 };
 hipError_t net_stage(Net& net, int stage, int t, hipStream_t s);
-hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_t s);
+// keep: LSTM keep_same_state (the pi_and_v recurrent state is not advanced)
+hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_t s, bool keep = false);
+hipError_t net_reset_state(Net& net, int e0, int n, hipStream_t s);
 
 // Nature head (nature.hip)
 int64_t nature_slab_floats(const Net& net);
@@ -133,12 +154,13 @@ hipError_t nature_stage(Net& net, int stage, int t, hipStream_t s);
 hipError_t launch_heads_bwd(const float* dl, const float* dv, const float* Wpi, const float* Wv, int A, int H,
                             const float* mask, float* out, int64_t S, hipStream_t s);
 
+// layout: FrameLayout of the ring (FRAMES_RGB: conv1 W (16, 3, 8, 8) on input planes 1..3)
 hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int t,
                            const float* W1, const float* b1, const float* W2, const float* b2, float* a1, float* a2,
-                           hipStream_t s, bool rgb = false, int e0 = 0, int ne = -1);
+                           hipStream_t s, int layout = FRAMES_RING, int e0 = 0, int ne = -1);
 hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int S,
                            const float* a1, const float* da2, const float* W2, float* slab, float* gW2, float* gb2,
-                           float* gW1, float* gb1, hipStream_t s, bool reduce = true, bool rgb = false);
+                           float* gW1, float* gb1, hipStream_t s, bool reduce = true, int layout = FRAMES_RING);
 int64_t conv_bwd_slab_floats(int S);
 int conv_bwd_blocks(int S);       // workgroups (= slab slices) of launch_conv_bwd
 
@@ -150,6 +172,7 @@ struct PolicyArgs {
   const int64_t* ctl;       // step counter (Philox counter = ctl[STEP] + step_off)
   int64_t step_off;
   int env_offset, mode;     // mode: 0 none, 1 sample, 2 greedy
+  uint32_t stream;          // Philox counter word 3: 0 = window draws, 1 = pi_and_v draws
   float *logits, *probs, *logp, *v, *ent;
   int32_t* act;
   float* logp_a;
@@ -158,7 +181,7 @@ inline PolicyArgs make_policy_args(const float* Wpi, const float* bpi, const flo
                                    uint64_t seed, const int64_t* ctl, int64_t step_off, int env_offset, int mode,
                                    float* logits, float* probs, float* logp, float* v, float* ent, int32_t* act,
                                    float* logp_a) {
-  return PolicyArgs{Wpi, bpi, Wv, bv, A, (uint32_t)seed, (uint32_t)(seed >> 32), ctl, step_off, env_offset, mode,
+  return PolicyArgs{Wpi, bpi, Wv, bv, A, (uint32_t)seed, (uint32_t)(seed >> 32), ctl, step_off, env_offset, mode, 0u,
                     logits, probs, logp, v, ent, act, logp_a};
 }
 
@@ -167,6 +190,9 @@ int fc_fwd_tiles(int n);      // tickets needed for n envs
 hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b, float* slab, int* tickets,
                          float* hfc, hipStream_t s);
 hipError_t launch_policy_args(const float* h, int64_t n, const PolicyArgs& pa, hipStream_t s, int hid);
+// policy arguments of a forward on explicit states (arl_forward_states): slot
+// T, a sampled action from Philox stream 1 keyed by a per-call host counter
+PolicyArgs states_policy_args(Net& net, int mode);
 // FC split-K reduce (partials of launch_fc_fwd with tickets == nullptr) + bias
 // + relu -> hfc, then the policy / value heads on the same 16 rows
 hipError_t launch_policy_fc(const float* slab, int n, const float* fc_bias, float* hfc, const PolicyArgs& pa,
@@ -192,9 +218,12 @@ hipError_t launch_policy(const float* h, int64_t n, const float* Wpi, const floa
                          const float* bv, int A, uint64_t seed, const int64_t* ctl, int64_t step_off,
                          int env_offset, int mode, float* logits, float* probs, float* logp, float* v,
                          float* ent, int32_t* act, float* logp_a, hipStream_t s, int hid = HID);
+// dones: bit 0 = the transition t -> t+1 ended the episode; bit 1 = step t lies
+// past the end of this window (arl_truncate_window: no loss, no gradient).
+// pcoef = pi_loss_coef; keep_scale: keep_loss_scale_same (a3c.py:110-121)
 hipError_t launch_returns(const float* rewards, const uint8_t* dones, const float* v, const float* probs,
                           const float* logp, const int32_t* act, int T, int n, int A, double gamma, float beta,
                           float vcoef, int clip_reward, float* dlogits, float* dv, float* loss, hipStream_t s,
-                          int64_t* ctl_snap = nullptr);
+                          int64_t* ctl_snap = nullptr, float pcoef = 1.f, int keep_scale = 0);
 
 }  // namespace arl

@@ -79,7 +79,8 @@ struct ConvBwdArgs {
   const float* W2;     // (32, 16, 4, 4)
   int S, spb;
   float* slab;         // (G, SLAB)
-  int rgb;             // frames (R, n, 3, 84, 84), input planes [0, R, G, B]
+  int layout;          // FrameLayout (FRAMES_RGB: (R, n, 3, 84, 84), planes [0, R, G, B];
+                       // FRAMES_STACK: (R, n, 4, 84, 84))
 };
 
 struct Prefetch {
@@ -106,7 +107,9 @@ __device__ inline void prefetch_sample(const ConvBwdArgs& a, int s, Prefetch& r)
     if (i < XQ) {
       const int c = i / 504, rem = i - c * 504, y = rem / 6, q = rem - y * 6;
       if (c >= 4 - nv) {
-        const int64_t pl = a.rgb ? ((int64_t)rs * a.n + e) * 3 + (c - 1) : (int64_t)slot[c] * a.n + e;
+        const int64_t pl = a.layout == FRAMES_STACK ? ((int64_t)rs * a.n + e) * 4 + c
+                           : a.layout == FRAMES_RGB ? ((int64_t)rs * a.n + e) * 3 + (c - 1)
+                                                    : (int64_t)slot[c] * a.n + e;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(a.frames + pl * PLANE + y * 84) + 4 * q;
         if (q < 5) { v.x = src[0]; v.y = src[1]; v.z = src[2]; v.w = src[3]; }
         else v.x = src[0];
@@ -408,17 +411,17 @@ int64_t conv_bwd_slab_floats(int S) { return (int64_t)conv_bwd_blocks(S) * SLAB;
 
 hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int S,
                            const float* a1, const float* da2, const float* W2, float* slab, float* gW2, float* gb2,
-                           float* gW1, float* gb1, hipStream_t s, bool reduce, bool rgb) {
+                           float* gW1, float* gb1, hipStream_t s, bool reduce, int layout) {
   if (S <= 0) return hipSuccess;
   const int G0 = conv_bwd_blocks(S);
   const int spb = (S + G0 - 1) / G0;
   const int G = (S + spb - 1) / spb;
-  ConvBwdArgs a{frames, nvalid, ctl, n, R, a1, da2, W2, S, spb, slab, rgb ? 1 : 0};
+  ConvBwdArgs a{frames, nvalid, ctl, n, R, a1, da2, W2, S, spb, slab, layout};
   hipLaunchKernelGGL(conv_bwd_kernel, dim3(G), dim3(NT), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !reduce) return e;
   hipLaunchKernelGGL(reduce_conv_bwd_kernel, dim3((SLAB + 15) / 16), dim3(256), 0, s, slab, G, gW2, gb2, gW1, gb1,
-                     rgb ? 1 : 0);
+                     layout == FRAMES_RGB ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -66,7 +66,8 @@ struct ConvFwdArgs {
   const float* b2;
   float* a1;            // (n, 16, 400)
   float* a2;            // (n, 32, 81)
-  int rgb;              // frames (R, n, 3, 84, 84): planes [0, R, G, B] of slot ks % R
+  int layout;           // FrameLayout: FRAMES_RGB = (R, n, 3, 84, 84), planes [0, R, G, B] of slot ks % R;
+                        // FRAMES_STACK = (R, n, 4, 84, 84), the 4 planes of slot ks % R
   int e0;               // first env of this launch (env = e0 + blockIdx.x)
 };
 
@@ -95,15 +96,18 @@ conv_fwd_kernel(ConvFwdArgs a) {
       xv[j] = make_uint4(0, 0, 0, 0);
       if (!(ARL_ABLATE & 4) && i < 4 * V && c >= 4 - nv)   // planes older than the last reset read as 0
         xv[j] = reinterpret_cast<const uint4*>(
-            a.frames + (a.rgb ? ((int64_t)rs * a.n + e) * 3 + (c - 1) : (int64_t)slot[c] * a.n + e) * PLANE)[o];
+            a.frames + (a.layout == FRAMES_STACK ? ((int64_t)rs * a.n + e) * 4 + c
+                        : a.layout == FRAMES_RGB ? ((int64_t)rs * a.n + e) * 3 + (c - 1)
+                                                 : (int64_t)slot[c] * a.n + e) * PLANE)[o];
     }
     // W1: thread -> 8 consecutive k of one oc; W2: thread -> (oc, 4 ic, 4 taps)
     const int w1oc = tid >> 5, w1k = (8 * tid) & 255;
     const int w2oc = tid >> 4, ic4 = (tid >> 2) & 3, tg = tid & 3;
 #if !(ARL_ABLATE & 8)
     float4 w1a = make_float4(0.f, 0.f, 0.f, 0.f), w1b = w1a;   // RGB: input plane 0 is the zero pad
-    if (!a.rgb || w1k >= 64) {
-      const float4* w1p = reinterpret_cast<const float4*>(a.rgb ? a.W1 + w1oc * 192 + w1k - 64 : a.W1 + 8 * tid);
+    const bool rgb = a.layout == FRAMES_RGB;
+    if (!rgb || w1k >= 64) {
+      const float4* w1p = reinterpret_cast<const float4*>(rgb ? a.W1 + w1oc * 192 + w1k - 64 : a.W1 + 8 * tid);
       w1a = w1p[0];
       w1b = w1p[1];
     }
@@ -267,11 +271,11 @@ conv_fwd_kernel(ConvFwdArgs a) {
 
 hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int t,
                            const float* W1, const float* b1, const float* W2, const float* b2, float* a1, float* a2,
-                           hipStream_t s, bool rgb, int e0, int ne) {
+                           hipStream_t s, int layout, int e0, int ne) {
   if (n <= 0) return hipSuccess;
   if (ne < 0) ne = n;
   if (ne <= 0) return hipSuccess;
-  ConvFwdArgs a{frames, nvalid, ctl, n, R, t, W1, b1, W2, b2, a1, a2, rgb ? 1 : 0, e0};
+  ConvFwdArgs a{frames, nvalid, ctl, n, R, t, W1, b1, W2, b2, a1, a2, layout, e0};
   hipLaunchKernelGGL(conv_fwd_kernel, dim3(ne), dim3(NT), 0, s, a);
   return hipGetLastError();
 }

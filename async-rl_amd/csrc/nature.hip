@@ -315,7 +315,7 @@ hipError_t nature_forward_f32(Net& net, const float* x, int n, int mode, hipStre
                                                  EpiConv{a1, P + net.o_c1b, NC1, NP1}, n * NP1, NC1, 256, 1, s)));
   ARL_TRY(conv23_fwd(net, n, a1, a2, a3, s));
   ARL_TRY(fc_fwd(net, n, a3, h, s));
-  return policy_at(net, T, n, mode, h, s);
+  return launch_policy_args(h, n, states_policy_args(net, mode), s, NHID);
 }
 
 hipError_t nature_learn(Net& net, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s) {
@@ -328,7 +328,7 @@ hipError_t nature_learn(Net& net, double gamma, float beta, float vcoef, int cli
   ARL_TRY(launch_returns(net.at<float>(net.w_rewards), net.at<uint8_t>(net.w_dones), net.at<float>(net.w_v),
                          net.at<float>(net.w_probs), net.at<float>(net.w_logp), net.at<int32_t>(net.w_act), T, n, A,
                          gamma, beta, vcoef, clip_reward, dl, dv, net.at<float>(net.w_loss), s,
-                         net.at<int64_t>(net.w_ctl)));
+                         net.at<int64_t>(net.w_ctl), net.pi_coef, net.keep_scale));
   const float* h = net.at<float>(net.w_hfc);
   // heads: weight grads (ones column = bias) and dfc = dh * (h > 0)
   ARL_TRY((launch_gemm<16, 64, 32, 1, 4, GS, GM>(HeadsGA{dl, dv, A}, OnesColB{h, NHID},

@@ -194,14 +194,18 @@ static int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_offset, uint64_t seed,
               std::string& err) {
   const bool rgb = (arch & ARCH_RGB) != 0;
-  arch &= ~ARCH_RGB;
-  if (rgb && arch == ARCH_FF_NATURE) {
-    err = "ARCH_RGB applies to the NIPS head (FF or LSTM) only (train_a3c_doom.py:25-63)";
+  const bool stk = (arch & ARCH_STACK) != 0;
+  arch &= ~(ARCH_RGB | ARCH_STACK);
+  if ((rgb || stk) && arch == ARCH_FF_NATURE) {
+    err = "ARCH_RGB / ARCH_STACK apply to the NIPS head (FF or LSTM) only";
     return false;
   }
+  if (rgb && stk) { err = "ARCH_RGB and ARCH_STACK are exclusive"; return false; }
   net.rgb = rgb;
+  net.stack = stk;
+  net.layout = rgb ? FRAMES_RGB : stk ? FRAMES_STACK : FRAMES_RING;
   if (arch != ARCH_FF && arch != ARCH_LSTM && arch != ARCH_FF_NATURE) {
-    err = "arch must be 0 (FF), 1 (LSTM) or 2 (FF, Nature head), optionally | 16 (RGB)";
+    err = "arch must be 0 (FF), 1 (LSTM) or 2 (FF, Nature head), optionally | 16 (RGB) or | 32 (STACK)";
     return false;
   }
   if (n_actions < 1 || n_actions > MAXA) { err = "n_actions must be in [1, 32]"; return false; }
@@ -279,7 +283,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   };
   const bool L = arch == ARCH_LSTM;
   net.w_ctl = buf("ctl", CTL_SIZE * 8);
-  net.w_frames = buf("frames", (int64_t)net.R * n * PLANE * (rgb ? 3 : 1));
+  net.w_frames = buf("frames", (int64_t)net.R * n * PLANE * (rgb ? 3 : stk ? 4 : 1));
   net.w_nvalid = buf("nvalid", (int64_t)net.R * n);
   net.w_reset = buf("reset", T1 * n);
   net.w_rewards = buf("rewards", S * 4);
@@ -318,6 +322,11 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   net.w_norm = buf("norm_partials", (int64_t)net.norm_blocks * 8);
   net.w_tick = buf("tickets", (int64_t)fc_fwd_tiles((int)n) * 4);
   net.w_loss = buf("loss", n * 2 * 4);
+  net.w_eval_h = buf("eval_h", L ? n * HID * 4 : 0);
+  net.w_eval_c = buf("eval_c", L ? n * HID * 4 : 0);
+  net.w_eval_hn = buf("eval_hn", L ? n * HID * 4 : 0);
+  net.w_eval_cn = buf("eval_cn", L ? n * HID * 4 : 0);
+  net.w_eval_reset = buf("eval_reset", L ? n : 0);
   net.ws_bytes = wo;
   return true;
 }
@@ -366,7 +375,7 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne) {
   if (!(part & ACT_AFTER_CONV))
     ARL_TRY(launch_conv_fwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
                             net.at<int64_t>(net.w_ctl), n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W,
-                            P + net.o_c2b, a1, a2, s, net.rgb, e0, ne));
+                            P + net.o_c2b, a1, a2, s, net.layout, e0, ne));
   if (part & ACT_CONV_ONLY) return hipSuccess;
   const int64_t o = (int64_t)t * n + e0;
   float* fc_slab = net.at<float>(net.w_slab) + (int64_t)FC_SPLIT * e0 * HID;
@@ -408,11 +417,28 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne) {
                        net.at<int32_t>(net.w_act) + o, net.at<float>(net.w_logpa) + o, s);
 }
 
-// Drop-in pi_and_v on explicit f32 states (dqn_phi output), FF only; results
-// land in activation slot T (the bootstrap slot) of the workspace.
-hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_t s) {
+// Policy arguments of a forward on explicit states (slot T): a sampled action
+// draws from Philox stream 1 with a host counter, one per call, so repeated
+// calls on the same state are independent draws and never collide with the
+// window's draws (stream 0, counter = step + t).
+PolicyArgs states_policy_args(Net& net, int mode) {
+  PolicyArgs pa = slot_policy_args(net, net.T, mode);
+  if (mode == 1) {
+    pa.ctl = net.at<int64_t>(net.w_ctl) + CTL_ZERO;
+    pa.step_off = net.eval_draws++;
+    pa.stream = 1u;
+  }
+  return pa;
+}
+
+// Drop-in pi_and_v on explicit f32 states (dqn_phi output); results land in
+// activation slot T (the bootstrap slot) of the workspace.  LSTM: the
+// recurrent state is the pi_and_v state (eval_h / eval_c, reset flags
+// eval_reset = "state is None"), separate from the lockstep window's; it
+// advances unless keep (keep_same_state, a3c_ale.py:57-60).
+hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_t s, bool keep) {
   if (net.arch == ARCH_FF_NATURE) return nature_forward_f32(net, x, n, mode, s);
-  if (net.arch != ARCH_FF || n > net.N) return hipErrorInvalidValue;
+  if (n > net.N) return hipErrorInvalidValue;
   const int T = net.T, N = net.N;
   float* a1 = net.at<float>(net.w_a1) + (int64_t)T * N * A1;
   float* a2 = net.at<float>(net.w_a2) + (int64_t)T * N * A2;
@@ -426,8 +452,35 @@ hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_
                                                       EpiConv{a2, P + net.o_c2b, C2_OC, C2_P}, n * C2_P, C2_OC, 256,
                                                       1, s)));
   ARL_TRY(fc_forward(net, n, a2, hfc, s));
-  const PolicyArgs pa = slot_policy_args(net, T, mode);
-  return launch_policy_args(hfc, n, pa, s, HID);
+  const float* hpol = hfc;
+  if (net.arch == ARCH_LSTM) {
+    float* gates = net.at<float>(net.w_gates) + (int64_t)T * N * GATES;
+    float* eh = net.at<float>(net.w_eval_h);
+    float* ec = net.at<float>(net.w_eval_c);
+    float* hn = net.at<float>(net.w_eval_hn);
+    float* cn = net.at<float>(net.w_eval_cn);
+    uint8_t* rs = net.at<uint8_t>(net.w_eval_reset);
+    ARL_TRY((launch_gemm<32, 64, 32, 2, 2, GK, GK>(LstmGateA{hfc, eh, rs}, LstmGateB{P + net.o_luW, P + net.o_llW},
+                                                   EpiBias{gates, P + net.o_lub, GATES}, n, GATES, 2 * HID, 1, s)));
+    const int64_t cnt = (int64_t)n * HID;
+    hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, gates, ec, rs, cn,
+                       hn, cnt);
+    ARL_TRY(hipGetLastError());
+    if (!keep) {
+      ARL_TRY(hipMemcpyAsync(eh, hn, cnt * 4, hipMemcpyDeviceToDevice, s));
+      ARL_TRY(hipMemcpyAsync(ec, cn, cnt * 4, hipMemcpyDeviceToDevice, s));
+      ARL_TRY(hipMemsetAsync(rs, 0, n, s));
+    }
+    hpol = hn;
+  }
+  const PolicyArgs pa = states_policy_args(net, mode);
+  return launch_policy_args(hpol, n, pa, s, HID);
+}
+
+// A3CLSTM.reset_state (a3c_ale.py:65-66) for the pi_and_v state of rows [e0, e0 + n)
+hipError_t net_reset_state(Net& net, int e0, int n, hipStream_t s) {
+  if (net.arch != ARCH_LSTM) return hipSuccess;
+  return hipMemsetAsync(net.at<uint8_t>(net.w_eval_reset) + e0, 1, n, s);
 }
 
 // ---------------------------------------------------------------- backward
@@ -462,7 +515,8 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
   if (part == LEARN_RETURNS)
     return launch_returns(net.at<float>(net.w_rewards), net.at<uint8_t>(net.w_dones), net.at<float>(net.w_v),
                           net.at<float>(net.w_probs), net.at<float>(net.w_logp), net.at<int32_t>(net.w_act), T, n, A,
-                          gamma, beta, vcoef, clip_reward, dl, dv, nullptr, s, net.at<int64_t>(net.w_ctl));
+                          gamma, beta, vcoef, clip_reward, dl, dv, net.at<float>(net.w_loss), s,
+                          net.at<int64_t>(net.w_ctl), net.pi_coef, net.keep_scale);
   // heads: weight grads (ones column = bias) and dh
   if (part == LEARN_HEADS_DW) {
     ARL_TRY((launch_gemm<16, 64, 32, 1, 4, GS, GM>(HeadsGA{dl, dv, A}, OnesColB{hheads, HID},
@@ -487,7 +541,7 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
     // straight from the frame ring
     return launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
                            net.at<int64_t>(net.w_ctl), n, net.R, S, a1, da2, P + net.o_c2W, slab, G + net.o_c2W,
-                           G + net.o_c2b, G + net.o_c1W, G + net.o_c1b, s, /*reduce=*/true, net.rgb);
+                           G + net.o_c2b, G + net.o_c1W, G + net.o_c1b, s, /*reduce=*/true, net.layout);
   if (part != LEARN_TRUNK) return hipErrorInvalidValue;
   ARL_TRY(launch_heads_bwd(dl, dv, P + net.o_piW, P + net.o_vW, A, HID, L ? nullptr : hfc,
                            L ? net.at<float>(net.w_dh) : dfc, S, s));
@@ -547,7 +601,7 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
       return launch_conv_fwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
                              net.at<int64_t>(net.w_ctl), n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W,
                              P + net.o_c2b, net.at<float>(net.w_a1) + (int64_t)t * n * A1, a2 + (int64_t)t * n * A2,
-                             s, net.rgb);
+                             s, net.layout);
     case STAGE_FC_FWD:   // as in net_act: FF runs the partials-only FC, its reduce is in the policy stage
       if (net.arch != ARCH_LSTM)
         return launch_fc_fwd(a2 + (int64_t)t * n * A2, n, P + net.o_fcW, P + net.o_fcb, slab, nullptr, nullptr, s);
@@ -576,7 +630,7 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
       return launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
                              net.at<int64_t>(net.w_ctl), n, net.R, S, net.at<float>(net.w_a1),
                              net.at<float>(net.w_da2), P + net.o_c2W, slab, G + net.o_c2W, G + net.o_c2b,
-                             G + net.o_c1W, G + net.o_c1b, s, /*reduce=*/false, net.rgb);
+                             G + net.o_c1W, G + net.o_c1b, s, /*reduce=*/false, net.layout);
     default:
       return hipErrorInvalidValue;
   }

@@ -332,6 +332,39 @@ rgb_ring_kernel(RingArgs a) {
   }
 }
 
+// In-loop ring for ARCH_STACK nets: the env's whole 4-screen stack of obs step
+// k (ale.py:91-94 ALE.state, oldest first) goes to slot k % R (frames (R, n,
+// 4, 84, 84)); nvalid = 4; the reward / done / reset bookkeeping of
+// phi_ring_kernel.  pair_pool == null: bookkeeping only (a terminal
+// observation, whose state a3c.py:72-73 never reads).  One workgroup per env,
+// 16-byte copies.
+__global__ void __launch_bounds__(256)
+stack_ring_kernel(RingArgs a) {
+  const int e = a.e0 + blockIdx.x;
+  const int64_t k = a.ctl[CTL_STEP] + a.t;
+  const int slot = (int)(k % a.R);
+  const int64_t pidx = k % a.pool_len;
+  if (a.pair_pool != nullptr) {
+    constexpr int V = 4 * PLANE / 16;   // 1764 uint4 per stack
+    const uint4* src = reinterpret_cast<const uint4*>(a.pair_pool + (pidx * a.n + e) * (int64_t)(4 * PLANE));
+    uint4* dst = reinterpret_cast<uint4*>(a.frames + ((int64_t)slot * a.n + e) * (4 * PLANE));
+    for (int i = threadIdx.x; i < V; i += 256) dst[i] = src[i];
+  }
+  if (threadIdx.x == 0) {
+    const uint8_t d = a.done_pool ? a.done_pool[pidx * a.n + e] : 0;
+    const bool rs = a.force_reset || d != 0;
+    if (a.pair_pool != nullptr) {
+      a.nvalid[(int64_t)slot * a.n + e] = 4;
+      a.reset_flags[(int64_t)a.t * a.n + e] = rs ? 1 : 0;
+    }
+    if (a.t >= 1) {
+      float r = a.reward_pool ? a.reward_pool[pidx * a.n + e] : 0.f;
+      a.rewards[(int64_t)(a.t - 1) * a.n + e] = r;
+      a.dones[(int64_t)(a.t - 1) * a.n + e] = d;
+    }
+  }
+}
+
 // dqn_phi.py:14-16: float32(x) / 255.0 (IEEE correctly rounded division).
 __global__ void dqn_phi_kernel(const uint8_t* __restrict__ in, float* __restrict__ out, int64_t count) {
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
@@ -388,6 +421,11 @@ hipError_t launch_phi_stack(const uint8_t* pairs, const uint8_t* prev_stack, con
 
 hipError_t launch_phi_ring(const RingArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(phi_ring_kernel, dim3(NBANDS, (unsigned)(a.ne < 0 ? a.n : a.ne)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_stack_ring(const RingArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(stack_ring_kernel, dim3((unsigned)(a.ne < 0 ? a.n : a.ne)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -114,19 +114,25 @@ hipError_t launch_policy(const float* h, int64_t n, const float* Wpi, const floa
 // rewards/dones (T, n); v/probs/logp/act indexed (T+1, n[, A]) with row T =
 // the bootstrap value v(s_T) computed with the pre-update parameters.
 // R accumulates in float64 (Python float at a3c.py:83-92) and restarts at 0
-// at every terminal, so each episode segment in the window is one a3c update.
-// Thread (t, e) runs the reverse recurrence R = R*gamma + r from T-1 down to
-// its own t -- the same operations in the same order as a sequential scan, so
-// R_t is bit-identical -- with every reward / done of its env loaded up front
-// (no dependent loads in the chain).  The per-env losses are then summed in
-// the reference's order (t = T-1 .. 0) through LDS.  ctl != null: also
-// snapshot the step counter (CTL_STEP_SNAP) for the optimizer's fused advance.
-// Block = EB envs x T steps (EB = 256 / T), env fastest.
+// at every terminal (dones bit 0), so each episode segment in the window is
+// one a3c update.  Thread (t, e) runs the reverse recurrence R = R*gamma + r
+// from T-1 down to its own t -- the same operations in the same order as a
+// sequential scan, so R_t is bit-identical -- with every reward / done of its
+// env loaded up front (no dependent loads in the chain).  Steps flagged past
+// the window's end (dones bit 1, arl_truncate_window: the reference's window
+// closed early at a terminal, a3c.py:77-78) get no loss and a zero gradient.
+// Loss scale (a3c.py:110-121): pi terms * pi_loss_coef, v terms * v_loss_coef,
+// and with keep_loss_scale_same both * t_max / len for a segment that a
+// terminal closed after len < t_max steps.  The per-env losses are then
+// summed in the reference's order (t = T-1 .. 0) through LDS.  ctl != null:
+// also snapshot the step counter (CTL_STEP_SNAP) for the optimizer's fused
+// advance.  Block = EB envs x T steps (EB = 256 / T), env fastest.
 __global__ void __launch_bounds__(256)
 returns_kernel(const float* __restrict__ rewards, const uint8_t* __restrict__ dones, const float* __restrict__ v,
                const float* __restrict__ probs, const float* __restrict__ logp, const int32_t* __restrict__ act, int T,
                int n, int A, double gamma, float beta, float vcoef, int clip_reward, float* __restrict__ dlogits,
-               float* __restrict__ dv, float* __restrict__ loss, int64_t* __restrict__ ctl) {
+               float* __restrict__ dv, float* __restrict__ loss, int64_t* __restrict__ ctl, float pcoef,
+               int keep_scale) {
   __shared__ float lpi[256], lv[256];
   if (ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) ctl[CTL_STEP_SNAP] = ctl[CTL_STEP];
   const int EB = 256 / T;
@@ -134,35 +140,61 @@ returns_kernel(const float* __restrict__ rewards, const uint8_t* __restrict__ do
   const int e = blockIdx.x * EB + el;
   const bool on = t < T && e < n;
   if (on) {
-    double R = (double)v[(int64_t)T * n + e];
-    for (int tt = T - 1; tt >= t; --tt) {
-      const int64_t i = (int64_t)tt * n + e;
-      double r = (double)rewards[i];
-      if (clip_reward) r = r < -1.0 ? -1.0 : (r > 1.0 ? 1.0 : r);
-      if (dones[i]) R = 0.0;
-      R = __dadd_rn(__dmul_rn(R, gamma), r);
-    }
     const int64_t i = (int64_t)t * n + e;
-    const float Rf = (float)R;
-    const float vi = v[i];
-    const float adv = __fsub_rn(Rf, vi);
-    const float* pr = probs + i * A;
-    const float* lp = logp + i * A;
-    float H = 0.f;
-    for (int k = 0; k < A; ++k) H = __fadd_rn(H, __fmul_rn(pr[k], lp[k]));
-    H = -H;
-    const int a = act[i];
     float* dl = dlogits + i * A;
-    for (int k = 0; k < A; ++k) {
-      const float oh = (k == a) ? 1.f : 0.f;
-      const float t1 = __fmul_rn(-adv, __fsub_rn(oh, pr[k]));
-      const float t2 = __fmul_rn(__fmul_rn(beta, pr[k]), __fadd_rn(lp[k], H));
-      dl[k] = __fadd_rn(t1, t2);
+    if (dones[i] & 2) {   // past the end of this window
+      for (int k = 0; k < A; ++k) dl[k] = 0.f;
+      dv[i] = 0.f;
+      lpi[tid] = 0.f;
+      lv[tid] = 0.f;
+    } else {
+      double R = (double)v[(int64_t)T * n + e];
+      int seg_end = -1;   // first terminal at or after t: closes t's segment
+      for (int tt = T - 1; tt >= t; --tt) {
+        const int64_t j = (int64_t)tt * n + e;
+        double r = (double)rewards[j];
+        if (clip_reward) r = r < -1.0 ? -1.0 : (r > 1.0 ? 1.0 : r);
+        if (dones[j] & 1) {
+          R = 0.0;
+          seg_end = tt;
+        }
+        R = __dadd_rn(__dmul_rn(R, gamma), r);
+      }
+      float pf = pcoef, vf = vcoef;
+      if (keep_scale && seg_end >= 0) {
+        int seg_start = 0;
+        for (int tt = t - 1; tt >= 0; --tt)
+          if (dones[(int64_t)tt * n + e] & 1) {
+            seg_start = tt + 1;
+            break;
+          }
+        const int len = seg_end - seg_start + 1;
+        if (len < T) {
+          const float factor = (float)((double)T / (double)len);
+          pf = __fmul_rn(pf, factor);
+          vf = __fmul_rn(vf, factor);
+        }
+      }
+      const float Rf = (float)R;
+      const float vi = v[i];
+      const float adv = __fsub_rn(Rf, vi);
+      const float* pr = probs + i * A;
+      const float* lp = logp + i * A;
+      float H = 0.f;
+      for (int k = 0; k < A; ++k) H = __fadd_rn(H, __fmul_rn(pr[k], lp[k]));
+      H = -H;
+      const int a = act[i];
+      for (int k = 0; k < A; ++k) {
+        const float oh = (k == a) ? 1.f : 0.f;
+        const float t1 = __fmul_rn(-adv, __fsub_rn(oh, pr[k]));
+        const float t2 = __fmul_rn(__fmul_rn(beta, pr[k]), __fadd_rn(lp[k], H));
+        dl[k] = __fmul_rn(pf, __fadd_rn(t1, t2));
+      }
+      const float dvv = __fsub_rn(vi, Rf);
+      dv[i] = __fmul_rn(vf, dvv);
+      lpi[tid] = __fmul_rn(pf, __fadd_rn(__fmul_rn(lp[a], adv), __fmul_rn(beta, H)));
+      lv[tid] = __fmul_rn(vf, __fmul_rn(__fmul_rn(dvv, dvv), 0.5f));
     }
-    const float dvv = __fsub_rn(vi, Rf);
-    dv[i] = __fmul_rn(vcoef, dvv);
-    lpi[tid] = __fadd_rn(__fmul_rn(lp[a], adv), __fmul_rn(beta, H));
-    lv[tid] = __fmul_rn(vcoef, __fmul_rn(__fmul_rn(dvv, dvv), 0.5f));
   }
   if (loss == nullptr) return;
   __syncthreads();
@@ -180,12 +212,12 @@ returns_kernel(const float* __restrict__ rewards, const uint8_t* __restrict__ do
 hipError_t launch_returns(const float* rewards, const uint8_t* dones, const float* v, const float* probs,
                           const float* logp, const int32_t* act, int T, int n, int A, double gamma, float beta,
                           float vcoef, int clip_reward, float* dlogits, float* dv, float* loss, hipStream_t s,
-                          int64_t* ctl_snap) {
+                          int64_t* ctl_snap, float pcoef, int keep_scale) {
   if (n <= 0) return hipSuccess;
   if (T < 1 || T > 256) return hipErrorInvalidValue;
   const int EB = 256 / T;
   hipLaunchKernelGGL(returns_kernel, dim3((n + EB - 1) / EB), dim3(256), 0, s, rewards, dones, v, probs, logp, act, T,
-                     n, A, gamma, beta, vcoef, clip_reward, dlogits, dv, loss, ctl_snap);
+                     n, A, gamma, beta, vcoef, clip_reward, dlogits, dv, loss, ctl_snap, pcoef, keep_scale);
   return hipGetLastError();
 }
 

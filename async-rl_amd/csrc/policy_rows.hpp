@@ -93,7 +93,7 @@ __device__ inline void policy_rows16(const float* __restrict__ h, int64_t row0, 
     if (mode == 1) {
       const int64_t step = pa.ctl[CTL_STEP] + pa.step_off;
       const uint4 r = philox4x32_10(make_uint4((uint32_t)(pa.env_offset + row), (uint32_t)step,
-                                               (uint32_t)((uint64_t)step >> 32), 0u), pa.seed_lo, pa.seed_hi);
+                                               (uint32_t)((uint64_t)step >> 32), pa.stream), pa.seed_lo, pa.seed_hi);
       u = (float)(r.x >> 8) * 5.9604644775390625e-08f;
     }
     float H = 0.f, cdf = 0.f, best = -1.f, la = 0.f;

@@ -227,7 +227,7 @@ def main():
     conv_bwd_flop = NAT_CONV_BWD_FLOP_PER_SAMPLE if nat else DOOM_CONV_BWD_FLOP_PER_SAMPLE if doom else \
         CONV_BWD_FLOP_PER_SAMPLE
     hid_bytes = 2 * HID_BYTES if nat else HID_BYTES
-    model = Model(A, n_envs=N, t_max=T, seed=1234, env_offset=rank * N, init_seed=0, device=dev)
+    model = Model(A, n_envs=N, t_max=T, seed=1234, env_offset=rank * N, init_seed=0, device=dev, frames="pairs")
     opt = RMSpropAsync(lr=7e-4, eps=1e-1, alpha=0.99).setup(model)
     opt.add_hook(GradientClipping(40))
     opt.anneal_total_steps = 8 * 10 ** 7        # a3c_ale.py:200 --steps default

@@ -21,6 +21,8 @@
 extern "C" {
 #endif
 
+#define ARL_ABI_VERSION 2
+
 #define ARL_OK 0
 #define ARL_EINVAL 1   /* bad argument (shape, pointer, alignment) */
 #define ARL_EHIP 2     /* HIP runtime error (launch failure) */
@@ -32,6 +34,9 @@ extern "C" {
 #define ARL_ARCH_RGB 16   /* flag for FF / LSTM: the ViZDoom models of train_a3c_doom.py:25-63
                              (NIPSDQNHead(n_input_channels=3) on one RGB screen, no frame stack);
                              observations come through arl_observe_rgb */
+#define ARL_ARCH_STACK 32 /* flag for FF / LSTM: observations are whole 4-screen stacks (ale.py:91-94
+                             ALE.state, as A3C.act receives them, a3c.py:67,72-73), one per ring
+                             slot; they come through arl_observe_stack */
 
 #define ARL_RESIZE_SCALAR 0  /* OpenCV FixedPtCast vertical pass (canonical) */
 #define ARL_RESIZE_SIMD 1    /* OpenCV VResizeLinearVec_32s8u (mulhi) pass */
@@ -116,6 +121,27 @@ int arl_observe(arl_net* net, int t, const uint8_t* pair_pool, const float* rewa
 int arl_observe_rgb(arl_net* net, int t, const uint8_t* img_pool, int H, int W, const float* reward_pool,
                     const uint8_t* done_pool, int64_t pool_len, int force_reset, int resize_mode, void* stream);
 
+/* arl_observe for an ARL_ARCH_STACK net: stack_pool (pool_len, n, 4, 84, 84)
+ * uint8 (ale.py:91-94 ALE.state: the 4 screens oldest first, zeros before
+ * an episode's first screen), conv input = dqn_phi of it (dqn_phi.py:4-17).
+ * stack_pool == NULL (t >= 1): ingest only the reward / done of the
+ * transition into a terminal observation, whose state the reference never
+ * feeds to the model (a3c.py:72-73, 165-167). */
+int arl_observe_stack(arl_net* net, int t, const uint8_t* stack_pool, const float* reward_pool,
+                      const uint8_t* done_pool, int64_t pool_len, int force_reset, void* stream);
+
+/* The reference's early window end (a3c.py:77-78: an update at a terminal
+ * after t_len < t_max steps): window steps [t_len, t_max) carry no loss and
+ * no gradient in the next arl_learn (their done flags get bit 1, rewards 0).
+ * Observations of the next window overwrite the flags again. */
+int arl_truncate_window(arl_net* net, int t_len, void* stream);
+
+/* Loss options of A3C.__init__ (a3c.py:33-36, 110-121): pi_loss_coef scales
+ * the policy + entropy terms; keep_loss_scale_same scales both losses of a
+ * segment that a terminal closed after len < t_max steps by t_max / len.
+ * Host state of the handle, read when arl_learn launches (defaults 1, 0). */
+int arl_net_set_loss(arl_net* net, double pi_loss_coef, int keep_loss_scale_same);
+
 /* A3C.act forward + sample at window step t (a3c.py:154-164): pi_and_v of
  * the ring state, softmax policy output, Philox inverse-CDF action.  t ==
  * t_max is the bootstrap value of the window end (a3c.py:85, pre-update
@@ -199,11 +225,20 @@ int arl_advance(arl_net* net, void* stream);
 int arl_optimize_advance(arl_net* net, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
                          double clip, void* stream);
 
-/* A3CFF.pi_and_v on explicit f32 states (a3c_ale.py:38-40; input from
- * dqn_phi).  n <= n_envs; outputs in the workspace's bootstrap slot.  mode
- * as arl_act_mode: 0 no action, 1 sampled (action_indices, Philox counter =
- * step + t_max), 2 greedy (most_probable_actions). */
+/* A3CFF / A3CLSTM.pi_and_v on explicit f32 states (a3c_ale.py:38-40,55-63;
+ * input from dqn_phi), rows 0..n-1, n <= n_envs; outputs in the workspace's
+ * bootstrap slot.  mode as arl_act_mode: 0 no action, 1 sampled
+ * (action_indices from Philox stream 1, counter = number of sampling
+ * forward_states calls so far on this handle: repeated calls draw afresh),
+ * 2 greedy (most_probable_actions).  LSTM: the recurrent state is the
+ * handle's pi_and_v state (not the lockstep window's); it advances unless
+ * mode | ARL_FWD_KEEP_STATE (keep_same_state, a3c_ale.py:57-60). */
+#define ARL_FWD_KEEP_STATE 16
 int arl_forward_states(arl_net* net, const float* states, int64_t n, int mode, void* stream);
+
+/* A3CLSTM.reset_state (a3c_ale.py:65-66) of the pi_and_v state, rows
+ * [e0, e0 + n): the next forward starts from h = c = None.  No-op for FF. */
+int arl_reset_state(arl_net* net, int64_t e0, int64_t n, void* stream);
 
 /* ------------------------------------------------------------------ granular ops */
 
@@ -224,11 +259,15 @@ int arl_policy(const float* h, int64_t n, const float* W_pi, const float* b_pi, 
                float* entropy, int32_t* actions, float* action_log_probs, void* stream);
 
 /* a3c.py:82-126: returns + loss gradient over a (t_max, n) window. v, probs,
- * log_probs, actions are (t_max+1, n[, A]) with row t_max = bootstrap. */
+ * log_probs, actions are (t_max+1, n[, A]) with row t_max = bootstrap.
+ * dones: bit 0 = the transition t -> t+1 ended the episode (R = 0), bit 1 =
+ * step t is past the window's end (no loss).  loss: (n, 2) pi / v loss or
+ * NULL. */
 int arl_returns_lossgrad(const float* rewards, const uint8_t* dones, const float* v, const float* probs,
                          const float* log_probs, const int32_t* actions, int t_max, int64_t n, int n_actions,
-                         double gamma, double beta, double v_loss_coef, int clip_reward, float* dlogits,
-                         float* dv, float* loss, void* stream);
+                         double gamma, double beta, double pi_loss_coef, double v_loss_coef,
+                         int keep_loss_scale_same, int clip_reward, float* dlogits, float* dv, float* loss,
+                         void* stream);
 
 #ifdef __cplusplus
 }

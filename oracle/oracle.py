@@ -448,9 +448,31 @@ def sample_from_uniform(probs: np.ndarray, u: np.ndarray) -> np.ndarray:
 # n-step return, losses and their gradient: a3c.py:82-126
 # ----------------------------------------------------------------------------
 
+def segment_scale(dones, t_max, valid=None):
+    """a3c.py:116-121 (keep_loss_scale_same): the losses of a window that a
+    terminal closed after len < t_max steps are scaled by t_max / len.  In a
+    lockstep window every segment closed by a terminal is such a window; the
+    segment running into the window end is not scaled.  Returns (T, N) f64."""
+    T, N = dones.shape
+    valid = np.ones((T, N), bool) if valid is None else valid
+    scale = np.ones((T, N), np.float64)
+    for e in range(N):
+        start = 0
+        for t in range(T):
+            if not valid[t, e]:
+                break
+            if dones[t, e]:
+                ln = t - start + 1
+                if ln < t_max:
+                    scale[start:t + 1, e] = t_max / ln
+                start = t + 1
+    return scale
+
+
 def returns_and_lossgrad(rewards, dones, values, vboot, probs, logp, actions,
                          gamma=0.99, beta=0.01, v_loss_coef=0.5,
-                         clip_reward=True):
+                         clip_reward=True, pi_loss_coef=1.0,
+                         keep_loss_scale_same=False, t_max=None, valid=None):
     """Batched restatement of a3c.py:82-126 over a lockstep window.
 
     rewards, dones: (T, N) -- reward / terminal of transition t -> t+1
@@ -458,10 +480,16 @@ def returns_and_lossgrad(rewards, dones, values, vboot, probs, logp, actions,
     probs, logp: (T, N, A); actions: (T, N).
     R is accumulated in float64 like the Python float at a3c.py:83-92; each
     terminal restarts it at 0 (a segment per episode, a3c.py:82-83).
+    pi_loss_coef / v_loss_coef scale the two losses (a3c.py:110-114);
+    keep_loss_scale_same scales terminal-closed segments shorter than t_max
+    (default T) by t_max / len (a3c.py:116-121); valid (T, N) bool marks the
+    steps that belong to the window (the rest get no loss).
     Returns R (f32), advantage, dlogits (T,N,A), dv (T,N), pi_loss, v_loss.
     """
     T, N = rewards.shape
     A = probs.shape[2]
+    t_max = T if t_max is None else t_max
+    valid = np.ones((T, N), bool) if valid is None else np.asarray(valid, bool)
     r = np.asarray(rewards, np.float64)
     if clip_reward:
         r = np.clip(r, -1, 1)                     # a3c.py:69-70
@@ -475,13 +503,16 @@ def returns_and_lossgrad(rewards, dones, values, vboot, probs, logp, actions,
     H = entropy(probs, logp)
     onehot = np.zeros_like(probs)
     np.put_along_axis(onehot, actions[..., None].astype(np.int64), 1.0, axis=2)
+    scale = segment_scale(dones, t_max, valid) if keep_loss_scale_same else np.ones((T, N))
+    pf = (F32(pi_loss_coef) * scale.astype(np.float32)).astype(np.float32) * valid
+    vf = (F32(v_loss_coef) * scale.astype(np.float32)).astype(np.float32) * valid
     # d/dz of [-logpi(a)*adv - beta*H]  (a3c.py:103,105)
-    dlogits = (-adv[..., None] * (onehot - probs)
-               + F32(beta) * probs * (logp + H[..., None])).astype(np.float32)
-    dv = (F32(v_loss_coef) * (values - Rs)).astype(np.float32)   # a3c.py:108,113-114
+    dlogits = (pf[..., None] * (-adv[..., None] * (onehot - probs)
+               + F32(beta) * probs * (logp + H[..., None]))).astype(np.float32)
+    dv = (vf * (values - Rs)).astype(np.float32)   # a3c.py:108,113-114
     logp_a = np.take_along_axis(logp, actions[..., None].astype(np.int64), 2)[..., 0]
-    pi_loss = float(-(logp_a * adv).sum() - beta * H.sum())
-    v_loss = float(v_loss_coef * (((values - Rs) ** 2) / 2).sum())
+    pi_loss = float(-(pf * (logp_a * adv + F32(beta) * H)).sum())
+    v_loss = float((vf * (((values - Rs) ** 2) / 2)).sum())
     return Rs, adv, dlogits, dv, pi_loss, v_loss
 
 
@@ -608,7 +639,7 @@ class LSTMState:
 
 
 def ff_window_grads(params, states, actions, rewards, dones, boot_state,
-                    gamma=0.99, beta=0.01, v_loss_coef=0.5, arch=ARCH_FF):
+                    gamma=0.99, beta=0.01, v_loss_coef=0.5, arch=ARCH_FF, **loss_kw):
     """Gradient of one lockstep window for A3CFF at fixed theta.
 
     states: (T, N, 4, 84, 84) f32; boot_state (N,4,84,84) f32 = s_T.
@@ -623,14 +654,14 @@ def ff_window_grads(params, states, actions, rewards, dones, boot_state,
     A = logits.shape[1]
     R, adv, dlog, dv, pil, vl = returns_and_lossgrad(
         rewards, dones, v.reshape(T, N), vb, p.reshape(T, N, A),
-        lp.reshape(T, N, A), actions, gamma, beta, v_loss_coef)
+        lp.reshape(T, N, A), actions, gamma, beta, v_loss_coef, **loss_kw)
     g = ff_backward(params, x, acts, dlog.reshape(T * N, A), dv.reshape(T * N), arch)
     return g, dict(logits=logits.reshape(T, N, A), v=v.reshape(T, N), vboot=vb,
                    R=R, adv=adv, dlogits=dlog, dv=dv, pi_loss=pil, v_loss=vl)
 
 
 def lstm_window(params, states, actions, rewards, dones_prev, dones, boot_state,
-                st0: LSTMState, gamma=0.99, beta=0.01, v_loss_coef=0.5):
+                st0: LSTMState, gamma=0.99, beta=0.01, v_loss_coef=0.5, **loss_kw):
     """A3CLSTM window (a3c_ale.py:55-70) at fixed theta with truncated BPTT
     over the window (unchain_backward, a3c.py:144) and resets at terminals.
 
@@ -663,7 +694,7 @@ def lstm_window(params, states, actions, rewards, dones_prev, dones, boot_state,
     vb = linear(hbb, params["3/0/W"], params["3/0/b"])[:, 0]
     R, adv, dlog, dv, pil, vl = returns_and_lossgrad(
         rewards, dones, v.reshape(T, N), vb, p.reshape(T, N, A),
-        lp.reshape(T, N, A), actions, gamma, beta, v_loss_coef)
+        lp.reshape(T, N, A), actions, gamma, beta, v_loss_coef, **loss_kw)
     dl = dlog.reshape(T * N, A); dvf = dv.reshape(T * N)
     g = {}
     Hf = H.reshape(T * N, 256)
@@ -705,3 +736,107 @@ def lstm_window(params, states, actions, rewards, dones_prev, dones, boot_state,
 
 def flat_names(arch, n_actions):
     return [n for n, _ in param_shapes(arch, n_actions)]
+
+
+# ----------------------------------------------------------------------------
+# The reference's one-env agent: a3c.py:27-167 (A3C.act) driven call by call,
+# with GradientClipping + RMSpropAsync (a3c_ale.py:224-226) after each update
+# ----------------------------------------------------------------------------
+
+class A3CAgent:
+    """a3c.py:67-167 for one env (one reference process) on the oracle's
+    math.  act() mirrors the reference's control flow: the window restarts at
+    every update (t_start = t, a3c.py:152), a terminal call runs the R = 0
+    update and returns None (a3c.py:77-83,165-167), a full window
+    bootstraps from v(s) at the pre-update parameters and then acts on s with
+    the post-update ones (a3c.py:85,156).  Actions are drawn by inverse CDF
+    from Philox(seed; env 0, t_max * updates + step in window), or taken from
+    `action` when given.  Records per call and per update are appended to
+    self.calls / self.updates."""
+
+    def __init__(self, params, arch, n_actions, t_max=5, gamma=0.99, beta=0.01, pi_loss_coef=1.0,
+                 v_loss_coef=0.5, keep_loss_scale_same=False, clip=40.0, seed=0, clip_reward=True):
+        self.p = {k: np.asarray(v, np.float32).copy() for k, v in params.items()}
+        self.ms = {k: np.zeros_like(v) for k, v in self.p.items()}
+        self.arch, self.A, self.T = arch, n_actions, t_max
+        self.gamma, self.beta, self.clip, self.seed = gamma, beta, clip, seed
+        self.clip_reward = clip_reward
+        self.loss_kw = dict(pi_loss_coef=pi_loss_coef, keep_loss_scale_same=keep_loss_scale_same, t_max=t_max)
+        self.v_loss_coef = v_loss_coef
+        self.t = self.t_start = 0
+        self.n_upd = 0
+        self.rewards = {}
+        self.win_x, self.win_a = [], []
+        self.names = flat_names(arch, n_actions)
+        # LSTM: recurrent state after the latest step (None -> has = False)
+        self.h = np.zeros((1, 256), np.float32)
+        self.c = np.zeros((1, 256), np.float32)
+        self.has = False
+        self.win_st0 = None
+        self.calls, self.updates = [], []
+
+    def _forward(self, x, h, c, has):
+        a1, a2, hfc = nips_head(self.p, self.arch, x)
+        c2 = h2 = None
+        if self.arch == ARCH_LSTM:
+            _, c2, h2 = lstm_cell(self.p, self.arch, hfc, h, c, np.array([has]))
+            hfc = h2
+        w = "2/0" if self.arch == ARCH_LSTM else "1/0"
+        vw = "3/0" if self.arch == ARCH_LSTM else "2/0"
+        logits = linear(hfc, self.p[w + "/W"], self.p[w + "/b"])
+        v = linear(hfc, self.p[vw + "/W"], self.p[vw + "/b"])[:, 0]
+        return logits, v, c2, h2
+
+    def act(self, screens, reward, terminal, lr, action=None):
+        T = self.T
+        if self.clip_reward:
+            reward = float(np.clip(reward, -1, 1))            # a3c.py:69-70
+        x = None if terminal else PHI_LUT[np.asarray(screens, np.uint8)][None]
+        self.rewards[self.t - 1] = reward                     # a3c.py:75
+        if (terminal and self.t_start < self.t) or self.t - self.t_start == T:
+            self._update(x, terminal, lr)
+        if terminal:                                          # a3c.py:165-167
+            self.has = False
+            self.calls.append(None)
+            return None
+        logits, v, c2, h2 = self._forward(x, self.h, self.c, self.has)
+        p, lp = softmax(logits), log_softmax(logits)
+        if action is None:
+            u = sample_uniforms(self.seed, np.array([0]), T * self.n_upd + (self.t - self.t_start))
+            action = int(sample_from_uniform(p, u)[0])
+        if self.t == self.t_start:
+            self.win_st0 = LSTMState(self.h.copy(), self.c.copy(), np.array([self.has]))
+        if self.arch == ARCH_LSTM:
+            self.h, self.c, self.has = h2, c2, True
+        self.win_x.append(x[0])
+        self.win_a.append(action)
+        self.t += 1
+        self.calls.append(dict(action=action, probs=p[0], v=float(v[0]), entropy=float(entropy(p, lp)[0])))
+        return action
+
+    def _update(self, x, terminal, lr):
+        L = self.t - self.t_start
+        states = np.stack(self.win_x)[:, None]
+        acts = np.array(self.win_a, np.int32)[:, None]
+        r = np.array([[self.rewards[i]] for i in range(self.t_start, self.t)], np.float32)
+        d = np.zeros((L, 1), np.uint8)
+        if terminal:
+            d[L - 1] = 1
+        boot = states[-1] if terminal else x
+        kw = dict(gamma=self.gamma, beta=self.beta, v_loss_coef=self.v_loss_coef, **self.loss_kw)
+        if self.arch == ARCH_LSTM:
+            dprev = np.zeros((L, 1), np.uint8)
+            g, aux = lstm_window(self.p, states, acts, r, dprev, d, boot, self.win_st0, **kw)
+        else:
+            g, aux = ff_window_grads(self.p, states, acts, r, d, boot, **kw)
+        grads = [g[n] for n in self.names]
+        clipped, norm = clip_grads(grads, self.clip)
+        for n, gc in zip(self.names, clipped):
+            self.p[n], self.ms[n] = rmsprop_update(self.p[n], self.ms[n], gc, lr)
+        self.updates.append(dict(call=len(self.calls), L=L, terminal=terminal, R=aux["R"][:, 0].copy(),
+                                 v=aux["v"][:, 0].copy(), pi_loss=aux["pi_loss"], v_loss=aux["v_loss"],
+                                 grads=dict(g), norm=norm, params={n: self.p[n].copy() for n in self.names}))
+        self.n_upd += 1
+        self.t_start = self.t                                 # a3c.py:152
+        self.rewards = {}
+        self.win_x, self.win_a = [], []

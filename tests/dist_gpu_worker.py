@@ -19,7 +19,7 @@ from sim import make_pools  # noqa: E402
 
 
 def agent(n, off, group):
-    m = A3CFF(4, n_envs=n, t_max=5, seed=99, env_offset=off, init_seed=21)
+    m = A3CFF(4, n_envs=n, t_max=5, seed=99, env_offset=off, init_seed=21, frames="pairs")
     o = RMSpropAsync(lr=7e-4, eps=0.1, alpha=0.99).setup(m)
     o.add_hook(GradientClipping(40))
     return A3C(m, o, 5, 0.99, process_group=group)

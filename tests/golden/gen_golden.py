@@ -267,6 +267,209 @@ def gen_rmsprop():
     sys.path.remove(REF)
 
 
+# --------------------------------------------------------------------------
+# A3C update trajectories: a3c.py / policy_output.py / policy.py /
+# v_function.py / dqn_head.py / init_like_torch.py / rmsprop_async.py and the
+# model classes of a3c_ale.py:28-70 run verbatim on a torch-float64 Chainer
+# stub (tests/golden/chainer_stub.py), driven like a3c_ale.py:100-126 over the
+# reference's ALE wrapper on the scripted fake emulator.
+# --------------------------------------------------------------------------
+A3C_VARIANTS = {
+    # name: (arch, kwargs of a3c.A3C, GradientClipping threshold, beta, n act calls)
+    "ff": ("ff", dict(pi_loss_coef=1.0, v_loss_coef=0.5, keep_loss_scale_same=False), 40.0, 1e-2, 44),
+    "ff_opts": ("ff", dict(pi_loss_coef=0.5, v_loss_coef=1.0, keep_loss_scale_same=True), 0.05, 5e-2, 44),
+    "lstm": ("lstm", dict(pi_loss_coef=1.0, v_loss_coef=0.5, keep_loss_scale_same=False), 40.0, 1e-2, 44),
+    "lstm_opts": ("lstm", dict(pi_loss_coef=0.5, v_loss_coef=0.5, keep_loss_scale_same=True), 0.05, 1e-2, 44),
+}
+A3C_T, A3C_GAMMA, A3C_SEED, A3C_LR, A3C_STEPS = 5, 0.99, 1234, 7e-4, 10 ** 4
+A3C_INIT_SEED = 21     # oracle.init_like_torch(arch, A, default_rng(A3C_INIT_SEED)) = theta0
+SUBSET_MIN, SUBSET_K = 16384, 2048   # tensors larger than this are stored on a fixed index subset
+
+
+def _ref_model_classes():
+    """A3CFF / A3CLSTM, a3c_ale.py:28-70, executed from the reference's own
+    source text (the module as a whole does not parse on Python >= 3.7:
+    `import async`, a3c_ale.py:20)."""
+    import chainer
+    import dqn_head, policy, v_function, a3c  # noqa: E401  (reference modules)
+    from init_like_torch import init_like_torch
+    with open(os.path.join(REF, "a3c_ale.py")) as f:
+        lines = f.read().splitlines()
+    block = "\n".join(lines[27:70])
+    assert block.startswith("class A3CFF(") and "self.lstm.c.unchain_backward()" in lines[69]
+    ns = dict(chainer=chainer, L=chainer.links, F=chainer.functions, np=np, dqn_head=dqn_head, policy=policy,
+              v_function=v_function, a3c=a3c, init_like_torch=init_like_torch)
+    exec(compile("\n" * 27 + block, os.path.join(REF, "a3c_ale.py"), "exec"), ns)
+    return ns["A3CFF"], ns["A3CLSTM"]
+
+
+def _subset_index(name, numel):
+    return np.sort(np.random.default_rng(sum(map(ord, name))).choice(numel, SUBSET_K, replace=False))
+
+
+def gen_a3c():
+    import logging
+    import chainer_stub
+    chainer_stub.install()
+    install_cv2_stub()
+    install_ale_stub()
+    sys.path.insert(0, REF)
+    for k in [k for k in sys.modules if k in ("ale", "a3c", "policy_output", "policy")]:
+        del sys.modules[k]
+    import ale, a3c, rmsprop_async, policy_output  # noqa: E401  (reference modules)
+    from dqn_phi import dqn_phi
+    import chainer
+    A3CFF, A3CLSTM = _ref_model_classes()
+
+    class Capture(logging.Handler):          # the reference's own process-0 debug log (a3c.py:94-163)
+        def __init__(self):
+            super().__init__(logging.DEBUG)
+            self.recs = []
+
+        def emit(self, rec):
+            self.recs.append((rec.msg, rec.args))
+
+    out = {}
+    for vname, (arch, kw, clip, beta, K) in A3C_VARIANTS.items():
+        np.random.seed(17)
+        env = ale.ALE("fake.rom", seed=3, max_start_nullops=4)       # reference ALE on the fake emulator
+        n_actions = env.number_of_actions
+        np.random.seed(5)                                            # init_like_torch draws (a3c_ale.py:36,53)
+        model = (A3CFF if arch == "ff" else A3CLSTM)(n_actions)
+        # theta0 is then replaced by the oracle's seeded draw of the same
+        # distribution, so the tests regenerate it instead of storing 3-5 MB
+        init = oracle.init_like_torch(oracle.ARCH_FF if arch == "ff" else oracle.ARCH_LSTM, n_actions,
+                                      np.random.default_rng(A3C_INIT_SEED))
+        for n, p in model.namedparams():
+            assert p.data.shape == init[n.lstrip("/")].shape, n
+            p.data[...] = init[n.lstrip("/")]
+        opt = rmsprop_async.RMSpropAsync(lr=A3C_LR, eps=1e-1, alpha=0.99)
+        opt.setup(model)
+        opt.add_hook(chainer.optimizer.GradientClipping(clip))
+        agent = a3c.A3C(model, opt, A3C_T, A3C_GAMMA, beta=beta, process_idx=0, phi=dqn_phi, **kw)
+        names = [n.lstrip("/") for n, _ in model.namedparams()]
+        theta0 = {n.lstrip("/"): p.data.copy() for n, p in model.namedparams()}
+
+        # sampling: np.random.multinomial (policy_output.py:27) draws from the
+        # SAME Philox uniform the HIP sampler uses -- (seed; env 0, counter =
+        # t_max * updates so far + step in window) -- by inverse CDF over the
+        # f32 probabilities; the reference's epsneg shift is undone first
+        n_upd = [0]
+
+        def multinomial(n, pvals, size=None):
+            ctr = A3C_T * n_upd[0] + (agent.t - agent.t_start)
+            u = oracle.sample_uniforms(A3C_SEED, np.array([0]), ctr)
+            p = (np.asarray(pvals, np.float64) + np.finfo(np.float32).epsneg).astype(np.float32)
+            k = int(oracle.sample_from_uniform(p[None, :], u)[0])
+            h = np.zeros(len(pvals), np.int64)
+            h[k] = 1
+            return h
+
+        upd = []
+        real_update = opt.update
+
+        def update():
+            g = {n.lstrip("/"): p.grad.copy() for n, p in agent.shared_model.namedparams()}
+            real_update()
+            n_upd[0] += 1
+            upd.append((g, {n.lstrip("/"): p.data.copy() for n, p in agent.shared_model.namedparams()}))
+
+        opt.update = update
+        cap = Capture()
+        lg = logging.getLogger("a3c")
+        lg.setLevel(logging.DEBUG)
+        lg.addHandler(cap)
+        orig_mn = np.random.multinomial
+        np.random.multinomial = multinomial
+        states, rewards, terms, lrs, actions, calls_upd = [], [], [], [], [], []
+        try:
+            for k in range(K):                                       # a3c_ale.py:100-126
+                global_t = k + 1
+                lr = (A3C_STEPS - global_t - 1) / A3C_STEPS * A3C_LR
+                agent.optimizer.lr = lr
+                st = np.stack(env.state)
+                states.append(st)
+                rewards.append(float(env.reward))
+                terms.append(bool(env.is_terminal))
+                lrs.append(lr)
+                nu = len(upd)
+                a = agent.act(env.state, env.reward, env.is_terminal)
+                calls_upd.append(len(upd) > nu)
+                actions.append(-1 if a is None else int(a))
+                if env.is_terminal:
+                    env.initialize()
+                else:
+                    env.receive_action(a)
+        finally:
+            np.random.multinomial = orig_mn
+            lg.removeHandler(cap)
+        # per-call policy outputs from the debug lines 't:%s entropy:%s, probs:%s' (a3c.py:161-163)
+        probs = np.full((K, n_actions), np.nan)
+        ent = np.full(K, np.nan)
+        ci = [k for k in range(K) if actions[k] >= 0]
+        steplog = [r for r in cap.recs if r[0].startswith("t:")]
+        assert len(steplog) == len(ci)
+        for k, (_, args) in zip(ci, steplog):
+            ent[k] = float(np.asarray(args[1]).ravel()[0])
+            probs[k] = np.asarray(args[2]).ravel()
+        # per-update records: R per step ('s:%s v:%s R:%s'), losses, grad norm
+        Rs, vs, losses, norms = [], [], [], []
+        cur_R, cur_v = [], []
+        for msg, args in cap.recs:
+            if msg.startswith("s:"):
+                cur_v.append(float(np.asarray(args[1]).ravel()[0]))
+                cur_R.append(float(args[2]))
+            elif msg.startswith("pi_loss"):
+                losses.append((float(np.asarray(args[0]).ravel()[0]), float(np.asarray(args[1]).ravel()[0])))
+                Rs.append(cur_R[::-1])
+                vs.append(cur_v[::-1])
+                cur_R, cur_v = [], []
+            elif msg.startswith("grad norm"):
+                norms.append(float(args[0]))
+        U = len(upd)
+        assert U == len(Rs) == len(norms) and U >= 6, (U, len(Rs), len(norms))
+        pref = vname + "|"
+        out[pref + "arch"] = np.array(arch)
+        out[pref + "names"] = np.array(names)
+        out[pref + "kw"] = np.array([kw["pi_loss_coef"], kw["v_loss_coef"], float(kw["keep_loss_scale_same"]),
+                                     clip, beta, A3C_GAMMA, A3C_T, A3C_SEED, n_actions, A3C_INIT_SEED])
+        st = np.stack(states)
+        skey = "states|" + arch      # the fake emulator's frames ignore the actions: one copy per arch
+        if skey in out:
+            assert np.array_equal(out[skey], st)
+        out[skey] = st
+        out[pref + "rewards"] = np.array(rewards, np.float32)
+        out[pref + "terminals"] = np.array(terms)
+        out[pref + "lr"] = np.array(lrs)
+        out[pref + "actions"] = np.array(actions, np.int32)
+        out[pref + "probs"] = probs
+        out[pref + "entropy"] = ent
+        out[pref + "updates"] = np.array([k for k in range(K) if calls_upd[k]], np.int32)
+        Rm = np.full((U, A3C_T), np.nan)
+        vm = np.full((U, A3C_T), np.nan)
+        for u in range(U):
+            Rm[u, :len(Rs[u])] = Rs[u]
+            vm[u, :len(vs[u])] = vs[u]
+        out[pref + "R"] = Rm
+        out[pref + "v"] = vm
+        out[pref + "loss"] = np.array(losses)
+        out[pref + "grad_norm"] = np.array(norms)
+        for n in names:
+            g = np.stack([u[0][n] for u in upd])
+            p = np.stack([u[1][n] for u in upd])
+            if theta0[n].size > SUBSET_MIN:
+                idx = _subset_index(n, theta0[n].size)
+                out[pref + "idx|" + n] = idx
+                g = g.reshape(U, -1)[:, idx]
+                p = p.reshape(U, -1)[:, idx]
+            out[pref + "grad|" + n] = g
+            out[pref + "param|" + n] = p
+        print(vname, "calls", K, "updates", U, "terminal updates",
+              int(sum(terms[k] for k in range(K) if calls_upd[k])), "norms", np.round(norms, 3))
+    np.savez_compressed(os.path.join(HERE, "a3c_update_golden.npz"), **out)
+    sys.path.remove(REF)
+
+
 def gen_checkpoint():
     src = os.path.join(REF, "trained_model/breakout_ff/80000000_finish.h5")
     dst = os.path.join(HERE, "breakout_ff.npz")

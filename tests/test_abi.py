@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_errors():
     from asyncrl_amd._lib import lib
-    assert lib.arl_abi_version() == 1
+    assert lib.arl_abi_version() == 2
     h = ctypes.c_void_p()
     rc = lib.arl_net_create(ctypes.byref(h), 7, 4, 16, 5, 0, 0)
     assert rc == 1 and b"arch" in lib.arl_last_error()
@@ -38,16 +38,22 @@ def test_abi_version_and_errors():
     assert rc == 1
     rc = lib.arl_net_create(ctypes.byref(h), 2 | 16, 4, 16, 5, 0, 0)   # Nature head has no RGB model
     assert rc == 1 and b"RGB" in lib.arl_last_error()
+    for bad in (2 | 32, 16 | 32):                                        # STACK: NIPS FF / LSTM, not with RGB
+        assert lib.arl_net_create(ctypes.byref(h), bad, 4, 16, 5, 0, 0) == 1
     # calls on an unbound handle fail cleanly
     assert lib.arl_net_create(ctypes.byref(h), 0, 4, 16, 5, 0, 0) == 0
     assert lib.arl_act(h, 0, None) == 3
     assert lib.arl_act(h, 0, None) == 3 and b"bound" in lib.arl_last_error()
+    assert lib.arl_truncate_window(h, 2, None) == 3
+    assert lib.arl_net_set_loss(h, 0.5, 1) == 0                          # host state only
+    assert lib.arl_observe_stack(h, 0, None, None, None, 1, 0, None) == 3
     lib.arl_net_destroy(h)
 
 
 # 16 / 17: the ViZDoom models (ARL_ARCH_RGB, train_a3c_doom.py:25-63), conv1 W (16, 3, 8, 8)
+# 32 / 33: ARL_ARCH_STACK (whole ALE.state stacks per ring slot, the A3C.act drop-in)
 @pytest.mark.parametrize("arch,A,count", [(0, 4, 677429), (1, 6, 1203255), (2, 4, 1686693),
-                                          (16, 3, 676148), (17, 3, 1201460)])
+                                          (16, 3, 676148), (17, 3, 1201460), (32, 4, 677429), (33, 6, 1203255)])
 def test_param_layout_matches_chainer(arch, A, count):
     from asyncrl_amd._lib import lib
     from asyncrl_amd.net import param_shapes
@@ -73,7 +79,7 @@ def test_param_layout_matches_chainer(arch, A, count):
     assert 0 < ws < 4 << 30
     off, nb = ctypes.c_int64(), ctypes.c_int64()
     assert lib.arl_net_buffer(h, b"frames", ctypes.byref(off), ctypes.byref(nb)) == 0
-    assert nb.value == 9 * 256 * 84 * 84 * (3 if arch & 16 else 1) and off.value % 256 == 0
+    assert nb.value == 9 * 256 * 84 * 84 * (3 if arch & 16 else 4 if arch & 32 else 1) and off.value % 256 == 0
     assert lib.arl_net_buffer(h, b"nope", ctypes.byref(off), ctypes.byref(nb)) == 1
     lib.arl_net_destroy(h)
 

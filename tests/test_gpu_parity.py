@@ -254,7 +254,7 @@ def _run_ff(gpu, N, T, A, seed, kind, windows=2, ckpt=False, arch=O.ARCH_FF, p_d
         pairs, rewards, dones = make_pools(rng, P, N, kind) if p_done is None else \
             make_pools(rng, P, N, kind, p_done=p_done)
     Model = A3CFFNature if arch == O.ARCH_FF_NATURE else (DoomA3CFF if rgb else A3CFF)
-    model = Model(A, n_envs=N, t_max=T, seed=99, init_seed=seed)
+    model = Model(A, n_envs=N, t_max=T, seed=99, init_seed=seed, frames="pairs")
     if ckpt:
         model.net.load_params(load_checkpoint())
     opt = RMSpropAsync(lr=7e-4, eps=1e-1, alpha=0.99)
@@ -422,7 +422,7 @@ def test_lstm_windows_match_oracle(gpu, rgb, N, T, A):
         pairs, rewards, dones = make_rgb_pools(rng, P, N, p_done=0.2)
     else:
         pairs, rewards, dones = make_pools(rng, P, N, "palette", p_done=0.2)
-    model = (DoomA3CLSTM if rgb else A3CLSTM)(A, n_envs=N, t_max=T, seed=5, init_seed=31)
+    model = (DoomA3CLSTM if rgb else A3CLSTM)(A, n_envs=N, t_max=T, seed=5, init_seed=31, frames="pairs")
     opt = RMSpropAsync(lr=7e-4, eps=1e-1, alpha=0.99).setup(model)
     opt.add_hook(GradientClipping(40))
     agent = A3C(model, opt, T, 0.99)
@@ -494,7 +494,7 @@ def test_graph_replay_equals_eager(gpu):
     dp, dr, dd = dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu)
 
     def mk():
-        m = A3CFF(4, n_envs=N, t_max=T, seed=3, init_seed=4)
+        m = A3CFF(4, n_envs=N, t_max=T, seed=3, init_seed=4, frames="pairs")
         o = RMSpropAsync(lr=7e-4, eps=0.1, alpha=0.99).setup(m)
         o.add_hook(GradientClipping(40))
         o.anneal_total_steps, o.n_total_envs = 10 ** 6, N
@@ -521,7 +521,7 @@ def test_many_windows_stay_finite(gpu):
     rng = np.random.default_rng(61)
     N, T, P = 16, 5, 9
     pairs, rewards, dones = make_pools(rng, P, N, "palette")
-    m = A3CFF(4, n_envs=N, t_max=T, seed=1)
+    m = A3CFF(4, n_envs=N, t_max=T, seed=1, frames="pairs")
     o = RMSpropAsync(lr=7e-4, eps=0.1, alpha=0.99).setup(m)
     o.add_hook(GradientClipping(40))
     agent = A3C(m, o, T, 0.99)
@@ -553,7 +553,7 @@ def test_env_groups_identical(gpu, arch, N, groups):
     dp, dr, dd = dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu)
 
     def mk():
-        m = Model(A, n_envs=N, t_max=T, seed=5, init_seed=6)
+        m = Model(A, n_envs=N, t_max=T, seed=5, init_seed=6, frames="pairs")
         o = RMSpropAsync(lr=7e-4, eps=0.1, alpha=0.99).setup(m)
         o.add_hook(GradientClipping(40))
         o.anneal_total_steps, o.n_total_envs = 10 ** 6, N
@@ -593,7 +593,7 @@ def test_learn_fork_identical(gpu, arch):
     pairs, rewards, dones = make_pools(rng, P, N, "uniform", p_done=0.1)
     dp, dr, dd = dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu)
     Model = A3CFF if arch == "ff" else A3CLSTM
-    m = Model(4, n_envs=N, t_max=T, seed=5, init_seed=6)
+    m = Model(4, n_envs=N, t_max=T, seed=5, init_seed=6, frames="pairs")
     ag = A3C(m, RMSpropAsync(lr=7e-4, eps=0.1, alpha=0.99).setup(m), T, 0.99)
     ag.run_window(dp, dr, dd, P, first=True, split_update=True)
     net = ag.net
