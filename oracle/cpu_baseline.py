@@ -16,6 +16,7 @@ import time
 import numpy as np
 
 import oracle as O
+O.EXACT_SUMS = False   # time the f32 arithmetic Chainer does
 
 
 def run(seconds: float = 10.0, t_max: int = 5, n_actions: int = 4, seed: int = 0, pool: int = 16):

@@ -285,14 +285,19 @@ def conv2d(x: np.ndarray, W: np.ndarray, b: np.ndarray, s: int) -> np.ndarray:
     return y.reshape(x.shape[0], oh, ow, oc).transpose(0, 3, 1, 2).copy()
 
 
-def conv2d_backward(x, W, gy, s, need_dx=True):
-    """Gradient of conv2d w.r.t. W, b and (optionally) x."""
+def conv2d_backward(x, W, gy, s, need_dx=True, mag=None, names=None):
+    """Gradient of conv2d w.r.t. W, b and (optionally) x.  mag (dict) +
+    names (W, b): also store the L2 norm of each gradient element's summands
+    (grad_mag)."""
     oc, ic, k, _ = W.shape
     n = x.shape[0]
     cols, oh, ow = _im2col(x, k, s)
     gyf = gy.transpose(0, 2, 3, 1).reshape(-1, oc)
-    gW = (gyf.T @ cols.reshape(-1, ic * k * k)).reshape(W.shape)
-    gb = gyf.sum(axis=0, dtype=np.float32)
+    gW = gmm(gyf.T, cols.reshape(-1, ic * k * k)).reshape(W.shape)
+    gb = gsum(gyf)
+    if mag is not None:
+        mag[names[0]] = _mag_mm(gyf.T, cols.reshape(-1, ic * k * k)).reshape(W.shape)
+        mag[names[1]] = _mag_sum(gyf)
     gx = None
     if need_dx:
         gcol = (gyf @ W.reshape(oc, -1)).reshape(n, oh, ow, ic, k, k)
@@ -306,6 +311,27 @@ def conv2d_backward(x, W, gy, s, need_dx=True):
 
 def relu(x):
     return np.maximum(x, F32(0.0))
+
+
+# Weight-gradient reductions (sums over samples and positions, up to millions
+# of terms at the bench configs) are accumulated in float64 and rounded to
+# f32 once, so the oracle's own summation error stays far below the HIP
+# path's; the summands themselves are the f32 values of the restated graph.
+# The CPU baseline (oracle/cpu_baseline.py) sets this False to time
+# Chainer's f32 arithmetic.
+EXACT_SUMS = True
+
+
+def gmm(a, b):
+    """a @ b for a gradient reduction (float64 accumulation when EXACT_SUMS)."""
+    if EXACT_SUMS:
+        return (np.asarray(a, np.float64) @ np.asarray(b, np.float64)).astype(np.float32)
+    return (a @ b).astype(np.float32)
+
+
+def gsum(a, axis=0):
+    """Sum for a bias gradient (float64 accumulation when EXACT_SUMS)."""
+    return np.asarray(a).sum(axis=axis, dtype=np.float64 if EXACT_SUMS else np.float32).astype(np.float32)
 
 
 def linear(x, W, b=None):
@@ -520,22 +546,26 @@ def returns_and_lossgrad(rewards, dones, values, vboot, probs, logp, actions,
 # Backward (total_loss.backward(), a3c.py:129-130), restated by hand
 # ----------------------------------------------------------------------------
 
-def ff_backward(params, x, acts, dlogits, dv, arch=ARCH_FF):
+def ff_backward(params, x, acts, dlogits, dv, arch=ARCH_FF, dev_acts=None, mag=None):
     """Gradients of sum_i (dlogits_i . z_i + dv_i * v_i) for the A3CFF graph
     (a3c_ale.py:38-40) over a batch of samples.  acts = (a1, a2, h), or
-    (a1, a2, a3, h) for the Nature head."""
+    (a1, a2, a3, h) for the Nature head.  dev_acts: the HIP path's (a1, a2,
+    h) for tie-aware ReLU masks (relu_mask)."""
     h = acts[-1]
     g = {}
-    g["1/0/W"] = (dlogits.T @ h).astype(np.float32)
-    g["1/0/b"] = dlogits.sum(0, dtype=np.float32)
-    g["2/0/W"] = (dv[None, :] @ h).astype(np.float32)
-    g["2/0/b"] = np.array([dv.sum(dtype=np.float32)], np.float32)
+    g["1/0/W"] = gmm(dlogits.T, h)
+    g["1/0/b"] = gsum(dlogits)
+    g["2/0/W"] = gmm(dv[None, :], h)
+    g["2/0/b"] = gsum(dv[:, None])
+    if mag is not None:
+        mag["1/0/W"], mag["2/0/W"] = _mag_mm(dlogits.T, h), _mag_mm(dv[None, :], h)
+        mag["1/0/b"], mag["2/0/b"] = _mag_sum(dlogits), _mag_sum(dv[:, None])
     dh = dlogits @ params["1/0/W"] + dv[:, None] * params["2/0/W"]
     if arch == ARCH_FF_NATURE:
         _nature_backward(params, x, acts, dh.astype(np.float32), g)
     else:
         a1, a2, _ = acts
-        _head_backward(params, ARCH_FF, x, a1, a2, h, dh.astype(np.float32), g)
+        _head_backward(params, arch, x, a1, a2, h, dh.astype(np.float32), g, dev_acts, mag)
     return g
 
 
@@ -545,8 +575,8 @@ def _nature_backward(params, x, acts, dh, g):
     a1, a2, a3, h = acts
     n = x.shape[0]
     dfc = dh * (h > 0)
-    g[pname(arch, "fcW")] = (dfc.T @ a3.reshape(n, -1)).astype(np.float32)
-    g[pname(arch, "fcb")] = dfc.sum(0, dtype=np.float32)
+    g[pname(arch, "fcW")] = gmm(dfc.T, a3.reshape(n, -1))
+    g[pname(arch, "fcb")] = gsum(dfc)
     da3 = ((dfc @ params[pname(arch, "fcW")]).reshape(a3.shape) * (a3 > 0)).astype(np.float32)
     gW3, gb3, da2 = conv2d_backward(a2, params[pname(arch, "c3W")], da3, 1)
     g[pname(arch, "c3W")], g[pname(arch, "c3b")] = gW3, gb3
@@ -558,18 +588,64 @@ def _nature_backward(params, x, acts, dh, g):
     g[pname(arch, "c1W")], g[pname(arch, "c1b")] = gW1, gb1
 
 
-def _head_backward(params, arch, x, a1, a2, h, dh, g):
+def relu_mask(a, a_dev=None, rel=1e-5):
+    """ReLU gradient mask a > 0.  Tie-aware with a_dev (the HIP path's own
+    post-ReLU activations): where both are below rel * max|a| -- a
+    pre-activation within rounding of 0, where either sign is a correct f32
+    result -- the HIP path's decision is taken, so a parity test compares
+    the arithmetic rather than a coin flip at a tie."""
+    m = a > 0
+    if a_dev is None:
+        return m
+    a_dev = np.asarray(a_dev, np.float32).reshape(a.shape)
+    eps = F32(rel) * max(float(np.abs(a).max()), 1e-30)
+    tie = (a < eps) & (a_dev < eps)
+    return np.where(tie, a_dev > 0, m)
+
+
+def _mag_mm(a, b):
+    """Error scale of each element of the reduction a @ b (a = x^T, M x S;
+    b = y, S x N): sqrt(sum_s (|x_si| Y + X |y_sj|)^2), X and Y the largest
+    |x| and |y|.  An f32 operand value carries an absolute rounding error of
+    order eps * (its tensor's largest value) -- a pre-activation summed from
+    many terms, an advantage R - v, a near-zero ReLU output -- so a summand
+    x y is uncertain by about |x| dY + |y| dX; the element's error is that
+    summed in quadrature.  Tests hold |gpu - oracle| <= rtol * scale."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    X = float(np.abs(a).max()) if a.size else 0.0
+    Y = float(np.abs(b).max()) if b.size else 0.0
+    sq = (Y * Y) * (a * a).sum(1)[:, None] + 2.0 * X * Y * (np.abs(a) @ np.abs(b)) + (X * X) * (b * b).sum(0)[None, :]
+    return np.sqrt(sq)
+
+
+def _mag_sum(a):
+    """Error scale of a bias gradient (column sums of a, S x M): the summands'
+    own uncertainty X per term in quadrature, X sqrt(S) (the "ones" operand
+    is exact)."""
+    a = np.asarray(a, np.float64)
+    X = float(np.abs(a).max()) if a.size else 0.0
+    return np.full(a.shape[1], X * np.sqrt(a.shape[0]))
+
+
+def _head_backward(params, arch, x, a1, a2, h, dh, g, dev_acts=None, mag=None):
     n = x.shape[0]
-    dfc = dh * (h > 0)
-    g[pname(arch, "fcW")] = (dfc.T @ a2.reshape(n, -1)).astype(np.float32)
-    g[pname(arch, "fcb")] = dfc.sum(0, dtype=np.float32)
-    da2 = (dfc @ params[pname(arch, "fcW")]).reshape(a2.shape) * (a2 > 0)
+    d1, d2, dhh = dev_acts if dev_acts is not None else (None, None, None)
+    dfc = dh * relu_mask(h, dhh)
+    g[pname(arch, "fcW")] = gmm(dfc.T, a2.reshape(n, -1))
+    g[pname(arch, "fcb")] = gsum(dfc)
+    if mag is not None:
+        mag[pname(arch, "fcW")] = _mag_mm(dfc.T, a2.reshape(n, -1))
+        mag[pname(arch, "fcb")] = _mag_sum(dfc)
+    da2 = (dfc @ params[pname(arch, "fcW")]).reshape(a2.shape) * relu_mask(a2, d2)
     gW2, gb2, da1 = conv2d_backward(a1, params[pname(arch, "c2W")],
-                                    da2.astype(np.float32), 2)
+                                    da2.astype(np.float32), 2, mag=mag,
+                                    names=(pname(arch, "c2W"), pname(arch, "c2b")))
     g[pname(arch, "c2W")], g[pname(arch, "c2b")] = gW2, gb2
-    da1 = (da1 * (a1 > 0)).astype(np.float32)
+    da1 = (da1 * relu_mask(a1, d1)).astype(np.float32)
     gW1, gb1, _ = conv2d_backward(x, params[pname(arch, "c1W")], da1, 4,
-                                  need_dx=False)
+                                  need_dx=False, mag=mag,
+                                  names=(pname(arch, "c1W"), pname(arch, "c1b")))
     g[pname(arch, "c1W")], g[pname(arch, "c1b")] = gW1, gb1
 
 
@@ -639,7 +715,7 @@ class LSTMState:
 
 
 def ff_window_grads(params, states, actions, rewards, dones, boot_state,
-                    gamma=0.99, beta=0.01, v_loss_coef=0.5, arch=ARCH_FF, **loss_kw):
+                    gamma=0.99, beta=0.01, v_loss_coef=0.5, arch=ARCH_FF, dev_acts=None, **loss_kw):
     """Gradient of one lockstep window for A3CFF at fixed theta.
 
     states: (T, N, 4, 84, 84) f32; boot_state (N,4,84,84) f32 = s_T.
@@ -655,13 +731,14 @@ def ff_window_grads(params, states, actions, rewards, dones, boot_state,
     R, adv, dlog, dv, pil, vl = returns_and_lossgrad(
         rewards, dones, v.reshape(T, N), vb, p.reshape(T, N, A),
         lp.reshape(T, N, A), actions, gamma, beta, v_loss_coef, **loss_kw)
-    g = ff_backward(params, x, acts, dlog.reshape(T * N, A), dv.reshape(T * N), arch)
+    mag = {} if arch != ARCH_FF_NATURE else None
+    g = ff_backward(params, x, acts, dlog.reshape(T * N, A), dv.reshape(T * N), arch, dev_acts, mag)
     return g, dict(logits=logits.reshape(T, N, A), v=v.reshape(T, N), vboot=vb,
-                   R=R, adv=adv, dlogits=dlog, dv=dv, pi_loss=pil, v_loss=vl)
+                   R=R, adv=adv, dlogits=dlog, dv=dv, pi_loss=pil, v_loss=vl, grad_mag=mag)
 
 
 def lstm_window(params, states, actions, rewards, dones_prev, dones, boot_state,
-                st0: LSTMState, gamma=0.99, beta=0.01, v_loss_coef=0.5, **loss_kw):
+                st0: LSTMState, gamma=0.99, beta=0.01, v_loss_coef=0.5, dev_acts=None, **loss_kw):
     """A3CLSTM window (a3c_ale.py:55-70) at fixed theta with truncated BPTT
     over the window (unchain_backward, a3c.py:144) and resets at terminals.
 
@@ -698,10 +775,12 @@ def lstm_window(params, states, actions, rewards, dones_prev, dones, boot_state,
     dl = dlog.reshape(T * N, A); dvf = dv.reshape(T * N)
     g = {}
     Hf = H.reshape(T * N, 256)
-    g["2/0/W"] = (dl.T @ Hf).astype(np.float32)
-    g["2/0/b"] = dl.sum(0, dtype=np.float32)
-    g["3/0/W"] = (dvf[None, :] @ Hf).astype(np.float32)
-    g["3/0/b"] = np.array([dvf.sum(dtype=np.float32)], np.float32)
+    g["2/0/W"] = gmm(dl.T, Hf)
+    g["2/0/b"] = gsum(dl)
+    g["3/0/W"] = gmm(dvf[None, :], Hf)
+    g["3/0/b"] = gsum(dvf[:, None])
+    mag = {"2/0/W": _mag_mm(dl.T, Hf), "3/0/W": _mag_mm(dvf[None, :], Hf),
+           "2/0/b": _mag_sum(dl), "3/0/b": _mag_sum(dvf[:, None])}
     dH = (dl @ params["2/0/W"] + dvf[:, None] * params["3/0/W"]).reshape(T, N, 256)
     dh_next = np.zeros((N, 256), np.float32)
     dc_next = np.zeros((N, 256), np.float32)
@@ -723,14 +802,17 @@ def lstm_window(params, states, actions, rewards, dones_prev, dones, boot_state,
         dc_next = (dc * f * m).astype(np.float32)
         dh_next = ((dg @ params["1/lateral/W"]) * m).astype(np.float32)
     dGf = dG.reshape(T * N, 1024)
-    g["1/upward/W"] = (dGf.T @ hh.reshape(T * N, 256)).astype(np.float32)
-    g["1/upward/b"] = dGf.sum(0, dtype=np.float32)
-    g["1/lateral/W"] = (dGf.T @ np.stack(hprev_l).reshape(T * N, 256)).astype(np.float32)
+    g["1/upward/W"] = gmm(dGf.T, hh.reshape(T * N, 256))
+    g["1/upward/b"] = gsum(dGf)
+    g["1/lateral/W"] = gmm(dGf.T, np.stack(hprev_l).reshape(T * N, 256))
+    mag["1/upward/W"] = _mag_mm(dGf.T, hh.reshape(T * N, 256))
+    mag["1/upward/b"] = _mag_sum(dGf)
+    mag["1/lateral/W"] = _mag_mm(dGf.T, np.stack(hprev_l).reshape(T * N, 256))
     dx = (dGf @ params["1/upward/W"]).astype(np.float32)
-    _head_backward(params, arch, xs, a1, a2, hh.reshape(T * N, 256), dx, g)
+    _head_backward(params, arch, xs, a1, a2, hh.reshape(T * N, 256), dx, g, dev_acts, mag)
     aux = dict(logits=logits.reshape(T, N, A), v=v.reshape(T, N), vboot=vb,
                R=R, adv=adv, dlogits=dlog, dv=dv, pi_loss=pil, v_loss=vl,
-               h_last=h, c_last=c, has_last=has)
+               h_last=h, c_last=c, has_last=has, grad_mag=mag)
     return g, aux
 
 
