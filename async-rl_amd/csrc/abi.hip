@@ -149,6 +149,8 @@ int arl_net_reset(arl_net* h, void* s) {
   if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_nvalid, 0, (size_t)n.R * n.N, S(s));
   if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_reset, 1, (size_t)(n.T + 1) * n.N, S(s));
   if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_tick, 0, (size_t)arl::fc_fwd_tiles(n.N) * 4, S(s));
+  if (e == hipSuccess && n.w_fcb_tick)
+    e = hipMemsetAsync(n.ws + n.w_fcb_tick, 0, (size_t)arl::fc_bwd_tickets() * 4, S(s));
   if (e == hipSuccess && n.arch == arl::ARCH_LSTM) {
     e = hipMemsetAsync(n.ws + n.w_hbuf, 0, (size_t)(n.T + 2) * n.N * arl::HID * 4, S(s));
     if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_cbuf, 0, (size_t)(n.T + 2) * n.N * arl::HID * 4, S(s));

@@ -104,7 +104,7 @@ struct Net {
   int64_t ws_bytes;
   int64_t w_ctl, w_frames, w_nvalid, w_reset, w_rewards, w_dones, w_a1, w_a2, w_hfc, w_gates, w_hbuf,
       w_cbuf, w_logits, w_probs, w_logp, w_v, w_ent, w_logpa, w_act, w_dlogits, w_dv, w_dh, w_dfc,
-      w_dG, w_dhn, w_dcn, w_da2, w_slab, w_norm, w_loss, w_tick;
+      w_dG, w_dhn, w_dcn, w_da2, w_slab, w_norm, w_loss, w_tick, w_fcb_part = 0, w_fcb_tick = 0;
   int64_t w_a3 = 0, w_da1 = 0, w_da3 = 0;   // Nature head only
   // LSTM recurrent state of pi_and_v on explicit states (A3CLSTM.pi_and_v, a3c_ale.py:55-63):
   // h, c (n, 256), the step's outputs hn, cn, and reset flags (1 = state is None)
@@ -189,6 +189,11 @@ constexpr int FC_SPLIT = 8;   // fc forward split-K (one slice per XCD)
 int fc_fwd_tiles(int n);      // tickets needed for n envs
 hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b, float* slab, int* tickets,
                          float* hfc, hipStream_t s);
+// FC backward (fc_bwd.hip): dW / db straight into the gradient, da2 = (dfc W) * (a2 > 0)
+hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int S, float* gW, float* gb, float* da2,
+                         float* part, int* tick, hipStream_t s);
+int64_t fc_bwd_part_floats(int S);   // workspace of its in-launch split reduction
+int fc_bwd_tickets();                 // int counters, zero before the first launch (re-armed by it)
 hipError_t launch_policy_args(const float* h, int64_t n, const PolicyArgs& pa, hipStream_t s, int hid);
 // policy arguments of a forward on explicit states (arl_forward_states): slot
 // T, a sampled action from Philox stream 1 keyed by a per-call host counter

@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "arl_internal.hpp"
 #include "gemm.hpp"
@@ -82,6 +83,13 @@ struct LstmWB {         // B(s, j) = [x (256) | 1 | h_prev (256, 0 after reset)]
 };
 
 constexpr int BPTT_SPLIT = 4;   // split-K of the BPTT dh GEMM (K = 1024)
+
+// ARL_FC_BWD=gemm: the round-1 FC backward (generic split-K GEMM pair + slab
+// reduce) instead of fc_bwd_kernel -- A/B timing only
+static const bool FC_BWD_GEMM = [] {
+  const char* e = getenv("ARL_FC_BWD");
+  return e != nullptr && e[0] == 'g';
+}();
 
 struct MapResetMask {   // split-K reduce target: out[m][n] = reset[m] ? 0 : v
   float* out; const uint8_t* reset; int ld;
@@ -321,6 +329,8 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   }
   net.w_norm = buf("norm_partials", (int64_t)net.norm_blocks * 8);
   net.w_tick = buf("tickets", (int64_t)fc_fwd_tiles((int)n) * 4);
+  net.w_fcb_part = buf("fc_bwd_partials", NAT ? 0 : fc_bwd_part_floats((int)S) * 4);
+  net.w_fcb_tick = buf("fc_bwd_tickets", NAT ? 0 : (int64_t)fc_bwd_tickets() * 4);
   net.w_loss = buf("loss", n * 2 * 4);
   net.w_eval_h = buf("eval_h", L ? n * HID * 4 : 0);
   net.w_eval_c = buf("eval_c", L ? n * HID * 4 : 0);
@@ -530,8 +540,9 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
     return L ? launch_reduce_grad(slab_l, pl.lstm_w, GATES, 2 * HID + 1,
                                   MapDense{G, net.o_luW, net.o_lub, net.o_llW, HID}, s)
              : hipSuccess;
-  if (part == LEARN_FC_REDUCE)
-    return launch_reduce_grad(slab_f, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s);
+  if (part == LEARN_FC_REDUCE)   // the FC weight gradient is written by fc_bwd_kernel (LEARN_TRUNK)
+    return FC_BWD_GEMM ? launch_reduce_grad(slab_f, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s)
+                       : hipSuccess;
   const float* a2 = net.at<float>(net.w_a2);
   const float* a1 = net.at<float>(net.w_a1);
   float* da2 = net.at<float>(net.w_da2);
@@ -577,10 +588,12 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
                          64),
         s)));
   }
-  // 3. FC: dW (+ bias via ones column), da2 = (dfc W) * (a2 > 0)
-  //    as ONE launch: both are latency-bound and independent, so their
-  //    workgroups share the chip instead of running back to back
-  ARL_TRY((launch_gemm2_nt<64, 64, 32, 2, 4, 512, GM, GM, GK, GM>(   // 8 waves, 2 sub-tiles each
+  // 3. FC: dW + db straight into the gradient and da2 = (dfc W) * (a2 > 0),
+  //    one launch (fc_bwd.hip)
+  if (!FC_BWD_GEMM)
+    return launch_fc_bwd(dfc, a2, P + net.o_fcW, S, G + net.o_fcW, G + net.o_fcb, net.at<float>(net.w_da2),
+                         net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s);
+  ARL_TRY((launch_gemm2_nt<64, 64, 32, 2, 4, 512, GM, GM, GK, GM>(   // 8 waves, 2 sub-tiles each (ARL_FC_BWD=gemm)
       gemm_job<64, 32>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab_f, HID, A2 + 1}, HID, A2 + 1, S, pl.fc_w, 64),
       gemm_job<64, 32>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2}, EpiMask{da2, a2, A2}, S, A2, HID, 1, 64), s)));
   return hipSuccess;
@@ -618,6 +631,9 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
                            net.at<float>(net.w_v) + o, net.at<float>(net.w_ent) + o, nullptr, nullptr, s);
     }
     case STAGE_FC_BWD: {
+      if (!FC_BWD_GEMM)
+        return launch_fc_bwd(net.at<float>(net.w_dfc), a2, P + net.o_fcW, S, G + net.o_fcW, G + net.o_fcb,
+                             net.at<float>(net.w_da2), net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s);
       const Plans pl = make_plans(net);
       const float* dfc = net.at<float>(net.w_dfc);
       ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GM, GM>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab, HID, A2 + 1},
