@@ -61,6 +61,10 @@ class RMSpropAsync:
         on the bound model's device buffers (a3c.py:139).  advance_window:
         also end the lockstep window (arl_optimize_advance)."""
         net = self.target.net
+        if self.anneal_total_steps > 0 and self.n_total_envs <= 0:
+            # global_t per window = (window start + t_max) * n_total_envs: with 0
+            # envs it never moves and the anneal would silently keep lr fixed
+            raise ValueError("anneal_total_steps > 0 needs n_total_envs > 0 (envs over all ranks)")
         self.t += 1
         net.optimize(lr0=self.lr, total_steps=self.anneal_total_steps, n_total=self.n_total_envs,
                      alpha=self.alpha, eps=self.eps, clip=self.clip_threshold, stream=stream,

@@ -4,30 +4,35 @@
 //   dW[j][k] = sum_s dfc[s][j] a2[s][k],  db[j] = sum_s dfc[s][j]
 //   da2[s][k] = (sum_j dfc[s][j] W[j][k]) * (a2[s][k] > 0)
 // (dfc is already masked by hfc > 0).  One launch, two independent jobs:
-//   job A (dW, db): 256 (all j) x 32 (k) tiles -- every dfc row staged once
-//     per tile feeds 256 x 32 outputs, so the LDS-DMA bytes per FLOP stay
-//     under what a CU can stream -- over one of Z contiguous sample ranges.
-//     The Z range partials of a tile meet in the same launch: each workgroup
-//     takes a ticket when its range is done; the first Z - 1 publish their
-//     partial (write-through stores, then a per-tile "published" count), the
-//     last waits for that count, sums the Z partials in range order
-//     (deterministic whatever the arrival order) and writes dW / db straight
-//     into the flat gradient.  The last arriver's own partial never leaves
-//     its registers.  MFMA accumulators restart every 32-sample chunk; chunk
-//     sums are added in f64.  db: the k-tile 0 workgroups add the A fragments
-//     they already hold.
+//   job A (dW, db): 128 (j) x 64 (k) tiles over one of Z contiguous sample
+//     ranges (Z grows with S, ~400 samples a range).  The Z partials of a
+//     tile meet in the same launch: every workgroup publishes its partial
+//     (write-through stores, drained) and then takes a ticket; the holder of
+//     the last ticket sums the Z partials in range order -- deterministic
+//     whatever the arrival order -- straight into the flat gradient (its own
+//     from registers, rounded as published).  No workgroup waits on another.  MFMA
+//     accumulators restart every 128 samples; those sums add in f64.  db
+//     rides on the k-tile 0 workgroups: their n-wave-0 lanes add the A
+//     fragments they already hold.
 //   job B (da2): 128 (s) x 128 (k) tiles over K = 256, ReLU mask in the
-//     epilogue.
+//     epilogue (mask bits prefetched during the k loop, float4 buffer stores).
 // Operands stream HBM/L2 -> LDS by LDS-DMA (global_load_lds dwordx4) into two
-// 36 KB stages (K chunks of 32; the next chunk in flight while the current one
-// feeds the MFMAs); exact f32 MFMA (v_mfma_f32_16x16x4_f32); 512 threads.
-// The DMA writes lane-linear, so the LDS images are XOR-swizzled through the
-// global source address (physical 16-byte chunk = logical chunk ^ key):
-//   job A  A: dfc rows s, 256 floats of j, key 4*(row & 3)         b32 reads, rows kb + q
-//          B: a2 rows s, 32 floats of k,   key 4*((row >> 1) & 1)  b32 reads, rows kb + q
-//   job B  A: dfc rows s, 32 floats of j,  key (row >> 1) & 7      b128 reads (k-permuted)
-//          B: W rows j, 128 floats of k,   key 4*((row >> 2) & 3)  b32 reads, rows 16g + 4q + r
-// so every fragment read is free of bank conflicts.
+// 32 KB stages (K chunks of 32; the next chunk in flight while the current one
+// feeds the MFMAs); exact f32 MFMA (v_mfma_f32_16x16x4_f32); 256 threads, each
+// wave a 64 x 32 (job A) or 64 x 64 (job B) block of 16 x 16 tiles.
+// Fragment reads are wide: one lane's 16-byte read of 4 consecutive m (or n)
+// feeds 4 MFMA tiles whose rows (columns) interleave with stride 4 (8-byte
+// reads: 2 tiles, stride 2).  Job B's A operand is stored k-contiguous and is
+// read 4 consecutive k per lane, with the same k order on the B side.
+// The DMA writes lane-linear, so an LDS image is XOR-swizzled through the
+// global source address (physical 16-byte chunk = logical chunk ^ key) where
+// its read pattern would otherwise conflict:
+//   job A  A: dfc rows s, 128 floats of j   no key             b128 reads, rows kb + q
+//          B: a2 rows s, 64 floats of k     key 8*(row & 1)    b64 reads, rows kb + q
+//   job B  A: dfc rows s, 32 floats of j    key (row >> 1) & 7 b128 reads (k-permuted)
+//          B: W rows j, 128 floats of k     no key             b128 reads, rows 16g + 4q + r
+// (ds_read_b64 serves 32 lanes a cycle over 64 banks, ds_read_b128 16 lanes
+// in the groups {0-3, 12-15, 20-27}, ... -- MI355X_MICROARCH.md, LDS).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -40,16 +45,24 @@ namespace arl {
 
 namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int NT = 512;                 // 8 waves
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int BUF_DWORD3 = 0x00020000;  // raw buffer resource word 3 (gfx9 family): range-checked, no swizzle
+constexpr int OOB = 0x7ffffff0;         // a buffer offset past every range: the access is dropped
+constexpr int NT = 256;                 // 4 waves
 constexpr int NW = NT / 64;
 constexpr int BK = 32;                  // K chunk (rows of a stage)
-constexpr int STAGE = 9216;             // floats per LDS stage (job A: 32 x 256 + 32 x 32)
-constexpr int AK = 32;                  // job A: k columns per tile
-constexpr int NKA = A2 / AK;            // 81 job A tiles per range
+constexpr int STAGE = 8192;             // floats per LDS stage
+constexpr int AJ = 128, AK = 64;        // job A tile: 128 j x 64 k
+constexpr int NJA = HID / AJ;           // 2
+constexpr int NKA = (A2 + AK - 1) / AK; // 41 (the last one half full)
+constexpr int NTA = NJA * NKA;          // 82 job A tiles per range
 constexpr int BM = 128, BN = 128;       // job B tile
 constexpr int NKB = (A2 + BN - 1) / BN; // 21 (the last one a quarter full)
-constexpr int PART = HID * AK + HID;    // floats per published partial (dW tile + db)
-static_assert(A2 % AK == 0 && HID == 256, "tiles");
+constexpr int PART = AJ * AK + AJ;      // floats per published partial (dW tile + db)
+constexpr int FLUSH = 4;                // job A: f32 MFMA sums over 4 chunks (128 samples), then f64
+static_assert(HID % AJ == 0 && HID % BK == 0 && A2 % 4 == 0 && A2 % AK == 32, "tiles");
+static_assert(BK * (AJ + AK) <= STAGE && BM * BK + BK * BN <= STAGE, "stage size");
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -67,17 +80,16 @@ template <int R, int WC, int KEY>
 __device__ inline void stage_tile(float* dst, const float* __restrict__ g, int64_t ld, int row0, int rmax, int col0) {
   constexpr int CPR = WC / 4;                 // chunks per row
   constexpr int NI = R * WC * 4 / 1024;       // 1 KB pieces
-  static_assert(NI % NW == 0 || NI < NW, "pieces per wave");
+  static_assert(NI % NW == 0, "whole pieces per wave");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int it = wave; it < NI; it += NW) {
+  for (int ii = 0; ii < NI / NW; ++ii) {
+    const int it = ii * NW + wave;
     const int i = it * 64 + lane;             // chunk index in the tile image
     const int r = i / CPR, pc = i - r * CPR;
-    int key;
-    if constexpr (KEY == 0) key = 4 * (r & 3);
-    else if constexpr (KEY == 1) key = 4 * ((r >> 1) & 1);
+    int key = 0;
+    if constexpr (KEY == 1) key = 8 * (r & 1);
     else if constexpr (KEY == 2) key = (r >> 1) & 7;
-    else key = 4 * ((r >> 2) & 3);
     const int row = min(row0 + r, rmax);
     const float* src = g + (int64_t)row * ld + col0 + 4 * (pc ^ key);
     __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(dst + it * 256), 16, 0, 0);
@@ -86,219 +98,218 @@ __device__ inline void stage_tile(float* dst, const float* __restrict__ g, int64
 
 struct FcBwdArgs {
   const float* dfc;   // (S, 256)
-  const float* a2;    // (S, 2592)
-  const float* W;     // (256, 2592)
+  const float* a2;    // (S + 1, 2592): job A's last k tile reads 32 floats past a row's end
+  const float* W;     // (256, 2592) followed by more parameters
   int S, Z, kpz;      // job A: Z sample ranges of kpz samples (multiple of BK)
   float* gW;          // (256, 2592)
   float* gb;          // (256)
   float* da2;         // (S, 2592)
-  float* part;        // (NKA, Z, PART) published job A partials (slot z = range z)
-  int* tick;          // (2 * NKA): arrival ticket, published count per k tile
+  float* part;        // (NTA, Z, PART) published job A partials (slot z = range z)
+  int* tick;          // (NTA): arrival tickets per tile
   int b0;             // first job index of this launch (timing experiments)
-  int abl;            // ARL_FC_BWD_ABL bits (timing experiments only): 1 no MFMA, 2 no staging
+  int abl;            // ARL_FC_BWD_ABL bits (timing experiments only): 1 no MFMA, 2 no staging,
+                      // 4 no job A reduction (wrong dW), 8 no job A k loop
 };
 
 // ---------------------------------------------------------------- job A: dW, db
-__device__ void job_dw(const FcBwdArgs& a, int tile, float* lds) {
+__device__ void job_dw(const FcBwdArgs& a, int job, float* lds) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, col = lane & 15;
-  const int kt = tile % NKA, z = tile / NKA;
-  const int k0 = kt * AK;
+  const int wm = wave >> 1, wn = wave & 1;   // wave: 64 j x 32 k
+  const int tile = job % NTA, z = job / NTA;
+  const int kt = tile % NKA, jt = tile / NKA;
+  const int j0 = jt * AJ, k0 = kt * AK;
   const int r0 = z * a.kpz, r1 = min(a.S, r0 + a.kpz);
-  const bool bias = kt == 0;
-  const int nchunks = (r1 - r0 + BK - 1) / BK;
-  double tot[2][2][4];
+  const bool bias = kt == 0 && wn == 0;
+  const int nchunks = (a.abl & 8) ? 0 : max(0, (r1 - r0 + BK - 1) / BK);
+  // m-tile t: rows j = wm*64 + 4 col + t; n-tile u: cols k = wn*32 + 2 col + u
+  double s[4][2][4], sb[4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int t = 0; t < 4; ++t) {
+    sb[t] = 0.0;
 #pragma unroll
-    for (int jj = 0; jj < 2; ++jj)
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) tot[i][jj][e] = 0.0;
-  float bsum[2] = {0.f, 0.f};
+      for (int e = 0; e < 4; ++e) s[t][u][e] = 0.0;
+  }
   auto issue = [&](int c) {
     if (a.abl & 2) return;
     float* st = lds + (c & 1) * STAGE;
-    stage_tile<BK, HID, 0>(st, a.dfc, HID, r0 + c * BK, r1 - 1, 0);          // dfc[s][0..255]
-    stage_tile<BK, AK, 1>(st + BK * HID, a.a2, A2, r0 + c * BK, r1 - 1, k0);  // a2[s][k0..k0+31]
+    stage_tile<BK, AJ, 0>(st, a.dfc, HID, r0 + c * BK, r1 - 1, j0);         // dfc[s][j0 .. j0+127]
+    stage_tile<BK, AK, 1>(st + BK * AJ, a.a2, A2, r0 + c * BK, r1 - 1, k0);  // a2[s][k0 .. k0+63]
   };
+  const int nb = wn * 32 + 2 * col;
+  f32x4 acc[4][2], bs;
   if (nchunks > 0) issue(0);
   for (int c = 0; c < nchunks; ++c) {
-    if (c + 1 < nchunks) {
-      issue(c + 1);
-      // DMA pieces per wave per chunk: 4 of dfc, + 1 of a2 on waves 0..3
-      if (wave < 4) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // one barrier a chunk: past it, every wave has this chunk's DMA landed
+    // (its own pieces drained before the barrier) and has finished reading
+    // the other stage (chunk c - 1), which the next chunk's DMA then fills.
+    // (A third stage, two chunks in flight, measured no faster.)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // (lgkm: chunk c - 1's LDS reads returned)
     barrier_lds();
+    if (c + 1 < nchunks) issue(c + 1);
     const float* As = lds + (c & 1) * STAGE;
-    const float* Bs = As + BK * HID;
+    const float* Bs = As + BK * AJ;
     const int kvalid = r1 - (r0 + c * BK);   // rows >= kvalid: clamped copies, masked to 0
-    f32x4 acc[2][2];
+    if (c % FLUSH == 0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-    for (int ks = 0; ks < ((a.abl & 1) ? 0 : BK / 4); ++ks) {
-      const int r = 4 * ks + q;
-      const bool ok = r < kvalid;
-      float av[2], bv[2];
+        for (int u = 0; u < 2; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      bs = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (!(a.abl & 1)) {
+      // every fragment of the chunk first (counted LDS waits), then the MFMAs
+      f32x4 av[BK / 4];
+      f32x2 bv[BK / 4];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int m = wave * 32 + i * 16 + col;
-        const float v = As[r * HID + (((m >> 2) ^ (4 * q)) << 2) + (m & 3)];
-        av[i] = ok ? v : 0.f;
+      for (int ks = 0; ks < BK / 4; ++ks) {
+        const int r = 4 * ks + q;
+        av[ks] = *reinterpret_cast<const f32x4*>(As + r * AJ + wm * 64 + 4 * col);
+        bv[ks] = *reinterpret_cast<const f32x2*>(Bs + r * AK + (((nb >> 2) ^ (8 * (r & 1))) << 2) + (nb & 3));
+      }
+      if (kvalid < BK) {   // the range's last chunk only
+#pragma unroll
+        for (int ks = 0; ks < BK / 4; ++ks)
+          if (4 * ks + q >= kvalid) av[ks] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int n = jj * 16 + col;
-        bv[jj] = Bs[r * AK + (((n >> 2) ^ (4 * ((r >> 1) & 1))) << 2) + (n & 3)];
-      }
+      for (int ks = 0; ks < BK / 4; ++ks) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[jj], acc[i][jj], 0, 0, 0);
-      if (bias) {
-        bsum[0] = __fadd_rn(bsum[0], av[0]);
-        bsum[1] = __fadd_rn(bsum[1], av[1]);
+          for (int u = 0; u < 2; ++u)
+            acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[ks][t], bv[ks][u], acc[t][u], 0, 0, 0);
+        if (bias) bs += av[ks];
       }
     }
+    if (c % FLUSH == FLUSH - 1 || c == nchunks - 1) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int t = 0; t < 4; ++t) {
+        sb[t] += (double)bs[t];
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj)
+        for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) tot[i][jj][e] += (double)acc[i][jj][e];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier_lds();   // this stage is restaged two chunks on
+          for (int e = 0; e < 4; ++e) s[t][u][e] += (double)acc[t][u][e];
+      }
+    }
   }
-  // this range's partial, rounded to f32 (every range's partial is, whoever arrives last)
-  float p[2][2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) p[i][jj][e] = (float)tot[i][jj][e];
-  float pb[2] = {0.f, 0.f};
+  // C layout (16x16x4): lane (col, q) holds rows 4q + e, column col of each
+  // tile -> j = j0 + wm*64 + 16q + 4e + t, k = k0 + wn*32 + 2col + u
   if (bias) {   // lanes (col, q) hold sums over rows = q (mod 4): fixed-order quarter reduction
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      float v = bsum[i];
-      v = __fadd_rn(v, __shfl_xor(v, 16));
-      pb[i] = __fadd_rn(v, __shfl_xor(v, 32));
+    for (int t = 0; t < 4; ++t) {
+      double v = sb[t];
+      v = v + __shfl_xor(v, 16);
+      sb[t] = v + __shfl_xor(v, 32);
     }
   }
-  // C layout (16x16x4): lane (col, q) holds rows 4q + e of column col
-  auto out_index = [&](int i, int jj, int e) { return (wave * 32 + i * 16 + 4 * q + e) * AK + jj * 16 + col; };
-  if (a.Z > 1) {
+  auto pidx = [&](int t, int u, int e) { return (wm * 64 + 16 * q + 4 * e + t) * AK + wn * 32 + 2 * col + u; };
+  if (a.Z > 1 && !(a.abl & 4)) {
+    // every range publishes into its slot (write-through sc1 stores, drained),
+    // then takes a ticket; the holder of the last ticket sums the slots
+    float* dst = a.part + ((int64_t)tile * a.Z + z) * PART;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          __hip_atomic_store(dst + pidx(t, u, e), (float)s[t][u][e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (bias && q == 0)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        __hip_atomic_store(dst + AJ * AK + wm * 64 + 4 * col + t, (float)sb[t], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
+    __syncthreads();
     int* flag = reinterpret_cast<int*>(lds);   // the stages are free after the k loop's last barrier
     if (tid == 0) {
-      const int t = __hip_atomic_fetch_add(&a.tick[kt], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = t == a.Z - 1;
-    }
-    __syncthreads();   // (no DMA in flight here: its vmcnt(0) is free)
-    const int last = *flag;
-    if (!last) {   // publish into slot z: write-through (sc1) stores, drained, then the count
-      float* dst = a.part + ((int64_t)kt * a.Z + z) * PART;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            __hip_atomic_store(dst + out_index(i, jj, e), p[i][jj][e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (bias && q == 0)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          __hip_atomic_store(dst + HID * AK + wave * 32 + i * 16 + col, pb[i], __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
-      __syncthreads();
-      if (tid == 0) __hip_atomic_fetch_add(&a.tick[NKA + kt], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-    // last arriver: wait until the other Z - 1 partials are published (their
-    // workgroups already hold a ticket, so they are resident); bounded spin
-    if (tid == 0) {
-      for (int spin = 0; spin < (1 << 24); ++spin) {
-        if (__hip_atomic_load(&a.tick[NKA + kt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.Z - 1) break;
-        __builtin_amdgcn_s_sleep(2);
-      }
+      const int tk = __hip_atomic_fetch_add(&a.tick[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = tk == a.Z - 1;
     }
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // every partial load below is sc1
+    if (!*flag) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // every slot load below is sc1
   }
-  // sum the Z partials in range order (own range from registers), f64
-  double s[2][2][4];
-  double sb[2] = {0.0, 0.0};
+  // sum the Z partials in range order (own range from registers, rounded as
+  // published), f64; two slots' loads in flight at a time
+  double o[4][2][4], ob[4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int t = 0; t < 4; ++t) {
+    ob[t] = 0.0;
 #pragma unroll
-    for (int jj = 0; jj < 2; ++jj)
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) s[i][jj][e] = 0.0;
-  for (int zz = 0; zz < a.Z; ++zz) {
-    // a whole slot's values into registers first (one branch per slot, all
-    // loads in flight together), then the ordered f64 adds
-    float v[2][2][4], vb[2];
-    if (zz == z) {
+      for (int e = 0; e < 4; ++e) o[t][u][e] = 0.0;
+  }
+  for (int z2 = 0; z2 < a.Z; z2 += 2) {
+    float v[2][4][2][4], vb[2][4];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        vb[i] = pb[i];
+    for (int h = 0; h < 2; ++h) {
+      const int zz = min(z2 + h, a.Z - 1);
+      const float* src = a.part + ((int64_t)tile * a.Z + zz) * PART;
+      if (zz == z) {   // one wave-uniform branch per slot: every load of a slot in flight together
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
+        for (int t = 0; t < 4; ++t) {
+          vb[h][t] = (float)sb[t];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[i][jj][e] = p[i][jj][e];
-      }
-    } else {
-      const float* src = a.part + ((int64_t)kt * a.Z + zz) * PART;
+          for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        vb[i] = __hip_atomic_load(src + HID * AK + wave * 32 + i * 16 + col, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
+            for (int e = 0; e < 4; ++e) v[h][t][u][e] = (float)s[t][u][e];
+        }
+      } else {
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
+        for (int t = 0; t < 4; ++t) {
+          vb[h][t] = __hip_atomic_load(src + AJ * AK + wm * 64 + 4 * col + t, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);   // (garbage off the bias waves: unused)
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            v[i][jj][e] = __hip_atomic_load(src + out_index(i, jj, e), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              v[h][t][u][e] = __hip_atomic_load(src + pidx(t, u, e), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      sb[i] += (double)vb[i];
+    for (int h = 0; h < 2; ++h) {
+      if (z2 + h >= a.Z) break;
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj)
+      for (int t = 0; t < 4; ++t) {
+        ob[t] += (double)vb[h][t];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) s[i][jj][e] += (double)v[i][jj][e];
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[t][u][e] += (double)v[h][t][u][e];
+      }
     }
   }
+  const int k = k0 + wn * 32 + 2 * col;
+  if (k < A2) {   // the last k tile is half full (k even, A2 even: a pair is all in or out)
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj)
+    for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int j = wave * 32 + i * 16 + 4 * q + e;
-        a.gW[(int64_t)j * A2 + k0 + jj * 16 + col] = (float)s[i][jj][e];
+        const int j = j0 + wm * 64 + 16 * q + 4 * e + t;
+        float2 w;
+        w.x = (float)o[t][0][e];
+        w.y = (float)o[t][1][e];
+        *reinterpret_cast<float2*>(a.gW + (int64_t)j * A2 + k) = w;
       }
+  }
   if (bias && q == 0)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) a.gb[wave * 32 + i * 16 + col] = (float)sb[i];
-  if (a.Z > 1 && tid == 0) {   // re-arm for the next launch (a captured graph replays this one)
-    __hip_atomic_store(&a.tick[kt], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&a.tick[NKA + kt], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+    for (int t = 0; t < 4; ++t) a.gb[j0 + wm * 64 + 4 * col + t] = (float)ob[t];
+  if (a.Z > 1 && tid == 0 && !(a.abl & 4))   // re-arm for the next launch (a captured graph replays this one)
+    __hip_atomic_store(&a.tick[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------- job B: da2
 __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, col = lane & 15;
-  const int wm = wave >> 1, wn = wave & 1;   // wave: 32 s x 64 k
+  const int wm = wave >> 1, wn = wave & 1;   // wave: 64 s x 64 k
   const int kt = tile % NKB, st = tile / NKB;
   const int s0 = st * BM, k0 = kt * BN;
   constexpr int NCH = HID / BK;              // 8 chunks of 32 j
@@ -306,108 +317,133 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
     if (a.abl & 2) return;
     float* sg = lds + (c & 1) * STAGE;
     stage_tile<BM, BK, 2>(sg, a.dfc + c * BK, HID, s0, a.S - 1, 0);                    // dfc[s][j]
-    stage_tile<BK, BN, 3>(sg + BM * BK, a.W + (int64_t)c * BK * A2, A2, 0, BK - 1, k0);  // W[j][k0..k0+127]
+    stage_tile<BK, BN, 0>(sg + BM * BK, a.W + (int64_t)c * BK * A2, A2, 0, BK - 1, k0);  // W[j][k0..k0+127]
   };
-  f32x4 acc[2][4];
+  f32x4 acc[4][4];                           // m-tile i: rows 16 i + col; n-tile u: cols 4 col + u
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < 4; ++u) acc[i][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // ReLU mask of the tile (a2 > 0), one bit per output element -- bit 4e + u
+  // of mb[i] -- loaded a 16-row band per chunk during chunks 0..3 so that no
+  // load round trip is left for the epilogue.  Out-of-range rows / columns
+  // read 0 through the buffer's range check.
+  const int k = k0 + wn * 64 + 4 * col;
+  const bool kin = k < A2;                   // A2 % 4 == 0: a 4-run is all in or all out
+  const int rows = min(BM, a.S - s0);
+  const __amdgpu_buffer_rsrc_t msk = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.a2) + (int64_t)s0 * A2,
+                                                                       0, rows * A2 * 4, BUF_DWORD3);
+  unsigned mb[4] = {0u, 0u, 0u, 0u};
+  f32x4 mraw[4];
   issue(0);
-#pragma unroll 1
+#pragma unroll
   for (int c = 0; c < NCH; ++c) {
+    if (c + 1 < NCH) issue(c + 1);
+    if (c >= 1 && c <= 4) {   // the band loaded one chunk ago (the compiler's own vmcnt wait)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) mb[c - 1] |= (mraw[e][u] > 0.f ? 1u : 0u) << (4 * e + u);
+    }
+    if (c < 4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = wm * 64 + 16 * c + 4 * q + e;
+        mraw[e] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(msk, kin ? (row * A2 + k) * 4 : OOB, 0, 0));
+      }
+    }
+    // this chunk's DMA done: the next chunk's (4 + 4 pieces a wave) and this chunk's mask band may still fly
     if (c + 1 < NCH) {
-      issue(c + 1);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // 2 + 2 DMA pieces per wave per chunk
+      if (c < 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     barrier_lds();
     const float* As = lds + (c & 1) * STAGE;
     const float* Bs = As + BM * BK;
+    if (!(a.abl & 1)) {
+      // every fragment of the chunk first (counted LDS waits), then the MFMAs
+      f32x4 av[BK / 16][4], bv[BK / 16][4];
 #pragma unroll
-    for (int g = 0; g < ((a.abl & 1) ? 0 : BK / 16); ++g) {
-      f32x4 av[2];
+      for (int g = 0; g < BK / 16; ++g) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int m = wm * 32 + i * 16 + col;
-        av[i] = *reinterpret_cast<const f32x4*>(As + m * BK + (((4 * g + q) ^ ((m >> 1) & 7)) << 2));
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * g + 4 * q + r;
-        float bv[4];
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int n = wn * 64 + jj * 16 + col;
-          bv[jj] = Bs[row * BN + (((n >> 2) ^ (4 * q)) << 2) + (n & 3)];
+        for (int i = 0; i < 4; ++i) {
+          const int m = wm * 64 + i * 16 + col;
+          av[g][i] = *reinterpret_cast<const f32x4*>(As + m * BK + (((4 * g + q) ^ ((m >> 1) & 7)) << 2));
         }
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj)
-            acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][r], bv[jj], acc[i][jj], 0, 0, 0);
+        for (int r = 0; r < 4; ++r)   // k = 16 g + 4 q + r on both operands
+          bv[g][r] = *reinterpret_cast<const f32x4*>(Bs + (16 * g + 4 * q + r) * BN + wn * 64 + 4 * col);
       }
+#pragma unroll
+      for (int g = 0; g < BK / 16; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              acc[i][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][i][r], bv[g][r][u], acc[i][u], 0, 0, 0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     barrier_lds();
   }
-  // ReLU mask: every a2 value loaded first (clamped rows / columns, all in
-  // flight at once), then the guarded stores
-  float mk[2][4][4];
+  // lane (col, q) holds s = s0 + wm*64 + 16 i + 4 q + e, k = k0 + wn*64 + 4 col + u:
+  // 4 consecutive k per (i, e).  Straight-line buffer stores whose
+  // out-of-range lanes (s >= S, k >= A2) the buffer's range check drops -- no
+  // per-store branch, so no store waits for the one before it.
+  const __amdgpu_buffer_rsrc_t out =
+      __builtin_amdgcn_make_buffer_rsrc(a.da2 + (int64_t)s0 * A2, 0, rows * A2 * 4, BUF_DWORD3);
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int k = min(k0 + wn * 64 + jj * 16 + col, A2 - 1);
+    for (int e = 0; e < 4; ++e) {
+      const int row = wm * 64 + 16 * i + 4 * q + e;
+      f32x4 o;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int s = min(s0 + wm * 32 + i * 16 + 4 * q + e, a.S - 1);
-        mk[i][jj][e] = a.a2[(int64_t)s * A2 + k];
-      }
-    }
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int k = k0 + wn * 64 + jj * 16 + col;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int s = s0 + wm * 32 + i * 16 + 4 * q + e;
-        if (s < a.S && k < A2) a.da2[(int64_t)s * A2 + k] = mk[i][jj][e] > 0.f ? acc[i][jj][e] : 0.f;
-      }
+      for (int u = 0; u < 4; ++u) o[u] = (mb[i] >> (4 * e + u)) & 1u ? acc[i][u][e] : 0.f;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), out, kin ? (row * A2 + k) * 4 : OOB, 0, 0);
     }
 }
 
-__global__ void __launch_bounds__(NT)
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2)))
 fc_bwd_kernel(FcBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];   // 72 KB, the only LDS object
+  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];   // 64 KB, the only LDS object
   const int b = a.b0 + blockIdx.x;
-  const int na = NKA * a.Z;
+  const int na = NTA * a.Z;
   if (b < na) job_dw(a, b, lds);
   else job_da2(a, b - na, lds);
 }
 
-int fc_bwd_ranges(int S) { return std::max(1, std::min(3, (S + 4 * BK - 1) / (4 * BK))); }
+// ~400 samples per job A range, at most 16 ranges
+int fc_bwd_ranges(int S) {
+  static const char* zs = getenv("ARL_FC_BWD_Z");   // timing experiments only
+  if (zs) return std::max(1, std::min(16, atoi(zs)));
+  return std::max(1, std::min(16, (S + 200) / 400));
+}
 }  // namespace
 
-int64_t fc_bwd_part_floats(int S) { return (int64_t)NKA * fc_bwd_ranges(S) * PART; }
-int fc_bwd_tickets() { return 2 * NKA; }
+int64_t fc_bwd_part_floats(int S) { return (int64_t)NTA * fc_bwd_ranges(S) * PART; }
+int fc_bwd_tickets() { return NTA; }
 
-// Job B's last k tile stages W columns 2560..2687: the floats past the end of
-// W belong to the next parameters of the flat buffer (never stored).
+// Job A's last k tile stages a2 columns 2560..2623 and job B's last one W
+// columns 2560..2687: the floats past a row's end are the next row's (a2 has
+// the bootstrap slot after the window's S rows) or the next parameters' (W),
+// and are never stored.
 hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int S, float* gW, float* gb, float* da2,
                          float* part, int* tick, hipStream_t s) {
   if (S <= 0) return hipSuccess;
   const int Z = fc_bwd_ranges(S);
   int kpz = (S + Z - 1) / Z;
   kpz = (kpz + BK - 1) / BK * BK;
-  const int na = NKA * Z, nb = ((S + BM - 1) / BM) * NKB;
-  // ARL_FC_BWD_JOBS=a / b: launch one job alone (timing experiments only)
+  const int na = NTA * Z, nb = ((S + BM - 1) / BM) * NKB;
+  // ARL_FC_BWD_JOBS=a / b: launch one job alone; ARL_FC_BWD_ABL: ablations (timing experiments only)
   static const char* only = getenv("ARL_FC_BWD_JOBS");
+  static const char* abl = getenv("ARL_FC_BWD_ABL");
   const int b0 = (only && only[0] == 'b') ? na : 0;
   const int grid = (only && only[0] == 'a') ? na : (only && only[0] == 'b') ? nb : na + nb;
-  static const char* abl = getenv("ARL_FC_BWD_ABL");
   FcBwdArgs args{dfc, a2, W, S, Z, kpz, gW, gb, da2, part, tick, b0, abl ? atoi(abl) : 0};
   hipLaunchKernelGGL(fc_bwd_kernel, dim3(grid), dim3(NT), 0, s, args);
   return hipGetLastError();

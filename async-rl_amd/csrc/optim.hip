@@ -80,7 +80,9 @@ rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __res
   __shared__ double sh[8];
   if (c.ctl != nullptr && c.total > 0) {
     const int64_t gt = (c.ctl[c.ctl_idx] + c.t_max) * c.n_total;
-    c.lr = (float)(((double)(c.total - gt - 1) / (double)c.total) * c.lr0);
+    // clamped at 0: the reference stops training once global_t passes the
+    // step budget (run_a3c.py:64-68); a replay past it must not ascend
+    c.lr = (float)(((double)max(c.total - gt - 1, (int64_t)0) / (double)c.total) * c.lr0);
   }
   const int64_t n4 = n >> 2;
   float4* p4 = reinterpret_cast<float4*>(p);
