@@ -190,8 +190,18 @@ int fc_fwd_tiles(int n);      // tickets needed for n envs
 hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b, float* slab, int* tickets,
                          float* hfc, hipStream_t s);
 // FC backward (fc_bwd.hip): dW / db straight into the gradient, da2 = (dfc W) * (a2 > 0)
+// weight gradients of the policy / value heads (a3c.py:126-130 through
+// policy.py / v_function.py Linear layers): rows a < A from dlogits, row A
+// from dv, over the S samples of h (fc_bwd's job C)
+struct HeadsDW {
+  const float* dl;   // (S, A)
+  const float* dv;   // (S)
+  const float* h;    // (S, HID) fed to the heads
+  int A;
+  float *gWpi, *gbpi, *gWv, *gbv;
+};
 hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int S, float* gW, float* gb, float* da2,
-                         float* part, int* tick, hipStream_t s);
+                         float* part, int* tick, hipStream_t s, const HeadsDW* heads = nullptr);
 int64_t fc_bwd_part_floats(int S);   // workspace of its in-launch split reduction
 int fc_bwd_tickets();                 // int counters, zero before the first launch (re-armed by it)
 hipError_t launch_policy_args(const float* h, int64_t n, const PolicyArgs& pa, hipStream_t s, int hid);
@@ -230,5 +240,12 @@ hipError_t launch_returns(const float* rewards, const uint8_t* dones, const floa
                           const float* logp, const int32_t* act, int T, int n, int A, double gamma, float beta,
                           float vcoef, int clip_reward, float* dlogits, float* dv, float* loss, hipStream_t s,
                           int64_t* ctl_snap = nullptr, float pcoef = 1.f, int keep_scale = 0);
+// launch_returns + the heads' backward dh = dlogits Wpi + dv Wv (times
+// mask > 0 when mask is given) for hidden width HID, one launch (T <= 64)
+hipError_t launch_returns_heads(const float* rewards, const uint8_t* dones, const float* v, const float* probs,
+                                const float* logp, const int32_t* act, int T, int n, int A, double gamma, float beta,
+                                float vcoef, int clip_reward, float* dlogits, float* dv, float* loss, hipStream_t s,
+                                int64_t* ctl_snap, float pcoef, int keep_scale, const float* Wpi, const float* Wv,
+                                const float* mask, float* dh);
 
 }  // namespace arl

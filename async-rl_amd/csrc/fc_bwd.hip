@@ -3,7 +3,7 @@
 // (a3c.py:129-130):
 //   dW[j][k] = sum_s dfc[s][j] a2[s][k],  db[j] = sum_s dfc[s][j]
 //   da2[s][k] = (sum_j dfc[s][j] W[j][k]) * (a2[s][k] > 0)
-// (dfc is already masked by hfc > 0).  One launch, two independent jobs:
+// (dfc is already masked by hfc > 0).  One launch, three independent jobs:
 //   job A (dW, db): 128 (j) x 64 (k) tiles over one of Z contiguous sample
 //     ranges (Z grows with S, ~400 samples a range).  The Z partials of a
 //     tile meet in the same launch: every workgroup publishes its partial
@@ -16,6 +16,9 @@
 //     fragments they already hold.
 //   job B (da2): 128 (s) x 128 (k) tiles over K = 256, ReLU mask in the
 //     epilogue (mask bits prefetched during the k loop, float4 buffer stores).
+//   job C (optional): the policy / value heads' weight gradients, a small
+//     f64 VALU reduction over S that runs beside A and B instead of as two
+//     launches of its own (job_heads below).
 // Operands stream HBM/L2 -> LDS by LDS-DMA (global_load_lds dwordx4) into two
 // 32 KB stages (K chunks of 32; the next chunk in flight while the current one
 // feeds the MFMAs); exact f32 MFMA (v_mfma_f32_16x16x4_f32); 256 threads, each
@@ -106,6 +109,8 @@ struct FcBwdArgs {
   float* da2;         // (S, 2592)
   float* part;        // (NTA, Z, PART) published job A partials (slot z = range z)
   int* tick;          // (NTA): arrival tickets per tile
+  HeadsDW hd;         // job C (hd.dl null: none)
+  int nc;             // job C workgroups
   int b0;             // first job index of this launch (timing experiments)
   int abl;            // ARL_FC_BWD_ABL bits (timing experiments only): 1 no MFMA, 2 no staging,
                       // 4 no job A reduction (wrong dW), 8 no job A k loop
@@ -408,13 +413,77 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
     }
 }
 
+// ---------------------------------------------------------------- job C: heads dW, db
+// Workgroup jt: columns j = 16 jt + (tid & 15) of h; the 16 thread rows
+// p = tid >> 4 take the samples s = p (mod 16), four samples' loads in flight
+// before their FMAs, and accumulate rows a = 0..A (dlogits columns, then dv)
+// in f64, 8 rows a pass.  The partitions meet in LDS and are summed in order.
+// Column 16 of workgroup 0 is the bias (h = 1), summed by its column-0 threads.
+constexpr int CW = 16, NP = NT / CW;     // 16 columns x 16 sample partitions
+constexpr int NJC = HID / CW;            // 16 workgroups
+__device__ void job_heads(const FcBwdArgs& a, int jt, float* lds) {
+  const HeadsDW& d = a.hd;
+  const int tid = threadIdx.x, jj = tid % CW, p = tid / CW;
+  const int j = jt * CW + jj;
+  const int R = d.A + 1;
+  const bool bias = jt == 0 && jj == 0;
+  double* red = reinterpret_cast<double*>(lds);   // [NP][8][CW + 1] partials
+  for (int a0 = 0; a0 < R; a0 += 8) {
+    double acc[8], accb[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) acc[r] = accb[r] = 0.0;
+    for (int s0 = p; s0 < a.S; s0 += 4 * NP) {
+      float hv[4], gv[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {   // every load first (clamped rows, zero weight past S)
+        const int s = min(s0 + u * NP, a.S - 1);
+        const float ok = s0 + u * NP < a.S ? 1.f : 0.f;
+        hv[u] = d.h[(int64_t)s * HID + j] * ok;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int row = min(a0 + r, d.A);
+          gv[u][r] = (row < d.A ? d.dl[(int64_t)s * d.A + row] : d.dv[s]) * ok;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          acc[r] = fma((double)gv[u][r], (double)hv[u], acc[r]);
+          accb[r] += (double)gv[u][r];
+        }
+    }
+    __syncthreads();   // the previous pass's partials are consumed
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      red[(p * 8 + r) * (CW + 1) + jj] = acc[r];
+      if (bias) red[(p * 8 + r) * (CW + 1) + CW] = accb[r];
+    }
+    __syncthreads();
+    for (int i = tid; i < 8 * (CW + 1); i += NT) {   // (row, column) of this pass, partitions in order
+      const int r = i / (CW + 1), c = i - r * (CW + 1), row = a0 + r;
+      if (row >= R || (c == CW && jt != 0)) continue;
+      double v = 0.0;
+      for (int q = 0; q < NP; ++q) v += red[(q * 8 + r) * (CW + 1) + c];
+      if (c < CW) {
+        if (row < d.A) d.gWpi[(int64_t)row * HID + jt * CW + c] = (float)v;
+        else d.gWv[jt * CW + c] = (float)v;
+      } else {
+        if (row < d.A) d.gbpi[row] = (float)v;
+        else d.gbv[0] = (float)v;
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2)))
 fc_bwd_kernel(FcBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];   // 64 KB, the only LDS object
   const int b = a.b0 + blockIdx.x;
   const int na = NTA * a.Z;
-  if (b < na) job_dw(a, b, lds);
-  else job_da2(a, b - na, lds);
+  if (b < a.nc) job_heads(a, b, lds);   // first: the smallest, longest-latency jobs
+  else if (b < a.nc + na) job_dw(a, b - a.nc, lds);
+  else job_da2(a, b - a.nc - na, lds);
 }
 
 // ~400 samples per job A range, at most 16 ranges
@@ -433,7 +502,7 @@ int fc_bwd_tickets() { return NTA; }
 // the bootstrap slot after the window's S rows) or the next parameters' (W),
 // and are never stored.
 hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int S, float* gW, float* gb, float* da2,
-                         float* part, int* tick, hipStream_t s) {
+                         float* part, int* tick, hipStream_t s, const HeadsDW* heads) {
   if (S <= 0) return hipSuccess;
   const int Z = fc_bwd_ranges(S);
   int kpz = (S + Z - 1) / Z;
@@ -442,9 +511,12 @@ hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int 
   // ARL_FC_BWD_JOBS=a / b: launch one job alone; ARL_FC_BWD_ABL: ablations (timing experiments only)
   static const char* only = getenv("ARL_FC_BWD_JOBS");
   static const char* abl = getenv("ARL_FC_BWD_ABL");
-  const int b0 = (only && only[0] == 'b') ? na : 0;
-  const int grid = (only && only[0] == 'a') ? na : (only && only[0] == 'b') ? nb : na + nb;
-  FcBwdArgs args{dfc, a2, W, S, Z, kpz, gW, gb, da2, part, tick, b0, abl ? atoi(abl) : 0};
+  if (heads != nullptr && (heads->A < 1 || heads->dl == nullptr)) return hipErrorInvalidValue;
+  const int nc = heads != nullptr ? NJC : 0;
+  const int b0 = (only && only[0] == 'b') ? nc + na : (only && only[0] == 'a') ? nc : 0;
+  const int grid = (only && only[0] == 'a') ? na : (only && only[0] == 'b') ? nb : nc + na + nb;
+  FcBwdArgs args{dfc, a2, W, S, Z, kpz, gW, gb, da2, part, tick, heads ? *heads : HeadsDW{}, nc, b0,
+                 abl ? atoi(abl) : 0};
   hipLaunchKernelGGL(fc_bwd_kernel, dim3(grid), dim3(NT), 0, s, args);
   return hipGetLastError();
 }

@@ -91,6 +91,12 @@ static const bool FC_BWD_GEMM = [] {
   return e != nullptr && e[0] == 'g';
 }();
 
+// ARL_RETURNS_SPLIT=1: returns and the heads' dh as two launches -- A/B timing only
+static const bool RETURNS_SPLIT = [] {
+  const char* e = getenv("ARL_RETURNS_SPLIT");
+  return e != nullptr && e[0] == '1';
+}();
+
 struct MapResetMask {   // split-K reduce target: out[m][n] = reset[m] ? 0 : v
   float* out; const uint8_t* reset; int ld;
   __device__ void put(int m, int n, float v) const { out[(int64_t)m * ld + n] = reset[m] ? 0.f : v; }
@@ -522,13 +528,26 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
   float* dfc = net.at<float>(net.w_dfc);
   // 1. n-step returns + loss gradient wrt logits / v (a3c.py:82-126); also
   //    snapshots the step counter for the optimizer's fused advance
+  //    and, in the same launch, the heads' backward dh (FF: dfc = dh * (hfc > 0))
+  if (part == LEARN_RETURNS && RETURNS_SPLIT) {
+    ARL_TRY(launch_returns(net.at<float>(net.w_rewards), net.at<uint8_t>(net.w_dones), net.at<float>(net.w_v),
+                           net.at<float>(net.w_probs), net.at<float>(net.w_logp), net.at<int32_t>(net.w_act), T, n, A,
+                           gamma, beta, vcoef, clip_reward, dl, dv, net.at<float>(net.w_loss), s,
+                           net.at<int64_t>(net.w_ctl), net.pi_coef, net.keep_scale));
+    return launch_heads_bwd(dl, dv, P + net.o_piW, P + net.o_vW, A, HID, L ? nullptr : hfc,
+                            L ? net.at<float>(net.w_dh) : dfc, S, s);
+  }
   if (part == LEARN_RETURNS)
-    return launch_returns(net.at<float>(net.w_rewards), net.at<uint8_t>(net.w_dones), net.at<float>(net.w_v),
-                          net.at<float>(net.w_probs), net.at<float>(net.w_logp), net.at<int32_t>(net.w_act), T, n, A,
-                          gamma, beta, vcoef, clip_reward, dl, dv, net.at<float>(net.w_loss), s,
-                          net.at<int64_t>(net.w_ctl), net.pi_coef, net.keep_scale);
-  // heads: weight grads (ones column = bias) and dh
+    return launch_returns_heads(net.at<float>(net.w_rewards), net.at<uint8_t>(net.w_dones), net.at<float>(net.w_v),
+                                net.at<float>(net.w_probs), net.at<float>(net.w_logp), net.at<int32_t>(net.w_act), T,
+                                n, A, gamma, beta, vcoef, clip_reward, dl, dv, net.at<float>(net.w_loss), s,
+                                net.at<int64_t>(net.w_ctl), net.pi_coef, net.keep_scale, P + net.o_piW, P + net.o_vW,
+                                L ? nullptr : hfc, L ? net.at<float>(net.w_dh) : dfc);
+  // heads: weight grads (ones column = bias) and dh.  With the fused FC
+  // backward the weight grads are its job C (LEARN_TRUNK): nothing here.
+  const HeadsDW heads{dl, dv, hheads, A, G + net.o_piW, G + net.o_pib, G + net.o_vW, G + net.o_vb};
   if (part == LEARN_HEADS_DW) {
+    if (!FC_BWD_GEMM) return hipSuccess;
     ARL_TRY((launch_gemm<16, 64, 32, 1, 4, GS, GM>(HeadsGA{dl, dv, A}, OnesColB{hheads, HID},
                                                    EpiSlab{slab_h, A + 1, HID + 1}, A + 1, HID + 1, S, pl.heads_w,
                                                    s)));
@@ -554,8 +573,7 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
                            net.at<int64_t>(net.w_ctl), n, net.R, S, a1, da2, P + net.o_c2W, slab, G + net.o_c2W,
                            G + net.o_c2b, G + net.o_c1W, G + net.o_c1b, s, /*reduce=*/true, net.layout);
   if (part != LEARN_TRUNK) return hipErrorInvalidValue;
-  ARL_TRY(launch_heads_bwd(dl, dv, P + net.o_piW, P + net.o_vW, A, HID, L ? nullptr : hfc,
-                           L ? net.at<float>(net.w_dh) : dfc, S, s));
+  // (the heads' dh was written by LEARN_RETURNS)
   // 2. LSTM: truncated BPTT over the window, gate weight gradients, dfc
   if (L) {
     const float* gates = net.at<float>(net.w_gates);
@@ -592,7 +610,7 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
   //    one launch (fc_bwd.hip)
   if (!FC_BWD_GEMM)
     return launch_fc_bwd(dfc, a2, P + net.o_fcW, S, G + net.o_fcW, G + net.o_fcb, net.at<float>(net.w_da2),
-                         net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s);
+                         net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s, &heads);
   ARL_TRY((launch_gemm2_nt<64, 64, 32, 2, 4, 512, GM, GM, GK, GM>(   // 8 waves, 2 sub-tiles each (ARL_FC_BWD=gemm)
       gemm_job<64, 32>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab_f, HID, A2 + 1}, HID, A2 + 1, S, pl.fc_w, 64),
       gemm_job<64, 32>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2}, EpiMask{da2, a2, A2}, S, A2, HID, 1, 64), s)));
@@ -631,9 +649,14 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
                            net.at<float>(net.w_v) + o, net.at<float>(net.w_ent) + o, nullptr, nullptr, s);
     }
     case STAGE_FC_BWD: {
-      if (!FC_BWD_GEMM)
+      if (!FC_BWD_GEMM) {   // with the heads' weight gradients (job C), as in LEARN_TRUNK
+        const float* hh = net.arch == ARCH_LSTM ? net.at<float>(net.w_hbuf) + (int64_t)n * HID : hfc;
+        const HeadsDW heads{net.at<float>(net.w_dlogits), net.at<float>(net.w_dv), hh, net.A, G + net.o_piW,
+                            G + net.o_pib, G + net.o_vW, G + net.o_vb};
         return launch_fc_bwd(net.at<float>(net.w_dfc), a2, P + net.o_fcW, S, G + net.o_fcW, G + net.o_fcb,
-                             net.at<float>(net.w_da2), net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s);
+                             net.at<float>(net.w_da2), net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s,
+                             &heads);
+      }
       const Plans pl = make_plans(net);
       const float* dfc = net.at<float>(net.w_dfc);
       ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GM, GM>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab, HID, A2 + 1},

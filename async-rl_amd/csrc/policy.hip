@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "arl_internal.hpp"
 #include "policy_rows.hpp"
 
@@ -127,85 +129,241 @@ hipError_t launch_policy(const float* h, int64_t n, const float* Wpi, const floa
 // summed in the reference's order (t = T-1 .. 0) through LDS.  ctl != null:
 // also snapshot the step counter (CTL_STEP_SNAP) for the optimizer's fused
 // advance.  Block = EB envs x T steps (EB = 256 / T), env fastest.
-__global__ void __launch_bounds__(256)
-returns_kernel(const float* __restrict__ rewards, const uint8_t* __restrict__ dones, const float* __restrict__ v,
-               const float* __restrict__ probs, const float* __restrict__ logp, const int32_t* __restrict__ act, int T,
-               int n, int A, double gamma, float beta, float vcoef, int clip_reward, float* __restrict__ dlogits,
-               float* __restrict__ dv, float* __restrict__ loss, int64_t* __restrict__ ctl, float pcoef,
-               int keep_scale) {
-  __shared__ float lpi[256], lv[256];
-  if (ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) ctl[CTL_STEP_SNAP] = ctl[CTL_STEP];
-  const int EB = 256 / T;
-  const int tid = threadIdx.x, t = tid / EB, el = tid - t * EB;
-  const int e = blockIdx.x * EB + el;
-  const bool on = t < T && e < n;
-  if (on) {
-    const int64_t i = (int64_t)t * n + e;
-    float* dl = dlogits + i * A;
-    if (dones[i] & 2) {   // past the end of this window
-      for (int k = 0; k < A; ++k) dl[k] = 0.f;
-      dv[i] = 0.f;
-      lpi[tid] = 0.f;
-      lv[tid] = 0.f;
-    } else {
-      double R = (double)v[(int64_t)T * n + e];
-      int seg_end = -1;   // first terminal at or after t: closes t's segment
-      for (int tt = T - 1; tt >= t; --tt) {
-        const int64_t j = (int64_t)tt * n + e;
-        double r = (double)rewards[j];
-        if (clip_reward) r = r < -1.0 ? -1.0 : (r > 1.0 ? 1.0 : r);
-        if (dones[j] & 1) {
+struct ReturnsArgs {
+  const float* rewards;
+  const uint8_t* dones;
+  const float* v;
+  const float* probs;
+  const float* logp;
+  const int32_t* act;
+  int T, n, A;
+  double gamma;
+  float beta, vcoef, pcoef;
+  int clip_reward, keep_scale;
+  float* dlogits;
+  float* dv;
+  float* loss;
+  int64_t* ctl;
+};
+
+// dlogits / dv of (step t, env e); returns the two loss terms of the step
+// (pi term without the sign, v term) through lpi / lv
+// Every load of the thread is issued before the arithmetic that uses it
+// (register arrays with static indices, clamped offsets): a load after a
+// store the compiler cannot disambiguate, or under a per-lane branch, would
+// wait for the one before it.  Windows up to RW steps keep their rewards /
+// dones in registers; longer ones loop over memory.
+constexpr int RW = 8;
+struct RetIn {   // everything returns_one reads of step (t, e)
+  float pr[MAXA], lp[MAXA], rw[RW];
+  int dn[RW];
+  float vboot, vi;
+  int ac, di;
+};
+__device__ inline void returns_load(const ReturnsArgs& a, int t, int e, RetIn& in) {
+  const int T = a.T, n = a.n, A = a.A;
+  const int64_t i = (int64_t)t * n + e;
+#pragma unroll
+  for (int k = 0; k < MAXA; ++k) {
+    const int64_t o = i * A + min(k, A - 1);
+    in.pr[k] = a.probs[o];
+    in.lp[k] = a.logp[o];
+  }
+#pragma unroll
+  for (int k = 0; k < RW; ++k) {
+    const int64_t o = (int64_t)min(k, T - 1) * n + e;
+    in.rw[k] = a.rewards[o];
+    in.dn[k] = a.dones[o];
+  }
+  in.vboot = a.v[(int64_t)T * n + e];
+  in.vi = a.v[i];
+  in.ac = a.act[i];
+  in.di = a.dones[i];
+}
+__device__ inline void returns_compute(const ReturnsArgs& a, int t, int e, const RetIn& in, float& lpi, float& lv,
+                                       float* sdl) {
+  const int T = a.T, n = a.n, A = a.A;
+  const int64_t i = (int64_t)t * n + e;
+  const float* pr = in.pr;
+  const float* lp = in.lp;
+  const float* rw = in.rw;
+  const int* dn = in.dn;
+  const float vboot = in.vboot, vi = in.vi;
+  const int ac = in.ac, di = in.di;
+  float* dl = a.dlogits + i * A;
+  if (di & 2) {   // past the end of this window
+    for (int k = 0; k < A; ++k) dl[k] = 0.f;
+    a.dv[i] = 0.f;
+    if (sdl)
+      for (int k = 0; k <= A; ++k) sdl[k] = 0.f;
+    lpi = 0.f;
+    lv = 0.f;
+    return;
+  }
+  auto clip = [&](double r) { return a.clip_reward ? (r < -1.0 ? -1.0 : (r > 1.0 ? 1.0 : r)) : r; };
+  double R = (double)vboot;
+  int seg_end = -1;   // first terminal at or after t: closes t's segment
+  int seg_start = 0;  // first step after the last terminal before t
+  if (T <= RW) {
+#pragma unroll
+    for (int k = RW - 1; k >= 0; --k)
+      if (k < T && k >= t) {
+        if (dn[k] & 1) {
           R = 0.0;
-          seg_end = tt;
+          seg_end = k;
         }
-        R = __dadd_rn(__dmul_rn(R, gamma), r);
+        R = __dadd_rn(__dmul_rn(R, a.gamma), clip((double)rw[k]));
       }
-      float pf = pcoef, vf = vcoef;
-      if (keep_scale && seg_end >= 0) {
-        int seg_start = 0;
-        for (int tt = t - 1; tt >= 0; --tt)
-          if (dones[(int64_t)tt * n + e] & 1) {
-            seg_start = tt + 1;
-            break;
-          }
-        const int len = seg_end - seg_start + 1;
-        if (len < T) {
-          const float factor = (float)((double)T / (double)len);
-          pf = __fmul_rn(pf, factor);
-          vf = __fmul_rn(vf, factor);
-        }
+#pragma unroll
+    for (int k = 0; k < RW; ++k)
+      if (k < t && (dn[k] & 1)) seg_start = k + 1;
+  } else {
+    for (int tt = T - 1; tt >= t; --tt) {
+      const int64_t j = (int64_t)tt * n + e;
+      if (a.dones[j] & 1) {
+        R = 0.0;
+        seg_end = tt;
       }
-      const float Rf = (float)R;
-      const float vi = v[i];
-      const float adv = __fsub_rn(Rf, vi);
-      const float* pr = probs + i * A;
-      const float* lp = logp + i * A;
-      float H = 0.f;
-      for (int k = 0; k < A; ++k) H = __fadd_rn(H, __fmul_rn(pr[k], lp[k]));
-      H = -H;
-      const int a = act[i];
-      for (int k = 0; k < A; ++k) {
-        const float oh = (k == a) ? 1.f : 0.f;
-        const float t1 = __fmul_rn(-adv, __fsub_rn(oh, pr[k]));
-        const float t2 = __fmul_rn(__fmul_rn(beta, pr[k]), __fadd_rn(lp[k], H));
-        dl[k] = __fmul_rn(pf, __fadd_rn(t1, t2));
+      R = __dadd_rn(__dmul_rn(R, a.gamma), clip((double)a.rewards[j]));
+    }
+    for (int tt = t - 1; tt >= 0; --tt)
+      if (a.dones[(int64_t)tt * n + e] & 1) {
+        seg_start = tt + 1;
+        break;
       }
-      const float dvv = __fsub_rn(vi, Rf);
-      dv[i] = __fmul_rn(vf, dvv);
-      lpi[tid] = __fmul_rn(pf, __fadd_rn(__fmul_rn(lp[a], adv), __fmul_rn(beta, H)));
-      lv[tid] = __fmul_rn(vf, __fmul_rn(__fmul_rn(dvv, dvv), 0.5f));
+  }
+  float pf = a.pcoef, vf = a.vcoef;
+  if (a.keep_scale && seg_end >= 0) {
+    const int len = seg_end - seg_start + 1;
+    if (len < T) {
+      const float factor = (float)((double)T / (double)len);
+      pf = __fmul_rn(pf, factor);
+      vf = __fmul_rn(vf, factor);
     }
   }
-  if (loss == nullptr) return;
-  __syncthreads();
-  if (t == 0 && on) {
-    float pi_loss = 0.f, v_loss = 0.f;
-    for (int tt = T - 1; tt >= 0; --tt) {
-      pi_loss = __fsub_rn(pi_loss, lpi[tt * EB + el]);
-      v_loss = __fadd_rn(v_loss, lv[tt * EB + el]);
+  const float Rf = (float)R;
+  const float adv = __fsub_rn(Rf, vi);
+  float H = 0.f, lpa = 0.f;
+#pragma unroll
+  for (int k = 0; k < MAXA; ++k)
+    if (k < A) {
+      H = __fadd_rn(H, __fmul_rn(pr[k], lp[k]));
+      if (k == ac) lpa = lp[k];
     }
-    loss[2 * e] = pi_loss;
-    loss[2 * e + 1] = v_loss;
+  H = -H;
+#pragma unroll
+  for (int k = 0; k < MAXA; ++k)
+    if (k < A) {
+      const float oh = (k == ac) ? 1.f : 0.f;
+      const float t1 = __fmul_rn(-adv, __fsub_rn(oh, pr[k]));
+      const float t2 = __fmul_rn(__fmul_rn(a.beta, pr[k]), __fadd_rn(lp[k], H));
+      const float d = __fmul_rn(pf, __fadd_rn(t1, t2));
+      dl[k] = d;
+      if (sdl) sdl[k] = d;
+    }
+  const float dvv = __fsub_rn(vi, Rf);
+  const float dvo = __fmul_rn(vf, dvv);
+  a.dv[i] = dvo;
+  if (sdl) sdl[A] = dvo;
+  lpi = __fmul_rn(pf, __fadd_rn(__fmul_rn(lpa, adv), __fmul_rn(a.beta, H)));
+  lv = __fmul_rn(vf, __fmul_rn(__fmul_rn(dvv, dvv), 0.5f));
+}
+__device__ inline void returns_one(const ReturnsArgs& a, int t, int e, float& lpi, float& lv) {
+  RetIn in;
+  returns_load(a, t, e, in);
+  returns_compute(a, t, e, in, lpi, lv, nullptr);
+}
+
+// per-env losses summed in the reference's order (t = T-1 .. 0)
+__device__ inline void env_loss(const ReturnsArgs& a, const float* lpi, const float* lv, int EB, int el, int e) {
+  float pi_loss = 0.f, v_loss = 0.f;
+  for (int tt = a.T - 1; tt >= 0; --tt) {
+    pi_loss = __fsub_rn(pi_loss, lpi[tt * EB + el]);
+    v_loss = __fadd_rn(v_loss, lv[tt * EB + el]);
+  }
+  a.loss[2 * e] = pi_loss;
+  a.loss[2 * e + 1] = v_loss;
+}
+
+__global__ void __launch_bounds__(256)
+returns_kernel(ReturnsArgs a) {
+  __shared__ float lpi[256], lv[256];
+  if (a.ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) a.ctl[CTL_STEP_SNAP] = a.ctl[CTL_STEP];
+  const int EB = 256 / a.T;
+  const int tid = threadIdx.x, t = tid / EB, el = tid - t * EB;
+  const int e = blockIdx.x * EB + el;
+  const bool on = t < a.T && e < a.n;
+  if (on) returns_one(a, t, e, lpi[tid], lv[tid]);
+  if (a.loss == nullptr) return;
+  __syncthreads();
+  if (t == 0 && on) env_loss(a, lpi, lv, EB, el, e);
+}
+
+// returns_kernel + the heads' backward (a3c.py:129-130 through policy.py /
+// v_function.py): dh[s][j] = sum_k dlogits[s][k] Wpi[k][j] + dv[s] Wv[j],
+// times (mask[s][j] > 0) when mask is given, for the EB envs x T steps of
+// the block (EB = 32 / T: at most 32 rows) -- the rows the block's own
+// threads just produced, handed over in LDS.  Thread j of the block owns
+// column j (HID = 256 = blockDim): its Wpi / Wv column and its mask entries
+// are loaded up front, beside the returns' own loads.
+__device__ inline int rh_envs(int T) { return 1; }
+__global__ void __launch_bounds__(256)
+returns_heads_kernel(ReturnsArgs a, const float* __restrict__ Wpi, const float* __restrict__ Wv,
+                     const float* __restrict__ mask, float* __restrict__ dh, int abl) {
+  __shared__ float lpi[64], lv[64];
+  __shared__ float sdl[64 * (MAXA + 1)];
+  if (a.ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) a.ctl[CTL_STEP_SNAP] = a.ctl[CTL_STEP];
+  const int T = a.T, n = a.n, A = a.A;
+  const int EB = rh_envs(T), rows = T * EB;   // rows <= 64
+  const int tid = threadIdx.x, t = tid / EB, el = tid - t * EB;
+  const int e0 = blockIdx.x * EB;
+  const int e = e0 + el;
+  const bool on = t < T && e < n;
+  const int j = tid;
+  // this thread's mask entries and head-weight column, in flight during the returns
+  // (unconditional loads at clamped offsets: a load under a per-lane branch
+  // would wait for each one in turn)
+  float mv[32];
+  int64_t so[32];
+  auto rows_from = [&](int r0) {
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const int r = r0 + u, l = r % EB;
+      const bool ok = r < rows && e0 + l < n;
+      so[u] = ok ? ((int64_t)(r / EB) * n + e0 + l) * HID + j : -1;
+    }
+    if (mask != nullptr) {
+#pragma unroll
+      for (int u = 0; u < 32; ++u) mv[u] = mask[so[u] < 0 ? j : so[u]];
+    } else {
+#pragma unroll
+      for (int u = 0; u < 32; ++u) mv[u] = 1.f;
+    }
+  };
+  rows_from(0);
+  float wc[MAXA + 1];   // column j of Wpi / Wv (clamped offsets: every load issued together)
+#pragma unroll
+  for (int k = 0; k <= MAXA; ++k) wc[k] = k < A ? Wpi[min(k, A - 1) * HID + j] : Wv[j];
+  RetIn in;   // off threads load a valid step (t, e) and discard it
+  returns_load(a, min(t, T - 1), min(e, n - 1), in);
+  __shared__ float w[(MAXA + 1) * HID];   // thread j's own column
+#pragma unroll
+  for (int k = 0; k <= MAXA; ++k)
+    if (k <= A) w[k * HID + j] = k < A ? wc[k] : wc[MAXA];
+  if (on && !(abl & 2)) returns_compute(a, t, e, in, lpi[tid], lv[tid], sdl + tid * (A + 1));   // row tid = t * EB + el
+  __syncthreads();
+  if (a.loss != nullptr && t == 0 && on) env_loss(a, lpi, lv, EB, el, e);
+  for (int r0 = 0; r0 < ((abl & 1) ? 0 : rows); r0 += 32) {
+    if (r0 > 0) rows_from(r0);   // T > 32: the second 32 rows
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      if (so[u] < 0) continue;
+      const float* d = sdl + (r0 + u) * (A + 1);
+      float acc = 0.f;
+      for (int k = 0; k < A; ++k) acc = __fadd_rn(acc, __fmul_rn(d[k], w[k * HID + j]));
+      acc = __fadd_rn(acc, __fmul_rn(d[A], w[A * HID + j]));
+      dh[so[u]] = mv[u] > 0.f ? acc : 0.f;
+    }
   }
 }
 
@@ -216,8 +374,25 @@ hipError_t launch_returns(const float* rewards, const uint8_t* dones, const floa
   if (n <= 0) return hipSuccess;
   if (T < 1 || T > 256) return hipErrorInvalidValue;
   const int EB = 256 / T;
-  hipLaunchKernelGGL(returns_kernel, dim3((n + EB - 1) / EB), dim3(256), 0, s, rewards, dones, v, probs, logp, act, T,
-                     n, A, gamma, beta, vcoef, clip_reward, dlogits, dv, loss, ctl_snap, pcoef, keep_scale);
+  const ReturnsArgs ra{rewards, dones, v, probs, logp, act, T, n, A, gamma, beta, vcoef, pcoef, clip_reward,
+                       keep_scale, dlogits, dv, loss, ctl_snap};
+  hipLaunchKernelGGL(returns_kernel, dim3((n + EB - 1) / EB), dim3(256), 0, s, ra);
+  return hipGetLastError();
+}
+
+hipError_t launch_returns_heads(const float* rewards, const uint8_t* dones, const float* v, const float* probs,
+                                const float* logp, const int32_t* act, int T, int n, int A, double gamma, float beta,
+                                float vcoef, int clip_reward, float* dlogits, float* dv, float* loss, hipStream_t s,
+                                int64_t* ctl_snap, float pcoef, int keep_scale, const float* Wpi, const float* Wv,
+                                const float* mask, float* dh) {
+  if (n <= 0) return hipSuccess;
+  if (T < 1 || T > 64 || A < 1 || A > MAXA) return hipErrorInvalidValue;
+  const int EB = 1;   // rh_envs
+  const ReturnsArgs ra{rewards, dones, v, probs, logp, act, T, n, A, gamma, beta, vcoef, pcoef, clip_reward,
+                       keep_scale, dlogits, dv, loss, ctl_snap};
+  static const char* ab = getenv("ARL_RH_ABL");   // timing experiments only: 1 no dh, 2 no returns
+  hipLaunchKernelGGL(returns_heads_kernel, dim3((n + EB - 1) / EB), dim3(256), 0, s, ra, Wpi, Wv, mask, dh,
+                     ab ? atoi(ab) : 0);
   return hipGetLastError();
 }
 

@@ -185,7 +185,9 @@ int arl_learn(arl_net* net, double gamma, double beta, double v_loss_coef, int c
  * gradients) may run on a second stream once part 0 (returns + loss
  * gradient) is done, and parts 3 (LSTM gate reduce) and 4 (FC reduce) once
  * part 2 (heads dh, LSTM BPTT, FC dW + da2 GEMMs) is done, concurrently with
- * part 5 (conv backward); the gradient is complete when both streams are. */
+ * part 5 (conv backward); the gradient is complete when both streams are.
+ * With the fused FC backward (the default) part 2's launch also writes the
+ * heads weight gradients and the FC reduce, so parts 1 and 4 enqueue nothing. */
 #define ARL_LEARN_RETURNS 0
 #define ARL_LEARN_HEADS_DW 1
 #define ARL_LEARN_TRUNK 2
@@ -211,7 +213,7 @@ enum {
                                nets reduce + bias + relu in the same launch */
   ARL_STAGE_POLICY = 3,     /* pi / v heads + softmax policy output (no action); FF nets first
                                reduce the FC partials + bias + relu into h (as in a window step) */
-  ARL_STAGE_FC_BWD = 4,     /* FC dW / db and da2 GEMMs */
+  ARL_STAGE_FC_BWD = 4,     /* FC dW / db and da2 GEMMs (+ the pi / v heads dW / db) */
   ARL_STAGE_CONV_BWD = 5    /* fused conv backward (conv2 dW, convT, conv1 dW) into per-block slabs */
 };
 int arl_run_stage(arl_net* net, int stage, int t, void* stream);
