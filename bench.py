@@ -207,6 +207,17 @@ def bench_phi(a, world, rank, dev, n_default):
 
 def main():
     a = parse()
+    mp_ctx = None
+    if a.cpu_seconds > 0 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        # CPU baseline leg (ii) workers are forked by a forkserver started
+        # here, before anything touches the GPU (no worker is a fork of a GPU
+        # process); it preloads the oracle's CPU baseline module
+        import multiprocessing as mp
+        from multiprocessing import forkserver
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        mp_ctx = mp.get_context("forkserver")
+        mp_ctx.set_forkserver_preload(["cpu_baseline"])
+        forkserver.ensure_running()
     world, rank, local = init_dist()
     dev = torch.device("cuda", local)
     w_arch, w_envs, w_A = WORKLOADS[a.workload]
@@ -379,7 +390,11 @@ def main():
     if rank == 0 and world == 1 and a.cpu_seconds > 0 and arch == "ff":
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import cpu_baseline  # noqa: E402  (oracle/, CPU baseline leg only)
-        cpu = cpu_baseline.run(seconds=a.cpu_seconds, t_max=T, n_actions=4)
+        cpu = cpu_baseline.run(seconds=a.cpu_seconds, t_max=T, n_actions=4)        # leg (i): 1 process, 1 core
+        cpu["cpu_model"] = cpu_baseline.cpu_model()
+        par = cpu_baseline.run_parallel(seconds=a.cpu_seconds, t_max=T, n_actions=4, ctx=mp_ctx)   # leg (ii)
+        cpu["parallel"] = par
+        cpu["gpu_vs_parallel"] = round(value / par["value"], 1)
 
     if rank == 0:
         out = {

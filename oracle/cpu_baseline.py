@@ -3,6 +3,8 @@ process (a3c_ale.py:92-171 train_loop -> a3c.py:67-167 act), batch 1,
 single-threaded (OMP_NUM_THREADS=1 as at a3c_ale.py:186), timed on the host.
 
 TEST / BASELINE INFRASTRUCTURE ONLY (imported by bench.py's cpu_baseline leg).
+run() is leg (i), one process on one core; run_parallel() leg (ii), P
+processes in the reference's style.
 Per env-step: ale.py:59-89 current_screen + deque push, dqn_phi, NIPS-head
 forward + heads (batch 1), softmax / log-softmax / entropy, one draw; every
 t_max steps: bootstrap forward, n-step returns, backward over the window,
@@ -76,10 +78,72 @@ def run(seconds: float = 10.0, t_max: int = 5, n_actions: int = 4, seed: int = 0
     el = time.perf_counter() - t0
     if limiter is not None:
         limiter.unregister() if hasattr(limiter, "unregister") else None
-    return {"value": steps / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
+    return {"value": steps / el, "unit": "env-steps/s", "cores": 1, "kind": "port", "steps": steps,
+            "seconds": round(el, 3),
             "sample": f"{steps} env-steps ({steps // t_max} windows of t_max={t_max}) of one batch-1 "
                       f"A3C-FF actor-learner (NumPy restatement, 1 thread), {el:.1f} s"}
 
 
+def _worker(args):
+    seconds, t_max, n_actions, seed = args
+    return run(seconds, t_max, n_actions, seed)
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def host_cores():
+    """(physical cores, logical CPUs, CPUs this process may run on)."""
+    import os
+    try:
+        import psutil
+        phys = psutil.cpu_count(logical=False)
+    except Exception:  # pragma: no cover
+        phys = None
+    logical = os.cpu_count() or 1
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        avail = logical
+    return phys or logical, logical, avail
+
+
+def run_parallel(seconds: float = 10.0, t_max: int = 5, n_actions: int = 4, procs: int | None = None,
+                 cap: int = 16, ctx=None):
+    """Leg (ii) of BASELINE.md §2: P independent actor-learner processes in
+    the reference's style (async.py:68-90 run_async -- one process per
+    core, OMP_NUM_THREADS=1 each, a3c_ale.py:186), P = min(physical cores,
+    CPUs this process may use, cap); the box's CPU share for one GPU is 16,
+    hence the default cap.  Each process owns its parameters (the
+    reference's shared RawArrays add Hogwild write traffic, not arithmetic).
+    Aggregate env-steps/s = sum of steps / the slowest process's time.
+    ctx: a multiprocessing context -- pass a forkserver started before the
+    GPU was touched (bench.py) so no worker is forked from a GPU process."""
+    import multiprocessing as mp
+    phys, logical, avail = host_cores()
+    P = procs if procs else max(1, min(phys, avail, cap))
+    ctx = ctx if ctx is not None else mp.get_context("forkserver")
+    with ctx.Pool(P) as pool:
+        res = pool.map(_worker, [(seconds, t_max, n_actions, 1000 + i) for i in range(P)])
+    steps = [r["steps"] for r in res]
+    rates = [r["value"] for r in res]
+    el = max(r["seconds"] for r in res)
+    return {"value": sum(steps) / el, "unit": "env-steps/s", "cores": P, "kind": "port",
+            "sample": f"{P} processes x ~{seconds:.0f} s of the batch-1 A3C-FF actor-learner (NumPy restatement, "
+                      f"1 thread each), {sum(steps)} env-steps in total; per-process {min(rates):.1f}-"
+                      f"{max(rates):.1f} env-steps/s",
+            "cpu_model": cpu_model(), "physical_cores": phys, "logical_cpus": logical, "cpus_allowed": avail}
+
+
 if __name__ == "__main__":
     print(run(5.0))
+    print(run_parallel(5.0))
