@@ -288,7 +288,9 @@ int arl_act_envs(arl_net* h, int t, int e0, int ne, int mode, void* s) {
 
 int arl_run_stage(arl_net* h, int stage, int t, void* s) {
   NEED_BOUND(h);
-  if (stage < ARL_STAGE_CONV_FWD || stage > ARL_STAGE_CONV_BWD) return fail(ARL_EINVAL, "run_stage: unknown stage");
+  if (stage < ARL_STAGE_CONV_FWD || stage > ARL_STAGE_GRAD_SQNORM) return fail(ARL_EINVAL, "run_stage: unknown stage");
+  if (stage >= ARL_STAGE_RETURNS && h->net.arch == arl::ARCH_FF_NATURE)
+    return fail(ARL_EINVAL, "run_stage: returns / conv reduce / grad sqnorm stages are NIPS-head only");
   if (t < 0 || t > h->net.T) return fail(ARL_EINVAL, "run_stage: t out of [0, t_max]");
   return hip_status(arl::net_stage(h->net, stage, t, S(s)), "run_stage");
 }

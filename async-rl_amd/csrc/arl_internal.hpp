@@ -137,7 +137,8 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
 hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
                         float clip, hipStream_t s, bool advance = false);
 hipError_t net_advance(Net& net, hipStream_t s);
-enum Stage { STAGE_CONV_FWD = 1, STAGE_FC_FWD = 2, STAGE_POLICY = 3, STAGE_FC_BWD = 4, STAGE_CONV_BWD = 5 };
+enum Stage { STAGE_CONV_FWD = 1, STAGE_FC_FWD = 2, STAGE_POLICY = 3, STAGE_FC_BWD = 4, STAGE_CONV_BWD = 5,
+             STAGE_RETURNS = 6, STAGE_CONV_REDUCE = 7, STAGE_GRAD_SQNORM = 8 };
 hipError_t net_stage(Net& net, int stage, int t, hipStream_t s);
 // keep: LSTM keep_same_state (the pi_and_v recurrent state is not advanced)
 hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_t s, bool keep = false);
@@ -163,6 +164,9 @@ hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const i
                            float* gW1, float* gb1, hipStream_t s, bool reduce = true, int layout = FRAMES_RING);
 int64_t conv_bwd_slab_floats(int S);
 int conv_bwd_blocks(int S);       // workgroups (= slab slices) of launch_conv_bwd
+// the slab reduce launch_conv_bwd(reduce = true) ends with, alone
+hipError_t launch_conv_reduce(const float* slab, int S, float* gW2, float* gb2, float* gW1, float* gb1, hipStream_t s,
+                              int layout);
 
 // arguments of the softmax policy / value heads (policy_rows.hpp)
 struct PolicyArgs {

@@ -420,8 +420,14 @@ hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const i
   hipLaunchKernelGGL(conv_bwd_kernel, dim3(G), dim3(NT), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !reduce) return e;
-  hipLaunchKernelGGL(reduce_conv_bwd_kernel, dim3((SLAB + 15) / 16), dim3(256), 0, s, slab, G, gW2, gb2, gW1, gb1,
-                     layout == FRAMES_RGB ? 1 : 0);
+  return launch_conv_reduce(slab, S, gW2, gb2, gW1, gb1, s, layout);
+}
+
+hipError_t launch_conv_reduce(const float* slab, int S, float* gW2, float* gb2, float* gW1, float* gb1, hipStream_t s,
+                              int layout) {
+  if (S <= 0) return hipSuccess;
+  hipLaunchKernelGGL(reduce_conv_bwd_kernel, dim3((SLAB + 15) / 16), dim3(256), 0, s, slab, conv_bwd_blocks(S), gW2,
+                     gb2, gW1, gb1, layout == FRAMES_RGB ? 1 : 0);
   return hipGetLastError();
 }
 

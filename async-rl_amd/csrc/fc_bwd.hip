@@ -69,6 +69,10 @@ static_assert(BK * (AJ + AK) <= STAGE && BM * BK + BK * BN <= STAGE, "stage size
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
+__device__ inline uint64_t pack2(float lo, float hi) {
+  return (uint64_t)__float_as_uint(lo) | ((uint64_t)__float_as_uint(hi) << 32);
+}
+
 __device__ inline void barrier_lds() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -215,13 +219,14 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds) {
     // every range publishes into its slot (write-through sc1 stores, drained),
     // then takes a ticket; the holder of the last ticket sums the slots
     float* dst = a.part + ((int64_t)tile * a.Z + z) * PART;
+    // the (u = 0, 1) pair of a lane is 8 contiguous bytes: one 64-bit store,
+    // so a quarter-wave writes 128 contiguous bytes (whole sectors)
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          __hip_atomic_store(dst + pidx(t, u, e), (float)s[t][u][e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int e = 0; e < 4; ++e)
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(dst + pidx(t, 0, e)), pack2((float)s[t][0][e], (float)s[t][1][e]),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (bias && q == 0)
 #pragma unroll
       for (int t = 0; t < 4; ++t)
@@ -270,10 +275,12 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds) {
           vb[h][t] = __hip_atomic_load(src + AJ * AK + wm * 64 + 4 * col + t, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);   // (garbage off the bias waves: unused)
 #pragma unroll
-          for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              v[h][t][u][e] = __hip_atomic_load(src + pidx(t, u, e), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (int e = 0; e < 4; ++e) {
+            const uint64_t w = __hip_atomic_load(reinterpret_cast<const uint64_t*>(src + pidx(t, 0, e)),
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[h][t][0][e] = __uint_as_float((unsigned)w);
+            v[h][t][1][e] = __uint_as_float((unsigned)(w >> 32));
+          }
         }
       }
     }

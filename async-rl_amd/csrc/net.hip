@@ -670,6 +670,12 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
                              net.at<int64_t>(net.w_ctl), n, net.R, S, net.at<float>(net.w_a1),
                              net.at<float>(net.w_da2), P + net.o_c2W, slab, G + net.o_c2W, G + net.o_c2b,
                              G + net.o_c1W, G + net.o_c1b, s, /*reduce=*/false, net.layout);
+    case STAGE_RETURNS:   // the LEARN_RETURNS launch (returns + loss gradient + heads dh), default coefficients
+      return net_learn_part(net, LEARN_RETURNS, 0.99, 0.01f, 0.5f, 1, s);
+    case STAGE_CONV_REDUCE:
+      return launch_conv_reduce(slab, S, G + net.o_c2W, G + net.o_c2b, G + net.o_c1W, G + net.o_c1b, s, net.layout);
+    case STAGE_GRAD_SQNORM:
+      return launch_grad_sqnorm(net.g, net.param_floats, net.at<double>(net.w_norm), net.norm_blocks, s);
     default:
       return hipErrorInvalidValue;
   }

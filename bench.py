@@ -81,6 +81,59 @@ def parse():
     return ap.parse_args()
 
 
+CONV_SLAB_FLOATS = 12336                    # conv_slab.hpp SLAB: one conv_bwd workgroup's partial gradient
+
+
+def conv_bwd_blocks(S):
+    """conv_bwd.hip conv_bwd_blocks: slab slices of the conv backward."""
+    g0 = min(S, 256)
+    spb = -(-S // g0)
+    return -(-S // spb)
+
+
+def returns_bytes(N, T, A, mask=True, hid=256):
+    """Algorithmic bytes of the learner's first launch (policy.hip
+    returns_heads_kernel): read rewards, dones, v (T + 1 rows), probs, logp,
+    actions, [the h > 0 mask], the heads' weights; write dlogits, dv, the
+    per-env losses and dh."""
+    S = N * T
+    return (S * (4 + 1 + 4 + 8 * A + 4) + 4 * N + (A + 1) * hid * 4 + (S * hid * 4 if mask else 0)
+            + S * (4 * A + 4) + 8 * N + S * hid * 4)
+
+
+def source_version():
+    """Digest of the HIP sources and the C-ABI header: PMC traffic files
+    record the version they were measured on, and the bench uses one only
+    when it matches the tree it runs."""
+    import glob
+    import hashlib
+    h = hashlib.sha1()
+    files = sorted(glob.glob(os.path.join(ROOT, "async-rl_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(ROOT, "async-rl_amd", "csrc", "*.hpp")) +
+                   glob.glob(os.path.join(ROOT, "include", "*.h")))
+    for fn in files:
+        with open(fn, "rb") as f:
+            h.update(os.path.basename(fn).encode() + b"\0" + f.read())
+    return h.hexdigest()[:12]
+
+
+def measured_traffic(N, T, arch, kernel):
+    """HBM bytes per dispatch of `kernel` from a profiles/traffic_*.json
+    measured on this source version at this config (scripts/traffic.py), else None."""
+    import glob
+    ver = source_version()
+    for tf in sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_*.json"))):
+        try:
+            with open(tf) as f:
+                tj = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if (tj.get("source_version") == ver and tj.get("envs") == N and tj.get("t_max") == T
+                and tj.get("arch") == arch and kernel in tj.get("kernels", {})):
+            return tj["kernels"][kernel]
+    return None
+
+
 def init_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -184,11 +237,7 @@ def bench_phi(a, world, rank, dev, n_default):
     if rank == 0:
         work = n * PHI_STACK_BYTES_PER_PAIR
         ach = work / (us * 1e-6) / 1e9
-        traffic = None
-        tf = os.path.join(ROOT, "profiles", "traffic_r01_c5.json")
-        if os.path.exists(tf):
-            with open(tf) as f:
-                traffic = json.load(f).get("kernels", {}).get("phi_stack_kernel")
+        traffic = measured_traffic(n, 0, "phi", "phi_stack_kernel")
         out = {"metric": "env-steps/sec (phi+forward+sample+update) at 1/2/4/8 MI355X; % roofline",
                "value": round(n * world * a.steps / elapsed, 1), "unit": "frame pairs/s (phi stage only)",
                "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -351,12 +400,23 @@ def main():
             ("policy", "policy_kernel" if (nat or lstm) else "policy_fc_kernel (FC reduce + heads)",
              lambda i: net.run_stage("policy", i % T, stream=stream), T + 1, "hbm",
              N * (hid_bytes + 12 * A + 12) + (0 if (nat or lstm) else N * (FC_SPLIT + 1) * hid_bytes)),
-            ("fc_bwd", "gemm_kernel x2 + reduce_grad_kernel", lambda i: net.run_stage("fc_bwd", 0, stream=stream),
-             1, "mfma", 2 * fc_fwd_flop * S),
+            ("fc_bwd", "gemm_kernel x2 + reduce_grad_kernel" if nat else "fc_bwd_kernel (dW + da2 + heads dW)",
+             lambda i: net.run_stage("fc_bwd", 0, stream=stream), 1, "mfma", 2 * fc_fwd_flop * S),
             ("conv_bwd", "gemm_kernel x9 + reduce_grad_kernel x3" if nat else "conv_bwd_kernel",
              lambda i: net.run_stage("conv_bwd", 0, stream=stream), 1, "mfma", S * conv_bwd_flop),
             ("rmsprop", "rmsprop_kernel", lambda i: net.optimize(lr0=1e-12, clip=0.0, stream=stream), 1, "hbm",
              net.n_params * RMSPROP_BYTES_PER_PARAM),
+            # the learner's small HBM-bound launches (NIPS heads): returns + loss gradient + heads dh,
+            # the conv backward's slab reduce, the gradient's squared norm (GradientClipping)
+            None if nat else
+            ("returns", "returns_heads_kernel", lambda i: net.run_stage("returns", stream=stream), 1, "hbm",
+             returns_bytes(N, T, A, mask=not lstm)),
+            None if nat else
+            ("conv_reduce", "reduce_conv_bwd_kernel", lambda i: net.run_stage("conv_reduce", stream=stream), 1,
+             "hbm", (conv_bwd_blocks(S) + 1) * CONV_SLAB_FLOATS * 4),
+            None if nat else
+            ("grad_sqnorm", "grad_sqnorm_kernel", lambda i: net.run_stage("grad_sqnorm", stream=stream), 1, "hbm",
+             net.n_params * 4),
         ]
         kernels = {}
         with torch.cuda.stream(stream):
@@ -370,15 +430,9 @@ def main():
                                  "launches_per_window": calls, "window_share_us": round(us * calls, 1),
                                  "achieved": round(ach, 2), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
                                  ("bytes" if bound == "hbm" else "flop") + "_per_launch": int(work)}
-        dom = max((k for k in kernels if k not in ("fc_bwd",)), key=lambda k: kernels[k]["window_share_us"])
+        dom = max(kernels, key=lambda k: kernels[k]["window_share_us"])
         d = kernels[dom]
-        traffic = None
-        import glob
-        for tf in sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json"))):
-            with open(tf) as f:
-                tj = json.load(f)
-            if tj.get("envs") == N and tj.get("t_max") == T and tj.get("arch") == arch:
-                traffic = tj.get("kernels", {}).get(d["kernel"].split()[0], traffic)
+        traffic = measured_traffic(N, T, arch, d["kernel"].split()[0])
         roof = {"bound": d["bound"], "kernel": d["kernel"], "achieved": d["achieved"], "peak": d["peak"],
                 "unit": d["unit"], "frac": d["frac"], "traffic": traffic, "avg_launch_us": d["avg_launch_us"],
                 "work_per_launch": d.get("flop_per_launch", d.get("bytes_per_launch")),

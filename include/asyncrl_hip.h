@@ -214,7 +214,11 @@ enum {
   ARL_STAGE_POLICY = 3,     /* pi / v heads + softmax policy output (no action); FF nets first
                                reduce the FC partials + bias + relu into h (as in a window step) */
   ARL_STAGE_FC_BWD = 4,     /* FC dW / db and da2 GEMMs (+ the pi / v heads dW / db) */
-  ARL_STAGE_CONV_BWD = 5    /* fused conv backward (conv2 dW, convT, conv1 dW) into per-block slabs */
+  ARL_STAGE_CONV_BWD = 5,   /* fused conv backward (conv2 dW, convT, conv1 dW) into per-block slabs */
+  ARL_STAGE_RETURNS = 6,    /* n-step returns + loss gradient + heads dh (gamma 0.99, beta 0.01, v coef 0.5,
+                               clipped rewards): the learner's first launch */
+  ARL_STAGE_CONV_REDUCE = 7,  /* the conv backward's slab reduce into the conv gradients */
+  ARL_STAGE_GRAD_SQNORM = 8   /* squared-norm partials of the whole gradient (GradientClipping) */
 };
 int arl_run_stage(arl_net* net, int stage, int t, void* stream);
 

@@ -3,7 +3,9 @@
 (HBM section) prescribes: FETCH_SIZE (KiB) counts wide 16-B/lane reads at
 half their bytes on gfx950 -> x2; WRITE_SIZE (KiB) is exact for 16-B stores.
 
-    python scripts/traffic.py gpurun_out/pmc [--envs 256 --t-max 5 --arch ff] > profiles/traffic_r01.json
+    python scripts/traffic.py gpurun_out/pmc [--envs 256 --t-max 5 --arch ff] > profiles/traffic_r02_c2.json
+(the file records the source version it was measured on; bench.py uses a
+traffic file only when that matches the tree it runs -- bench.source_version)
 """
 import argparse
 import re
@@ -50,7 +52,14 @@ def main():
     ap.add_argument("--envs", type=int, default=256)
     ap.add_argument("--t-max", type=int, default=5)
     ap.add_argument("--arch", default="ff")
+    ap.add_argument("--version", default=None, help="source version measured (default: this tree's, "
+                                                        "bench.source_version)")
     a = ap.parse_args()
+    if a.version is None:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from bench import source_version
+        a.version = source_version()
     fetch = per_kernel(os.path.join(a.pmc_dir, "fetch_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(a.pmc_dir, "write_counter_collection.csv"), "WRITE_SIZE")
     kernels, raw = {}, {}
@@ -58,7 +67,7 @@ def main():
         f, w = fetch.get(k, 0.0), write.get(k, 0.0)
         raw[k] = {"FETCH_SIZE_KiB": round(f, 1), "WRITE_SIZE_KiB": round(w, 1)}
         kernels[k] = int(2 * f * 1024 + w * 1024)
-    print(json.dumps({"envs": a.envs, "t_max": a.t_max, "arch": a.arch,
+    print(json.dumps({"envs": a.envs, "t_max": a.t_max, "arch": a.arch, "source_version": a.version,
                       "unit": "bytes per dispatch (2 x FETCH_SIZE + WRITE_SIZE, KiB -> B)",
                       "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, --kernel-trace only",
                       "kernels": kernels, "raw": raw}, indent=1))
