@@ -20,7 +20,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "bf16split.hpp"
 
 namespace arl {
 
@@ -316,168 +315,6 @@ inline hipError_t launch_gemm2(const J1& j1, const J2& j2, hipStream_t s) {
   return launch_gemm2_nt<BM, BN, BK, WM, WN, 256, AV1, BV1, AV2, BV2>(j1, j2, s);
 }
 
-// ---------------------------------------------------------------- bf16x6 variant
-// Same implicit GEMM, same accessors, on the bf16 matrix cores with exact
-// 3-way bf16 splits of both f32 operands (bf16split.hpp: the 6 product terms
-// of weight >= 2^-16, big / small accumulators; measured error below the
-// exact-f32 chain's).  v_mfma_f32_16x16x32_bf16 runs 16x the FLOP rate of the
-// f32-input MFMA, so 6 of them per f32 product still move ~2.7x the f32 work.
-// LDS: per plane (h, m, l) an [BM][BK + 8] and a [BN][BK + 8] bf16 image with
-// k contiguous (row pitch 80 B at BK = 32 keeps the 16 rows of one
-// ds_read_b128 on distinct banks); each 32-deep k-step is one MFMA per term.
-// Operand modes: GK (k-contiguous, load4) or GS (any accessor, scalar loads
-// coalesced along the rows); both stage 4 consecutive k per thread.
-template <int BM, int BN, int BK, int WM, int WN, class AOp, class BOp, class EOp, int AV = GS, int BV = GS>
-__global__ void __launch_bounds__(256)
-gemm_x6_kernel(AOp A, BOp B, EOp E, int M, int N, int K, int k_per_split) {
-  static_assert(WM * WN == 4, "4 waves");
-  static_assert(BK % 32 == 0, "k-steps of 32");
-  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
-  static_assert(TM >= 1 && TN >= 1, "tile too small for wave layout");
-  constexpr int LDK = BK + 8;                       // bf16 per LDS row
-  constexpr int A_PER = (BM * BK) / 256, B_PER = (BK * BN) / 256;
-  static_assert(AV != GM && BV != GM, "x6 gathers k-quads: GK (load4) or GS (scalar) only");
-  __shared__ __attribute__((aligned(16))) uint16_t As[3][BM * LDK];
-  __shared__ __attribute__((aligned(16))) uint16_t Bs[3][BN * LDK];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN, z = blockIdx.z;
-  const int kbeg = z * k_per_split;
-  const int kend = min(kbeg + k_per_split, K);
-
-  f32x4 big[TM][TN], sml[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) big[i][j] = sml[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // gather: thread -> (row, k-quad) pairs; 4 consecutive k of one row per
-  // pair, so each pair lands in LDS as one 8-byte write per plane.  GK: the
-  // operand is k-contiguous (load4, threads walk k within a row); otherwise
-  // threads walk the rows (coalesced scalar loads) and load the 4 k singly.
-  constexpr int AQ = A_PER / 4, BQ = B_PER / 4;
-  static_assert(A_PER % 4 == 0 && B_PER % 4 == 0, "k-quads");
-  float ra[A_PER], rb[B_PER];
-  auto a_pair = [&](int i, int& mm, int& kq) {
-    const int q = tid + 256 * i;
-    if constexpr (AV == GK) { kq = q % (BK / 4); mm = q / (BK / 4); } else { mm = q % BM; kq = q / BM; }
-  };
-  auto b_pair = [&](int i, int& nn, int& kq) {
-    const int q = tid + 256 * i;
-    if constexpr (BV == GK) { kq = q % (BK / 4); nn = q / (BK / 4); } else { nn = q % BN; kq = q / BN; }
-  };
-  auto gather = [&](int kc) {
-#pragma unroll
-    for (int i = 0; i < AQ; ++i) {
-      int mm, kq;
-      a_pair(i, mm, kq);
-      const int m = m0 + mm, k = kc + 4 * kq;
-      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (m < M) {
-        if constexpr (AV == GK) {
-          if (k + 3 < kend) x = A.load4(m, k);
-          else {
-            if (k < kend) x.x = A.load(m, k);
-            if (k + 1 < kend) x.y = A.load(m, k + 1);
-            if (k + 2 < kend) x.z = A.load(m, k + 2);
-          }
-        } else {
-          if (k < kend) x.x = A.load(m, k);
-          if (k + 1 < kend) x.y = A.load(m, k + 1);
-          if (k + 2 < kend) x.z = A.load(m, k + 2);
-          if (k + 3 < kend) x.w = A.load(m, k + 3);
-        }
-      }
-      ra[4 * i] = x.x; ra[4 * i + 1] = x.y; ra[4 * i + 2] = x.z; ra[4 * i + 3] = x.w;
-    }
-#pragma unroll
-    for (int i = 0; i < BQ; ++i) {
-      int nn, kq;
-      b_pair(i, nn, kq);
-      const int n = n0 + nn, k = kc + 4 * kq;
-      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (n < N) {
-        if constexpr (BV == GK) {
-          if (k + 3 < kend) x = B.load4(k, n);
-          else {
-            if (k < kend) x.x = B.load(k, n);
-            if (k + 1 < kend) x.y = B.load(k + 1, n);
-            if (k + 2 < kend) x.z = B.load(k + 2, n);
-          }
-        } else {
-          if (k < kend) x.x = B.load(k, n);
-          if (k + 1 < kend) x.y = B.load(k + 1, n);
-          if (k + 2 < kend) x.z = B.load(k + 2, n);
-          if (k + 3 < kend) x.w = B.load(k + 3, n);
-        }
-      }
-      rb[4 * i] = x.x; rb[4 * i + 1] = x.y; rb[4 * i + 2] = x.z; rb[4 * i + 3] = x.w;
-    }
-  };
-  auto store3x4 = [&](uint16_t* h, int idx, const float* x, int plane_stride) {   // 4 consecutive k, 8-B aligned
-    uint32_t h01, m01, l01, h23, m23, l23;
-    split3_pack(x[0], x[1], h01, m01, l01);
-    split3_pack(x[2], x[3], h23, m23, l23);
-    *reinterpret_cast<uint2*>(h + idx) = make_uint2(h01, h23);
-    *reinterpret_cast<uint2*>(h + idx + plane_stride) = make_uint2(m01, m23);
-    *reinterpret_cast<uint2*>(h + idx + 2 * plane_stride) = make_uint2(l01, l23);
-  };
-  auto commit = [&]() {
-#pragma unroll
-    for (int i = 0; i < AQ; ++i) {
-      int mm, kq;
-      a_pair(i, mm, kq);
-      store3x4(&As[0][0], mm * LDK + 4 * kq, ra + 4 * i, BM * LDK);
-    }
-#pragma unroll
-    for (int i = 0; i < BQ; ++i) {
-      int nn, kq;
-      b_pair(i, nn, kq);
-      store3x4(&Bs[0][0], nn * LDK + 4 * kq, rb + 4 * i, BN * LDK);
-    }
-  };
-
-  if (kbeg < kend) {
-    gather(kbeg);
-    for (int kc = kbeg; kc < kend; kc += BK) {
-      __syncthreads();
-      commit();
-      __syncthreads();
-      if (kc + BK < kend) gather(kc + BK);
-#pragma unroll
-      for (int ks = 0; ks < BK / 32; ++ks) {
-        const int ko = 32 * ks + 8 * (lane >> 4);
-        bf16x8 af[3][TM], bf[3][TN];
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-            af[p][i] = *reinterpret_cast<const bf16x8*>(&As[p][(wm * (BM / WM) + 16 * i + (lane & 15)) * LDK + ko]);
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            bf[p][j] = *reinterpret_cast<const bf16x8*>(&Bs[p][(wn * (BN / WN) + 16 * j + (lane & 15)) * LDK + ko]);
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            mfma_x6(af[0][i], af[1][i], af[2][i], bf[0][j], bf[1][j], bf[2][j], big[i][j], sml[i][j]);
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
-        if (m < M && n < N) E.store(m, n, __fadd_rn(big[i][j][r], sml[i][j][r]), z);
-      }
-    }
-}
-
 template <int BM, int BN, int BK, int WM, int WN, int AV = GS, int BV = GS, class AOp, class BOp, class EOp>
 inline hipError_t launch_gemm(const AOp& A, const BOp& B, const EOp& E, int M, int N, int K,
                               int splits, hipStream_t s) {
@@ -489,20 +326,6 @@ inline hipError_t launch_gemm(const AOp& A, const BOp& B, const EOp& E, int M, i
   dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN, splits);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AOp, BOp, EOp, AV, BV>), grid, dim3(256), 0, s,
                      A, B, E, M, N, K, kps);
-  return hipGetLastError();
-}
-
-template <int BM, int BN, int BK, int WM, int WN, int AV = GS, int BV = GS, class AOp, class BOp, class EOp>
-inline hipError_t launch_gemm_x6(const AOp& A, const BOp& B, const EOp& E, int M, int N, int K, int splits,
-                                 hipStream_t s) {
-  if (M <= 0 || N <= 0 || K <= 0) return hipSuccess;
-  if (splits < 1) splits = 1;
-  int kps = (K + splits - 1) / splits;
-  kps = ((kps + BK - 1) / BK) * BK;
-  splits = (K + kps - 1) / kps;
-  dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN, splits);
-  hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, BK, WM, WN, AOp, BOp, EOp, AV, BV>), grid, dim3(256), 0, s, A, B, E, M,
-                     N, K, kps);
   return hipGetLastError();
 }
 
