@@ -60,12 +60,12 @@ constexpr int AJ = 128, AK = 64;        // job A tile: 128 j x 64 k
 constexpr int NJA = HID / AJ;           // 2
 constexpr int NKA = (A2 + AK - 1) / AK; // 41 (the last one half full)
 constexpr int NTA = NJA * NKA;          // 82 job A tiles per range
-constexpr int BM = 128, BN = 128;       // job B tile
+constexpr int BN = 128;                 // job B tile: 32 MT samples x 128 k
 constexpr int NKB = (A2 + BN - 1) / BN; // 21 (the last one a quarter full)
 constexpr int PART = AJ * AK + AJ;      // floats per published partial (dW tile + db)
 constexpr int FLUSH = 4;                // job A: f32 MFMA sums over 4 chunks (128 samples), then f64
 static_assert(HID % AJ == 0 && HID % BK == 0 && A2 % 4 == 0 && A2 % AK == 32, "tiles");
-static_assert(BK * (AJ + AK) <= STAGE && BM * BK + BK * BN <= STAGE, "stage size");
+static_assert(BK * (AJ + AK) <= STAGE && 128 * BK + BK * BN <= STAGE, "stage size");
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -318,71 +318,77 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds) {
 }
 
 // ---------------------------------------------------------------- job B: da2
+// MT m-tiles per wave: workgroup tiles of BMT = 32 MT samples x 128 k
+template <int MT>
 __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
+  constexpr int BMT = 32 * MT;
+  constexpr int PIECES = (BMT * BK + BK * BN) / 256 / NW;   // LDS-DMA pieces per wave per chunk
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, col = lane & 15;
-  const int wm = wave >> 1, wn = wave & 1;   // wave: 64 s x 64 k
+  const int wm = wave >> 1, wn = wave & 1;   // wave: 16 MT s x 64 k
   const int kt = tile % NKB, st = tile / NKB;
-  const int s0 = st * BM, k0 = kt * BN;
+  const int s0 = st * BMT, k0 = kt * BN;
   constexpr int NCH = HID / BK;              // 8 chunks of 32 j
   auto issue = [&](int c) {
     if (a.abl & 2) return;
     float* sg = lds + (c & 1) * STAGE;
-    stage_tile<BM, BK, 2>(sg, a.dfc + c * BK, HID, s0, a.S - 1, 0);                    // dfc[s][j]
-    stage_tile<BK, BN, 0>(sg + BM * BK, a.W + (int64_t)c * BK * A2, A2, 0, BK - 1, k0);  // W[j][k0..k0+127]
+    stage_tile<BMT, BK, 2>(sg, a.dfc + c * BK, HID, s0, a.S - 1, 0);                    // dfc[s][j]
+    stage_tile<BK, BN, 0>(sg + BMT * BK, a.W + (int64_t)c * BK * A2, A2, 0, BK - 1, k0);  // W[j][k0..k0+127]
   };
-  f32x4 acc[4][4];                           // m-tile i: rows 16 i + col; n-tile u: cols 4 col + u
+  f32x4 acc[MT][4];                          // m-tile i: rows 16 i + col; n-tile u: cols 4 col + u
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[i][u] = f32x4{0.f, 0.f, 0.f, 0.f};
   // ReLU mask of the tile (a2 > 0), one bit per output element -- bit 4e + u
-  // of mb[i] -- loaded a 16-row band per chunk during chunks 0..3 so that no
+  // of mb[i] -- loaded a 16-row band per chunk during chunks 0..MT-1 so that no
   // load round trip is left for the epilogue.  Out-of-range rows / columns
   // read 0 through the buffer's range check.
   const int k = k0 + wn * 64 + 4 * col;
   const bool kin = k < A2;                   // A2 % 4 == 0: a 4-run is all in or all out
-  const int rows = min(BM, a.S - s0);
+  const int rows = min(BMT, a.S - s0);
   const __amdgpu_buffer_rsrc_t msk = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.a2) + (int64_t)s0 * A2,
                                                                        0, rows * A2 * 4, BUF_DWORD3);
-  unsigned mb[4] = {0u, 0u, 0u, 0u};
+  unsigned mb[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) mb[i] = 0u;
   f32x4 mraw[4];
   issue(0);
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     if (c + 1 < NCH) issue(c + 1);
-    if (c >= 1 && c <= 4) {   // the band loaded one chunk ago (the compiler's own vmcnt wait)
+    if (c >= 1 && c <= MT) {   // the band loaded one chunk ago (the compiler's own vmcnt wait)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int u = 0; u < 4; ++u) mb[c - 1] |= (mraw[e][u] > 0.f ? 1u : 0u) << (4 * e + u);
     }
-    if (c < 4) {
+    if (c < MT) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int row = wm * 64 + 16 * c + 4 * q + e;
+        const int row = wm * 16 * MT + 16 * c + 4 * q + e;
         mraw[e] = __builtin_bit_cast(
             f32x4, __builtin_amdgcn_raw_buffer_load_b128(msk, kin ? (row * A2 + k) * 4 : OOB, 0, 0));
       }
     }
-    // this chunk's DMA done: the next chunk's (4 + 4 pieces a wave) and this chunk's mask band may still fly
+    // this chunk's DMA done: the next chunk's PIECES a wave and this chunk's mask band may still fly
     if (c + 1 < NCH) {
-      if (c < 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      if (c < MT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES + 4) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     barrier_lds();
     const float* As = lds + (c & 1) * STAGE;
-    const float* Bs = As + BM * BK;
+    const float* Bs = As + BMT * BK;
     if (!(a.abl & 1)) {
       // every fragment of the chunk first (counted LDS waits), then the MFMAs
-      f32x4 av[BK / 16][4], bv[BK / 16][4];
+      f32x4 av[BK / 16][MT], bv[BK / 16][4];
 #pragma unroll
       for (int g = 0; g < BK / 16; ++g) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = wm * 64 + i * 16 + col;
+        for (int i = 0; i < MT; ++i) {
+          const int m = wm * 16 * MT + i * 16 + col;
           av[g][i] = *reinterpret_cast<const f32x4*>(As + m * BK + (((4 * g + q) ^ ((m >> 1) & 7)) << 2));
         }
 #pragma unroll
@@ -394,7 +400,7 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < MT; ++i)
 #pragma unroll
             for (int u = 0; u < 4; ++u)
               acc[i][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][i][r], bv[g][r][u], acc[i][u], 0, 0, 0);
@@ -402,17 +408,17 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     barrier_lds();
   }
-  // lane (col, q) holds s = s0 + wm*64 + 16 i + 4 q + e, k = k0 + wn*64 + 4 col + u:
+  // lane (col, q) holds s = s0 + wm*16*MT + 16 i + 4 q + e, k = k0 + wn*64 + 4 col + u:
   // 4 consecutive k per (i, e).  Straight-line buffer stores whose
   // out-of-range lanes (s >= S, k >= A2) the buffer's range check drops -- no
   // per-store branch, so no store waits for the one before it.
   const __amdgpu_buffer_rsrc_t out =
       __builtin_amdgcn_make_buffer_rsrc(a.da2 + (int64_t)s0 * A2, 0, rows * A2 * 4, BUF_DWORD3);
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int row = wm * 64 + 16 * i + 4 * q + e;
+      const int row = wm * 16 * MT + 16 * i + 4 * q + e;
       f32x4 o;
 #pragma unroll
       for (int u = 0; u < 4; ++u) o[u] = (mb[i] >> (4 * e + u)) & 1u ? acc[i][u][e] : 0.f;
@@ -483,6 +489,7 @@ __device__ void job_heads(const FcBwdArgs& a, int jt, float* lds) {
   }
 }
 
+template <int MT>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2)))
 fc_bwd_kernel(FcBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];   // 64 KB, the only LDS object
@@ -490,7 +497,7 @@ fc_bwd_kernel(FcBwdArgs a) {
   const int na = NTA * a.Z;
   if (b < a.nc) job_heads(a, b, lds);   // first: the smallest, longest-latency jobs
   else if (b < a.nc + na) job_dw(a, b - a.nc, lds);
-  else job_da2(a, b - a.nc - na, lds);
+  else job_da2<MT>(a, b - a.nc - na, lds);
 }
 
 // ~400 samples per job A range, at most 16 ranges
@@ -514,7 +521,10 @@ hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int 
   const int Z = fc_bwd_ranges(S);
   int kpz = (S + Z - 1) / Z;
   kpz = (kpz + BK - 1) / BK * BK;
-  const int na = NTA * Z, nb = ((S + BM - 1) / BM) * NKB;
+  // ARL_FC_BWD_BM=64: job B on 64-sample tiles (2 m-tiles per wave) -- A/B timing
+  static const char* bm = getenv("ARL_FC_BWD_BM");
+  const int MT = (bm && atoi(bm) == 64) ? 2 : 4, BMT = 32 * MT;
+  const int na = NTA * Z, nb = ((S + BMT - 1) / BMT) * NKB;
   // ARL_FC_BWD_JOBS=a / b: launch one job alone; ARL_FC_BWD_ABL: ablations (timing experiments only)
   static const char* only = getenv("ARL_FC_BWD_JOBS");
   static const char* abl = getenv("ARL_FC_BWD_ABL");
@@ -524,7 +534,8 @@ hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int 
   const int grid = (only && only[0] == 'a') ? na : (only && only[0] == 'b') ? nb : nc + na + nb;
   FcBwdArgs args{dfc, a2, W, S, Z, kpz, gW, gb, da2, part, tick, heads ? *heads : HeadsDW{}, nc, b0,
                  abl ? atoi(abl) : 0};
-  hipLaunchKernelGGL(fc_bwd_kernel, dim3(grid), dim3(NT), 0, s, args);
+  if (MT == 2) hipLaunchKernelGGL(fc_bwd_kernel<2>, dim3(grid), dim3(NT), 0, s, args);
+  else hipLaunchKernelGGL(fc_bwd_kernel<4>, dim3(grid), dim3(NT), 0, s, args);
   return hipGetLastError();
 }
 
