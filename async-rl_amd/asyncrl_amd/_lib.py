@@ -63,6 +63,8 @@ SIGNATURES = {
     "arl_observe_envs": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_i64,
                                  c_int, c_int, c_void_p]),
     "arl_act_envs": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "arl_observe_act_envs": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int,
+                                     c_int, c_void_p]),
     "arl_run_stage": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "arl_learn": (c_int, [c_void_p, c_double, c_double, c_double, c_int, c_void_p]),
     "arl_learn_part": (c_int, [c_void_p, c_int, c_double, c_double, c_double, c_int, c_void_p]),

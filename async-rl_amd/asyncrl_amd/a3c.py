@@ -327,19 +327,16 @@ class A3C:
             torch.as_tensor(is_state_terminal, device=net.device).to(torch.uint8).contiguous()
         pairs = pairs.contiguous()
         if self.t == 0:
-            net.observe(0, pairs, r, d, 1, force_reset=True, resize_mode=self.resize_mode)
-            net.act(0)
+            net.observe_act(0, pairs, r, d, 1, force_reset=True, resize_mode=self.resize_mode)
             ta = 0
         elif self.t % T == 0:
-            net.observe(T, pairs, r, d, 1, resize_mode=self.resize_mode)
-            net.act(T)                       # bootstrap v(s_T), pre-update params
+            net.observe_act(T, pairs, r, d, 1, resize_mode=self.resize_mode)   # bootstrap v(s_T), pre-update params
             self._update()
             net.act(0)                       # a3c.py:154-164 with post-update params
             ta = 0
         else:
             ta = self.t % T
-            net.observe(ta, pairs, r, d, 1, resize_mode=self.resize_mode)
-            net.act(ta)
+            net.observe_act(ta, pairs, r, d, 1, resize_mode=self.resize_mode)
         self.t += 1
         return net.step_outputs(ta)["actions"].clone()
 
@@ -390,25 +387,37 @@ class A3C:
 
     def _forward_chain(self, pair_pool, reward_pool, done_pool, pool_len, first, stream, envs):
         """T x (observe, act) + the bootstrap observe / act for envs (all if
-        None) on `stream`.  For an env group, returns an event recorded after
-        the chain's first kernel (the first observe, or the conv launch of
-        step 0 when the window starts from the previous bootstrap obs)."""
+        None) on `stream`; each observe + act is one launch shorter where the
+        net fuses them (DeviceNet.observe_act).  For an env group, returns an
+        event recorded after the chain's first kernel (the first conv launch,
+        with or without its observation)."""
         net, T = self.net, self.t_max
         ev = None
+        stagger = envs is not None and STAGGER
         for t in range(T + 1):
-            if t > 0 or first:
-                net.observe(t, pair_pool, reward_pool, done_pool, pool_len, force_reset=(t == 0),
-                            resize_mode=self.resize_mode, stream=stream, envs=envs)
-            if envs is not None and ev is None and STAGGER:
-                if t == 0 and not first:
-                    net.act(t, mode=1 | ACT_CONV_ONLY, stream=stream, envs=envs)
+            obs = t > 0 or first
+            if stagger and ev is None:
+                if obs and not net.fused_observe:      # the first kernel is the observation
+                    net.observe(t, pair_pool, reward_pool, done_pool, pool_len, force_reset=(t == 0),
+                                resize_mode=self.resize_mode, stream=stream, envs=envs)
                     ev = torch.cuda.Event()
                     ev.record(stream)
-                    net.act(t, mode=1 | ACT_AFTER_CONV, stream=stream, envs=envs)
+                    net.act(t, stream=stream, envs=envs)
                     continue
+                if obs:
+                    net.observe_act(t, pair_pool, reward_pool, done_pool, pool_len, force_reset=(t == 0),
+                                    resize_mode=self.resize_mode, mode=1 | ACT_CONV_ONLY, stream=stream, envs=envs)
+                else:
+                    net.act(t, mode=1 | ACT_CONV_ONLY, stream=stream, envs=envs)
                 ev = torch.cuda.Event()
                 ev.record(stream)
-            net.act(t, stream=stream, envs=envs)
+                net.act(t, mode=1 | ACT_AFTER_CONV, stream=stream, envs=envs)
+                continue
+            if obs:
+                net.observe_act(t, pair_pool, reward_pool, done_pool, pool_len, force_reset=(t == 0),
+                                resize_mode=self.resize_mode, stream=stream, envs=envs)
+            else:
+                net.act(t, stream=stream, envs=envs)
         return ev
 
     def finish_window(self, stream=None, conv=None):

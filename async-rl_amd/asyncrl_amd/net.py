@@ -58,6 +58,9 @@ def init_like_torch(arch: int, n_actions: int, rng: np.random.Generator):
 # 1.609, C4 0.641 -> 0.676): each cross-stream edge of the window graph costs
 # more on the critical path than the ~19 us of reduces it hides.
 LEARN_FORK = os.environ.get("ARL_LEARN_FORK", "0") == "1"
+# observe + act of a step in one launch (phi fused into the conv forward, conv_fwd_kernel<true>).
+# Off by default: measured slower than phi_ring_kernel + conv_fwd_kernel at C2 / C4
+FUSE_OBS = os.environ.get("ARL_FUSE_OBS", "0") == "1"
 
 
 class DeviceNet:
@@ -186,6 +189,27 @@ class DeviceNet:
             check(lib.arl_act_envs(self._h, t, envs[0], envs[1], mode, stream_handle(stream)), "arl_act_envs")
             return
         check(lib.arl_act_mode(self._h, t, mode, stream_handle(stream)), "arl_act_mode")
+
+    @property
+    def fused_observe(self) -> bool:
+        """observe + act of a step as one launch (arl_observe_act_envs): frame-pair
+        nets with the NIPS head, when enabled (ARL_FUSE_OBS=1 or the instance
+        attribute fuse_obs = True)."""
+        return getattr(self, "fuse_obs", FUSE_OBS) and not (self.rgb or self.stack or self.arch == ARCH_FF_NATURE)
+
+    def observe_act(self, t: int, pair_pool: torch.Tensor, reward_pool=None, done_pool=None, pool_len: int = 1,
+                    force_reset: bool = False, resize_mode: int = RESIZE_SCALAR, mode: int = 1, stream=None,
+                    envs=None):
+        """observe(t, ...) then act(t, mode) of envs (all if None), fused into
+        one conv launch where the net allows it (fused_observe)."""
+        if not self.fused_observe:
+            self.observe(t, pair_pool, reward_pool, done_pool, pool_len, force_reset, resize_mode, stream, envs)
+            self.act(t, mode, stream, envs)
+            return
+        e0, ne = envs if envs is not None else (0, -1)
+        check(lib.arl_observe_act_envs(self._h, t, e0, ne, ptr(pair_pool), ptr(reward_pool), ptr(done_pool), pool_len,
+                                       int(force_reset), resize_mode, mode, stream_handle(stream)),
+              "arl_observe_act_envs")
 
     def default_env_groups(self) -> int:
         """Forward chains per window that measured fastest on one MI355X

@@ -159,16 +159,15 @@ int arl_net_reset(arl_net* h, void* s) {
   return hip_status(e, "net_reset");
 }
 
-static int observe_common(arl_net* h, int t, const uint8_t* pool, const float* reward_pool,
-                          const uint8_t* done_pool, int64_t pool_len, int force_reset, int mode, int H, int W,
-                          void* s, int e0 = 0, int ne = -1) {
+// validates an observation and fills its ring arguments (0 = ok)
+static int ring_args(arl_net* h, int t, const uint8_t* pool, const float* reward_pool, const uint8_t* done_pool,
+                     int64_t pool_len, int force_reset, int mode, int H, int W, int e0, int ne, arl::RingArgs& a) {
   arl::Net& n = h->net;
   if (t < 0 || t > n.T) return fail(ARL_EINVAL, "observe: t out of [0, t_max]");
   if ((!pool && n.layout != arl::FRAMES_STACK) || pool_len < 1)
     return fail(ARL_EINVAL, "observe: need the frame pool and pool_len >= 1");
   if (!aligned(pool, 16)) return fail(ARL_EINVAL, "observe: the frame pool must be 16-byte aligned");
   if (n.N > 65535) return fail(ARL_EINVAL, "observe: n_envs > 65535");
-  arl::RingArgs a;
   a.pair_pool = pool;
   a.reward_pool = reward_pool;
   a.done_pool = done_pool;
@@ -188,6 +187,15 @@ static int observe_common(arl_net* h, int t, const uint8_t* pool, const float* r
   a.W = W;
   a.e0 = e0;
   a.ne = ne;
+  return 0;
+}
+
+static int observe_common(arl_net* h, int t, const uint8_t* pool, const float* reward_pool,
+                          const uint8_t* done_pool, int64_t pool_len, int force_reset, int mode, int H, int W,
+                          void* s, int e0 = 0, int ne = -1) {
+  arl::RingArgs a;
+  if (int rc = ring_args(h, t, pool, reward_pool, done_pool, pool_len, force_reset, mode, H, W, e0, ne, a)) return rc;
+  const arl::Net& n = h->net;
   return hip_status(n.layout == arl::FRAMES_RGB     ? arl::launch_rgb_ring(a, S(s))
                     : n.layout == arl::FRAMES_STACK ? arl::launch_stack_ring(a, S(s))
                                                     : arl::launch_phi_ring(a, S(s)),
@@ -284,6 +292,28 @@ int arl_act_envs(arl_net* h, int t, int e0, int ne, int mode, void* s) {
   if (int rc = check_env_range(h->net, e0, ne)) return rc;
   if (part != 0 && h->net.arch == arl::ARCH_FF_NATURE) return fail(ARL_EINVAL, "act: Nature head has no conv split");
   return hip_status(arl::net_act(h->net, t, mode, S(s), e0, ne), "act");
+}
+
+int arl_observe_act_envs(arl_net* h, int t, int e0, int ne, const uint8_t* pair_pool, const float* reward_pool,
+                         const uint8_t* done_pool, int64_t pool_len, int force_reset, int resize_mode, int mode,
+                         void* s) {
+  NEED_BOUND(h);
+  const arl::Net& n = h->net;
+  if (n.rgb || n.stack || n.arch == arl::ARCH_FF_NATURE)
+    return fail(ARL_ESTATE, "observe_act: frame-pair nets with the NIPS head only (use arl_observe + arl_act)");
+  if (ne < 0) {
+    e0 = 0;
+    ne = n.N;
+  }
+  if (int rc = check_env_range(n, e0, ne)) return rc;
+  if (resize_mode < 0 || resize_mode > (ARL_RESIZE_SIMD | ARL_RESIZE_CROP)) return fail(ARL_EINVAL, "bad resize_mode");
+  const int part = mode & ~3;
+  if (mode < 0 || (mode & 3) > 2 || (part != 0 && part != ARL_ACT_CONV_ONLY))
+    return fail(ARL_EINVAL, "observe_act: mode must be 0 / 1 / 2, optionally | ARL_ACT_CONV_ONLY");
+  arl::RingArgs a;
+  if (int rc = ring_args(h, t, pair_pool, reward_pool, done_pool, pool_len, force_reset, resize_mode, 0, 0, e0, ne, a))
+    return rc;
+  return hip_status(arl::net_act(h->net, t, mode, S(s), e0, ne, &a), "observe_act");
 }
 
 int arl_run_stage(arl_net* h, int stage, int t, void* s) {

@@ -127,7 +127,9 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
 // mode: 0 none, 1 sample, 2 greedy, | ACT_CONV_ONLY / ACT_AFTER_CONV (env-group staggering:
 // the step split after its conv launch); envs [e0, e0 + ne) (ne < 0: all)
 constexpr int ACT_CONV_ONLY = 4, ACT_AFTER_CONV = 8;
-hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0 = 0, int ne = -1);
+// obs != null (FRAMES_RING nets, not with ACT_AFTER_CONV): the observation of step t is fused
+// into the conv launch (launch_phi_conv_fwd) -- arl_observe + arl_act in one step
+hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0 = 0, int ne = -1, const RingArgs* obs = nullptr);
 // learner parts (net_learn_part); see net.hip for which may run concurrently
 enum { LEARN_RETURNS = 0, LEARN_HEADS_DW, LEARN_TRUNK, LEARN_GATES_REDUCE, LEARN_FC_REDUCE, LEARN_CONV, LEARN_PARTS };
 hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s);
@@ -159,6 +161,9 @@ hipError_t launch_heads_bwd(const float* dl, const float* dv, const float* Wpi, 
 hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int t,
                            const float* W1, const float* b1, const float* W2, const float* b2, float* a1, float* a2,
                            hipStream_t s, int layout = FRAMES_RING, int e0 = 0, int ne = -1);
+// phi_ring_kernel + conv_fwd_kernel in one launch (one workgroup per env of ring.e0 + [0, ring.ne))
+hipError_t launch_phi_conv_fwd(const RingArgs& ring, const float* W1, const float* b1, const float* W2,
+                               const float* b2, float* a1, float* a2, hipStream_t s);
 hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int S,
                            const float* a1, const float* da2, const float* W2, float* slab, float* gW2, float* gb2,
                            float* gW1, float* gb1, hipStream_t s, bool reduce = true, int layout = FRAMES_RING);

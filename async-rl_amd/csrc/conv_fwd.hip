@@ -1,5 +1,8 @@
 // Fused forward of the NIPS head's two conv layers (dqn_head.py:41-42,48-52)
-// for one env per workgroup, straight from the uint8 frame ring:
+// for one env per workgroup, straight from the uint8 frame ring -- optionally
+// with the observation itself fused in front (PHI: phi of the env's new frame
+// pair, ale.py:59-89, written to the ring slot and used as conv input plane 3
+// from LDS; the ring bookkeeping of phi_ring_kernel):
 //   a1 = relu(conv(x/255, W1, s4) + b1)   (16 x 20 x 20)  -> LDS + HBM (kept for backward)
 //   a2 = relu(conv(a1, W2, s2) + b2)      (32 x 9 x 9)    -> HBM
 // Both contractions run on the bf16 matrix cores with exact bf16 splits of
@@ -10,9 +13,18 @@
 // LDS (145.5 KB, one 512-thread workgroup per CU = 2 waves per SIMD):
 //   xb   4 screens as bf16 [ic][y][x]                         56,448 B
 //   R1   W1 split planes [3][oc][k] (rows padded to 528 B),   25,344 B
-//        then (after every wave holds its W1 fragments) the a1 split planes
+//        then (after every wave is done with W1) the a1 split planes
 //        [3][pixel][ic] with an XOR swizzle of the 16-byte slots  38,400 B
 //   W2p  W2 split planes [3][oc][tap][ic] (rows 528 B)         50,688 B
+//        (PHI: first the gray tap rows of the new screen [84][2][160] and the
+//        resize coefficient tables, 27,720 B)
+//
+// PHI schedule: the bookkeeping loads, the three older ring planes and the
+// weights are issued first, then the 168 x 2 source rows of the pair (161 KB,
+// 24 x 16 B per thread, all in flight).  conv1's k-steps over input planes
+// 0..2 (6 of 8) run on the matrix cores while the pair lands; then max +
+// luminance -> gray rows, the resize -> plane 3 (ring slot + LDS), conv1's
+// last two k-steps.  Each tile's k order is the unfused kernel's (bit-identical).
 //
 // conv1: M = 400 positions (25 tiles), N = 16 oc, K = 256 ordered (ic, ky, kx):
 //   k-step s, lane quarter g -> (ic, ky) = divmod(4 s + g, 8), kx = 0..7, i.e.
@@ -27,10 +39,12 @@
 
 #include "arl_internal.hpp"
 #include "bf16split.hpp"
+#include "phi_ops.hpp"
 
 #ifndef ARL_ABLATE
-#define ARL_ABLATE 0   // timing experiments only (bits: 1 conv1 MFMA, 2 conv2 MFMA, 4 staging loads,
-                       // 8 weight loads + splits, 16 epilogue /255 as a multiply)
+#define ARL_ABLATE 0   // timing experiments only (bits: 1 conv1 MFMA, 2 conv2 MFMA, 4 staging loads
+                       // (ring path), 16 epilogue /255 as a multiply; PHI: 32 pair loads, 64 max +
+                       // luminance, 128 resize)
 #endif
 
 namespace arl {
@@ -48,6 +62,13 @@ constexpr int L_R1 = L_XB + 4 * XB_PLANE;   // 56,448
 constexpr int L_W2 = L_R1 + 3 * A1P;        // 94,848
 constexpr int L_END = L_W2 + 3 * W2P;       // 145,536
 static_assert(3 * W1P <= 3 * A1P, "W1 planes fit the a1 region");
+// PHI: gray tap rows + coefficient tables in the W2 region (W2 is split into it after the resize)
+constexpr int G_ROWS = 2 * DST;                       // 168 (output row, tap) source rows
+constexpr int L_GRAY = L_W2;                          // [84][2][160] uint8
+constexpr int L_XOFS = L_GRAY + G_ROWS * SRC_W;       // int16 xofs[84], xa0[84], xa1[84], yb0[84], yb1[84]
+static_assert(L_XOFS + 5 * DST * 2 <= L_END, "gray rows + tables fit the W2 region");
+constexpr int PHI_TASKS = G_ROWS * 10;                // (row, 16-pixel chunk): 1680
+constexpr int PHI_J = (PHI_TASKS + NT - 1) / NT;      // 4
 }  // namespace
 
 // a1 plane byte offset of (pixel P, ic half h): 16-byte slot 2P + h with its
@@ -69,8 +90,67 @@ struct ConvFwdArgs {
   int layout;           // FrameLayout: FRAMES_RGB = (R, n, 3, 84, 84), planes [0, R, G, B] of slot ks % R;
                         // FRAMES_STACK = (R, n, 4, 84, 84), the 4 planes of slot ks % R
   int e0;               // first env of this launch (env = e0 + blockIdx.x)
+  RingArgs ring;        // PHI: the observation (pair pool, bookkeeping); frames / nvalid / ctl / n / R / t as above
 };
 
+// W1 (16, 4, 8, 8) f32 -> the split planes [3][oc][k] in LDS: thread tid
+// stages 8 consecutive k of one oc (RGB nets: W1 (16, 3, 8, 8) on input
+// planes 1..3, zeros for plane 0)
+__device__ inline void w1_load(const float* W1, bool rgb, int tid, float4& w1a, float4& w1b) {
+  const int w1oc = tid >> 5, w1k = (8 * tid) & 255;
+  w1a = w1b = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (!rgb || w1k >= 64) {
+    const float4* w1p = reinterpret_cast<const float4*>(rgb ? W1 + w1oc * 192 + w1k - 64 : W1 + 8 * tid);
+    w1a = w1p[0];
+    w1b = w1p[1];
+  }
+}
+__device__ inline void w1_split_store(uint8_t* lds, int tid, float4 w1a, float4 w1b) {
+  const int w1oc = tid >> 5, w1k = (8 * tid) & 255;
+  uint4 ph, pm, pl;
+  split3_pack(w1a.x, w1a.y, ph.x, pm.x, pl.x);
+  split3_pack(w1a.z, w1a.w, ph.y, pm.y, pl.y);
+  split3_pack(w1b.x, w1b.y, ph.z, pm.z, pl.z);
+  split3_pack(w1b.z, w1b.w, ph.w, pm.w, pl.w);
+  uint8_t* d = lds + L_R1 + w1oc * WROW + w1k * 2;
+  *reinterpret_cast<uint4*>(d) = ph;
+  *reinterpret_cast<uint4*>(d + W1P) = pm;
+  *reinterpret_cast<uint4*>(d + 2 * W1P) = pl;
+}
+
+// W2 slice of thread tid (oc, 4 ic, 4 taps) -> the split planes in LDS
+__device__ inline void w2_load(const float* W2, int tid, float4 (&w2v)[4]) {
+  const int w2oc = tid >> 4, ic4 = (tid >> 2) & 3, tg = tid & 3;
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii) w2v[ii] = reinterpret_cast<const float4*>(W2)[(w2oc * 16 + 4 * ic4 + ii) * 4 + tg];
+}
+__device__ inline void w2_split_store(uint8_t* lds, int tid, const float4 (&w2v)[4]) {
+  const int w2oc = tid >> 4, ic4 = (tid >> 2) & 3, tg = tid & 3;
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) {
+    const float v0 = w2v[0][tt], v1 = w2v[1][tt], v2 = w2v[2][tt], v3 = w2v[3][tt];
+    uint2 ph, pm, pl;
+    split3_pack(v0, v1, ph.x, pm.x, pl.x);
+    split3_pack(v2, v3, ph.y, pm.y, pl.y);
+    uint8_t* d = lds + L_W2 + w2oc * WROW + ((4 * tg + tt) * 16 + 4 * ic4) * 2;
+    *reinterpret_cast<uint2*>(d) = ph;
+    *reinterpret_cast<uint2*>(d + W2P) = pm;
+    *reinterpret_cast<uint2*>(d + 2 * W2P) = pl;
+  }
+}
+
+// 16 uint8 pixels -> 16 bf16 in LDS (exact)
+__device__ inline void px16_store(uint8_t* d, uint4 x) {
+  uint4 lo, hi;
+  lo.x = px_pair_bf16(x.x, 0); lo.y = px_pair_bf16(x.x, 1);
+  lo.z = px_pair_bf16(x.y, 0); lo.w = px_pair_bf16(x.y, 1);
+  hi.x = px_pair_bf16(x.z, 0); hi.y = px_pair_bf16(x.z, 1);
+  hi.z = px_pair_bf16(x.w, 0); hi.w = px_pair_bf16(x.w, 1);
+  reinterpret_cast<uint4*>(d)[0] = lo;
+  reinterpret_cast<uint4*>(d)[1] = hi;
+}
+
+template <bool PHI>
 __global__ void __launch_bounds__(NT)
 conv_fwd_kernel(ConvFwdArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[L_END];
@@ -78,125 +158,220 @@ conv_fwd_kernel(ConvFwdArgs a) {
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, col = lane & 15;
   const int e = a.e0 + blockIdx.x;
-  // ---- stage: all global loads first, then bf16 conversion / splitting into LDS
-  {
-    const int64_t ks = a.ctl[CTL_STEP] + a.t;
-    const int rs = (int)(ks % a.R);
+  const bool rgb = a.layout == FRAMES_RGB;
+  constexpr int V = PLANE / 16;              // 441 uint4 per screen
+  const int64_t ks = a.ctl[CTL_STEP] + a.t;
+  const int rs = (int)(ks % a.R);
+  // conv1 tiles w, w + 8, w + 16 (and 24 on wave 0): 25 tiles over 8 waves in one
+  // pass, 3-4 independent accumulator chains per wave (per-tile k order s = 0..7)
+  constexpr int TJ = 4;
+  const bool has3 = wave + 24 < 25;   // wave-uniform
+  int baseX[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int tl = (j < 3 || has3) ? wave + 8 * j : wave;
+    const int p = tl * 16 + col, oy = p / 20, ox = p - oy * 20;
+    baseX[j] = L_XB + (4 * oy) * XB_ROW + 8 * ox;
+  }
+  f32x4 big[TJ], sml[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) big[j] = sml[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // k-step s of every tile; W1 fragments of lane (oc = col, g): k = 8 (4 s + g) + 0..7
+  auto conv1_step = [&](int s, bf16x8 wh, bf16x8 wm, bf16x8 wl) {
+    const int u = 4 * s + g, off = (u >> 3) * XB_PLANE + (u & 7) * XB_ROW;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const bf16x8 xa = lds_load8_a8(lds, baseX[j] + off);
+      mfma_x3(xa, wh, wm, wl, big[j], sml[j]);
+    }
+    if (has3) {
+      const bf16x8 xa = lds_load8_a8(lds, baseX[3] + off);
+      mfma_x3(xa, wh, wm, wl, big[3], sml[3]);
+    }
+  };
+  auto w1_frag = [&](int s, bf16x8& wh, bf16x8& wm, bf16x8& wl) {
+    const int off = L_R1 + col * WROW + (4 * s + g) * 16;
+    wh = lds_load<bf16x8>(lds, off);
+    wm = lds_load<bf16x8>(lds, off + W1P);
+    wl = lds_load<bf16x8>(lds, off + 2 * W1P);
+  };
+  if constexpr (PHI) {
+    const RingArgs& o = a.ring;
+    const int64_t pidx = ks % o.pool_len;
+    const uint8_t* pr = o.pair_pool + (pidx * a.n + e) * (int64_t)PAIR;
+    // ---- issue: bookkeeping, older ring planes, weights, then the pair's tap rows
+    const RingObs ob = ring_obs_load(o, e, ks);
+    constexpr int NX = (3 * V + NT - 1) / NT;   // 3
+    uint4 xv[NX];
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const int i = tid + NT * j;
+      const int c = i / V, oo = i - c * V;
+      // loaded whatever nvalid says (planes older than the last reset are zeroed below); slots past
+      // the third plane reload its last 16 bytes, so every thread issues the same number of loads
+      const int cc = i < 3 * V ? c : 2, oc = i < 3 * V ? oo : V - 1;
+      xv[j] = reinterpret_cast<const uint4*>(a.frames + ((int64_t)((rs + a.R - 3 + cc) % a.R) * a.n + e) * PLANE)[oc];
+    }
+    float4 w1a, w1b, w2v[4];
+    w1_load(a.W1, false, tid, w1a, w1b);
+    w2_load(a.W2, tid, w2v);
+    // every wave's small loads reach the memory pipeline before any wave's pair loads (the CU
+    // serves them in issue order): the staging below then waits only for these
+    __builtin_amdgcn_s_barrier();
+    uint4 px[PHI_J][6];
+#pragma unroll
+    for (int j = 0; j < PHI_J; ++j) {   // unconditional (tasks past the end reload task 0) so the load
+      const int i0 = tid + NT * j;        // counter stays exact for the partial waits below
+      const int i = i0 < PHI_TASKS ? i0 : 0;
+      const int r = i / 10, c = i - 10 * r, dy = r >> 1, tap = r & 1;
+      int so, b0, b1;
+      if (o.mode & 2) resize_coeff(dy + CROP_TOP, SRC_H, CROP_H, so, b0, b1);
+      else resize_coeff(dy, SRC_H, DST, so, b0, b1);
+      const int sy = so + tap > SRC_H - 1 ? SRC_H - 1 : so + tap;
+      const uint4* pc = reinterpret_cast<const uint4*>(pr + (size_t)sy * SRC_W * 3 + c * 48);
+      const uint4* pp = reinterpret_cast<const uint4*>(pr + FRAME_BYTES + (size_t)sy * SRC_W * 3 + c * 48);
+      if (ARL_ABLATE & 32) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) px[j][q] = make_uint4(i + q, sy, c, q);
+      } else {
+        px[j][0] = pc[0]; px[j][1] = pc[1]; px[j][2] = pc[2];
+        px[j][3] = pp[0]; px[j][4] = pp[1]; px[j][5] = pp[2];
+      }
+    }
+    // ---- while the pair lands: bookkeeping, coefficient tables, planes 0..2, W1 planes
+    const int nv = ob.nv;
+    if (tid == 0) ring_obs_store(o, e, ks, ob);
+    int16_t* tab = reinterpret_cast<int16_t*>(lds + L_XOFS);
+    if (tid < DST) {
+      int so, a0, a1;
+      resize_coeff(tid, SRC_W, DST, so, a0, a1);
+      tab[tid] = (int16_t)so; tab[DST + tid] = (int16_t)a0; tab[2 * DST + tid] = (int16_t)a1;
+    } else if (tid >= 128 && tid < 128 + DST) {
+      const int dy = tid - 128;
+      int so, b0, b1;
+      if (o.mode & 2) resize_coeff(dy + CROP_TOP, SRC_H, CROP_H, so, b0, b1);
+      else resize_coeff(dy, SRC_H, DST, so, b0, b1);
+      tab[3 * DST + dy] = (int16_t)b0; tab[4 * DST + dy] = (int16_t)b1;
+    }
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const int i = tid + NT * j;
+      if (i < 3 * V) {
+        const int c = i / V, oo = i - c * V;
+        px16_store(lds + L_XB + c * XB_PLANE + oo * 32, c >= 4 - nv ? xv[j] : make_uint4(0, 0, 0, 0));
+      }
+    }
+    w1_split_store(lds, tid, w1a, w1b);
+    __syncthreads();
+    // ---- conv1 k-steps over input planes 0..2 on the matrix cores
+#pragma unroll
+    for (int s = 0; s < ((ARL_ABLATE & 1) ? 0 : 6); ++s) {
+      bf16x8 wh, wm, wl;
+      w1_frag(s, wh, wm, wl);
+      conv1_step(s, wh, wm, wl);
+    }
+    // ---- max of the pair + luminance -> gray tap rows (row r = 2 dy + tap)
+#pragma unroll
+    for (int j = 0; j < PHI_J; ++j) {
+      const int i = tid + NT * j;
+      if (i < PHI_TASKS) {
+        const int r = i / 10, c = i - 10 * r;
+        *reinterpret_cast<uint4*>(lds + L_GRAY + r * SRC_W + c * 16) =
+            (ARL_ABLATE & 64) ? make_uint4(px[j][0].x ^ px[j][3].x, px[j][1].y ^ px[j][4].y, px[j][2].z ^ px[j][5].z,
+                                           px[j][0].w ^ px[j][5].w)
+                              : max_luminance16(px[j][0], px[j][1], px[j][2], px[j][3], px[j][4], px[j][5]);
+      }
+    }
+    __syncthreads();
+    // ---- resize -> the ring slot (HBM, for later steps and the backward) and conv input plane 3 (LDS):
+    // thread -> column quad q (its horizontal taps read once) x rows dy0 + 24 k
+    uint8_t* dst = o.frames + ((int64_t)rs * a.n + e) * PLANE;
+    constexpr int RS_ROWS = 24;                 // 21 quads x 24 row starts = 504 threads
+    if (!(ARL_ABLATE & 128) && tid < (DST / 4) * RS_ROWS) {
+      const int q = tid % (DST / 4), dy0 = tid / (DST / 4);
+      int sx[4], sx1[4], ha0[4], ha1[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int dx = q * 4 + jj;
+        sx[jj] = tab[dx];
+        sx1[jj] = sx[jj] + 1 < SRC_W ? sx[jj] + 1 : SRC_W - 1;
+        ha0[jj] = tab[DST + dx];
+        ha1[jj] = tab[2 * DST + dx];
+      }
+#pragma unroll
+      for (int k = 0; k < (DST + RS_ROWS - 1) / RS_ROWS; ++k) {
+        const int dy = dy0 + RS_ROWS * k;
+        if (dy < DST) {
+          const int b0 = tab[3 * DST + dy], b1 = tab[4 * DST + dy];
+          const uint8_t* g0 = lds + L_GRAY + (2 * dy) * SRC_W;
+          const uint8_t* g1 = g0 + SRC_W;
+          uint32_t packed = 0;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int r0 = (int)g0[sx[jj]] * ha0[jj] + (int)g0[sx1[jj]] * ha1[jj];
+            const int r1 = (int)g1[sx[jj]] * ha0[jj] + (int)g1[sx1[jj]] * ha1[jj];
+            packed |= (uint32_t)resize_vpass(r0, r1, b0, b1, o.mode) << (8 * jj);
+          }
+          *reinterpret_cast<uint32_t*>(dst + dy * DST + q * 4) = packed;
+          *reinterpret_cast<uint2*>(lds + L_XB + 3 * XB_PLANE + (dy * DST + q * 4) * 2) =
+              make_uint2(px_pair_bf16(packed, 0), px_pair_bf16(packed, 1));
+        }
+      }
+    }
+    __syncthreads();   // plane 3 complete, the gray rows dead
+    w2_split_store(lds, tid, w2v);   // conv2 reads it after the barrier in front of conv2
+    // ---- conv1's last k-steps (input plane 3)
+#pragma unroll
+    for (int s = 6; s < ((ARL_ABLATE & 1) ? 0 : 8); ++s) {
+      bf16x8 wh, wm, wl;
+      w1_frag(s, wh, wm, wl);
+      conv1_step(s, wh, wm, wl);
+    }
+    __syncthreads();   // every wave is done with the W1 planes: the a1 planes overwrite them
+  } else {
+    // ---- stage: all global loads first, then bf16 conversion / splitting into LDS
     const int nv = a.nvalid[(int64_t)rs * a.n + e];
     int slot[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) slot[c] = (rs + a.R - 3 + c) % a.R;
-    constexpr int V = PLANE / 16;              // 441 uint4 per screen
     constexpr int NX = (4 * V + NT - 1) / NT;  // 4
     uint4 xv[NX];
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const int i = tid + NT * j;
-      const int c = i / V, o = i - c * V;
+      const int c = i / V, oo = i - c * V;
       xv[j] = make_uint4(0, 0, 0, 0);
       if (!(ARL_ABLATE & 4) && i < 4 * V && c >= 4 - nv)   // planes older than the last reset read as 0
         xv[j] = reinterpret_cast<const uint4*>(
             a.frames + (a.layout == FRAMES_STACK ? ((int64_t)rs * a.n + e) * 4 + c
                         : a.layout == FRAMES_RGB ? ((int64_t)rs * a.n + e) * 3 + (c - 1)
-                                                 : (int64_t)slot[c] * a.n + e) * PLANE)[o];
+                                                 : (int64_t)slot[c] * a.n + e) * PLANE)[oo];
     }
-    // W1: thread -> 8 consecutive k of one oc; W2: thread -> (oc, 4 ic, 4 taps)
-    const int w1oc = tid >> 5, w1k = (8 * tid) & 255;
-    const int w2oc = tid >> 4, ic4 = (tid >> 2) & 3, tg = tid & 3;
-#if !(ARL_ABLATE & 8)
-    float4 w1a = make_float4(0.f, 0.f, 0.f, 0.f), w1b = w1a;   // RGB: input plane 0 is the zero pad
-    const bool rgb = a.layout == FRAMES_RGB;
-    if (!rgb || w1k >= 64) {
-      const float4* w1p = reinterpret_cast<const float4*>(rgb ? a.W1 + w1oc * 192 + w1k - 64 : a.W1 + 8 * tid);
-      w1a = w1p[0];
-      w1b = w1p[1];
-    }
-    float4 w2v[4];
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii)
-      w2v[ii] = reinterpret_cast<const float4*>(a.W2)[(w2oc * 16 + 4 * ic4 + ii) * 4 + tg];
-#endif
+    float4 w1a, w1b, w2v[4];
+    w1_load(a.W1, rgb, tid, w1a, w1b);
+    w2_load(a.W2, tid, w2v);
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const int i = tid + NT * j;
       if (i < 4 * V) {
-        const int c = i / V, o = i - c * V;
-        uint4 lo, hi;
-        lo.x = px_pair_bf16(xv[j].x, 0); lo.y = px_pair_bf16(xv[j].x, 1);
-        lo.z = px_pair_bf16(xv[j].y, 0); lo.w = px_pair_bf16(xv[j].y, 1);
-        hi.x = px_pair_bf16(xv[j].z, 0); hi.y = px_pair_bf16(xv[j].z, 1);
-        hi.z = px_pair_bf16(xv[j].w, 0); hi.w = px_pair_bf16(xv[j].w, 1);
-        uint4* d = reinterpret_cast<uint4*>(lds + L_XB + c * XB_PLANE + o * 32);
-        d[0] = lo;
-        d[1] = hi;
+        const int c = i / V, oo = i - c * V;
+        px16_store(lds + L_XB + c * XB_PLANE + oo * 32, xv[j]);
       }
     }
-#if !(ARL_ABLATE & 8)
-    {
-      uint4 ph, pm, pl;
-      split3_pack(w1a.x, w1a.y, ph.x, pm.x, pl.x);
-      split3_pack(w1a.z, w1a.w, ph.y, pm.y, pl.y);
-      split3_pack(w1b.x, w1b.y, ph.z, pm.z, pl.z);
-      split3_pack(w1b.z, w1b.w, ph.w, pm.w, pl.w);
-      uint8_t* d = lds + L_R1 + w1oc * WROW + w1k * 2;
-      *reinterpret_cast<uint4*>(d) = ph;
-      *reinterpret_cast<uint4*>(d + W1P) = pm;
-      *reinterpret_cast<uint4*>(d + 2 * W1P) = pl;
-    }
+    w1_split_store(lds, tid, w1a, w1b);
+    w2_split_store(lds, tid, w2v);
+    __syncthreads();
+    // W1 fragments in registers (96 VGPRs), then the W1 planes are free for a1
+    bf16x8 w1h[8], w1m[8], w1l[8];
 #pragma unroll
-    for (int tt = 0; tt < 4; ++tt) {
-      const float v0 = w2v[0][tt], v1 = w2v[1][tt], v2 = w2v[2][tt], v3 = w2v[3][tt];
-      uint2 ph, pm, pl;
-      split3_pack(v0, v1, ph.x, pm.x, pl.x);
-      split3_pack(v2, v3, ph.y, pm.y, pl.y);
-      uint8_t* d = lds + L_W2 + w2oc * WROW + ((4 * tg + tt) * 16 + 4 * ic4) * 2;
-      *reinterpret_cast<uint2*>(d) = ph;
-      *reinterpret_cast<uint2*>(d + W2P) = pm;
-      *reinterpret_cast<uint2*>(d + 2 * W2P) = pl;
-    }
-#endif
-  }
-  __syncthreads();
-  // ---- conv1 B fragments: lane (oc = col, g), k-step s -> k = 8 (4 s + g) + 0..7
-  bf16x8 w1h[8], w1m[8], w1l[8];
+    for (int s = 0; s < 8; ++s) w1_frag(s, w1h[s], w1m[s], w1l[s]);
+    __syncthreads();
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    const int off = L_R1 + col * WROW + (4 * s + g) * 16;
-    w1h[s] = lds_load<bf16x8>(lds, off);
-    w1m[s] = lds_load<bf16x8>(lds, off + W1P);
-    w1l[s] = lds_load<bf16x8>(lds, off + 2 * W1P);
+    for (int s = 0; s < ((ARL_ABLATE & 1) ? 0 : 8); ++s) conv1_step(s, w1h[s], w1m[s], w1l[s]);
   }
-  __syncthreads();   // the W1 planes are overwritten by the a1 planes below
   const float bias1 = a.b1[col];
   float* a1g = a.a1 + (int64_t)e * A1;
-  // tiles w, w + 8, w + 16 (and 24 on wave 0): 25 tiles over 8 waves in one pass,
-  // 3-4 independent accumulator chains per wave (per-tile k order unchanged)
   {
-    constexpr int TJ = 4;
-    const bool has3 = wave + 24 < 25;   // wave-uniform
-    int baseX[TJ];
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const int tl = (j < 3 || has3) ? wave + 8 * j : wave;
-      const int p = tl * 16 + col, oy = p / 20, ox = p - oy * 20;
-      baseX[j] = L_XB + (4 * oy) * XB_ROW + 8 * ox;
-    }
-    f32x4 big[TJ], sml[TJ];
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) big[j] = sml[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < ((ARL_ABLATE & 1) ? 0 : 8); ++s) {
-      const int u = 4 * s + g, off = (u >> 3) * XB_PLANE + (u & 7) * XB_ROW;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const bf16x8 xa = lds_load8_a8(lds, baseX[j] + off);
-        mfma_x3(xa, w1h[s], w1m[s], w1l[s], big[j], sml[j]);
-      }
-      if (has3) {
-        const bf16x8 xa = lds_load8_a8(lds, baseX[3] + off);
-        mfma_x3(xa, w1h[s], w1m[s], w1l[s], big[3], sml[3]);
-      }
-    }
     // C rows g*4 + r -> positions tile*16 + g*4 + r, col = oc
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
@@ -275,8 +450,18 @@ hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const i
   if (n <= 0) return hipSuccess;
   if (ne < 0) ne = n;
   if (ne <= 0) return hipSuccess;
-  ConvFwdArgs a{frames, nvalid, ctl, n, R, t, W1, b1, W2, b2, a1, a2, layout, e0};
-  hipLaunchKernelGGL(conv_fwd_kernel, dim3(ne), dim3(NT), 0, s, a);
+  ConvFwdArgs a{frames, nvalid, ctl, n, R, t, W1, b1, W2, b2, a1, a2, layout, e0, RingArgs{}};
+  hipLaunchKernelGGL(conv_fwd_kernel<false>, dim3(ne), dim3(NT), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_phi_conv_fwd(const RingArgs& ring, const float* W1, const float* b1, const float* W2,
+                               const float* b2, float* a1, float* a2, hipStream_t s) {
+  const int ne = ring.ne < 0 ? ring.n : ring.ne;
+  if (ne <= 0) return hipSuccess;
+  ConvFwdArgs a{ring.frames, ring.nvalid, ring.ctl, ring.n, ring.R, ring.t, W1, b1, W2, b2, a1, a2, FRAMES_RING,
+                ring.e0, ring};
+  hipLaunchKernelGGL(conv_fwd_kernel<true>, dim3(ne), dim3(NT), 0, s, a);
   return hipGetLastError();
 }
 

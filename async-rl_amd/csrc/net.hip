@@ -372,7 +372,7 @@ static PolicyArgs slot_policy_args(const Net& net, int t, int mode) {
 // of window slot t.  Disjoint env ranges touch disjoint rows of every buffer
 // (the FC split-K slab and tickets included: e0 is a multiple of the FC's
 // 32-row tile), so ranges can run concurrently on separate streams.
-hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne) {
+hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne, const RingArgs* obs) {
   if (ne < 0) {
     e0 = 0;
     ne = net.N;
@@ -388,7 +388,11 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne) {
   float* a2 = net.at<float>(net.w_a2) + (int64_t)t * n * A2;
   float* hfc = net.at<float>(net.w_hfc) + ((int64_t)t * n + e0) * HID;
   const float* P = net.p;
-  if (!(part & ACT_AFTER_CONV))
+  if (obs != nullptr) {
+    if (net.layout != FRAMES_RING || (part & ACT_AFTER_CONV) || obs->e0 != e0 || obs->ne != ne)
+      return hipErrorInvalidValue;
+    ARL_TRY(launch_phi_conv_fwd(*obs, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W, P + net.o_c2b, a1, a2, s));
+  } else if (!(part & ACT_AFTER_CONV))
     ARL_TRY(launch_conv_fwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
                             net.at<int64_t>(net.w_ctl), n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W,
                             P + net.o_c2b, a1, a2, s, net.layout, e0, ne));

@@ -21,48 +21,12 @@
 #include <stdint.h>
 
 #include "arl_internal.hpp"
+#include "phi_ops.hpp"
 
 namespace arl {
 
-constexpr int SRC_H = 210, SRC_W = 160, DST = 84;
 constexpr int BAND = 12;                   // output rows per workgroup
 constexpr int NBANDS = DST / BAND;         // 7
-constexpr int FRAME_BYTES = SRC_H * SRC_W * 3;   // 100,800
-constexpr int CROP_H = 110, CROP_TOP = (110 - 84) - 8;   // ale.py:75-81: resize to 110 rows, crop 18 .. 101
-
-
-// OpenCV INTER_LINEAR coefficients for one axis (see oracle.resize_coeffs):
-// f = (float)((d+0.5)*scale-0.5); s = floor(f); f -= s; clamps; a = rint(c*2048)
-__device__ inline void resize_coeff(int d, int ssize, int dsize, int& ofs, int& a0, int& a1) {
-  const double inv_scale = (double)dsize / (double)ssize;
-  const double scale = 1.0 / inv_scale;
-  float f = (float)__dsub_rn(__dmul_rn((double)d + 0.5, scale), 0.5);
-  int s = (int)floorf(f);
-  f = __fsub_rn(f, (float)s);
-  if (s < 0) { f = 0.f; s = 0; }
-  if (s >= ssize - 1) { f = 0.f; s = ssize - 1; }
-  const float c0 = __fsub_rn(1.f, f);
-  ofs = s;
-  a0 = (int)rintf(__fmul_rn(c0, 2048.f));
-  a1 = (int)rintf(__fmul_rn(f, 2048.f));
-}
-
-__device__ inline uint32_t umax_bytes(uint32_t a, uint32_t b) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    uint32_t x = (a >> (8 * i)) & 0xffu, y = (b >> (8 * i)) & 0xffu;
-    r |= (x > y ? x : y) << (8 * i);
-  }
-  return r;
-}
-
-// ale.py:67-69, float64, left-to-right, explicit RN ops (no FMA contraction)
-__device__ inline uint32_t luminance(uint32_t r, uint32_t g, uint32_t b) {
-  const double v = __dadd_rn(__dadd_rn(__dmul_rn((double)r, 0.2126), __dmul_rn((double)g, 0.0722)),
-                             __dmul_rn((double)b, 0.7152));
-  return (uint32_t)v;   // astype(uint8): truncation (v in [0, 255))
-}
 
 struct PhiShared {
   uint8_t gray[BAND][2][SRC_W];   // [output row][tap][x]
@@ -105,22 +69,7 @@ __device__ inline void phi_band(const uint8_t* __restrict__ cur, const uint8_t* 
     else resize_coeff(dy0 + tid - 96, SRC_H, DST, o, b0, b1);
     sh.yofs[tid - 96] = (int16_t)o; sh.yb0[tid - 96] = (int16_t)b0; sh.yb1[tid - 96] = (int16_t)b1;
   }
-  if (stager) {
-    uint32_t w[12] = {umax_bytes(c0.x, p0.x), umax_bytes(c0.y, p0.y), umax_bytes(c0.z, p0.z),
-                      umax_bytes(c0.w, p0.w), umax_bytes(c1.x, p1.x), umax_bytes(c1.y, p1.y),
-                      umax_bytes(c1.z, p1.z), umax_bytes(c1.w, p1.w), umax_bytes(c2.x, p2.x),
-                      umax_bytes(c2.y, p2.y), umax_bytes(c2.z, p2.z), umax_bytes(c2.w, p2.w)};
-    uint32_t g[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int p = 0; p < 16; ++p) {
-      const int b = 3 * p;
-      const uint32_t R = (w[b >> 2] >> (8 * (b & 3))) & 0xffu;
-      const uint32_t G = (w[(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 0xffu;
-      const uint32_t B = (w[(b + 2) >> 2] >> (8 * ((b + 2) & 3))) & 0xffu;
-      g[p >> 2] |= luminance(R, G, B) << (8 * (p & 3));
-    }
-    *reinterpret_cast<uint4*>(&sh.gray[ly][tap][c * 16]) = make_uint4(g[0], g[1], g[2], g[3]);
-  }
+  if (stager) *reinterpret_cast<uint4*>(&sh.gray[ly][tap][c * 16]) = max_luminance16(c0, c1, c2, p0, p1, p2);
   __syncthreads();
   // resize: task = (local row ly, group of 4 output columns q) -> 12*21 = 252
   if (tid < BAND * (DST / 4)) {
@@ -135,13 +84,7 @@ __device__ inline void phi_band(const uint8_t* __restrict__ cur, const uint8_t* 
       const int a0 = sh.xa0[dx], a1 = sh.xa1[dx];
       const int r0 = (int)sh.gray[ly][0][sx] * a0 + (int)sh.gray[ly][0][sx1] * a1;
       const int r1 = (int)sh.gray[ly][1][sx] * a0 + (int)sh.gray[ly][1][sx1] * a1;
-      int v;
-      if ((mode & 1) == 0) {   // FixedPtCast<int, uchar, 22>
-        v = (b0 * r0 + b1 * r1 + (1 << 21)) >> 22;
-      } else {                 // VResizeLinearVec_32s8u (mulhi form)
-        v = ((((r0 >> 4) * b0) >> 16) + (((r1 >> 4) * b1) >> 16) + 2) >> 2;
-      }
-      v = v < 0 ? 0 : (v > 255 ? 255 : v);
+      const int v = resize_vpass(r0, r1, b0, b1, mode);
       packed |= (uint32_t)v << (8 * j);
     }
     *reinterpret_cast<uint32_t*>(out + (size_t)(dy0 + ly) * DST + q * 4) = packed;
@@ -196,19 +139,7 @@ phi_ring_kernel(RingArgs a) {
   const uint8_t* pr = a.pair_pool + (pidx * a.n + e) * (int64_t)(2 * FRAME_BYTES);
   uint8_t* dst = a.frames + ((int64_t)slot * a.n + e) * PLANE;
   phi_band(pr, pr + FRAME_BYTES, dst, blockIdx.x * BAND, a.mode, sh);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    const uint8_t d = a.done_pool ? a.done_pool[pidx * a.n + e] : 0;
-    const bool rs = a.force_reset || d != 0;
-    const int pslot = (int)((k + a.R - 1) % a.R);
-    int nv = rs ? 1 : (int)a.nvalid[(int64_t)pslot * a.n + e] + 1;
-    a.nvalid[(int64_t)slot * a.n + e] = (uint8_t)(nv > 4 ? 4 : nv);
-    a.reset_flags[(int64_t)a.t * a.n + e] = rs ? 1 : 0;
-    if (a.t >= 1) {
-      float r = a.reward_pool ? a.reward_pool[pidx * a.n + e] : 0.f;
-      a.rewards[(int64_t)(a.t - 1) * a.n + e] = r;
-      a.dones[(int64_t)(a.t - 1) * a.n + e] = d;
-    }
-  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) ring_obs_store(a, e, k, ring_obs_load(a, e, k));
 }
 
 // ---------------------------------------------------------------- RGB (Doom)

@@ -30,7 +30,7 @@ sys.path.insert(0, os.environ.get("ASYNCRL_PKG_ROOT") or os.path.join(ROOT, "asy
 
 from asyncrl_amd import A3C, A3CFF, A3CFFNature, A3CLSTM, DoomA3CFF, DoomA3CLSTM, GradientClipping, RMSpropAsync  # noqa: E402
 from asyncrl_amd import _lib  # noqa: E402
-from asyncrl_amd._lib import LEARN_CONV  # noqa: E402
+from asyncrl_amd._lib import ACT_CONV_ONLY, LEARN_CONV  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 F32_MFMA_PEAK_TFS = 157.3      # dense fp32 matrix peak (spec)
@@ -50,6 +50,7 @@ NAT_CONV_FWD_FLOP_PER_ENV = 2 * (400 * 32 * 256 + 81 * 64 * 512 + 49 * 64 * 576)
 NAT_FC_FWD_FLOP_PER_ENV = 2 * 3136 * 512
 NAT_CONV_BWD_FLOP_PER_SAMPLE = 2 * (2 * 49 * 64 * 576 + 2 * 81 * 64 * 512 + 400 * 32 * 256)
 PHI_STACK_BYTES_PER_PAIR = 201600 + 3 * 7056 + 4 * 7056   # pair + 3 prior planes + 4-plane stack
+PLANE_BYTES, A1_FLOATS, A2_FLOATS = 7056, 6400, 2592     # ring plane; conv1 / conv2 activations kept for backward
 
 # BASELINE.json configs[1..4] -> (arch, envs per GPU, actions)
 WORKLOADS = {"c2": ("ff", 256, 4), "c3": ("lstm", 1024, 6), "c4": ("ff", 512, 4), "c5": ("phi", 16384, 0)}
@@ -386,12 +387,19 @@ def main():
             ev1.synchronize()
             return 1e3 * ev0.elapsed_time(ev1) / a.kernel_reps
 
+        fused = net.fused_observe   # steps 1..T: phi inside the conv launch; step 0 (window start) conv only
         specs = [  # name, kernel, launch fn, launches per window, bound, algorithmic work per launch
+            # phi + conv fused (conv_fwd_kernel<true>): reads the frame pair and the 3 older ring planes,
+            # writes the new plane, a1 and a2
+            ("phi_conv", "conv_fwd_kernel<true> (phi + conv1 + conv2)",
+             lambda i: net.observe_act(1 + i % T, pairs, rewards, dones, P, mode=ACT_CONV_ONLY, stream=stream),
+             T, "hbm", N * (phi_bytes + 3 * PLANE_BYTES + 4 * (A1_FLOATS + A2_FLOATS))) if fused else None,
             ("phi", "rgb_ring_kernel" if doom else "phi_ring_kernel",
-             lambda i: net.observe(1 + i % T, pairs, rewards, dones, P, stream=stream), T + 1, "hbm",
+             lambda i: net.observe(1 + i % T, pairs, rewards, dones, P, stream=stream), 0 if fused else T + 1, "hbm",
              N * phi_bytes),
-            ("conv_fwd", "gemm_kernel x3 (implicit-GEMM convs)" if nat else "conv_fwd_kernel",
-             lambda i: net.run_stage("conv_fwd", i % T, stream=stream), T + 1, "mfma", N * conv_fwd_flop),
+            ("conv_fwd", "gemm_kernel x3 (implicit-GEMM convs)" if nat else "conv_fwd_kernel<false>",
+             lambda i: net.run_stage("conv_fwd", i % T, stream=stream), 1 if fused else T + 1, "mfma",
+             N * conv_fwd_flop),
             ("fc_fwd", "gemm_kernel + reduce_grad_kernel" if nat else "fc_fwd_kernel" if lstm else
              "fc_fwd_kernel (split-K partials)",
              lambda i: net.run_stage("fc_fwd", i % T, stream=stream), T + 1, "mfma", N * fc_fwd_flop),
@@ -430,6 +438,11 @@ def main():
                                  "launches_per_window": calls, "window_share_us": round(us * calls, 1),
                                  "achieved": round(ach, 2), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
                                  ("bytes" if bound == "hbm" else "flop") + "_per_launch": int(work)}
+                if name == "phi_conv":   # its MFMA side: the conv layers' FLOPs at the same launch time
+                    tf = N * conv_fwd_flop / (us * 1e-6) / 1e12
+                    kernels[name]["mfma"] = {"flop_per_launch": int(N * conv_fwd_flop), "achieved": round(tf, 2),
+                                             "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                                             "frac": round(tf / F32_MFMA_PEAK_TFS, 4)}
         dom = max(kernels, key=lambda k: kernels[k]["window_share_us"])
         d = kernels[dom]
         traffic = measured_traffic(N, T, arch, d["kernel"].split()[0])

@@ -175,6 +175,18 @@ int arl_observe_envs(arl_net* net, int t, int e0, int ne, const uint8_t* pool, i
 #define ARL_ACT_AFTER_CONV 8
 int arl_act_envs(arl_net* net, int t, int e0, int ne, int mode, void* stream);
 
+/* arl_observe_envs + arl_act_envs of the same step in one call (frame-pair
+ * nets with the NIPS head: FF, LSTM): the observation's phi, ring write and
+ * bookkeeping run inside the conv launch (one workgroup per env reads its
+ * frame pair, writes the new screen to the ring and convolves it from LDS),
+ * so the step is one launch shorter.  Same results as the two calls
+ * (ale.py:59-89 + a3c.py:154-164).  ne < 0: all envs.  mode as arl_act_envs,
+ * optionally | ARL_ACT_CONV_ONLY (the rest of the step then follows with
+ * arl_act_envs(.., mode | ARL_ACT_AFTER_CONV)). */
+int arl_observe_act_envs(arl_net* net, int t, int e0, int ne, const uint8_t* pair_pool, const float* reward_pool,
+                         const uint8_t* done_pool, int64_t pool_len, int force_reset, int resize_mode, int mode,
+                         void* stream);
+
 /* Window update, gradient part (a3c.py:82-130): n-step returns with R = 0 at
  * terminals, advantage / entropy / value loss gradient, backward through
  * heads, [LSTM BPTT], FC, conv2, conv1 -> grads (overwritten). */

@@ -615,3 +615,59 @@ def test_learn_fork_identical(gpu, arch):
         g = net.view(got[0], name)
         assert torch.isfinite(g).all() and not (g == 1234.5).any(), name
     assert torch.equal(got[0], got[1]) and torch.equal(got[0], got[2])
+
+
+@pytest.mark.parametrize("arch,N,groups,resize_mode", [("ff", 96, 1, 0), ("ff", 256, 2, 0), ("ff", 64, 1, 1),
+                                                         ("ff", 64, 1, 2), ("lstm", 80, 2, 0)])
+def test_fused_observe_identical(gpu, arch, N, groups, resize_mode):
+    """observe + act fused into one conv launch (arl_observe_act_envs,
+    conv_fwd_kernel<true>) vs arl_observe + arl_act: bit-identical ring
+    planes, nvalid / reset / reward / done bookkeeping, conv activations,
+    actions, values, gradients and parameters over eager and graph-captured
+    windows, with env groups and every resize mode."""
+    from asyncrl_amd import A3C, A3CFF, A3CLSTM, GradientClipping, RMSpropAsync
+    rng = np.random.default_rng(97)
+    T, P = 5, 7
+    Model = A3CFF if arch == "ff" else A3CLSTM
+    pairs, rewards, dones = make_pools(rng, P, N, "uniform", p_done=0.15)
+    dp, dr, dd = dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu)
+
+    def mk(fuse):
+        m = Model(4, n_envs=N, t_max=T, seed=5, init_seed=6, frames="pairs")
+        m.net.fuse_obs = fuse
+        o = RMSpropAsync(lr=7e-4, eps=0.1, alpha=0.99).setup(m)
+        o.add_hook(GradientClipping(40))
+        return A3C(m, o, T, 0.99, resize_mode=resize_mode)
+
+    outs = []
+    for fuse in (False, True):
+        ag = mk(fuse)
+        assert ag.net.fused_observe == fuse
+        ag.run_window(dp, dr, dd, P, first=True, env_groups=groups)
+        ag.run_window(dp, dr, dd, P, env_groups=groups)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            ag.run_window(dp, dr, dd, P, stream=s, env_groups=groups)
+        s.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            ag.run_window(dp, dr, dd, P, stream=s, env_groups=groups, split_update=True)
+        g.replay()
+        torch.cuda.synchronize()
+        net = ag.net
+        R = net.t_max + 4
+        o = {"frames": net.buffer("frames", torch.uint8, (R, N, 84, 84)).clone(),
+             "nvalid": net.buffer("nvalid", torch.uint8, (R, N)).clone(),
+             "reset": net.buffer("reset", torch.uint8, (T + 1, N)).clone(),
+             "rewards": net.buffer("rewards", torch.float32, (T, N)).clone(),
+             "dones": net.buffer("dones", torch.uint8, (T, N)).clone(),
+             "a1": net.buffer("a1", torch.float32, (T + 1, N, 6400)).clone(),
+             "a2": net.buffer("a2", torch.float32, (T + 1, N, 2592)).clone(),
+             "actions": net.buffer("actions", torch.int32, (T + 1, N)).clone(),
+             "v": net.buffer("v", torch.float32, (T + 1, N)).clone(),
+             "grads": net.grads.clone(), "params": net.params.clone(), "ms": net.ms.clone()}
+        outs.append(o)
+    assert int(outs[0]["nvalid"].min()) >= 1 and int(outs[0]["reset"][1:].sum()) > 0   # resets happened
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
