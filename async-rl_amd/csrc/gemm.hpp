@@ -131,6 +131,15 @@ __device__ inline void gemm_gather(const AOp& A, const BOp& B, int M, int N, int
   }
 }
 
+// an epilogue type with `static constexpr bool kTile = true` gets the whole
+// output tile at once (E.tile) instead of per-element stores
+template <class E, class = void>
+struct epi_tile_flag { static constexpr bool value = false; };
+template <class E>
+struct epi_tile_flag<E, decltype((void)E::kTile)> { static constexpr bool value = E::kTile; };
+template <class E>
+constexpr bool epi_is_tile() { return epi_tile_flag<E>::value; }
+
 // One BM x BN output tile (split-K slice z) of the implicit GEMM; the body of
 // gemm_kernel and of gemm2_kernel (two independent GEMMs in one launch).
 template <int BM, int BN, int BK, int WM, int WN, int AV, int BV, int NTH, class AOp, class BOp, class EOp>
@@ -247,17 +256,34 @@ __device__ inline void gemm_tile(const AOp& A, const BOp& B, const EOp& E, int M
   }
 
   // C/D map for 16x16x4 f32: col = lane & 15, row = (lane >> 4) * 4 + r
+  if constexpr (epi_is_tile<EOp>()) {
+    // whole-tile epilogue (e.g. the LSTM cell on a gate tile): the raw tile in
+    // LDS (the B staging area, row stride BN), then E.tile on all threads
+    static_assert(BK * LDB >= BM * BN, "tile fits the B staging area");
+    __syncthreads();   // the last chunk is consumed
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
-        if (m < M && n < N) E.store(m, n, acc[i][j][r], z);
+        for (int r = 0; r < 4; ++r)
+          Bs[(wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r) * BN + wn * (BN / WN) + j * 16 + (lane & 15)] =
+              acc[i][j][r];
+    __syncthreads();
+    E.template tile<BM, BN, NTH>(Bs, m0, n0, M, N);
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
+          if (m < M && n < N) E.store(m, n, acc[i][j][r], z);
+        }
       }
-    }
+  }
 }
 
 template <int BM, int BN, int BK, int WM, int WN, class AOp, class BOp, class EOp, int AV = GS, int BV = GS>

@@ -126,6 +126,78 @@ __global__ void lstm_cell_fwd_kernel(const float* __restrict__ gates, const floa
   h_out[i] = __fmul_rn(og, tanhf(c));
 }
 
+// The LSTM gate GEMM's epilogue with the cell fused in (one launch per step):
+// the gate tile (BM rows x BN interleaved gate columns = BN / 4 units) gets the
+// bias, is written out (the backward reads it), and each (row, unit) runs
+// lstm_cell_fwd_kernel's arithmetic -- the same operations on the same values
+// (bit-identical).
+struct EpiLstmCell {
+  static constexpr bool kTile = true;
+  float* __restrict__ gates; const float* __restrict__ b; const float* __restrict__ c_prev;
+  const uint8_t* __restrict__ reset; float* __restrict__ c_out; float* __restrict__ h_out;
+  template <int BM, int BN, int NTH>
+  __device__ void tile(const float* T, int m0, int n0, int M, int) const {
+    for (int it = threadIdx.x; it < BM * (BN / 4); it += NTH) {
+      const int ml = it / (BN / 4), u = it - ml * (BN / 4), m = m0 + ml, n = n0 + 4 * u;
+      if (m >= M) continue;
+      const float4 bb = *reinterpret_cast<const float4*>(b + n);
+      const float4 v = *reinterpret_cast<const float4*>(T + ml * BN + 4 * u);
+      const float4 g = make_float4(__fadd_rn(v.x, bb.x), __fadd_rn(v.y, bb.y), __fadd_rn(v.z, bb.z),
+                                   __fadd_rn(v.w, bb.w));
+      *reinterpret_cast<float4*>(gates + (int64_t)m * GATES + n) = g;
+      const int64_t i = (int64_t)m * HID + (n >> 2);
+      const float a = tanhf(g.x), ig = sigm(g.y), fg = sigm(g.z), og = sigm(g.w);
+      const float cp = reset[m] ? 0.f : c_prev[i];
+      const float c = __fadd_rn(__fmul_rn(a, ig), __fmul_rn(fg, cp));
+      c_out[i] = c;
+      h_out[i] = __fmul_rn(og, tanhf(c));
+    }
+  }
+};
+
+// ARL_LSTM_SPLIT=1: the LSTM cell as its own launches (forward: after the gate
+// GEMM; backward: after the BPTT reduce) -- A/B timing only
+static const bool LSTM_SPLIT = [] {
+  const char* e = getenv("ARL_LSTM_SPLIT");
+  return e != nullptr && e[0] == '1';
+}();
+
+// gates = [x | h] [Wu ; Wl]^T + b, then the cell: c_out, h_out (rows [0, n))
+template <class AOp, class BOp>
+static hipError_t lstm_gates_cell(const AOp& A, const BOp& B, const float* bias, float* gates, const float* c_prev,
+                                  const uint8_t* reset, float* c_out, float* h_out, int n, hipStream_t s) {
+  if (!LSTM_SPLIT)
+    return launch_gemm<32, 64, 32, 2, 2, GK, GK>(A, B, EpiLstmCell{gates, bias, c_prev, reset, c_out, h_out}, n, GATES,
+                                                 2 * HID, 1, s);
+  const hipError_t e = launch_gemm<32, 64, 32, 2, 2, GK, GK>(A, B, EpiBias{gates, bias, GATES}, n, GATES, 2 * HID, 1, s);
+  if (e != hipSuccess) return e;
+  const int64_t cnt = (int64_t)n * HID;
+  hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, gates, c_prev, reset,
+                     c_out, h_out, cnt);
+  return hipGetLastError();
+}
+
+// F.lstm backward of element i = (m, unit) at step t: dh = dL/dh_t (heads +
+// carried), dcn in: dc carried from t+1 (first: none), out: dc carried to t-1.
+__device__ inline void lstm_cell_bwd_elem(const float* __restrict__ gates, const float* __restrict__ c_t,
+                                          const float* __restrict__ c_prev, bool rs, float dh, float* __restrict__ dcn,
+                                          float* __restrict__ dG, bool first, int64_t i) {
+  const float4 g = reinterpret_cast<const float4*>(gates)[i];
+  const float a = tanhf(g.x), ig = sigm(g.y), fg = sigm(g.z), og = sigm(g.w);
+  const float c = c_t[i];
+  const float tc = tanhf(c);
+  float dc = __fmul_rn(__fmul_rn(dh, og), __fsub_rn(1.f, __fmul_rn(tc, tc)));
+  if (!first) dc = __fadd_rn(dc, dcn[i]);
+  const float cp = rs ? 0.f : c_prev[i];
+  float4 d;
+  d.x = __fmul_rn(__fmul_rn(dc, ig), __fsub_rn(1.f, __fmul_rn(a, a)));
+  d.y = __fmul_rn(__fmul_rn(__fmul_rn(dc, a), ig), __fsub_rn(1.f, ig));
+  d.z = __fmul_rn(__fmul_rn(__fmul_rn(dc, cp), fg), __fsub_rn(1.f, fg));
+  d.w = __fmul_rn(__fmul_rn(__fmul_rn(dh, tc), og), __fsub_rn(1.f, og));
+  reinterpret_cast<float4*>(dG)[i] = d;
+  dcn[i] = rs ? 0.f : __fmul_rn(dc, fg);
+}
+
 // F.lstm backward for step t.  dH: dL/dh_t from the heads; dhn/dcn: carried
 // from step t+1 (ignored when first); writes dG (interleaved) and dcn for t-1.
 __global__ void lstm_cell_bwd_kernel(const float* __restrict__ gates, const float* __restrict__ c_t,
@@ -135,22 +207,26 @@ __global__ void lstm_cell_bwd_kernel(const float* __restrict__ gates, const floa
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   const int64_t m = i / HID;
-  const float4 g = reinterpret_cast<const float4*>(gates)[i];
-  const float a = tanhf(g.x), ig = sigm(g.y), fg = sigm(g.z), og = sigm(g.w);
-  const float c = c_t[i];
-  const float tc = tanhf(c);
   const float dh = first ? dH[i] : __fadd_rn(dH[i], dhn[i]);
-  float dc = __fmul_rn(__fmul_rn(dh, og), __fsub_rn(1.f, __fmul_rn(tc, tc)));
-  if (!first) dc = __fadd_rn(dc, dcn[i]);
-  const bool rs = reset[m] != 0;
-  const float cp = rs ? 0.f : c_prev[i];
-  float4 d;
-  d.x = __fmul_rn(__fmul_rn(dc, ig), __fsub_rn(1.f, __fmul_rn(a, a)));
-  d.y = __fmul_rn(__fmul_rn(__fmul_rn(dc, a), ig), __fsub_rn(1.f, ig));
-  d.z = __fmul_rn(__fmul_rn(__fmul_rn(dc, cp), fg), __fsub_rn(1.f, fg));
-  d.w = __fmul_rn(__fmul_rn(__fmul_rn(dh, tc), og), __fsub_rn(1.f, og));
-  reinterpret_cast<float4*>(dG)[i] = d;
-  dcn[i] = rs ? 0.f : __fmul_rn(dc, fg);
+  lstm_cell_bwd_elem(gates, c_t, c_prev, reset[m] != 0, dh, dcn, dG, first != 0, i);
+}
+
+// The BPTT split-K reduce of step t (dh_{t-1} = (dG_t Wl) * (no reset at t),
+// reduce_grad_kernel + MapResetMask) fused with the cell backward of step t-1:
+// the carried dh never leaves registers.  Same f64 sum order as
+// reduce_grad_kernel for splits <= 4 (((s0 + s1) + s2) + s3), bit-identical.
+__global__ void lstm_dh_cell_bwd_kernel(const float* __restrict__ slab, int splits, const uint8_t* __restrict__ reset_t,
+                                        const float* __restrict__ gates, const float* __restrict__ c_t,
+                                        const float* __restrict__ c_prev, const uint8_t* __restrict__ reset,
+                                        const float* __restrict__ dH, float* __restrict__ dcn, float* __restrict__ dG,
+                                        int64_t count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const int64_t m = i / HID;
+  double v = 0.0;
+  for (int z = 0; z < splits; ++z) v += (double)slab[(int64_t)z * count + i];
+  const float dhn = reset_t[m] ? 0.f : (float)v;
+  lstm_cell_bwd_elem(gates, c_t, c_prev, reset[m] != 0, __fadd_rn(dH[i], dhn), dcn, dG, false, i);
 }
 
 // dh[s][j] = sum_k dlogits[s][k] Wpi[k][j] + dv[s] Wv[j]; with mask: * (h > 0)
@@ -422,12 +498,9 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne, con
     float* cout = net.at<float>(net.w_cbuf) + (r0 + n) * HID;
     const uint8_t* rs = net.at<uint8_t>(net.w_reset) + r0;
     // gates = [x | h] [Wu ; Wl]^T + b (split-K 2 + a bias reduce measured slower: 28.5 vs 27.7 us)
-    ARL_TRY((launch_gemm<32, 64, 32, 2, 2, GK, GK>(LstmGateA{hfc, hprev, rs}, LstmGateB{P + net.o_luW, P + net.o_llW},
-                                                   EpiBias{gates, P + net.o_lub, GATES}, ne, GATES, 2 * HID, 1, s)));
-    const int64_t cnt = (int64_t)ne * HID;
-    hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, gates, cprev, rs,
-                       cout, hout, cnt);
-    ARL_TRY(hipGetLastError());
+    // the cell runs in the GEMM's epilogue (EpiLstmCell; ARL_LSTM_SPLIT=1: a separate launch)
+    ARL_TRY(lstm_gates_cell(LstmGateA{hfc, hprev, rs}, LstmGateB{P + net.o_luW, P + net.o_llW}, P + net.o_lub, gates,
+                            cprev, rs, cout, hout, ne, s));
     hpol = hout;
   }
   return launch_policy(hpol, ne, P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
@@ -480,12 +553,9 @@ hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_
     float* hn = net.at<float>(net.w_eval_hn);
     float* cn = net.at<float>(net.w_eval_cn);
     uint8_t* rs = net.at<uint8_t>(net.w_eval_reset);
-    ARL_TRY((launch_gemm<32, 64, 32, 2, 2, GK, GK>(LstmGateA{hfc, eh, rs}, LstmGateB{P + net.o_luW, P + net.o_llW},
-                                                   EpiBias{gates, P + net.o_lub, GATES}, n, GATES, 2 * HID, 1, s)));
+    ARL_TRY(lstm_gates_cell(LstmGateA{hfc, eh, rs}, LstmGateB{P + net.o_luW, P + net.o_llW}, P + net.o_lub, gates, ec,
+                            rs, cn, hn, n, s));
     const int64_t cnt = (int64_t)n * HID;
-    hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, gates, ec, rs, cn,
-                       hn, cnt);
-    ARL_TRY(hipGetLastError());
     if (!keep) {
       ARL_TRY(hipMemcpyAsync(eh, hn, cnt * 4, hipMemcpyDeviceToDevice, s));
       ARL_TRY(hipMemcpyAsync(ec, cn, cnt * 4, hipMemcpyDeviceToDevice, s));
@@ -589,17 +659,31 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
     float* dcn = net.at<float>(net.w_dcn);
     const float* dH = net.at<float>(net.w_dh);
     const int64_t cnt = (int64_t)n * HID;
+    // step T-1's cell, then per step t: dh_{t-1} = (dG_t Wl) * (no reset at t) as a split-K GEMM
+    // (K = 1024 split 4 ways) and its reduce fused with step t-1's cell (lstm_dh_cell_bwd_kernel)
+    const unsigned cblocks = (unsigned)((cnt + 255) / 256);
+    const int splits = effective_splits<32>(GATES, BPTT_SPLIT);
+    static_assert(BPTT_SPLIT <= 4, "lstm_dh_cell_bwd_kernel sums in reduce_grad_kernel's order for <= 4 splits");
     for (int t = T - 1; t >= 0; --t) {
       const int64_t o = (int64_t)t * n;
-      hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s,
-                         gates + o * GATES, cbuf + (o + n) * HID, cbuf + o * HID, rs + o, dH + o * HID, dhn, dcn,
-                         dG + o * GATES, t == T - 1 ? 1 : 0, cnt);
-      ARL_TRY(hipGetLastError());
-      if (t > 0) {   // dh_{t-1} = (dG_t Wl) * (no reset): K = 1024 split 4 ways + reduce
+      if (t == T - 1 || LSTM_SPLIT) {
+        hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3(cblocks), dim3(256), 0, s, gates + o * GATES,
+                           cbuf + (o + n) * HID, cbuf + o * HID, rs + o, dH + o * HID, dhn, dcn, dG + o * GATES,
+                           t == T - 1 ? 1 : 0, cnt);
+        ARL_TRY(hipGetLastError());
+      }
+      if (t > 0) {
         ARL_TRY((launch_gemm<32, 64, 32, 2, 2, GK, GM>(RowMajor{dG + o * GATES, GATES}, RowMajor{P + net.o_llW, HID},
                                                        EpiSlab{slab, n, HID}, n, HID, GATES, BPTT_SPLIT, s)));
-        ARL_TRY(launch_reduce_grad(slab, effective_splits<32>(GATES, BPTT_SPLIT), n, HID,
-                                   MapResetMask{dhn, rs + o, HID}, s));
+        if (LSTM_SPLIT) {
+          ARL_TRY(launch_reduce_grad(slab, splits, n, HID, MapResetMask{dhn, rs + o, HID}, s));
+        } else {
+          const int64_t op = o - n;   // step t-1
+          hipLaunchKernelGGL(lstm_dh_cell_bwd_kernel, dim3(cblocks), dim3(256), 0, s, slab, splits, rs + o,
+                             gates + op * GATES, cbuf + (op + n) * HID, cbuf + op * HID, rs + op, dH + op * HID, dcn,
+                             dG + op * GATES, cnt);
+          ARL_TRY(hipGetLastError());
+        }
       }
     }
     // gate weight gradients and dfc = (dG Wu) * (hfc > 0): independent, one launch

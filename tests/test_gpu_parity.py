@@ -4,6 +4,8 @@ reference-generated golden fixtures.
 Tolerances (stated per test): integer / byte / index work is bit-exact;
 fp32 contractions |gpu - oracle| <= 1e-5 * max(|oracle|, ||oracle||_inf)
 (norm-scaled); the RMSProp kernel is bit-exact vs the reference."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -671,3 +673,23 @@ def test_fused_observe_identical(gpu, arch, N, groups, resize_mode):
     assert int(outs[0]["nvalid"].min()) >= 1 and int(outs[0]["reset"][1:].sum()) > 0   # resets happened
     for k in outs[0]:
         assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+def test_lstm_fused_cell_identical(gpu, tmp_path):
+    """The LSTM cell fused into the gate GEMM's epilogue (forward, act and
+    pi_and_v) and into the BPTT reduce (backward) gives the same bits as the
+    cell as separate launches (ARL_LSTM_SPLIT=1): hidden / cell states, gates,
+    actions, values, gradients, parameters."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    outs = []
+    for split in ("0", "1"):
+        f = str(tmp_path / f"lstm_{split}.npz")
+        env = dict(os.environ, ARL_LSTM_SPLIT=split)
+        subprocess.run([sys.executable, os.path.join(here, "lstm_split_worker.py"), f], env=env, check=True,
+                       timeout=240)
+        outs.append(np.load(f))
+    assert int((outs[0]["hbuf"] != 0).sum()) > 0
+    for k in outs[0].files:
+        assert np.array_equal(outs[0][k], outs[1][k]), k
