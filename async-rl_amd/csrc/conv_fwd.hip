@@ -96,17 +96,18 @@ struct ConvFwdArgs {
 // W1 (16, 4, 8, 8) f32 -> the split planes [3][oc][k] in LDS: thread tid
 // stages 8 consecutive k of one oc (RGB nets: W1 (16, 3, 8, 8) on input
 // planes 1..3, zeros for plane 0)
+// (unconditional loads from a clamped address: a load under a per-lane branch
+// is waited for at the branch's end; the RGB zero pad is applied at the split)
 __device__ inline void w1_load(const float* W1, bool rgb, int tid, float4& w1a, float4& w1b) {
   const int w1oc = tid >> 5, w1k = (8 * tid) & 255;
-  w1a = w1b = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (!rgb || w1k >= 64) {
-    const float4* w1p = reinterpret_cast<const float4*>(rgb ? W1 + w1oc * 192 + w1k - 64 : W1 + 8 * tid);
-    w1a = w1p[0];
-    w1b = w1p[1];
-  }
+  const float4* w1p =
+      reinterpret_cast<const float4*>(rgb ? W1 + w1oc * 192 + (w1k >= 64 ? w1k - 64 : 0) : W1 + 8 * tid);
+  w1a = w1p[0];
+  w1b = w1p[1];
 }
-__device__ inline void w1_split_store(uint8_t* lds, int tid, float4 w1a, float4 w1b) {
+__device__ inline void w1_split_store(uint8_t* lds, int tid, float4 w1a, float4 w1b, bool rgb = false) {
   const int w1oc = tid >> 5, w1k = (8 * tid) & 255;
+  if (rgb && w1k < 64) w1a = w1b = make_float4(0.f, 0.f, 0.f, 0.f);
   uint4 ph, pm, pl;
   split3_pack(w1a.x, w1a.y, ph.x, pm.x, pl.x);
   split3_pack(w1a.z, w1a.w, ph.y, pm.y, pl.y);
@@ -160,6 +161,10 @@ conv_fwd_kernel(ConvFwdArgs a) {
   const int e = a.e0 + blockIdx.x;
   const bool rgb = a.layout == FRAMES_RGB;
   constexpr int V = PLANE / 16;              // 441 uint4 per screen
+  // the biases first: loads issued at the top land before the staging waits
+  // (loaded at the epilogues they were waited for there)
+  const float bias1 = a.b1[col];
+  const float bias2 = a.b2[16 * (wave & 1) + col];
   const int64_t ks = a.ctl[CTL_STEP] + a.t;
   const int rs = (int)(ks % a.R);
   // conv1 tiles w, w + 8, w + 16 (and 24 on wave 0): 25 tiles over 8 waves in one
@@ -329,8 +334,13 @@ conv_fwd_kernel(ConvFwdArgs a) {
     }
     __syncthreads();   // every wave is done with the W1 planes: the a1 planes overwrite them
   } else {
-    // ---- stage: all global loads first, then bf16 conversion / splitting into LDS
+    // ---- stage: every global load in flight at once (nvalid, the weights, all
+    // four ring planes whatever nvalid says), then bf16 conversion / splitting
+    // into LDS; planes older than the last reset are zeroed here
     const int nv = a.nvalid[(int64_t)rs * a.n + e];
+    float4 w1a, w1b, w2v[4];
+    w1_load(a.W1, rgb, tid, w1a, w1b);
+    w2_load(a.W2, tid, w2v);
     int slot[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) slot[c] = (rs + a.R - 3 + c) % a.R;
@@ -339,26 +349,24 @@ conv_fwd_kernel(ConvFwdArgs a) {
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const int i = tid + NT * j;
-      const int c = i / V, oo = i - c * V;
-      xv[j] = make_uint4(0, 0, 0, 0);
-      if (!(ARL_ABLATE & 4) && i < 4 * V && c >= 4 - nv)   // planes older than the last reset read as 0
-        xv[j] = reinterpret_cast<const uint4*>(
-            a.frames + (a.layout == FRAMES_STACK ? ((int64_t)rs * a.n + e) * 4 + c
-                        : a.layout == FRAMES_RGB ? ((int64_t)rs * a.n + e) * 3 + (c - 1)
-                                                 : (int64_t)slot[c] * a.n + e) * PLANE)[oo];
+      // past the fourth plane: reload its last 16 bytes (every thread issues NX loads)
+      const int c = i < 4 * V ? i / V : 3, oo = i < 4 * V ? i - c * V : V - 1;
+      // RGB: conv plane 0 is the zero pad (c - 1 < 0 reads plane 0 and is zeroed below, nvalid = 3)
+      xv[j] = reinterpret_cast<const uint4*>(
+          a.frames + (a.layout == FRAMES_STACK ? ((int64_t)rs * a.n + e) * 4 + c
+                      : a.layout == FRAMES_RGB ? ((int64_t)rs * a.n + e) * 3 + (c > 0 ? c - 1 : 0)
+                                               : (int64_t)slot[c] * a.n + e) * PLANE)[oo];
     }
-    float4 w1a, w1b, w2v[4];
-    w1_load(a.W1, rgb, tid, w1a, w1b);
-    w2_load(a.W2, tid, w2v);
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const int i = tid + NT * j;
       if (i < 4 * V) {
         const int c = i / V, oo = i - c * V;
-        px16_store(lds + L_XB + c * XB_PLANE + oo * 32, xv[j]);
+        px16_store(lds + L_XB + c * XB_PLANE + oo * 32,
+                   (!(ARL_ABLATE & 4) && c >= 4 - nv) ? xv[j] : make_uint4(0, 0, 0, 0));
       }
     }
-    w1_split_store(lds, tid, w1a, w1b);
+    w1_split_store(lds, tid, w1a, w1b, rgb);
     w2_split_store(lds, tid, w2v);
     __syncthreads();
     // W1 fragments in registers (96 VGPRs), then the W1 planes are free for a1
@@ -369,7 +377,6 @@ conv_fwd_kernel(ConvFwdArgs a) {
 #pragma unroll
     for (int s = 0; s < ((ARL_ABLATE & 1) ? 0 : 8); ++s) conv1_step(s, w1h[s], w1m[s], w1l[s]);
   }
-  const float bias1 = a.b1[col];
   float* a1g = a.a1 + (int64_t)e * A1;
   {
     // C rows g*4 + r -> positions tile*16 + g*4 + r, col = oc
@@ -428,7 +435,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
       }
     }
     float* a2g = a.a2 + (int64_t)e * A2;
-    const float b = a.b2[oc];
+    const float b = bias2;   // b2[oc]
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int p = 16 * mA + g * 4 + r;

@@ -68,6 +68,7 @@ policy_fc_kernel(const float* __restrict__ slab, int n, const float* __restrict_
   const int tid = threadIdx.x;
   const int64_t row0 = (int64_t)blockIdx.x * PF_ROWS;
   constexpr int V4 = PF_ROWS * HID / 4 / 256;   // float4 per thread per slab
+  const HeadsPrefetch<HID> pf = heads_prefetch<HID>(pa);   // in flight with the slab loads
   f32x4v p[V4][FC_SPLIT];
 #pragma unroll
   for (int z = 0; z < FC_SPLIT; ++z)
@@ -93,7 +94,7 @@ policy_fc_kernel(const float* __restrict__ slab, int n, const float* __restrict_
     if (row0 + r < n) *reinterpret_cast<float4*>(hfc + (row0 + r) * HID + c) = o;
   }
   __syncthreads();
-  policy_rows16<HID, false, true, PF_ROWS>(hl, row0, n, pa, part, zs);
+  policy_rows16<HID, false, true, PF_ROWS>(hl, row0, n, pa, part, zs, &pf);
 }
 
 hipError_t launch_policy_fc(const float* slab, int n, const float* fc_bias, float* hfc, const PolicyArgs& pa,

@@ -23,6 +23,7 @@ __device__ inline uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <int HW> struct HeadsPrefetch;
 
 // One group of 16 env rows (row0 .. row0 + 15) of the softmax policy / value
 // heads; part / zs are LDS scratch of the calling workgroup (all 256 threads
@@ -31,14 +32,51 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // group's 16 rows (row i at h + i * HW, e.g. LDS filled by the caller).
 // ROWS < 16: only rows row0 .. row0 + ROWS - 1 are this group's (the other
 // MFMA rows repeat the last one and are not stored).
+// Every global load of the heads, issued first (a caller can issue it before
+// its own loads and pass it in): the B fragments of each 16-column head tile
+// from clamped rows (a load under a per-lane branch is waited for at the
+// branch's end; columns past A are zeroed at use), the bias of the zs entry
+// the thread forms first, the step counter of the Philox draw.
+template <int HW>
+struct HeadsPrefetch {
+  static constexpr int KW = HW / 4, NS = KW / 16, NTM = (MAXA + 1 + 15) / 16;
+  f32x4 wv[NTM][NS];
+  float bias;
+  int64_t step;
+};
+template <int HW>
+__device__ inline HeadsPrefetch<HW> heads_prefetch(const PolicyArgs& pa) {
+  using P = HeadsPrefetch<HW>;
+  const int A = pa.A;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  P pf;
+#pragma unroll
+  for (int nt = 0; nt < P::NTM; ++nt) {
+    if (16 * nt > A) break;   // wave-uniform
+    const int j = min(16 * nt + col, A);   // head column: j < A -> pi logit j, j == A -> value
+    const float* wrow = (j < A ? pa.Wpi + (int64_t)j * HW : pa.Wv) + P::KW * w;
+#pragma unroll
+    for (int s = 0; s < P::NS; ++s) pf.wv[nt][s] = *reinterpret_cast<const f32x4*>(wrow + 16 * s + 4 * g);
+  }
+  const int bj = tid % (A + 1);
+  pf.bias = bj < A ? pa.bpi[bj] : pa.bv[0];
+  pf.step = pa.mode == 1 ? pa.ctl[CTL_STEP] + pa.step_off : 0;
+  return pf;
+}
+
 template <int HW, bool COH, bool LOCAL = false, int ROWS = 16>
 __device__ inline void policy_rows16(const float* __restrict__ h, int64_t row0, int64_t n, const PolicyArgs& pa,
-                                     float (*part)[16][MAXA + 2], float (*zs)[MAXA + 2]) {
+                                     float (*part)[16][MAXA + 2], float (*zs)[MAXA + 2],
+                                     const HeadsPrefetch<HW>* pre = nullptr) {
   // 4 waves split K = HW into quarters; partial tiles summed in wave order
   constexpr int KW = HW / 4, NS = KW / 16;
   const int A = pa.A;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int64_t rowc = min(row0 + (col < ROWS ? col : ROWS - 1), n - 1);   // A row of this lane (rows past n: any valid row, not stored)
+  const HeadsPrefetch<HW> pf = pre != nullptr ? *pre : heads_prefetch<HW>(pa);
+  const f32x4 (&wv)[HeadsPrefetch<HW>::NTM][NS] = pf.wv;
+  const float bias = pf.bias;
+  const int64_t step = pf.step;
   f32x4 hv[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
@@ -50,18 +88,18 @@ __device__ inline void policy_rows16(const float* __restrict__ h, int64_t row0, 
       hv[s] = *reinterpret_cast<const f32x4*>(src);
     }
   }
-  for (int nt = 0; 16 * nt <= A; ++nt) {
-    const int j = 16 * nt + col;   // head column: j < A -> pi logit j, j == A -> value
-    const float* wrow = (j < A ? pa.Wpi + (int64_t)j * HW : pa.Wv) + KW * w;
+#pragma unroll
+  for (int nt = 0; nt < HeadsPrefetch<HW>::NTM; ++nt) {
+    if (16 * nt > A) break;   // wave-uniform
+    const int j = 16 * nt + col;
     f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      f32x4 wv = {0.f, 0.f, 0.f, 0.f};
-      if (j <= A) wv = *reinterpret_cast<const f32x4*>(wrow + 16 * s + 4 * g);
-      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][0], wv[0], c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][1], wv[1], c1, 0, 0, 0);
-      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][2], wv[2], c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][3], wv[3], c1, 0, 0, 0);
+      const f32x4 wf = j <= A ? wv[nt][s] : f32x4{0.f, 0.f, 0.f, 0.f};
+      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][0], wf[0], c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][1], wf[1], c1, 0, 0, 0);
+      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][2], wf[2], c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][3], wf[3], c1, 0, 0, 0);
     }
     if (j <= A) {
 #pragma unroll
@@ -72,7 +110,7 @@ __device__ inline void policy_rows16(const float* __restrict__ h, int64_t row0, 
   for (int i = tid; i < 16 * (A + 1); i += 256) {
     const int r = i / (A + 1), j = i - r * (A + 1);
     float z = __fadd_rn(__fadd_rn(part[0][r][j], part[1][r][j]), __fadd_rn(part[2][r][j], part[3][r][j]));
-    zs[r][j] = __fadd_rn(z, j < A ? pa.bpi[j] : pa.bv[0]);
+    zs[r][j] = __fadd_rn(z, i == tid ? bias : (j < A ? pa.bpi[j] : pa.bv[0]));   // (i != tid only for A >= 16)
   }
   __syncthreads();
   const int64_t row = row0 + tid;
@@ -91,7 +129,6 @@ __device__ inline void policy_rows16(const float* __restrict__ h, int64_t row0, 
     const int mode = pa.mode;
     float u = 2.f;   // > any cdf: no draw
     if (mode == 1) {
-      const int64_t step = pa.ctl[CTL_STEP] + pa.step_off;
       const uint4 r = philox4x32_10(make_uint4((uint32_t)(pa.env_offset + row), (uint32_t)step,
                                                (uint32_t)((uint64_t)step >> 32), pa.stream), pa.seed_lo, pa.seed_hi);
       u = (float)(r.x >> 8) * 5.9604644775390625e-08f;
