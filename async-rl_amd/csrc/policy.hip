@@ -155,17 +155,20 @@ struct ReturnsArgs {
 // wait for the one before it.  Windows up to RW steps keep their rewards /
 // dones in registers; longer ones loop over memory.
 constexpr int RW = 8;
+// AM >= A: the action count the registers are sized for (4 / 8 / MAXA)
+template <int AM>
 struct RetIn {   // everything returns_one reads of step (t, e)
-  float pr[MAXA], lp[MAXA], rw[RW];
+  float pr[AM], lp[AM], rw[RW];
   int dn[RW];
   float vboot, vi;
   int ac, di;
 };
-__device__ inline void returns_load(const ReturnsArgs& a, int t, int e, RetIn& in) {
+template <int AM>
+__device__ inline void returns_load(const ReturnsArgs& a, int t, int e, RetIn<AM>& in) {
   const int T = a.T, n = a.n, A = a.A;
   const int64_t i = (int64_t)t * n + e;
 #pragma unroll
-  for (int k = 0; k < MAXA; ++k) {
+  for (int k = 0; k < AM; ++k) {
     const int64_t o = i * A + min(k, A - 1);
     in.pr[k] = a.probs[o];
     in.lp[k] = a.logp[o];
@@ -181,7 +184,8 @@ __device__ inline void returns_load(const ReturnsArgs& a, int t, int e, RetIn& i
   in.ac = a.act[i];
   in.di = a.dones[i];
 }
-__device__ inline void returns_compute(const ReturnsArgs& a, int t, int e, const RetIn& in, float& lpi, float& lv,
+template <int AM>
+__device__ inline void returns_compute(const ReturnsArgs& a, int t, int e, const RetIn<AM>& in, float& lpi, float& lv,
                                        float* sdl) {
   const int T = a.T, n = a.n, A = a.A;
   const int64_t i = (int64_t)t * n + e;
@@ -246,14 +250,14 @@ __device__ inline void returns_compute(const ReturnsArgs& a, int t, int e, const
   const float adv = __fsub_rn(Rf, vi);
   float H = 0.f, lpa = 0.f;
 #pragma unroll
-  for (int k = 0; k < MAXA; ++k)
+  for (int k = 0; k < AM; ++k)
     if (k < A) {
       H = __fadd_rn(H, __fmul_rn(pr[k], lp[k]));
       if (k == ac) lpa = lp[k];
     }
   H = -H;
 #pragma unroll
-  for (int k = 0; k < MAXA; ++k)
+  for (int k = 0; k < AM; ++k)
     if (k < A) {
       const float oh = (k == ac) ? 1.f : 0.f;
       const float t1 = __fmul_rn(-adv, __fsub_rn(oh, pr[k]));
@@ -270,7 +274,7 @@ __device__ inline void returns_compute(const ReturnsArgs& a, int t, int e, const
   lv = __fmul_rn(vf, __fmul_rn(__fmul_rn(dvv, dvv), 0.5f));
 }
 __device__ inline void returns_one(const ReturnsArgs& a, int t, int e, float& lpi, float& lv) {
-  RetIn in;
+  RetIn<MAXA> in;
   returns_load(a, t, e, in);
   returns_compute(a, t, e, in, lpi, lv, nullptr);
 }
@@ -308,11 +312,15 @@ returns_kernel(ReturnsArgs a) {
 // column j (HID = 256 = blockDim): its Wpi / Wv column and its mask entries
 // are loaded up front, beside the returns' own loads.
 __device__ inline int rh_envs(int T) { return 1; }
+// AM >= A actions, RB rows (steps) per pass: the register arrays (mask
+// entries, head-weight column, loaded probs / log-probs) are sized for the
+// window, e.g. 5 rows and 4 actions at C2 instead of 32 and 32
+template <int AM, int RB>
 __global__ void __launch_bounds__(256)
 returns_heads_kernel(ReturnsArgs a, const float* __restrict__ Wpi, const float* __restrict__ Wv,
                      const float* __restrict__ mask, float* __restrict__ dh, int abl) {
   __shared__ float lpi[64], lv[64];
-  __shared__ float sdl[64 * (MAXA + 1)];
+  __shared__ float sdl[64 * (AM + 1)];
   if (a.ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) a.ctl[CTL_STEP_SNAP] = a.ctl[CTL_STEP];
   const int T = a.T, n = a.n, A = a.A;
   const int EB = rh_envs(T), rows = T * EB;   // rows <= 64
@@ -324,40 +332,40 @@ returns_heads_kernel(ReturnsArgs a, const float* __restrict__ Wpi, const float* 
   // this thread's mask entries and head-weight column, in flight during the returns
   // (unconditional loads at clamped offsets: a load under a per-lane branch
   // would wait for each one in turn)
-  float mv[32];
-  int64_t so[32];
+  float mv[RB];
+  int64_t so[RB];
   auto rows_from = [&](int r0) {
 #pragma unroll
-    for (int u = 0; u < 32; ++u) {
+    for (int u = 0; u < RB; ++u) {
       const int r = r0 + u, l = r % EB;
       const bool ok = r < rows && e0 + l < n;
       so[u] = ok ? ((int64_t)(r / EB) * n + e0 + l) * HID + j : -1;
     }
     if (mask != nullptr) {
 #pragma unroll
-      for (int u = 0; u < 32; ++u) mv[u] = mask[so[u] < 0 ? j : so[u]];
+      for (int u = 0; u < RB; ++u) mv[u] = mask[so[u] < 0 ? j : so[u]];
     } else {
 #pragma unroll
-      for (int u = 0; u < 32; ++u) mv[u] = 1.f;
+      for (int u = 0; u < RB; ++u) mv[u] = 1.f;
     }
   };
   rows_from(0);
-  float wc[MAXA + 1];   // column j of Wpi / Wv (clamped offsets: every load issued together)
+  float wc[AM + 1];   // column j of Wpi / Wv (clamped offsets: every load issued together)
 #pragma unroll
-  for (int k = 0; k <= MAXA; ++k) wc[k] = k < A ? Wpi[min(k, A - 1) * HID + j] : Wv[j];
-  RetIn in;   // off threads load a valid step (t, e) and discard it
+  for (int k = 0; k <= AM; ++k) wc[k] = k < A ? Wpi[min(k, A - 1) * HID + j] : Wv[j];
+  RetIn<AM> in;   // off threads load a valid step (t, e) and discard it
   returns_load(a, min(t, T - 1), min(e, n - 1), in);
-  __shared__ float w[(MAXA + 1) * HID];   // thread j's own column
+  __shared__ float w[(AM + 1) * HID];   // thread j's own column
 #pragma unroll
-  for (int k = 0; k <= MAXA; ++k)
-    if (k <= A) w[k * HID + j] = k < A ? wc[k] : wc[MAXA];
+  for (int k = 0; k <= AM; ++k)
+    if (k <= A) w[k * HID + j] = k < A ? wc[k] : wc[AM];
   if (on && !(abl & 2)) returns_compute(a, t, e, in, lpi[tid], lv[tid], sdl + tid * (A + 1));   // row tid = t * EB + el
   __syncthreads();
   if (a.loss != nullptr && t == 0 && on) env_loss(a, lpi, lv, EB, el, e);
-  for (int r0 = 0; r0 < ((abl & 1) ? 0 : rows); r0 += 32) {
-    if (r0 > 0) rows_from(r0);   // T > 32: the second 32 rows
+  for (int r0 = 0; r0 < ((abl & 1) ? 0 : rows); r0 += RB) {
+    if (r0 > 0) rows_from(r0);   // T > RB: the next RB rows
 #pragma unroll
-    for (int u = 0; u < 32; ++u) {
+    for (int u = 0; u < RB; ++u) {
       if (so[u] < 0) continue;
       const float* d = sdl + (r0 + u) * (A + 1);
       float acc = 0.f;
@@ -392,8 +400,15 @@ hipError_t launch_returns_heads(const float* rewards, const uint8_t* dones, cons
   const ReturnsArgs ra{rewards, dones, v, probs, logp, act, T, n, A, gamma, beta, vcoef, pcoef, clip_reward,
                        keep_scale, dlogits, dv, loss, ctl_snap};
   static const char* ab = getenv("ARL_RH_ABL");   // timing experiments only: 1 no dh, 2 no returns
-  hipLaunchKernelGGL(returns_heads_kernel, dim3((n + EB - 1) / EB), dim3(256), 0, s, ra, Wpi, Wv, mask, dh,
-                     ab ? atoi(ab) : 0);
+  const dim3 grid((n + EB - 1) / EB), blk(256);
+  const int ablv = ab ? atoi(ab) : 0;
+  if (T <= 8) {
+    if (A <= 4) hipLaunchKernelGGL((returns_heads_kernel<4, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh, ablv);
+    else if (A <= 8) hipLaunchKernelGGL((returns_heads_kernel<8, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh, ablv);
+    else hipLaunchKernelGGL((returns_heads_kernel<MAXA, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh, ablv);
+  } else {
+    hipLaunchKernelGGL((returns_heads_kernel<MAXA, 32>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh, ablv);
+  }
   return hipGetLastError();
 }
 
