@@ -7,8 +7,9 @@
 //   * split-K 8 ways, one K slice (324) per XCD (blockIdx % 8 = split): each
 //     XCD's L2 holds just its 324-column slice of a2 and W;
 //   * 32 x 64 output tile per workgroup; the whole 96 x 324 operand block
-//     (124 KB) is staged by LDS-DMA (global_load_lds_dwordx4) in one burst --
-//     every load in flight at once, one wait, one barrier;
+//     (124 KB) is staged by LDS-DMA (global_load_lds_dwordx4) in one burst of
+//     three K chunks -- every load in flight at once; the MFMAs of a chunk
+//     start when it has landed (one wait + barrier per chunk);
 //   * v_mfma_f32_16x16x4_f32, 8 waves with one 16 x 16 sub-tile each, operands read as
 //     ds_read_b128 feeding 4 k-steps each (k permuted identically for A/B);
 //   * partial tiles go to a slab; the last workgroup of each tile (device
@@ -35,59 +36,102 @@ namespace {
 constexpr int FBM = 32, FBN = 64, FSPLIT = FC_SPLIT;
 constexpr int FKS = A2 / FSPLIT;          // 324 columns per split
 constexpr int FROWS = FBM + FBN;          // 96 staged rows (32 of a2, 64 of W)
-constexpr int FV = FKS / 4;               // 81 float4 per row
-constexpr int FVEC = FROWS * FV;          // 7776 float4 per workgroup
-constexpr int FINSTR = (FVEC + 63) / 64;  // 122 wave-instructions of LDS-DMA
 constexpr int FT = 512;                   // threads: 8 waves, one 16 x 16 output sub-tile each
 constexpr int FW = FT / 64;
 static_assert(A2 % (4 * FSPLIT) == 0, "K slice must be whole float4s");
 static_assert(HID % FBN == 0, "N tiles");
+// The K slice is staged in three chunks (112 + 112 + 100 columns), each a
+// [96][stride] block of LDS (row strides 29 / 29 / 26 float4: 116 / 116 / 104
+// floats put the 16 rows a b128 read touches on distinct bank quads); the
+// chunks are issued back to back, and the MFMAs of chunk c run while chunks
+// c+1.. are still landing.  A pad slot of a row (the 29th float4 of a 28-wide
+// chunk, 26th of the 25-wide one) re-loads the row's last float4.
+constexpr int FCH = 3;
+__host__ __device__ constexpr int ch_k0(int c) { return c == 0 ? 0 : c == 1 ? 112 : 224; }
+__host__ __device__ constexpr int ch_w(int c) { return c < 2 ? 28 : 25; }          // float4 used per row
+__host__ __device__ constexpr int ch_ld(int c) { return c < 2 ? 29 : 26; }         // float4 per row (padded)
+__host__ __device__ constexpr int ch_pieces(int c) { return (FROWS * ch_ld(c) + 63) / 64; }   // 44, 44, 39
+// float4 offset of chunk c: whole pieces, so a chunk's last (partly past-the-end) piece lands in
+// its own region, never in the next chunk's
+__host__ __device__ constexpr int ch_base(int c) { return c == 0 ? 0 : c == 1 ? 44 * 64 : 88 * 64; }
+static_assert(ch_pieces(0) == 44 && ch_pieces(1) == 44, "chunk bases");
+constexpr int FLDS4 = ch_base(2) + ch_pieces(2) * 64;   // float4 of LDS incl. the last piece's overhang
+static_assert(ch_k0(2) + 100 == FKS && ch_w(0) * 4 == 112 && ch_w(2) * 4 == 100, "chunks cover the slice");
+// pieces of wave w in chunk c (piece it -> wave it % 8)
+__host__ __device__ constexpr int ch_wave_pieces(int c, int w) { return (ch_pieces(c) - w + FW - 1) / FW; }
 }  // namespace
+
+__device__ inline void fc_wait_vm(int n) {   // s_waitcnt vmcnt(n), n wave-uniform, 0..16
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
 
 __global__ void __launch_bounds__(FT)
 fc_fwd_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, const float* __restrict__ bias,
               float* __restrict__ slab, int* __restrict__ tickets, float* __restrict__ hfc) {
-  __shared__ __attribute__((aligned(16))) float S[FROWS * FKS];   // 124,416 B
+  __shared__ __attribute__((aligned(16))) float S[FLDS4 * 4];   // 130,048 B
   __shared__ int is_last;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int split = blockIdx.x % FSPLIT, tile = blockIdx.x / FSPLIT;
   constexpr int NTN = HID / FBN;
   const int m0 = (tile / NTN) * FBM, n0 = (tile % NTN) * FBN, k0 = split * FKS;
 
-  // ---- stage: float4 i -> row i / 81, column 4 (i % 81); LDS image is the
-  // unpadded [96][324] block, lane-linear per wave-instruction
-  for (int it = wave; it < ((ARL_ABLATE & 128) ? 0 : FINSTR); it += FW) {
-    const int i = it * 64 + lane;
-    if (i < FVEC) {
-      const int r = i / FV, c = i - r * FV;
-      const float* src;
-      if (r < FBM) src = a2 + (int64_t)min(m0 + r, n - 1) * A2;   // rows past n: any valid row, never stored
-      else src = W + (int64_t)(n0 + r - FBM) * A2;
-      __builtin_amdgcn_global_load_lds(src + k0 + 4 * c, (__attribute__((address_space(3))) void*)(S + it * 256),
-                                       16, 0, 0);
+  // ---- stage: every chunk's LDS-DMA pieces issued back to back; slot i of
+  // chunk c -> row i / ld, float4 column min(i % ld, w - 1) of the chunk
+#pragma unroll
+  for (int c = 0; c < FCH; ++c) {
+    for (int it = wave; it < ((ARL_ABLATE & 128) ? 0 : ch_pieces(c)); it += FW) {
+      const int i = min(it * 64 + lane, FROWS * ch_ld(c) - 1);
+      const int r = i / ch_ld(c), cc = min(i - r * ch_ld(c), ch_w(c) - 1);
+      const float* src = r < FBM ? a2 + (int64_t)min(m0 + r, n - 1) * A2   // rows past n: any valid row, never stored
+                                 : W + (int64_t)(n0 + r - FBM) * A2;
+      __builtin_amdgcn_global_load_lds(src + k0 + ch_k0(c) + 4 * cc,
+                                       (__attribute__((address_space(3))) void*)(S + 4 * (ch_base(c) + it * 64)), 16,
+                                       0, 0);
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
 
-  // ---- MFMA: wave -> m sub-tile (wave & 1), n sub-tile (wave >> 1)
+  // ---- MFMA: wave -> m sub-tile (wave & 1), n sub-tile (wave >> 1); chunk c
+  // after this wave's pieces of it have landed and a barrier (everyone's)
   const int q = lane >> 4, col = lane & 15;
   const int ms = wave & 1, ns = wave >> 1;
-  const float* Ar = S + (ms * 16 + col) * FKS + 4 * q;
-  const float* B0 = S + (FBM + ns * 16 + col) * FKS + 4 * q;
   f32x4 c0 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 5
-  for (int s = 0; s < ((ARL_ABLATE & 512) ? 0 : FKS / 16); ++s) {   // 20 groups of 16 k: lane quarter q holds k = 16 s + 4 q + r
-    const f32x4 av = *reinterpret_cast<const f32x4*>(Ar + 16 * s);
-    const f32x4 b0 = *reinterpret_cast<const f32x4*>(B0 + 16 * s);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], b0[r], c0, 0, 0, 0);
+  for (int c = 0; c < FCH; ++c) {
+    int later = 0;
+#pragma unroll
+    for (int c2 = c + 1; c2 < FCH; ++c2) later += ch_wave_pieces(c2, wave);
+    if (!(ARL_ABLATE & 128)) fc_wait_vm(later);
+    // LDS-only barrier: __syncthreads()'s fence would drain vmcnt, i.e. wait for the later chunks too
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const float* Ar = S + 4 * ch_base(c) + (ms * 16 + col) * 4 * ch_ld(c) + 4 * q;
+    const float* B0 = S + 4 * ch_base(c) + (FBM + ns * 16 + col) * 4 * ch_ld(c) + 4 * q;
+    constexpr int G16[FCH] = {7, 7, 6};   // whole 16-k groups per chunk
+#pragma unroll
+    for (int s = 0; s < ((ARL_ABLATE & 512) ? 0 : G16[c]); ++s) {   // lane quarter q holds k = 16 s + 4 q + r
+      const f32x4 av = *reinterpret_cast<const f32x4*>(Ar + 16 * s);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(B0 + 16 * s);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], b0[r], c0, 0, 0, 0);
+    }
+    if (c == FCH - 1 && !(ARL_ABLATE & 512)) {   // tail k = 320 + q (chunk column 96 + q)
+      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ar[96 - 3 * q], B0[96 - 3 * q], c0, 0, 0, 0);
+    }
   }
-  {  // tail k = 320 + q
-    constexpr int KT = (FKS / 16) * 16;
-    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ar[KT - 3 * q], B0[KT - 3 * q], c0, 0, 0, 0);
-  }
-  static_assert(FKS - (FKS / 16) * 16 == 4, "one tail k-step");
 
   // ---- partials: C row q*4 + r -> env m, col -> hidden unit.  Partials and
   // ticket use device-scope (sc1) accesses, which bypass the per-XCD L2s'

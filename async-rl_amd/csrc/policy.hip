@@ -55,9 +55,13 @@ hipError_t launch_policy_args(const float* h, int64_t n, const PolicyArgs& pa, h
 // summed in split order 0..7 from 0.f, then + bias, relu -- the same f32 op
 // sequence as the ticket path, so hfc is bit-identical -- written to hfc (the
 // backward reads it) and to LDS, where the heads read it.
-// PF_ROWS env rows per workgroup (4: 64 workgroups at 256 envs, each reading
-// 32 KB of partials; 16 rows per workgroup left the reduce on 16 CUs)
-constexpr int PF_ROWS = 4;
+// PF_ROWS env rows per workgroup (1: 256 workgroups at 256 envs, each reading
+// 8 KB of partials; measured 4.33 us vs 4.57 at 2 rows, 4.62 at 4, 5.56 at 16,
+// where the reduce ran on 16 CUs)
+#ifndef ARL_PF_ROWS
+#define ARL_PF_ROWS 1
+#endif
+constexpr int PF_ROWS = ARL_PF_ROWS;
 __global__ void __launch_bounds__(256)
 policy_fc_kernel(const float* __restrict__ slab, int n, const float* __restrict__ fc_bias, float* __restrict__ hfc,
                  PolicyArgs pa) {
@@ -67,20 +71,22 @@ policy_fc_kernel(const float* __restrict__ slab, int n, const float* __restrict_
   typedef float f32x4v __attribute__((ext_vector_type(4)));
   const int tid = threadIdx.x;
   const int64_t row0 = (int64_t)blockIdx.x * PF_ROWS;
-  constexpr int V4 = PF_ROWS * HID / 4 / 256;   // float4 per thread per slab
+  constexpr int NV = PF_ROWS * HID / 4;          // float4 per slab of this group
+  constexpr int V4 = (NV + 255) / 256;           // per thread
   const HeadsPrefetch<HID> pf = heads_prefetch<HID>(pa);   // in flight with the slab loads
   f32x4v p[V4][FC_SPLIT];
 #pragma unroll
   for (int z = 0; z < FC_SPLIT; ++z)
 #pragma unroll
     for (int j = 0; j < V4; ++j) {
-      const int idx = tid + 256 * j, r = idx / (HID / 4), c = 4 * (idx % (HID / 4));
+      const int idx = min(tid + 256 * j, NV - 1), r = idx / (HID / 4), c = 4 * (idx % (HID / 4));
       const int64_t m = min(row0 + r, (int64_t)n - 1);
       p[j][z] = *reinterpret_cast<const f32x4v*>(slab + ((int64_t)z * n + m) * HID + c);
     }
 #pragma unroll
   for (int j = 0; j < V4; ++j) {
     const int idx = tid + 256 * j, r = idx / (HID / 4), c = 4 * (idx % (HID / 4));
+    if (idx >= NV) break;
     f32x4v acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int z = 0; z < FC_SPLIT; ++z)
