@@ -328,23 +328,36 @@ conv_bwd_kernel(ConvBwdArgs a) {
     }
     // ---- (1) conv2 weight gradient + bias; wave w: n-tiles (ic) 2w, 2w+1 x both m-tiles
     {
-      const int oc = tid & 31, ch = tid >> 5;   // 16 chunks of <= 6 positions
+      // 16 chunks of <= 6 positions, summed in order: the six reads in flight together
+      // (positions past 80 re-read position 80 and are dropped)
+      const int oc = tid & 31, ch = tid >> 5;
+      float v[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) v[k] = d2f[min(ch * 6 + k, C2_P - 1) * D2F_LD + oc];
       float t = 0.f;
-      for (int p = ch * 6; p < min(C2_P, ch * 6 + 6); ++p) t = __fadd_rn(t, d2f[p * D2F_LD + oc]);
+#pragma unroll
+      for (int k = 0; k < 6; ++k)
+        if (ch * 6 + k < C2_P) t = __fadd_rn(t, v[k]);
       b2sum = __fadd_rn(b2sum, t);
     }
     {
+      // position p = 4 ps + g = (oy, ox) stepped incrementally (ox += 4, wrap at 9)
+      // instead of a division per k-step; same k order
       const float* b0 = a1s + (2 * wave) * A1C + (col >> 2) * A1R + (col & 3);
+      int ox = g, boff = 2 * g, doff = g * D2F_LD;   // oy = 0
 #pragma unroll 3
       for (int ps = 0; ps < ((ARL_ABLATE & 8) ? 0 : 21); ++ps) {
-        const int p = 4 * ps + g;
-        const bool pv = p < C2_P;
-        const int pc = pv ? p : 0;
-        const int oy = pc / 9, ox = pc - oy * 9;
-        const float af0 = pv ? d2f[pc * D2F_LD + col] : 0.f;
-        const float af1 = pv ? d2f[pc * D2F_LD + 16 + col] : 0.f;
-        const int boff = (2 * oy) * A1R + 2 * ox;
-        const float bf0 = b0[boff], bf1 = b0[A1C + boff];
+        const bool pv = 4 * ps + g < C2_P;
+        const float af0 = pv ? d2f[doff + col] : 0.f;
+        const float af1 = pv ? d2f[doff + 16 + col] : 0.f;
+        const float bf0 = b0[pv ? boff : 0], bf1 = b0[A1C + (pv ? boff : 0)];
+        ox += 4;
+        doff += 4 * D2F_LD;
+        boff += 8;
+        if (ox >= 9) {   // next row: 2 a1 rows down, back 18 columns
+          ox -= 9;
+          boff += 2 * A1R - 18;
+        }
         acc1[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(af0, bf0, acc1[0][0], 0, 0, 0);
         acc1[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(af1, bf0, acc1[1][0], 0, 0, 0);
         acc1[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(af0, bf1, acc1[0][1], 0, 0, 0);
