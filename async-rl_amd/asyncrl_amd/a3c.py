@@ -51,6 +51,8 @@ from .policy_output import SoftmaxPolicyOutput
 STAGGER = os.environ.get("ARL_GROUP_STAGGER", "1") != "0"
 # > 1 rank: split the gradient all-reduce around the conv backward (ARL_OVERLAP_ALLREDUCE=0: one call)
 OVERLAP_ALLREDUCE = os.environ.get("ARL_OVERLAP_ALLREDUCE", "1") != "0"
+# one rank: GradientClipping's norm from the learner's conv reduce (ARL_NORM_FOLD=0: grad_sqnorm launch)
+NORM_FOLD = os.environ.get("ARL_NORM_FOLD", "1") != "0"
 
 _PHI_LUT = np.arange(256, dtype=np.float32) / np.float32(255.0)   # dqn_phi.py:14-16, per uint8 value
 
@@ -183,6 +185,8 @@ class A3C:
         scale = 1.0 if batch_loss == "sum" else 1.0 / (self.net.n_envs * self.world)
         self._vcoef = v_loss_coef * scale
         self.net.set_loss(pi_loss_coef * scale, keep_loss_scale_same)
+        # one rank: the update's clip norm comes from the learner's conv reduce (no all-reduce in between)
+        self.net.set_norm_fold(self.world == 1 and NORM_FOLD)
         self.t = 0          # env-steps taken (per env)
         self.t_start = 0    # a3c.py:56,152 (reference-contract act)
         self.single = self.net.stack and self.net.n_envs == 1

@@ -174,6 +174,11 @@ class DeviceNet:
         """Window steps [t_len, t_max) get no loss in the next learn (arl_truncate_window)."""
         check(lib.arl_truncate_window(self._h, t_len, stream_handle(stream)), "arl_truncate_window")
 
+    def set_norm_fold(self, on: bool = True):
+        """Fold the clip norm into learn()'s conv reduce (arl_net_set_norm_fold):
+        only when the gradient is not all-reduced between learn and update."""
+        check(lib.arl_net_set_norm_fold(self._h, int(on)), "arl_net_set_norm_fold")
+
     def set_loss(self, pi_loss_coef: float = 1.0, keep_loss_scale_same: bool = False):
         check(lib.arl_net_set_loss(self._h, pi_loss_coef, int(keep_loss_scale_same)), "arl_net_set_loss")
 

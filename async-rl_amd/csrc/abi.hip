@@ -239,6 +239,13 @@ int arl_truncate_window(arl_net* h, int t_len, void* s) {
   return hip_status(e, "truncate_window");
 }
 
+int arl_net_set_norm_fold(arl_net* h, int on) {
+  if (!h) return fail(ARL_EINVAL, "null net");
+  h->net.norm_fold = on != 0;
+  h->net.norm_ready = false;
+  return ARL_OK;
+}
+
 int arl_net_set_loss(arl_net* h, double pi_loss_coef, int keep_loss_scale_same) {
   if (!h) return fail(ARL_EINVAL, "null net");
   h->net.pi_coef = (float)pi_loss_coef;

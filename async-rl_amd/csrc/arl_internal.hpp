@@ -90,6 +90,11 @@ struct Net {
   float pi_coef = 1.f;
   int keep_scale = 0;
   int64_t eval_draws = 0;  // sampling forward_states calls so far (Philox stream 1 counter)
+  // clip norm folded into the learner's conv reduce (arl_net_set_norm_fold; only valid when
+  // nothing changes the gradient between arl_learn and the update, e.g. no all-reduce):
+  // norm_ready = the last arl_learn left the partials, consumed by the next update
+  bool norm_fold = false, norm_ready = false;
+  int norm_rest_blocks = 64;
   int hid;                 // width of the layer the heads read (256 NIPS / LSTM, 512 Nature)
   int env_offset;          // global id of env 0 on this rank (RNG stream)
   uint64_t seed;
@@ -164,14 +169,23 @@ hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const i
 // phi_ring_kernel + conv_fwd_kernel in one launch (one workgroup per env of ring.e0 + [0, ring.ne))
 hipError_t launch_phi_conv_fwd(const RingArgs& ring, const float* W1, const float* b1, const float* W2,
                                const float* b2, float* a1, float* a2, hipStream_t s);
+// the gradient's squared norm folded into the conv slab reduce (parts == null: not folded)
+struct NormFold {
+  double* parts;            // conv_norm_parts(rest_blocks) f64 partials
+  const float* g;           // the flat gradient
+  int64_t rest_begin, rest_end;   // floats of g outside the conv tensors (final before the reduce)
+  int rest_blocks;
+};
+int conv_norm_parts(int rest_blocks);
 hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int S,
                            const float* a1, const float* da2, const float* W2, float* slab, float* gW2, float* gb2,
-                           float* gW1, float* gb1, hipStream_t s, bool reduce = true, int layout = FRAMES_RING);
+                           float* gW1, float* gb1, hipStream_t s, bool reduce = true, int layout = FRAMES_RING,
+                           const NormFold& nf = NormFold{});
 int64_t conv_bwd_slab_floats(int S);
 int conv_bwd_blocks(int S);       // workgroups (= slab slices) of launch_conv_bwd
 // the slab reduce launch_conv_bwd(reduce = true) ends with, alone
 hipError_t launch_conv_reduce(const float* slab, int S, float* gW2, float* gb2, float* gW1, float* gb1, hipStream_t s,
-                              int layout);
+                              int layout, const NormFold& nf = NormFold{});
 
 // arguments of the softmax policy / value heads (policy_rows.hpp)
 struct PolicyArgs {

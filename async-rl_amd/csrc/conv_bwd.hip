@@ -500,11 +500,47 @@ conv_bwd_kernel(ConvBwdArgs a) {
 // f64 sum of the G slabs in a fixed order: thread (o, zg) adds slabs zg,
 // zg + 16, ... of output o (a wave reads 64 consecutive outputs of one slab,
 // 256 contiguous bytes), then the 16 partials add in zg order
+// With a NormFold (the clip norm folded into this launch, NormFold.parts !=
+// null): every conv block also leaves the f64 sum of squares of the 64
+// gradient values it wrote in parts[block], and rest_blocks extra blocks sum
+// the squares of g[rest_begin, rest_end) -- the gradient the FC / heads / LSTM
+// backward has already finished -- into parts[nconv + b]; the optimizer then
+// reduces these partials instead of a separate grad_sqnorm launch.
 constexpr int RED_O = 64, RED_Z = 16;
+constexpr int RED_BLOCKS = (SLAB + RED_O - 1) / RED_O;   // 193
+__device__ inline double block_sum_f64_1024(double x, double* sh) {   // 1,024 threads, fixed order
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) sh[w] = x;
+  __syncthreads();
+  double t = 0.0;
+  for (int i = 0; i < RED_O * RED_Z / 64; ++i) t += sh[i];
+  return t;
+}
 __global__ void __launch_bounds__(RED_O * RED_Z)
 reduce_conv_bwd_kernel(const float* __restrict__ slab, int G, float* __restrict__ gW2, float* __restrict__ gb2,
-                       float* __restrict__ gW1, float* __restrict__ gb1, int rgb) {
+                       float* __restrict__ gW1, float* __restrict__ gb1, int rgb, NormFold nf) {
   __shared__ double part[RED_Z][RED_O];
+  __shared__ double shn[RED_O * RED_Z / 64];
+  if (blockIdx.x >= RED_BLOCKS) {   // squared-norm blocks over the rest of the gradient
+    const int b = blockIdx.x - RED_BLOCKS;
+    double t = 0.0;
+    const float4* g4 = reinterpret_cast<const float4*>(nf.g + nf.rest_begin);
+    const int64_t n4 = (nf.rest_end - nf.rest_begin) >> 2;
+    for (int64_t i = (int64_t)b * blockDim.x + threadIdx.x; i < n4; i += (int64_t)nf.rest_blocks * blockDim.x) {
+      const float4 v = g4[i];
+      t += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+    }
+    if (b == 0 && (int64_t)threadIdx.x < ((nf.rest_end - nf.rest_begin) & 3)) {
+      const float v = nf.g[nf.rest_begin + (n4 << 2) + threadIdx.x];
+      t += (double)v * v;
+    }
+    t = block_sum_f64_1024(t, shn);
+    if (threadIdx.x == 0) nf.parts[RED_BLOCKS + b] = t;
+    return;
+  }
   const int ol = threadIdx.x & (RED_O - 1), zg = threadIdx.x / RED_O;
   const int o = blockIdx.x * RED_O + ol;
   double t = 0.0;
@@ -521,12 +557,20 @@ reduce_conv_bwd_kernel(const float* __restrict__ slab, int G, float* __restrict_
   }
   part[zg][ol] = t;
   __syncthreads();
+  double sq = 0.0;
   if (zg == 0 && o < SLAB) {
     double v = 0.0;
     for (int g = 0; g < RED_Z; ++g) v += part[g][ol];
-    conv_slab_put(o, v, gW2, gb2, gW1, gb1, rgb);
+    const float gv = conv_slab_put(o, v, gW2, gb2, gW1, gb1, rgb);
+    sq = (double)gv * gv;
+  }
+  if (nf.parts != nullptr) {   // (block-uniform)
+    sq = block_sum_f64_1024(sq, shn);
+    if (threadIdx.x == 0) nf.parts[blockIdx.x] = sq;
   }
 }
+
+int conv_norm_parts(int rest_blocks) { return RED_BLOCKS + rest_blocks; }
 
 // workgroups (= slab slices): one per CU on the 256-CU part, at most one per sample
 int conv_bwd_blocks(int S) { return S < 256 ? S : 256; }
@@ -534,22 +578,22 @@ int64_t conv_bwd_slab_floats(int S) { return (int64_t)conv_bwd_blocks(S) * SLAB;
 
 hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int S,
                            const float* a1, const float* da2, const float* W2, float* slab, float* gW2, float* gb2,
-                           float* gW1, float* gb1, hipStream_t s, bool reduce, int layout) {
+                           float* gW1, float* gb1, hipStream_t s, bool reduce, int layout, const NormFold& nf) {
   if (S <= 0) return hipSuccess;
   const int G = conv_bwd_blocks(S);
   ConvBwdArgs a{frames, nvalid, ctl, n, R, a1, da2, W2, S, G, slab, layout};
   hipLaunchKernelGGL(conv_bwd_kernel, dim3(G), dim3(NT), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !reduce) return e;
-  return launch_conv_reduce(slab, S, gW2, gb2, gW1, gb1, s, layout);
+  return launch_conv_reduce(slab, S, gW2, gb2, gW1, gb1, s, layout, nf);
 }
 
 hipError_t launch_conv_reduce(const float* slab, int S, float* gW2, float* gb2, float* gW1, float* gb1, hipStream_t s,
-                              int layout) {
+                              int layout, const NormFold& nf) {
   if (S <= 0) return hipSuccess;
-  hipLaunchKernelGGL(reduce_conv_bwd_kernel, dim3((SLAB + RED_O - 1) / RED_O), dim3(RED_O * RED_Z), 0, s, slab,
-                     conv_bwd_blocks(S), gW2,
-                     gb2, gW1, gb1, layout == FRAMES_RGB ? 1 : 0);
+  const int extra = nf.parts != nullptr ? nf.rest_blocks : 0;
+  hipLaunchKernelGGL(reduce_conv_bwd_kernel, dim3(RED_BLOCKS + extra), dim3(RED_O * RED_Z), 0, s, slab,
+                     conv_bwd_blocks(S), gW2, gb2, gW1, gb1, layout == FRAMES_RGB ? 1 : 0, nf);
   return hipGetLastError();
 }
 

@@ -409,7 +409,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
     net.w_slab_fc = buf("slab_fc", (int64_t)pl.fc_w * HID * (A2 + 1) * 4);
     net.w_slab_lstm = buf("slab_lstm", L ? (int64_t)pl.lstm_w * GATES * (2 * HID + 1) * 4 : 0);
   }
-  net.w_norm = buf("norm_partials", (int64_t)net.norm_blocks * 8);
+  net.w_norm = buf("norm_partials", (int64_t)std::max(net.norm_blocks, conv_norm_parts(net.norm_rest_blocks)) * 8);
   net.w_tick = buf("tickets", (int64_t)fc_fwd_tiles((int)n) * 4);
   net.w_fcb_part = buf("fc_bwd_partials", NAT ? 0 : fc_bwd_part_floats((int)S) * 4);
   net.w_fcb_tick = buf("fc_bwd_tickets", NAT ? 0 : (int64_t)fc_bwd_tickets() * 4);
@@ -574,9 +574,25 @@ hipError_t net_reset_state(Net& net, int e0, int n, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- backward
+// the folded clip norm's arguments (none unless arl_net_set_norm_fold): the
+// conv tensors are [0, o_fcW) of the flat gradient, everything after is final
+// before the conv slab reduce
+static NormFold norm_fold_args(const Net& net) {
+  if (!net.norm_fold) return NormFold{};
+  return NormFold{net.at<double>(net.w_norm), net.g, net.o_fcW, net.param_floats, net.norm_rest_blocks};
+}
+
 hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s) {
   if (net.arch == ARCH_FF_NATURE) return nature_learn(net, gamma, beta, vcoef, clip_reward, s);
-  for (int part = 0; part < LEARN_PARTS; ++part) ARL_TRY(net_learn_part(net, part, gamma, beta, vcoef, clip_reward, s));
+  for (int part = 0; part < LEARN_CONV; ++part) ARL_TRY(net_learn_part(net, part, gamma, beta, vcoef, clip_reward, s));
+  // the conv part last; with norm_fold its slab reduce also leaves the clip norm's partials
+  // (every other gradient tensor is final by now: one stream)
+  const NormFold nf = norm_fold_args(net);
+  ARL_TRY(launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl),
+                          net.N, net.R, net.T * net.N, net.at<float>(net.w_a1), net.at<float>(net.w_da2),
+                          net.p + net.o_c2W, net.at<float>(net.w_slab), net.g + net.o_c2W, net.g + net.o_c2b,
+                          net.g + net.o_c1W, net.g + net.o_c1b, s, /*reduce=*/true, net.layout, nf));
+  net.norm_ready = net.norm_fold;
   return hipSuccess;
 }
 
@@ -587,6 +603,7 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
 // critical path (dh -> FC -> conv backward) reads what they write.
 hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s) {
   if (net.arch == ARCH_FF_NATURE) return hipErrorInvalidValue;
+  if (part == LEARN_RETURNS) net.norm_ready = false;   // a new gradient: no folded norm until net_learn's reduce
   const int n = net.N, T = net.T, A = net.A, S = T * n;
   const float* P = net.p;
   float* G = net.g;
@@ -761,7 +778,8 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
     case STAGE_RETURNS:   // the LEARN_RETURNS launch (returns + loss gradient + heads dh), default coefficients
       return net_learn_part(net, LEARN_RETURNS, 0.99, 0.01f, 0.5f, 1, s);
     case STAGE_CONV_REDUCE:
-      return launch_conv_reduce(slab, S, G + net.o_c2W, G + net.o_c2b, G + net.o_c1W, G + net.o_c1b, s, net.layout);
+      return launch_conv_reduce(slab, S, G + net.o_c2W, G + net.o_c2b, G + net.o_c1W, G + net.o_c1b, s, net.layout,
+                                norm_fold_args(net));   // as arl_learn launches it
     case STAGE_GRAD_SQNORM:
       return launch_grad_sqnorm(net.g, net.param_floats, net.at<double>(net.w_norm), net.norm_blocks, s);
     default:
@@ -776,13 +794,16 @@ hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_tot
   // arl_learn left the step snapshot (returns kernel), so the update kernel
   // can also advance the window
   const bool fused = advance;
-  if (do_clip) ARL_TRY(launch_grad_sqnorm(net.g, net.param_floats, parts, net.norm_blocks, s));
+  const bool folded = do_clip && net.norm_ready;   // partials left by arl_learn's conv reduce
+  net.norm_ready = false;
+  if (do_clip && !folded) ARL_TRY(launch_grad_sqnorm(net.g, net.param_floats, parts, net.norm_blocks, s));
+  const int nparts = folded ? conv_norm_parts(net.norm_rest_blocks) : net.norm_blocks;
   const bool L = net.arch == ARCH_LSTM;
   const AdvanceArgs adv{net.at<int64_t>(net.w_ctl), net.at<uint8_t>(net.w_reset),
                         L ? net.at<float>(net.w_hbuf) : nullptr, L ? net.at<float>(net.w_cbuf) : nullptr, net.T,
                         net.N};
   ARL_TRY(launch_rmsprop(net.p, net.ms, net.g, net.param_floats, lr0, alpha, eps, do_clip ? parts : nullptr,
-                         net.norm_blocks, clip, total_steps > 0 ? net.at<int64_t>(net.w_ctl) : nullptr, total_steps,
+                         nparts, clip, total_steps > 0 ? net.at<int64_t>(net.w_ctl) : nullptr, total_steps,
                          n_total, net.T, s, fused ? &adv : nullptr));
   return advance && !fused ? net_advance(net, s) : hipSuccess;
 }

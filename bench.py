@@ -31,6 +31,8 @@ sys.path.insert(0, os.environ.get("ASYNCRL_PKG_ROOT") or os.path.join(ROOT, "asy
 from asyncrl_amd import A3C, A3CFF, A3CFFNature, A3CLSTM, DoomA3CFF, DoomA3CLSTM, GradientClipping, RMSpropAsync  # noqa: E402
 from asyncrl_amd import _lib  # noqa: E402
 from asyncrl_amd._lib import ACT_CONV_ONLY, LEARN_CONV  # noqa: E402
+from asyncrl_amd import a3c as _a3c  # noqa: E402
+NORM_FOLD = getattr(_a3c, "NORM_FOLD", False)   # (older package builds in A/B runs: no fold)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 F32_MFMA_PEAK_TFS = 157.3      # dense fp32 matrix peak (spec)
@@ -420,11 +422,14 @@ def main():
             ("returns", "returns_heads_kernel", lambda i: net.run_stage("returns", stream=stream), 1, "hbm",
              returns_bytes(N, T, A, mask=not lstm)),
             None if nat else
-            ("conv_reduce", "reduce_conv_bwd_kernel", lambda i: net.run_stage("conv_reduce", stream=stream), 1,
-             "hbm", (conv_bwd_blocks(S) + 1) * CONV_SLAB_FLOATS * 4),
+            ("conv_reduce", "reduce_conv_bwd_kernel" + (" (+ clip norm)" if (world == 1 and NORM_FOLD) else ""),
+             lambda i: net.run_stage("conv_reduce", stream=stream), 1, "hbm",
+             (conv_bwd_blocks(S) + 1) * CONV_SLAB_FLOATS * 4 + (net.n_params * 4 if (world == 1 and NORM_FOLD) else 0)),
+            # with one rank the clip norm is folded into the conv reduce (A3C: arl_net_set_norm_fold), so
+            # the grad_sqnorm launch is not in the window; its time is listed for reference
             None if nat else
-            ("grad_sqnorm", "grad_sqnorm_kernel", lambda i: net.run_stage("grad_sqnorm", stream=stream), 1, "hbm",
-             net.n_params * 4),
+            ("grad_sqnorm", "grad_sqnorm_kernel", lambda i: net.run_stage("grad_sqnorm", stream=stream),
+             0 if (world == 1 and NORM_FOLD) else 1, "hbm", net.n_params * 4),
         ]
         kernels = {}
         with torch.cuda.stream(stream):

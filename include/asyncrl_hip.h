@@ -142,6 +142,15 @@ int arl_truncate_window(arl_net* net, int t_len, void* stream);
  * Host state of the handle, read when arl_learn launches (defaults 1, 0). */
 int arl_net_set_loss(arl_net* net, double pi_loss_coef, int keep_loss_scale_same);
 
+/* GradientClipping's squared norm (a3c_ale.py:226) folded into arl_learn:
+ * with on != 0, arl_learn's conv slab reduce also leaves the f64 partial
+ * sums of squares of the whole gradient (the conv tensors it writes, and the
+ * rest, final by then), and the next arl_optimize / arl_optimize_advance
+ * uses them instead of its own squared-norm launch.  Only valid when nothing
+ * changes the gradient in between (turn it off when the gradient is
+ * all-reduced across ranks); arl_learn_part never folds.  Default off. */
+int arl_net_set_norm_fold(arl_net* net, int on);
+
 /* A3C.act forward + sample at window step t (a3c.py:154-164): pi_and_v of
  * the ring state, softmax policy output, Philox inverse-CDF action.  t ==
  * t_max is the bootstrap value of the window end (a3c.py:85, pre-update

@@ -693,3 +693,33 @@ def test_lstm_fused_cell_identical(gpu, tmp_path):
     assert int((outs[0]["hbuf"] != 0).sum()) > 0
     for k in outs[0].files:
         assert np.array_equal(outs[0][k], outs[1][k]), k
+
+
+def test_norm_fold_matches_grad_sqnorm(gpu):
+    """The clip norm folded into the learner's conv reduce (one rank,
+    arl_net_set_norm_fold) against the separate grad_sqnorm launch: the same
+    gradient (bit-identical), and after clip + RMSProp parameters within 1e-6
+    (the f64 partial sums group differently), with clipping active."""
+    from asyncrl_amd import A3C, A3CFF, GradientClipping, RMSpropAsync
+    rng = np.random.default_rng(17)
+    N, T, P = 64, 5, 7
+    pairs, rewards, dones = make_pools(rng, P, N, "uniform", p_done=0.1)
+    dp, dr, dd = dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu)
+    outs = []
+    for fold in (False, True):
+        m = A3CFF(4, n_envs=N, t_max=T, seed=5, init_seed=6, frames="pairs")
+        o = RMSpropAsync(lr=7e-4, eps=0.1, alpha=0.99).setup(m)
+        o.add_hook(GradientClipping(1.0))   # small threshold: clipping is active
+        ag = A3C(m, o, T, 0.99)
+        ag.net.set_norm_fold(fold)
+        ag.run_window(dp, dr, dd, P, first=True)
+        torch.cuda.synchronize()
+        g = ag.net.grads.clone()                             # window 1's gradient (same parameters in both arms)
+        for w in range(2):
+            ag.run_window(dp, dr, dd, P)
+        torch.cuda.synchronize()
+        outs.append((g, ag.net.params.clone(), float(g.double().pow(2).sum().sqrt())))
+    assert outs[0][2] > 1.0                                  # the clip was active
+    assert torch.equal(outs[0][0], outs[1][0])               # same gradient bits
+    ok, err = close_normscaled(outs[1][1].cpu().numpy(), outs[0][1].cpu().numpy(), 1e-6)
+    assert ok, err
