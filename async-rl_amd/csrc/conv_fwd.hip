@@ -47,6 +47,10 @@
                        // luminance, 128 resize)
 #endif
 
+#ifndef ARL_CF_STAMP
+#define ARL_CF_STAMP 0   // timing experiments only: s_memtime at phase ends into a2 (results wrong)
+#endif
+
 namespace arl {
 
 namespace {
@@ -163,6 +167,14 @@ conv_fwd_kernel(ConvFwdArgs a) {
   constexpr int V = PLANE / 16;              // 441 uint4 per screen
   // the biases first: loads issued at the top land before the staging waits
   // (loaded at the epilogues they were waited for there)
+#if ARL_CF_STAMP
+  uint32_t stamp[8];
+  int nst = 0;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#define CF_STAMP() do { if (nst < 8) stamp[nst++] = (uint32_t)(__builtin_amdgcn_s_memtime() - t0); } while (0)
+#else
+#define CF_STAMP() do {} while (0)
+#endif
   const float bias1 = a.b1[col];
   const float bias2 = a.b2[16 * (wave & 1) + col];
   const int64_t ks = a.ctl[CTL_STEP] + a.t;
@@ -368,14 +380,20 @@ conv_fwd_kernel(ConvFwdArgs a) {
     }
     w1_split_store(lds, tid, w1a, w1b, rgb);
     w2_split_store(lds, tid, w2v);
+    CF_STAMP();   // 0: staged
     __syncthreads();
-    // W1 fragments in registers (96 VGPRs), then the W1 planes are free for a1
-    bf16x8 w1h[8], w1m[8], w1l[8];
+    CF_STAMP();   // 1: barrier
+    // conv1 with each k-step's W1 fragments read from LDS inside the loop (their
+    // reads overlap the MFMAs instead of forming a phase of their own), then a
+    // barrier: every wave is done with the W1 planes before the a1 planes overwrite them
 #pragma unroll
-    for (int s = 0; s < 8; ++s) w1_frag(s, w1h[s], w1m[s], w1l[s]);
+    for (int s = 0; s < ((ARL_ABLATE & 1) ? 0 : 8); ++s) {
+      bf16x8 wh, wm, wl;
+      w1_frag(s, wh, wm, wl);
+      conv1_step(s, wh, wm, wl);
+    }
+    CF_STAMP();   // 2: conv1 MFMAs issued
     __syncthreads();
-#pragma unroll
-    for (int s = 0; s < ((ARL_ABLATE & 1) ? 0 : 8); ++s) conv1_step(s, w1h[s], w1m[s], w1l[s]);
   }
   float* a1g = a.a1 + (int64_t)e * A1;
   {
@@ -401,7 +419,9 @@ conv_fwd_kernel(ConvFwdArgs a) {
       }
     }
   }
+  CF_STAMP();   // 3: a1 epilogue
   __syncthreads();
+  CF_STAMP();   // 4: barrier
   // ---- conv2: wave -> n-tile nt = w & 1 (oc = 16 nt + col), m-tiles w >> 1, (w >> 1) + 4
   {
     const int nt = wave & 1, oc = 16 * nt + col;
@@ -413,6 +433,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
       w2m[s] = lds_load<bf16x8>(lds, off + W2P);
       w2l[s] = lds_load<bf16x8>(lds, off + 2 * W2P);
     }
+    CF_STAMP();   // 5: W2 fragments
     const int mA = wave >> 1, mB = mA + 4;
     const bool hasB = mB < 6;
     const int posA = 16 * mA + col, posB = 16 * (hasB ? mB : mA) + col;   // A row of this lane
@@ -434,6 +455,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
         mfma_x6(ahB, amB, alB, w2h[s], w2m[s], w2l[s], bigB, smlB);
       }
     }
+    CF_STAMP();   // 6: conv2 MFMAs issued
     float* a2g = a.a2 + (int64_t)e * A2;
     const float b = bias2;   // b2[oc]
 #pragma unroll
@@ -448,6 +470,15 @@ conv_fwd_kernel(ConvFwdArgs a) {
         if (p < C2_P) a2g[oc * C2_P + p] = fmaxf(__fadd_rn(__fadd_rn(bigB[r], smlB[r]), b), 0.f);
       }
     }
+#if ARL_CF_STAMP
+    CF_STAMP();   // 7: end
+    if (lane == 0) {   // wave w's stamps -> a2[e][w * 8 ..]; wave 0 also the start time
+      uint32_t* o = reinterpret_cast<uint32_t*>(a2g) + wave * 10;
+      for (int k = 0; k < 8; ++k) o[k] = stamp[k];
+      o[8] = (uint32_t)t0;
+      o[9] = (uint32_t)(t0 >> 32);
+    }
+#endif
   }
 }
 
