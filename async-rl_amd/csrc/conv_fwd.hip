@@ -425,15 +425,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
   // ---- conv2: wave -> n-tile nt = w & 1 (oc = 16 nt + col), m-tiles w >> 1, (w >> 1) + 4
   {
     const int nt = wave & 1, oc = 16 * nt + col;
-    bf16x8 w2h[8], w2m[8], w2l[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int off = L_W2 + oc * WROW + (2 * s + (g >> 1)) * 32 + (g & 1) * 16;
-      w2h[s] = lds_load<bf16x8>(lds, off);
-      w2m[s] = lds_load<bf16x8>(lds, off + W2P);
-      w2l[s] = lds_load<bf16x8>(lds, off + 2 * W2P);
-    }
-    CF_STAMP();   // 5: W2 fragments
+    CF_STAMP();   // 5: (W2 fragments are read per k-step below)
     const int mA = wave >> 1, mB = mA + 4;
     const bool hasB = mB < 6;
     const int posA = 16 * mA + col, posB = 16 * (hasB ? mB : mA) + col;   // A row of this lane
@@ -443,16 +435,23 @@ conv_fwd_kernel(ConvFwdArgs a) {
     f32x4 bigA = {0.f, 0.f, 0.f, 0.f}, smlA = bigA, bigB = bigA, smlB = bigA;
 #pragma unroll
     for (int s = 0; s < ((ARL_ABLATE & 2) ? 0 : 8); ++s) {
+      bf16x8 w2h[1], w2m[1], w2l[1];   // this k-step's W2 fragments, read inside the loop
+      {
+        const int off = L_W2 + oc * WROW + (2 * s + (g >> 1)) * 32 + (g & 1) * 16;
+        w2h[0] = lds_load<bf16x8>(lds, off);
+        w2m[0] = lds_load<bf16x8>(lds, off + W2P);
+        w2l[0] = lds_load<bf16x8>(lds, off + 2 * W2P);
+      }
       const int tap = 2 * s + (g >> 1), dP = (tap >> 2) * 20 + (tap & 3);
       const int offA = L_R1 + a1_slot(PA0 + dP, g & 1);
       const bf16x8 ahA = lds_load<bf16x8>(lds, offA), amA = lds_load<bf16x8>(lds, offA + A1P),
                    alA = lds_load<bf16x8>(lds, offA + 2 * A1P);
-      mfma_x6(ahA, amA, alA, w2h[s], w2m[s], w2l[s], bigA, smlA);
+      mfma_x6(ahA, amA, alA, w2h[0], w2m[0], w2l[0], bigA, smlA);
       if (hasB) {
         const int offB = L_R1 + a1_slot(PB0 + dP, g & 1);
         const bf16x8 ahB = lds_load<bf16x8>(lds, offB), amB = lds_load<bf16x8>(lds, offB + A1P),
                      alB = lds_load<bf16x8>(lds, offB + 2 * A1P);
-        mfma_x6(ahB, amB, alB, w2h[s], w2m[s], w2l[s], bigB, smlB);
+        mfma_x6(ahB, amB, alB, w2h[0], w2m[0], w2l[0], bigB, smlB);
       }
     }
     CF_STAMP();   // 6: conv2 MFMAs issued
