@@ -46,6 +46,16 @@
 #ifndef ARL_ABLATE
 #define ARL_ABLATE 0   // timing experiments only (bits: 8 step 1, 16 step 2, 32 step 3, 64 prefetch loads)
 #endif
+// loop unrolling of steps 1-3 (A/B knobs)
+#ifndef ARL_S1_UNROLL
+#define ARL_S1_UNROLL 21   // fully unrolled: 65.9 vs 71.6 us at 3, 70.6 at 7 (253 VGPRs, no spill)
+#endif
+#ifndef ARL_S2_UNROLL
+#define ARL_S2_UNROLL 1
+#endif
+#ifndef ARL_S3_UNROLL
+#define ARL_S3_UNROLL 3
+#endif
 #ifndef ARL_CB_STAMP
 #define ARL_CB_STAMP 0   // timing experiments only: s_memtime at every barrier into the slab (results wrong)
 #endif
@@ -345,7 +355,7 @@ conv_bwd_kernel(ConvBwdArgs a) {
       // instead of a division per k-step; same k order
       const float* b0 = a1s + (2 * wave) * A1C + (col >> 2) * A1R + (col & 3);
       int ox = g, boff = 2 * g, doff = g * D2F_LD;   // oy = 0
-#pragma unroll 3
+#pragma unroll ARL_S1_UNROLL
       for (int ps = 0; ps < ((ARL_ABLATE & 8) ? 0 : 21); ++ps) {
         const bool pv = 4 * ps + g < C2_P;
         const float af0 = pv ? d2f[doff + col] : 0.f;
@@ -382,7 +392,7 @@ conv_bwd_kernel(ConvBwdArgs a) {
       // past the grid are computed and dropped.  Lane (col, g) ends up with
       // channels ic = 4 g + rr of one position.  Waves w < 4: tiles 0-3, w >= 4: 4-6.
       const int mt0 = wave < 4 ? 0 : 4, mt1 = wave < 4 ? 4 : 7;
-#pragma unroll 1
+#pragma unroll ARL_S2_UNROLL
       for (int mt = mt0; mt < mt1; ++mt) {
         const int cell = 12 + 16 * mt + col;
         f32x4 big = {0.f, 0.f, 0.f, 0.f}, sml = big;
@@ -419,7 +429,7 @@ conv_bwd_kernel(ConvBwdArgs a) {
     // = (oy, X0 = 8 c): 8 positions (oy, X0..X0+7).  Tile a = rows (ky, kx =
     // 4 a + (col & 3)): the a = 0 and a = 1 fragments of a lane are pixels
     // X0..X0+7 and X0+1..X0+8 of one phase row, converted once and packed twice.
-#pragma unroll 3
+#pragma unroll ARL_S3_UNROLL
     for (int ks = 0; ks < ((ARL_ABLATE & 32) ? 0 : 15); ++ks) {
       const int Gk = 4 * ks + g, oy = Gk / 3, c = Gk - 3 * oy;
       const int ob = L_D1 + col * D1_OC + oy * D1_ROW + 16 * c;
