@@ -395,6 +395,12 @@ conv_bwd_kernel(ConvBwdArgs a) {
 #pragma unroll ARL_S2_UNROLL
       for (int mt = mt0; mt < mt1; ++mt) {
         const int cell = 12 + 16 * mt + col;
+        // the position, its a1 > 0 mask and the da1 address first (clamped for dropped
+        // cells): the mask read is in flight with the B operand reads
+        const int cy = cell / 11, cx = cell - cy * 11;
+        const bool keep = cell < 121 && cx != 0;
+        const int oy = keep ? 2 * (cy - 1) + py : 0, ox = keep ? 2 * (cx - 1) + px : 0;
+        const uint32_t m = reinterpret_cast<const uint16_t*>(lds + L_MASK)[oy * 20 + ox];
         f32x4 big = {0.f, 0.f, 0.f, 0.f}, sml = big;
 #pragma unroll
         for (int ks = 0; ks < ((ARL_ABLATE & 16) ? 0 : 4); ++ks) {
@@ -404,10 +410,7 @@ conv_bwd_kernel(ConvBwdArgs a) {
                        bl = lds_load<bf16x8>(lds, o + 2 * D2P);
           mfma_x6(w2h[ks], w2m[ks], w2l[ks], bh, bm, bl, big, sml);
         }
-        const int cy = cell / 11, cx = cell - cy * 11;
-        if (cell < 121 && cx != 0) {
-          const int oy = 2 * (cy - 1) + py, ox = 2 * (cx - 1) + px;
-          const uint32_t m = reinterpret_cast<const uint16_t*>(lds + L_MASK)[oy * 20 + ox];
+        if (keep) {
           uint8_t* d = lds + L_D1 + (4 * g) * D1_OC + oy * D1_ROW + ox * 2;
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
