@@ -53,8 +53,35 @@ __device__ inline uint32_t px_pair_bf16(uint32_t w, int b) {
   return __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
 }
 
+// split 8 f32 (one lane's 8 k of a 16x16x32 fragment) into three bf16x8 planes
+__device__ inline void split3_x8(const float (&x)[8], bf16x8& h, bf16x8& m, bf16x8& l) {
+  typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
+  u32x4_ hh, mm, ll;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t a, b, c;
+    split3_pack(x[2 * k], x[2 * k + 1], a, b, c);
+    hh[k] = a;
+    mm[k] = b;
+    ll[k] = c;
+  }
+  h = __builtin_bit_cast(bf16x8, hh);
+  m = __builtin_bit_cast(bf16x8, mm);
+  l = __builtin_bit_cast(bf16x8, ll);
+}
+
 __device__ inline f32x4 mfma_bf16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// both split, one accumulator (small terms first): acc += the 6 terms of A.B
+__device__ inline f32x4 mfma_x6_acc(bf16x8 ah, bf16x8 am, bf16x8 al, bf16x8 bh, bf16x8 bm, bf16x8 bl, f32x4 acc) {
+  acc = mfma_bf16(al, bh, acc);
+  acc = mfma_bf16(ah, bl, acc);
+  acc = mfma_bf16(am, bm, acc);
+  acc = mfma_bf16(am, bh, acc);
+  acc = mfma_bf16(ah, bm, acc);
+  return mfma_bf16(ah, bh, acc);
 }
 
 // A exact in bf16 (pixels), B split: big += A.Bh; small += A.Bl + A.Bm

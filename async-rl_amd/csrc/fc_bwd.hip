@@ -43,6 +43,7 @@
 #include <cstdlib>
 
 #include "arl_internal.hpp"
+#include "bf16split.hpp"
 
 namespace arl {
 
@@ -121,6 +122,7 @@ struct FcBwdArgs {
 };
 
 // ---------------------------------------------------------------- job A: dW, db
+template <bool SPLIT>
 __device__ void job_dw(const FcBwdArgs& a, int job, float* lds) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, col = lane & 15;
@@ -183,14 +185,40 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds) {
         for (int ks = 0; ks < BK / 4; ++ks)
           if (4 * ks + q >= kvalid) av[ks] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
+      if constexpr (SPLIT) {
+        // one 16x16x32 bf16 step per tile pair: element i of lane (col, q)
+        // is sample 4 i + q, the same rows the f32 steps below read
+        bf16x8 bh[2], bm[2], bl[2];
 #pragma unroll
-      for (int ks = 0; ks < BK / 4; ++ks) {
+        for (int u = 0; u < 2; ++u) {
+          float x[8];
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+          for (int i = 0; i < 8; ++i) x[i] = bv[i][u];
+          split3_x8(x, bh[u], bm[u], bl[u]);
+        }
 #pragma unroll
-          for (int u = 0; u < 2; ++u)
-            acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[ks][t], bv[ks][u], acc[t][u], 0, 0, 0);
-        if (bias) bs += av[ks];
+        for (int t = 0; t < 4; ++t) {
+          float x[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) x[i] = av[i][t];
+          bf16x8 ah, am, al;
+          split3_x8(x, ah, am, al);
+#pragma unroll
+          for (int u = 0; u < 2; ++u) acc[t][u] = mfma_x6_acc(ah, am, al, bh[u], bm[u], bl[u], acc[t][u]);
+        }
+        if (bias)
+#pragma unroll
+          for (int ks = 0; ks < BK / 4; ++ks) bs += av[ks];
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < BK / 4; ++ks) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+              acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[ks][t], bv[ks][u], acc[t][u], 0, 0, 0);
+          if (bias) bs += av[ks];
+        }
       }
     }
     if (c % FLUSH == FLUSH - 1 || c == nchunks - 1) {
@@ -319,7 +347,7 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds) {
 
 // ---------------------------------------------------------------- job B: da2
 // MT m-tiles per wave: workgroup tiles of BMT = 32 MT samples x 128 k
-template <int MT>
+template <int MT, bool SPLIT>
 __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
   constexpr int BMT = 32 * MT;
   constexpr int PIECES = (BMT * BK + BK * BN) / 256 / NW;   // LDS-DMA pieces per wave per chunk
@@ -336,10 +364,15 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
     stage_tile<BK, BN, 0>(sg + BMT * BK, a.W + (int64_t)c * BK * A2, A2, 0, BK - 1, k0);  // W[j][k0..k0+127]
   };
   f32x4 acc[MT][4];                          // m-tile i: rows 16 i + col; n-tile u: cols 4 col + u
+  f32x4 sml[SPLIT ? MT : 1][4];              // split path: the 5 small terms (acc: the h.h term)
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[i][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < (SPLIT ? MT : 1); ++i)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) sml[i][u] = f32x4{0.f, 0.f, 0.f, 0.f};
   // ReLU mask of the tile (a2 > 0), one bit per output element -- bit 4e + u
   // of mb[i] -- loaded a 16-row band per chunk during chunks 0..MT-1 so that no
   // load round trip is left for the epilogue.  Out-of-range rows / columns
@@ -395,15 +428,42 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
         for (int r = 0; r < 4; ++r)   // k = 16 g + 4 q + r on both operands
           bv[g][r] = *reinterpret_cast<const f32x4*>(Bs + (16 * g + 4 * q + r) * BN + wn * 64 + 4 * col);
       }
+      if constexpr (SPLIT) {
+        // one 16x16x32 bf16 step per tile pair: element 4 g + r of lane
+        // (col, q) is k = 16 g + 4 q + r on both operands
+        bf16x8 bh[4], bm[4], bl[4];
 #pragma unroll
-      for (int g = 0; g < BK / 16; ++g)
+        for (int u = 0; u < 4; ++u) {
+          float x[8];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+          for (int g = 0; g < 2; ++g)
 #pragma unroll
-          for (int i = 0; i < MT; ++i)
+            for (int r = 0; r < 4; ++r) x[4 * g + r] = bv[g][r][u];
+          split3_x8(x, bh[u], bm[u], bl[u]);
+        }
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-              acc[i][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][i][r], bv[g][r][u], acc[i][u], 0, 0, 0);
+        for (int i = 0; i < MT; ++i) {
+          float x[8];
+#pragma unroll
+          for (int g = 0; g < 2; ++g)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) x[4 * g + r] = av[g][i][r];
+          bf16x8 ah, am, al;
+          split3_x8(x, ah, am, al);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) mfma_x6(ah, am, al, bh[u], bm[u], bl[u], acc[i][u], sml[i][u]);
+        }
+      } else {
+#pragma unroll
+        for (int g = 0; g < BK / 16; ++g)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+                acc[i][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][i][r], bv[g][r][u], acc[i][u], 0, 0, 0);
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     barrier_lds();
@@ -421,7 +481,11 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
       const int row = wm * 16 * MT + 16 * i + 4 * q + e;
       f32x4 o;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) o[u] = (mb[i] >> (4 * e + u)) & 1u ? acc[i][u][e] : 0.f;
+      for (int u = 0; u < 4; ++u) {
+        float v = acc[i][u][e];
+        if constexpr (SPLIT) v += sml[i][u][e];
+        o[u] = (mb[i] >> (4 * e + u)) & 1u ? v : 0.f;
+      }
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), out, kin ? (row * A2 + k) * 4 : OOB, 0, 0);
     }
 }
@@ -489,15 +553,15 @@ __device__ void job_heads(const FcBwdArgs& a, int jt, float* lds) {
   }
 }
 
-template <int MT>
+template <int MT, bool SPLIT>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2)))
 fc_bwd_kernel(FcBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];   // 64 KB, the only LDS object
   const int b = a.b0 + blockIdx.x;
   const int na = NTA * a.Z;
   if (b < a.nc) job_heads(a, b, lds);   // first: the smallest, longest-latency jobs
-  else if (b < a.nc + na) job_dw(a, b - a.nc, lds);
-  else job_da2<MT>(a, b - a.nc - na, lds);
+  else if (b < a.nc + na) job_dw<SPLIT>(a, b - a.nc, lds);
+  else job_da2<MT, SPLIT>(a, b - a.nc - na, lds);
 }
 
 // ~400 samples per job A range, at most 16 ranges
@@ -521,9 +585,13 @@ hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int 
   const int Z = fc_bwd_ranges(S);
   int kpz = (S + Z - 1) / Z;
   kpz = (kpz + BK - 1) / BK * BK;
-  // ARL_FC_BWD_BM=64: job B on 64-sample tiles (2 m-tiles per wave) -- A/B timing
+  // ARL_FC_BWD_F32=1: the exact-f32 16x16x4 MFMA steps instead of the bf16 splits (A/B timing).
+  // Job B tiles: 64 samples (2 m-tiles a wave) on the split path, whose small-term
+  // accumulators leave no room for 4 m-tiles; 128 on the f32 path unless ARL_FC_BWD_BM=64.
+  static const char* f32 = getenv("ARL_FC_BWD_F32");
   static const char* bm = getenv("ARL_FC_BWD_BM");
-  const int MT = (bm && atoi(bm) == 64) ? 2 : 4, BMT = 32 * MT;
+  const bool split = !(f32 && atoi(f32) == 1);
+  const int MT = (split || (bm && atoi(bm) == 64)) ? 2 : 4, BMT = 32 * MT;
   const int na = NTA * Z, nb = ((S + BMT - 1) / BMT) * NKB;
   // ARL_FC_BWD_JOBS=a / b: launch one job alone; ARL_FC_BWD_ABL: ablations (timing experiments only)
   static const char* only = getenv("ARL_FC_BWD_JOBS");
@@ -534,8 +602,9 @@ hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int 
   const int grid = (only && only[0] == 'a') ? na : (only && only[0] == 'b') ? nb : nc + na + nb;
   FcBwdArgs args{dfc, a2, W, S, Z, kpz, gW, gb, da2, part, tick, heads ? *heads : HeadsDW{}, nc, b0,
                  abl ? atoi(abl) : 0};
-  if (MT == 2) hipLaunchKernelGGL(fc_bwd_kernel<2>, dim3(grid), dim3(NT), 0, s, args);
-  else hipLaunchKernelGGL(fc_bwd_kernel<4>, dim3(grid), dim3(NT), 0, s, args);
+  if (split) hipLaunchKernelGGL((fc_bwd_kernel<2, true>), dim3(grid), dim3(NT), 0, s, args);
+  else if (MT == 2) hipLaunchKernelGGL((fc_bwd_kernel<2, false>), dim3(grid), dim3(NT), 0, s, args);
+  else hipLaunchKernelGGL((fc_bwd_kernel<4, false>), dim3(grid), dim3(NT), 0, s, args);
   return hipGetLastError();
 }
 
