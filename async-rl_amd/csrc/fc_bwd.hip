@@ -5,7 +5,7 @@
 //   da2[s][k] = (sum_j dfc[s][j] W[j][k]) * (a2[s][k] > 0)
 // (dfc is already masked by hfc > 0).  One launch, three independent jobs:
 //   job A (dW, db): 128 (j) x 64 (k) tiles over one of Z contiguous sample
-//     ranges (Z grows with S, ~400 samples a range).  The Z partials of a
+//     ranges (Z grows with S, ~800 samples a range).  The Z partials of a
 //     tile meet in the same launch: every workgroup publishes its partial
 //     (write-through stores, drained) and then takes a ticket; the holder of
 //     the last ticket sums the Z partials in range order -- deterministic
@@ -21,8 +21,11 @@
 //     launches of its own (job_heads below).
 // Operands stream HBM/L2 -> LDS by LDS-DMA (global_load_lds dwordx4) into two
 // 32 KB stages (K chunks of 32; the next chunk in flight while the current one
-// feeds the MFMAs); exact f32 MFMA (v_mfma_f32_16x16x4_f32); 256 threads, each
-// wave a 64 x 32 (job A) or 64 x 64 (job B) block of 16 x 16 tiles.
+// feeds the MFMAs).  A chunk is one 16x16x32 bf16 k-step per tile pair on exact
+// bf16 splits of the f32 fragments (bf16split.hpp: 6 MFMAs, f32-accurate; job B
+// keeps the 5 small terms in their own accumulator); ARL_FC_BWD_F32=1 runs the
+// exact-f32 v_mfma_f32_16x16x4_f32 steps instead.  256 threads, each wave a
+// 64 x 32 (job A) or 32 x 64 (job B; 64 x 64 on the f32 path) block of 16 x 16 tiles.
 // Fragment reads are wide: one lane's 16-byte read of 4 consecutive m (or n)
 // feeds 4 MFMA tiles whose rows (columns) interleave with stride 4 (8-byte
 // reads: 2 tiles, stride 2).  Job B's A operand is stored k-contiguous and is
@@ -564,11 +567,12 @@ fc_bwd_kernel(FcBwdArgs a) {
   else job_da2<MT, SPLIT>(a, b - a.nc - na, lds);
 }
 
-// ~400 samples per job A range, at most 16 ranges
+// ~800 samples per job A range, at most 16 ranges (bf16-split steps, sweep in
+// profiles/r02/fcb_split/z_sweep.txt: best Z 2 / 3-5 / 6 at S 1280 / 2560 / 5120)
 int fc_bwd_ranges(int S) {
   static const char* zs = getenv("ARL_FC_BWD_Z");   // timing experiments only
   if (zs) return std::max(1, std::min(16, atoi(zs)));
-  return std::max(1, std::min(16, (S + 200) / 400));
+  return std::max(1, std::min(16, (S + 400) / 800));
 }
 }  // namespace
 
