@@ -15,11 +15,24 @@
 // K is consumed in chunks of BK staged through LDS as f32 ([BK][BM+4] and
 // [BK][BN+4]; the +4 pad breaks the 2-way ds_read_b32 conflict between the two
 // k rows read by lanes 0-15 and 16-31).  The next chunk is gathered into
-// registers while the current one feeds the MFMAs.
+// registers while the current one feeds the MFMAs.  gemm_tile<..., SP = true>
+// (with BK a multiple of 32) runs each 32-deep piece of a chunk as one 16x16x32
+// bf16 step per tile pair on exact bf16 splits of the f32 fragments
+// (bf16split.hpp: 6 MFMAs, the 5 small terms in their own accumulator;
+// f32-accurate) instead of 8 exact-f32 16x16x4 steps: 2.7x fewer matrix-pipe
+// cycles for more VALU / LDS reads.  Off: these GEMMs wait on their register
+// gathers and scalar LDS reads, not on the matrix pipe -- every GEMM on it took
+// the LSTM C3 window 1.316 -> 1.377 ms, the dual weight-gradient kernel alone
+// (ARL_GEMM2_SPLIT=1) 1.319 -> 1.374 ms (profiles/r02/gemm_split/).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "bf16split.hpp"
+
+#ifndef ARL_GEMM2_SPLIT
+#define ARL_GEMM2_SPLIT 0   // A/B variant only (see above)
+#endif
 
 namespace arl {
 
@@ -142,7 +155,8 @@ constexpr bool epi_is_tile() { return epi_tile_flag<E>::value; }
 
 // One BM x BN output tile (split-K slice z) of the implicit GEMM; the body of
 // gemm_kernel and of gemm2_kernel (two independent GEMMs in one launch).
-template <int BM, int BN, int BK, int WM, int WN, int AV, int BV, int NTH, class AOp, class BOp, class EOp>
+template <int BM, int BN, int BK, int WM, int WN, int AV, int BV, int NTH, class AOp, class BOp, class EOp,
+          bool SP = false>
 __device__ inline void gemm_tile(const AOp& A, const BOp& B, const EOp& E, int M, int N, int K, int k_per_split,
                                  int bx, int by, int z) {
   static_assert(WM * WN == NTH / 64, "one wave per WM x WN slot");
@@ -171,11 +185,17 @@ __device__ inline void gemm_tile(const AOp& A, const BOp& B, const EOp& E, int M
   int kend = kbeg + k_per_split;
   if (kend > K) kend = K;
 
-  f32x4 acc[TM][TN];
+  // bf16-split steps (bf16split.hpp) when the chunk is whole 32-deep steps
+  constexpr bool SPLIT = SP && BK % 32 == 0;
+  f32x4 acc[TM][TN], sml[SPLIT ? TM : 1][SPLIT ? TN : 1];   // sml: the split's 5 small terms
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < (SPLIT ? TM : 1); ++i)
+#pragma unroll
+    for (int j = 0; j < (SPLIT ? TN : 1); ++j) sml[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   float ra[A_PER], rb[B_PER];
 
@@ -236,23 +256,55 @@ __device__ inline void gemm_tile(const AOp& A, const BOp& B, const EOp& E, int M
       commit();
       __syncthreads();
       if (kc + BK < kend) gather(kc + BK);   // overlap next gather with MFMAs
+      if constexpr (SPLIT) {
+        // 32-deep steps on bf16 splits: element e of lane (col, q) is k = 4 e + q,
+        // the rows the f32 steps below read
 #pragma unroll
-      for (int ks = 0; ks < BK / 4; ++ks) {
-        const int kr = ks * 4 + (lane >> 4);
-        float af[TM], bf[TN];
+        for (int kb = 0; kb < BK; kb += 32) {
+          bf16x8 bh[TN], bm[TN], bl[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-          af[i] = As[kr * LDA + wm * (BM / WM) + i * 16 + (lane & 15)];
+          for (int j = 0; j < TN; ++j) {
+            float x[8];
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          bf[j] = Bs[kr * LDB + wn * (BN / WN) + j * 16 + (lane & 15)];
+            for (int e = 0; e < 8; ++e) x[e] = Bs[(kb + 4 * e + (lane >> 4)) * LDB + wn * (BN / WN) + j * 16 + (lane & 15)];
+            split3_x8(x, bh[j], bm[j], bl[j]);
+          }
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+          for (int i = 0; i < TM; ++i) {
+            float x[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] = As[(kb + 4 * e + (lane >> 4)) * LDA + wm * (BM / WM) + i * 16 + (lane & 15)];
+            bf16x8 ah, am, al;
+            split3_x8(x, ah, am, al);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) mfma_x6(ah, am, al, bh[j], bm[j], bl[j], acc[i][j], sml[i][j]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < BK / 4; ++ks) {
+          const int kr = ks * 4 + (lane >> 4);
+          float af[TM], bf[TN];
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            af[i] = As[kr * LDA + wm * (BM / WM) + i * 16 + (lane & 15)];
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+            bf[j] = Bs[kr * LDB + wn * (BN / WN) + j * 16 + (lane & 15)];
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
       }
     }
+  }
+  if constexpr (SPLIT) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] += sml[i][j];
   }
 
   // C/D map for 16x16x4 f32: col = lane & 15, row = (lane >> 4) * 4 + r
@@ -308,11 +360,11 @@ gemm2_kernel(J1 j1, J2 j2) {
   const int g1 = j1.gx * j1.gy * j1.gz;
   if (b < g1) {
     const int x = b % j1.gx, y = (b / j1.gx) % j1.gy, z = b / (j1.gx * j1.gy);
-    gemm_tile<BM, BN, BK, WM, WN, AV1, BV1, NTH>(j1.A, j1.B, j1.E, j1.M, j1.N, j1.K, j1.kps, x, y, z);
+    gemm_tile<BM, BN, BK, WM, WN, AV1, BV1, NTH, decltype(j1.A), decltype(j1.B), decltype(j1.E), ARL_GEMM2_SPLIT>(j1.A, j1.B, j1.E, j1.M, j1.N, j1.K, j1.kps, x, y, z);
   } else {
     b -= g1;
     const int x = b % j2.gx, y = (b / j2.gx) % j2.gy, z = b / (j2.gx * j2.gy);
-    gemm_tile<BM, BN, BK, WM, WN, AV2, BV2, NTH>(j2.A, j2.B, j2.E, j2.M, j2.N, j2.K, j2.kps, x, y, z);
+    gemm_tile<BM, BN, BK, WM, WN, AV2, BV2, NTH, decltype(j2.A), decltype(j2.B), decltype(j2.E), ARL_GEMM2_SPLIT>(j2.A, j2.B, j2.E, j2.M, j2.N, j2.K, j2.kps, x, y, z);
   }
 }
 
