@@ -10,11 +10,15 @@
 //     (write-through stores, drained) and then takes a ticket; the holder of
 //     the last ticket sums the Z partials in range order -- deterministic
 //     whatever the arrival order -- straight into the flat gradient (its own
-//     from registers, rounded as published).  No workgroup waits on another.  MFMA
+//     from registers, rounded as published).  No workgroup waits on another
+//     (ARL_FC_BWD_SPIN=1: ticket first, the last range waits for the others'
+//     partials and never publishes its own -- writes 20.8 -> 18.2 MiB, but
+//     38.5 -> 41.6 us at C2, profiles/r02/rejected/fcb_spin/).  MFMA
 //     accumulators restart every 128 samples; those sums add in f64.  db
 //     rides on the k-tile 0 workgroups: their n-wave-0 lanes add the A
 //     fragments they already hold.
-//   job B (da2): 128 (s) x 128 (k) tiles over K = 256, ReLU mask in the
+//   job B (da2): 64 (s) x 128 (k) tiles over K = 256 (128 x 128 on the
+//     exact-f32 path), ReLU mask in the
 //     epilogue (mask bits prefetched during the k loop, float4 buffer stores).
 //   job C (optional): the policy / value heads' weight gradients, a small
 //     f64 VALU reduction over S that runs beside A and B instead of as two
@@ -116,15 +120,34 @@ struct FcBwdArgs {
   float* gb;          // (256)
   float* da2;         // (S, 2592)
   float* part;        // (NTA, Z, PART) published job A partials (slot z = range z)
-  int* tick;          // (NTA): arrival tickets per tile
+  int* tick;          // (2 NTA): arrival tickets per tile, then ready counts (spin)
   HeadsDW hd;         // job C (hd.dl null: none)
   int nc;             // job C workgroups
   int b0;             // first job index of this launch (timing experiments)
   int abl;            // ARL_FC_BWD_ABL bits (timing experiments only): 1 no MFMA, 2 no staging,
                       // 4 no job A reduction (wrong dW), 8 no job A k loop
+  int spin;           // job A reduce: ticket first, the last range waits for the others' partials
 };
 
 // ---------------------------------------------------------------- job A: dW, db
+// range z's partial of `tile` into its slot: write-through sc1 stores; the
+// (u = 0, 1) pair of a lane is 8 contiguous bytes, one 64-bit store, so a
+// quarter-wave writes 128 contiguous bytes (whole sectors)
+__device__ inline void publish_dw(const FcBwdArgs& a, int tile, int z, const double (&s)[4][2][4], const double (&sb)[4],
+                                  bool bias, int wm, int wn, int q, int col) {
+  float* dst = a.part + ((int64_t)tile * a.Z + z) * PART;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(dst + (wm * 64 + 16 * q + 4 * e + t) * AK + wn * 32 + 2 * col),
+                         pack2((float)s[t][0][e], (float)s[t][1][e]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (bias && q == 0)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      __hip_atomic_store(dst + AJ * AK + wm * 64 + 4 * col + t, (float)sb[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <bool SPLIT>
 __device__ void job_dw(const FcBwdArgs& a, int job, float* lds) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -246,7 +269,27 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds) {
     }
   }
   auto pidx = [&](int t, int u, int e) { return (wm * 64 + 16 * q + 4 * e + t) * AK + wn * 32 + 2 * col + u; };
-  if (a.Z > 1 && !(a.abl & 4)) {
+  if (a.Z > 1 && !(a.abl & 4) && a.spin) {
+    // ticket first: ranges holding tickets 0 .. Z-2 publish and count
+    // themselves in ready[tile]; the last waits for that count (every range it
+    // waits on has taken its ticket, so is resident and already publishing)
+    // and its own partial never leaves registers
+    int* flag = reinterpret_cast<int*>(lds);   // the stages are free after the k loop's last barrier
+    if (tid == 0) *flag = __hip_atomic_fetch_add(&a.tick[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*flag < a.Z - 1) {
+      publish_dw(a, tile, z, s, sb, bias, wm, wn, q, col);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(&a.tick[NTA + tile], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (tid == 0)
+      while (__hip_atomic_load(&a.tick[NTA + tile], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < a.Z - 1)
+        __builtin_amdgcn_s_sleep(1);
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // every slot load below is sc1
+  } else if (a.Z > 1 && !(a.abl & 4)) {
     // every range publishes into its slot (write-through sc1 stores, drained),
     // then takes a ticket; the holder of the last ticket sums the slots
     float* dst = a.part + ((int64_t)tile * a.Z + z) * PART;
@@ -344,8 +387,10 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds) {
   if (bias && q == 0)
 #pragma unroll
     for (int t = 0; t < 4; ++t) a.gb[j0 + wm * 64 + 4 * col + t] = (float)ob[t];
-  if (a.Z > 1 && tid == 0 && !(a.abl & 4))   // re-arm for the next launch (a captured graph replays this one)
+  if (a.Z > 1 && tid == 0 && !(a.abl & 4)) {   // re-arm for the next launch (a captured graph replays this one)
     __hip_atomic_store(&a.tick[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.spin) __hip_atomic_store(&a.tick[NTA + tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // ---------------------------------------------------------------- job B: da2
@@ -577,7 +622,7 @@ int fc_bwd_ranges(int S) {
 }  // namespace
 
 int64_t fc_bwd_part_floats(int S) { return (int64_t)NTA * fc_bwd_ranges(S) * PART; }
-int fc_bwd_tickets() { return NTA; }
+int fc_bwd_tickets() { return 2 * NTA; }   // arrival tickets, then ready counts (ARL_FC_BWD_SPIN)
 
 // Job A's last k tile stages a2 columns 2560..2623 and job B's last one W
 // columns 2560..2687: the floats past a row's end are the next row's (a2 has
@@ -604,8 +649,10 @@ hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int 
   const int nc = heads != nullptr ? NJC : 0;
   const int b0 = (only && only[0] == 'b') ? nc + na : (only && only[0] == 'a') ? nc : 0;
   const int grid = (only && only[0] == 'a') ? na : (only && only[0] == 'b') ? nb : nc + na + nb;
+  // ARL_FC_BWD_SPIN=1: ticket-first job A reduce (the last range's partial is never published)
+  static const char* spin = getenv("ARL_FC_BWD_SPIN");
   FcBwdArgs args{dfc, a2, W, S, Z, kpz, gW, gb, da2, part, tick, heads ? *heads : HeadsDW{}, nc, b0,
-                 abl ? atoi(abl) : 0};
+                 abl ? atoi(abl) : 0, (spin && atoi(spin) == 1) ? 1 : 0};
   if (split) hipLaunchKernelGGL((fc_bwd_kernel<2, true>), dim3(grid), dim3(NT), 0, s, args);
   else if (MT == 2) hipLaunchKernelGGL((fc_bwd_kernel<2, false>), dim3(grid), dim3(NT), 0, s, args);
   else hipLaunchKernelGGL((fc_bwd_kernel<4, false>), dim3(grid), dim3(NT), 0, s, args);
