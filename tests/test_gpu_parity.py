@@ -695,6 +695,31 @@ def test_lstm_fused_cell_identical(gpu, tmp_path):
         assert np.array_equal(outs[0][k], outs[1][k]), k
 
 
+def test_fc_bwd_variants(gpu, tmp_path):
+    """FC backward knobs at S = 1,280 (two dW ranges): the ticket-first reduce
+    (ARL_FC_BWD_SPIN=1) sums the same partials in the same order, so every
+    bit matches the default; the exact-f32 16x16x4 steps (ARL_FC_BWD_F32=1)
+    and the default bf16-split steps are both f32-accurate, so the window
+    gradients agree to 1e-5 of each tensor's scale (close_normscaled)."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    outs = {}
+    for name, extra in (("default", {}), ("spin", {"ARL_FC_BWD_SPIN": "1"}), ("f32", {"ARL_FC_BWD_F32": "1"})):
+        f = str(tmp_path / f"fcb_{name}.npz")
+        env = dict(os.environ, **extra)
+        env.pop("ARL_FC_BWD_Z", None)
+        subprocess.run([sys.executable, os.path.join(here, "fc_bwd_worker.py"), f], env=env, check=True, timeout=240)
+        outs[name] = np.load(f)
+    d, sp, f32 = outs["default"], outs["spin"], outs["f32"]
+    assert float(np.abs(d["grads1"]).max()) > 0
+    for k in d.files:
+        assert np.array_equal(d[k], sp[k]), k
+    ok, err = close_normscaled(f32["grads1"], d["grads1"], 1e-5)
+    assert ok, err
+    assert not np.array_equal(f32["grads1"], d["grads1"])   # the knob did switch the k-steps
+
+
 def test_norm_fold_matches_grad_sqnorm(gpu):
     """The clip norm folded into the learner's conv reduce (one rank,
     arl_net_set_norm_fold) against the separate grad_sqnorm launch: the same
