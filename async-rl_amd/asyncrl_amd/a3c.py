@@ -42,7 +42,7 @@ import torch
 
 from ._lib import (ACT_AFTER_CONV, ACT_CONV_ONLY, ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, ARCH_STACK,
                    LEARN_CONV, RESIZE_SCALAR)
-from .distributed import allreduce_grads, world_info
+from .distributed import allreduce_grads, dist_initialized, world_info
 from .net import DeviceNet, init_like_torch
 from . import serializers
 from .policy_output import SoftmaxPolicyOutput
@@ -162,7 +162,14 @@ class A3C:
     def __init__(self, model: A3CModel, optimizer, t_max: int, gamma: float, beta: float = 1e-2,
                  process_idx: int = 0, clip_reward: bool = True, phi=None, pi_loss_coef: float = 1.0,
                  v_loss_coef: float = 0.5, keep_loss_scale_same: bool = False, resize_mode: int = RESIZE_SCALAR,
-                 process_group=None, batch_loss: str = "sum"):
+                 process_group=None, batch_loss: str = "sum", collectives: bool | None = None):
+        """collectives: all-reduce the window gradient over the process group
+        (default: when torch.distributed is initialised with > 1 rank; True
+        also on a one-rank group, which runs the RCCL calls of the N > 1 path
+        on one GPU).  A one-env drop-in model (the reference-contract `act`)
+        updates at its own episode's terminals, so its ranks would enter the
+        collectives at different times: it refuses collectives, and with
+        collectives=False every rank is an independent learner."""
         if model.net.t_max != t_max:
             raise ValueError("model was built for a different t_max")
         if batch_loss not in ("sum", "mean"):
@@ -181,15 +188,22 @@ class A3C:
         self.pg = process_group
         self.world, self.rank = world_info(process_group)
         self.net = model.net
+        self.single = self.net.stack and self.net.n_envs == 1
+        self.collectives = self.world > 1 if collectives is None else bool(collectives)
+        if self.single and self.collectives:
+            raise ValueError("A3C: the one-env act() drop-in updates at its own terminals, so ranks cannot "
+                             "all-reduce in step; use an n-env model (act_batch / run_window) for data "
+                             "parallelism, or collectives=False for independent learners per rank")
+        if self.collectives and not dist_initialized():
+            raise ValueError("A3C: collectives=True needs torch.distributed initialised")
         # the loss of the lockstep batch: the sum over envs (and ranks), or its mean
-        scale = 1.0 if batch_loss == "sum" else 1.0 / (self.net.n_envs * self.world)
+        scale = 1.0 if batch_loss == "sum" else 1.0 / (self.net.n_envs * (self.world if self.collectives else 1))
         self._vcoef = v_loss_coef * scale
         self.net.set_loss(pi_loss_coef * scale, keep_loss_scale_same)
-        # one rank: the update's clip norm comes from the learner's conv reduce (no all-reduce in between)
-        self.net.set_norm_fold(self.world == 1 and NORM_FOLD)
+        # no all-reduce between learn and update: the clip norm comes from the learner's conv reduce
+        self.net.set_norm_fold(not self.collectives and NORM_FOLD)
         self.t = 0          # env-steps taken (per env)
         self.t_start = 0    # a3c.py:56,152 (reference-contract act)
-        self.single = self.net.stack and self.net.n_envs == 1
         self._episode_start = True
         self._copied = None
         self.net.reset()
@@ -213,7 +227,7 @@ class A3C:
         heads section (all but ~12k of the parameters) starts as soon as the
         FC reduce is done and runs on the collective stream while the conv
         backward computes; only the conv section waits for it."""
-        return self.world > 1 and OVERLAP_ALLREDUCE and self.net.arch != ARCH_FF_NATURE
+        return self.collectives and OVERLAP_ALLREDUCE and self.net.arch != ARCH_FF_NATURE
 
     def _learn(self, stream=None):
         """The gradient part of the window; with the overlapped all-reduce it
@@ -231,7 +245,7 @@ class A3C:
         with torch.cuda.stream(main):          # the collectives order against `main`
             if self._overlap_allreduce():
                 o = net.layout["0/2/W"][0]      # conv1 / conv2 live in [0, o)
-                work = allreduce_grads(net.grads[o:], self.pg, async_op=True)
+                work = allreduce_grads(net.grads[o:], self.pg, async_op=True, force=True)
                 if conv is not None:
                     conv()                      # e.g. a captured graph of the conv part
                 else:
@@ -239,9 +253,9 @@ class A3C:
                                     stream=main)
                 if work is not None:
                     work.wait()
-                allreduce_grads(net.grads[:o], self.pg)
-            else:
-                allreduce_grads(net.grads, self.pg)
+                allreduce_grads(net.grads[:o], self.pg, force=True)
+            elif self.collectives:
+                allreduce_grads(net.grads, self.pg, force=True)
             self.optimizer.update(stream=main, advance_window=True)
 
     def _update(self, stream=None):

@@ -15,8 +15,12 @@ import torch
 import torch.distributed as dist
 
 
+def dist_initialized() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
 def world_info(group=None):
-    if dist.is_available() and dist.is_initialized():
+    if dist_initialized():
         return dist.get_world_size(group), dist.get_rank(group)
     return 1, 0
 
@@ -29,13 +33,15 @@ def shard_envs(global_envs: int, world: int, rank: int):
     return n, rank * n
 
 
-def allreduce_grads(grads: torch.Tensor, group=None, async_op: bool = False):
+def allreduce_grads(grads: torch.Tensor, group=None, async_op: bool = False, force: bool = False):
     """Sum (a contiguous section of) the flat gradient over ranks in place
     (2.71 MB FF / 4.81 MB LSTM per window, latency-bound ring all-reduces).
-    async_op: return the work handle (None with one rank); its wait() makes
-    the current stream wait for the collective."""
+    async_op: return the work handle (None when nothing was issued); its
+    wait() makes the current stream wait for the collective.  With one rank
+    nothing is issued unless force=True (a one-rank process group still runs
+    the collective: the RCCL path rehearsed on a single GPU)."""
     world, _ = world_info(group)
-    if world > 1:
+    if world > 1 or (force and dist.is_available() and dist.is_initialized()):
         return dist.all_reduce(grads, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
     return None
 

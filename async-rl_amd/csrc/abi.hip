@@ -423,4 +423,12 @@ int arl_returns_lossgrad(const float* rewards, const uint8_t* dones, const float
                     "returns");
 }
 
+int arl_stream_copy(const void* src, void* dst, int64_t bytes, int blocks, void* s) {
+  if (bytes < 0 || (bytes > 0 && (!src || !dst))) return fail(ARL_EINVAL, "stream_copy: null pointer / bytes < 0");
+  if (bytes % 16 || !aligned(src, 16) || !aligned(dst, 16)) return fail(ARL_EINVAL, "stream_copy: 16-byte units");
+  if (blocks < 1 || blocks > 65535) return fail(ARL_EINVAL, "stream_copy: blocks out of [1, 65535]");
+  if (bytes == 0) return ARL_OK;
+  return hip_status(arl::launch_stream_copy(src, dst, bytes, blocks, S(s)), "stream_copy");
+}
+
 }  // extern "C"

@@ -185,4 +185,27 @@ hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double
   return hipGetLastError();
 }
 
+// HBM stream-copy peak (measurement only; SURVEY 8(d) "also report vs the
+// measured stream-copy peak"): 16-byte loads, four in flight per lane before
+// the first store, grid-stride over the buffer.
+__global__ void __launch_bounds__(256)
+stream_copy_kernel(const float4* __restrict__ src, float4* __restrict__ dst, int64_t n4) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n4; i += stride) dst[i] = src[i];
+}
+
+hipError_t launch_stream_copy(const void* src, void* dst, int64_t bytes, int blocks, hipStream_t s) {
+  hipLaunchKernelGGL(stream_copy_kernel, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const float4*>(src),
+                     reinterpret_cast<float4*>(dst), bytes / 16);
+  return hipGetLastError();
+}
+
 }  // namespace arl

@@ -1,5 +1,8 @@
 """Throughput of the batched A3C hot path (phi + forward + sample + n-step
-update) on MI355X -- BASELINE.json metric, configs[1] workload at N=1.
+update) on MI355X -- BASELINE.json metric.  Default workload: configs[3]'s
+per-GPU leg (C4: A3C-FF, 512 envs per GPU), so `--gpus 8` IS configs[3]
+(4096 envs over 8 GPUs, RCCL all-reduce) and the N=1 line is its
+weak-scaling unit; `--workload c2|c3|c5` selects the other configs.
 
 One bench *step* = one lockstep window: t_max x (phi of every env's frame
 pair into the ring, NIPS-head forward, softmax policy, Philox sample), the
@@ -10,13 +13,18 @@ step.  Inputs are synthetic 210x160x3 RGB frame pairs, rewards and terminal
 flags pre-generated in HBM (a pool of `--pool` steps, cycled).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+        --gpus N > 1 without WORLD_SIZE in the environment: this process starts
+        N ranks itself (one child process per GPU, like the reference's
+        run_async, async.py:68-90), touches no GPU, forwards rank 0's line.
+    torchrun --nproc-per-node N bench.py --gpus N ...   (the same ranks, started by torchrun)
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,13 +34,19 @@ import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 # ASYNCRL_PKG_ROOT: another build of the package (A/B timing, scripts/ab.sh)
-sys.path.insert(0, os.environ.get("ASYNCRL_PKG_ROOT") or os.path.join(ROOT, "async-rl_amd"))
+PKG_ROOT = os.environ.get("ASYNCRL_PKG_ROOT") or os.path.join(ROOT, "async-rl_amd")
+NORM_FOLD = False     # set by _import_pkg (older package builds in A/B runs: no fold)
 
-from asyncrl_amd import A3C, A3CFF, A3CFFNature, A3CLSTM, DoomA3CFF, DoomA3CLSTM, GradientClipping, RMSpropAsync  # noqa: E402
-from asyncrl_amd import _lib  # noqa: E402
-from asyncrl_amd._lib import ACT_CONV_ONLY, LEARN_CONV  # noqa: E402
-from asyncrl_amd import a3c as _a3c  # noqa: E402
-NORM_FOLD = getattr(_a3c, "NORM_FOLD", False)   # (older package builds in A/B runs: no fold)
+
+def _import_pkg():
+    """The package loads libasyncrl_hip.so (its code objects register with
+    the HIP runtime): only rank processes import it, never the launcher."""
+    global NORM_FOLD
+    sys.path.insert(0, PKG_ROOT)
+    import asyncrl_amd
+    from asyncrl_amd import a3c as _a3c
+    NORM_FOLD = getattr(_a3c, "NORM_FOLD", False)
+    return asyncrl_amd
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 F32_MFMA_PEAK_TFS = 157.3      # dense fp32 matrix peak (spec)
@@ -53,6 +67,7 @@ NAT_FC_FWD_FLOP_PER_ENV = 2 * 3136 * 512
 NAT_CONV_BWD_FLOP_PER_SAMPLE = 2 * (2 * 49 * 64 * 576 + 2 * 81 * 64 * 512 + 400 * 32 * 256)
 PHI_STACK_BYTES_PER_PAIR = 201600 + 3 * 7056 + 4 * 7056   # pair + 3 prior planes + 4-plane stack
 PLANE_BYTES, A1_FLOATS, A2_FLOATS = 7056, 6400, 2592     # ring plane; conv1 / conv2 activations kept for backward
+PHI_TAP_ROWS = 168          # source rows (of 210) the 84-row bilinear resize reads (phi.hip phi_band)
 
 # BASELINE.json configs[1..4] -> (arch, envs per GPU, actions)
 WORKLOADS = {"c2": ("ff", 256, 4), "c3": ("lstm", 1024, 6), "c4": ("ff", 512, 4), "c5": ("phi", 16384, 0)}
@@ -63,9 +78,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2",
-                    help="BASELINE.json configs: c2 FF 256 envs (default, the metric's config), c3 LSTM 1024 envs "
-                         "A=6, c4 FF 512 envs per GPU (4096 over 8), c5 phi stress 16384 frame pairs")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c4",
+                    help="BASELINE.json configs: c4 FF 512 envs per GPU (default: 4096 over 8 GPUs, the north-star "
+                         "target's config), c2 FF 256 envs, c3 LSTM 1024 envs A=6, c5 phi stress 16384 frame pairs")
+    ap.add_argument("--median-windows", type=int, default=200,
+                    help="after the timed region: this many more windows, each between two HIP events on the "
+                         "bench stream, for the per-window median / p10 / p90 (SURVEY 8(d)); 0 disables")
+    ap.add_argument("--copy-peak", type=int, default=1, help="1: measure the HBM stream-copy peak on this GPU")
     ap.add_argument("--envs-per-gpu", type=int, default=0, help="0: the workload's")
     ap.add_argument("--t-max", type=int, default=5)
     ap.add_argument("--arch", choices=["ff", "lstm", "nature", "doom_ff", "doom_lstm"], default=None,
@@ -82,6 +101,53 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="0 disables the CPU baseline leg")
     ap.add_argument("--kernel-reps", type=int, default=50)
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`--gpus N` (N > 1) run as a plain `python bench.py`: start the N rank
+    processes here, one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N,
+    MASTER_ADDR 127.0.0.1), the way the reference's run_async starts its
+    actor-learners (async.py:68-90).  This process never touches the GPU (no
+    torch.cuda call, no import of the HIP extension) and never execs: it
+    waits for the children, which inherit stdout (rank 0 prints the line),
+    and exits with the first failing child's status after stopping the rest
+    (a rank left alone would wait in a collective forever)."""
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        while any(p.poll() is None for p in procs):
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            time.sleep(0.1)
+    finally:
+        rc = rc or next((p.returncode for p in procs if p.returncode not in (None, 0)), 0)
+        if rc:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            deadline = time.time() + 10
+            for p in procs:
+                try:
+                    p.wait(max(0.1, deadline - time.time()))
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+    if rc:
+        print(f"bench.py: a rank failed (status {rc})", file=sys.stderr)
+    return 0 if rc == 0 else (rc if rc > 0 else 1)
 
 
 CONV_SLAB_FLOATS = 12336                    # conv_slab.hpp SLAB: one conv_bwd workgroup's partial gradient
@@ -146,13 +212,61 @@ def init_dist():
     backend = os.environ.get("ARL_BENCH_DIST_BACKEND", "nccl")
     if os.environ.get("ARL_BENCH_SHARE_GPU") == "1":
         local = 0
+    # ARL_BENCH_FORCE_DIST=1 at one rank: a one-rank process group and the full
+    # N > 1 window (sectioned all-reduce around the conv backward, eager
+    # collectives, the norm pass) -- the RCCL calls rehearsed on one GPU
+    force = os.environ.get("ARL_BENCH_FORCE_DIST") == "1"
     torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 or force:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    return world, rank, local
+    return world, rank, local, (world > 1 or force)
+
+
+def measure_copy_peak(dev, mib: int = 1024, reps: int = 10):
+    """HBM stream-copy rate on this GPU (arl_stream_copy: 16-byte loads, four
+    in flight per lane): a 1 GiB buffer (4x the 256 MiB Infinity Cache) copied
+    `reps` times per grid size; the best grid's read + write bytes / time."""
+    from asyncrl_amd._lib import check, lib, ptr
+    n = mib << 20
+    src = torch.ones(n // 4, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    s = torch.cuda.current_stream(dev)
+    best, best_blocks = 0.0, 0
+    for blocks in (1024, 2048, 4096, 8192):
+        for _ in range(2):
+            check(lib.arl_stream_copy(ptr(src), ptr(dst), n, blocks, s.cuda_stream), "arl_stream_copy")
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(s)
+        for _ in range(reps):
+            check(lib.arl_stream_copy(ptr(src), ptr(dst), n, blocks, s.cuda_stream), "arl_stream_copy")
+        ev1.record(s)
+        ev1.synchronize()
+        gbs = 2 * n * reps / (ev0.elapsed_time(ev1) * 1e-3) / 1e9
+        if gbs > best:
+            best, best_blocks = gbs, blocks
+    ok = bool(torch.equal(src, dst))
+    del src, dst
+    torch.cuda.empty_cache()
+    return {"GB/s": round(best, 1), "frac_of_spec": round(best / HBM_PEAK_GBS, 4), "bytes_per_copy": 2 * n,
+            "blocks": best_blocks, "kernel": "stream_copy_kernel (optim.hip)", "copy_verified": ok}
+
+
+def ranks_seen(dev) -> int:
+    """Ranks that took part in a SUM all-reduce of ones over the bench's
+    process group (the transport the gradient all-reduce uses)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1
+    t = torch.ones(1, dtype=torch.float32, device=dev)
+    dist.all_reduce(t)
+    return int(round(float(t.item())))
 
 
 def rgb_phi_bytes(H, W):
@@ -192,7 +306,7 @@ def synth_pools(n, pool, seed, dev, frames=True, pool_rd=None):
     return pairs, torch.from_numpy(rewards).to(dev), torch.from_numpy(dones).to(dev)
 
 
-def bench_phi(a, world, rank, dev, n_default):
+def bench_phi(a, world, rank, dev, n_default, copy_peak=None):
     """configs[4] (c5): dqn_phi preprocessing stress -- one step = one batch of
     n frame pairs 210x160 RGB -> max -> luminance -> 84x84 -> 4-plane stack
     (arl_phi_stack, materialised), ping-pong stacks, reset flags from rng(3).
@@ -217,7 +331,7 @@ def bench_phi(a, world, rank, dev, n_default):
         for _ in range(a.warmup):
             step()
     stream.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -228,12 +342,12 @@ def bench_phi(a, world, rank, dev, n_default):
             step()
         ev1.record(stream)
     stream.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     us = 1e3 * ev0.elapsed_time(ev1) / a.steps
-    if world > 1:
+    if dist.is_initialized():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -250,15 +364,17 @@ def bench_phi(a, world, rank, dev, n_default):
                           "pairs_per_gpu": n, "parallelism": "dp%d" % world},
                "roofline": {"bound": "hbm", "kernel": "phi_stack_kernel", "achieved": round(ach, 1),
                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                            "traffic": traffic, "avg_launch_us": round(us, 2), "work_per_launch": work},
+                            "traffic": traffic, "avg_launch_us": round(us, 2), "work_per_launch": work,
+                            "peak_measured": copy_peak["GB/s"] if copy_peak else None,
+                            "frac_measured_peak": round(ach / copy_peak["GB/s"], 4) if copy_peak else None},
+               "hbm_copy_peak": copy_peak,
                "cpu_baseline": None}
         print(json.dumps(out))
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
-def main():
-    a = parse()
+def main(a):
     mp_ctx = None
     if a.cpu_seconds > 0 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
         # CPU baseline leg (ii) workers are forked by a forkserver started
@@ -270,16 +386,25 @@ def main():
         mp_ctx = mp.get_context("forkserver")
         mp_ctx.set_forkserver_preload(["cpu_baseline"])
         forkserver.ensure_running()
-    world, rank, local = init_dist()
+    world, rank, local, collectives = init_dist()
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE {world}")
     dev = torch.device("cuda", local)
+    seen = ranks_seen(dev)
+    if collectives and seen != world:
+        raise SystemExit(f"bench.py: {seen} ranks answered the all-reduce, expected {world}")
+    pkg = _import_pkg()
+    A3C, RMSpropAsync, GradientClipping = pkg.A3C, pkg.RMSpropAsync, pkg.GradientClipping
+    from asyncrl_amd._lib import ACT_CONV_ONLY, LEARN_CONV
+    copy_peak = measure_copy_peak(dev) if (rank == 0 and a.copy_peak) else None
     w_arch, w_envs, w_A = WORKLOADS[a.workload]
     if w_arch == "phi":
-        return bench_phi(a, world, rank, dev, w_envs)
+        return bench_phi(a, world, rank, dev, w_envs, copy_peak)
     arch = a.arch or w_arch
     A = a.actions or (w_A if arch == w_arch else (6 if arch == "lstm" else 4))
     N, T = a.envs_per_gpu or w_envs, a.t_max
-    Model = {"ff": A3CFF, "lstm": A3CLSTM, "nature": A3CFFNature, "doom_ff": DoomA3CFF,
-             "doom_lstm": DoomA3CLSTM}[arch]
+    Model = {"ff": pkg.A3CFF, "lstm": pkg.A3CLSTM, "nature": pkg.A3CFFNature, "doom_ff": pkg.DoomA3CFF,
+             "doom_lstm": pkg.DoomA3CLSTM}[arch]
     nat = arch == "nature"
     lstm = arch in ("lstm", "doom_lstm")
     doom = arch.startswith("doom")
@@ -295,7 +420,7 @@ def main():
     opt.add_hook(GradientClipping(40))
     opt.anneal_total_steps = 8 * 10 ** 7        # a3c_ale.py:200 --steps default
     opt.n_total_envs = N * world
-    agent = A3C(model, opt, T, 0.99, beta=1e-2)
+    agent = A3C(model, opt, T, 0.99, beta=1e-2, collectives=collectives)
     if doom:
         dH, dW = a.doom_width * 3 // 4, a.doom_width
         pairs, rewards, dones = synth_rgb_pools(N, a.pool, rank, dev, dH, dW)
@@ -313,7 +438,7 @@ def main():
     def window():
         if graph is not None:
             graph.replay()
-            if world > 1:
+            if collectives:
                 agent.finish_window(stream=stream, conv=conv_graph.replay if conv_graph is not None else None)
             else:
                 agent.t += T
@@ -331,22 +456,22 @@ def main():
                 # one window; with >1 rank the all-reduce + optimizer stay eager, and with the
                 # overlapped all-reduce the conv backward is a second graph replayed while the
                 # FC / heads section of the gradient is on the wire (A3C._reduce_and_step)
-                agent.run_window(pairs, rewards, dones, P, stream=stream, split_update=(world > 1),
+                agent.run_window(pairs, rewards, dones, P, stream=stream, split_update=collectives,
                                  env_groups=(a.env_groups or None))
-            if world > 1 and agent._overlap_allreduce():
+            if collectives and agent._overlap_allreduce():
                 cg = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(cg, stream=stream):
-                    model.net.learn_parts([LEARN_CONV], agent.gamma, agent.beta, agent.v_loss_coef,
+                    model.net.learn_parts([LEARN_CONV], agent.gamma, agent.beta, agent._vcoef,
                                           agent.clip_reward, stream=stream)
                 conv_graph = cg
             graph = g
-            agent.t -= T if world == 1 else 0
+            agent.t -= 0 if collectives else T
             for _ in range(2):
                 window()
     stream.synchronize()
 
     # ---------------------------------------------------------------- timed region
-    if world > 1:
+    if collectives:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -354,17 +479,42 @@ def main():
         for _ in range(a.steps):
             window()
     stream.synchronize()
-    if world > 1:
+    if collectives:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if collectives:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     units = N * T * world * a.steps
     value = units / elapsed
     ms_step = 1e3 * elapsed / a.steps
+
+    # per-window distribution (median over >= 100 windows): more
+    # windows after the timed region, each between two HIP events on the bench
+    # stream (which every part of a window, collectives included, joins)
+    windows = None
+    if a.median_windows > 0:
+        M = a.median_windows
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(M + 1)]
+        with torch.cuda.stream(stream):
+            evs[0].record(stream)
+            for i in range(M):
+                window()
+                evs[i + 1].record(stream)
+        stream.synchronize()
+        ms = np.array([evs[i].elapsed_time(evs[i + 1]) for i in range(M)])
+        q = np.percentile(ms, [10, 50, 90])
+        med = float(q[1])
+        if collectives:
+            t = torch.tensor([med], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            med = float(t.item())
+        windows = {"n": M, "median_ms": round(med, 4), "p10_ms": round(float(q[0]), 4),
+                   "p90_ms": round(float(q[2]), 4), "median_env_steps_per_s": round(N * T * world / (med * 1e-3), 1),
+                   "note": "HIP events per window on the bench stream; median = max over ranks of each rank's "
+                           "median, p10 / p90 rank 0's"}
     finite = bool(torch.isfinite(model.net.params).all())
 
     # ---------------------------------------------------------------- per-kernel roofline
@@ -422,14 +572,14 @@ def main():
             ("returns", "returns_heads_kernel", lambda i: net.run_stage("returns", stream=stream), 1, "hbm",
              returns_bytes(N, T, A, mask=not lstm)),
             None if nat else
-            ("conv_reduce", "reduce_conv_bwd_kernel" + (" (+ clip norm)" if (world == 1 and NORM_FOLD) else ""),
+            ("conv_reduce", "reduce_conv_bwd_kernel" + (" (+ clip norm)" if (not collectives and NORM_FOLD) else ""),
              lambda i: net.run_stage("conv_reduce", stream=stream), 1, "hbm",
-             (conv_bwd_blocks(S) + 1) * CONV_SLAB_FLOATS * 4 + (net.n_params * 4 if (world == 1 and NORM_FOLD) else 0)),
+             (conv_bwd_blocks(S) + 1) * CONV_SLAB_FLOATS * 4 + (net.n_params * 4 if (not collectives and NORM_FOLD) else 0)),
             # with one rank the clip norm is folded into the conv reduce (A3C: arl_net_set_norm_fold), so
             # the grad_sqnorm launch is not in the window; its time is listed for reference
             None if nat else
             ("grad_sqnorm", "grad_sqnorm_kernel", lambda i: net.run_stage("grad_sqnorm", stream=stream),
-             0 if (world == 1 and NORM_FOLD) else 1, "hbm", net.n_params * 4),
+             0 if (not collectives and NORM_FOLD) else 1, "hbm", net.n_params * 4),
         ]
         kernels = {}
         with torch.cuda.stream(stream):
@@ -457,6 +607,24 @@ def main():
                 "peak_note": (("exact f32 MFMA (v_mfma_f32_16x16x4_f32) vs the dense fp32 matrix peak" if nat else
                                "f32-equivalent FLOP/s vs the dense fp32 matrix peak (bf16-split f32 emulation, "
                                "DESIGN.md)") if d["bound"] == "mfma" else "HBM3E spec peak")}
+        if copy_peak is not None:
+            # HBM-bound stages also against the copy rate measured on this GPU
+            for k in kernels.values():
+                if k["bound"] == "hbm":
+                    k["frac_measured_peak"] = round(k["achieved"] / copy_peak["GB/s"], 4)
+            if roof["bound"] == "hbm":
+                roof["peak_measured"] = copy_peak["GB/s"]
+                roof["frac_measured_peak"] = round(roof["achieved"] / copy_peak["GB/s"], 4)
+        if "phi" in kernels and not doom:
+            # phi on the bytes it moves: the 168 of 210 source rows the resize taps touch (x2 frames x
+            # 480 B) + the plane written, besides SURVEY 8(d)'s whole-pair basis
+            k = kernels["phi"]
+            moved = N * (PHI_TAP_ROWS * 160 * 3 * 2 + PLANE_BYTES)
+            ach = moved / (k["avg_launch_us"] * 1e-6) / 1e9
+            k["moved_basis"] = {"bytes_per_launch": moved, "achieved": round(ach, 2), "unit": "GB/s",
+                                "frac": round(ach / HBM_PEAK_GBS, 4)}
+            if copy_peak is not None:
+                k["moved_basis"]["frac_measured_peak"] = round(ach / copy_peak["GB/s"], 4)
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_seconds > 0 and arch == "ff":
@@ -482,12 +650,19 @@ def main():
                        "graph": use_graph, "env_groups": len(model.net.env_groups(a.env_groups or model.net.default_env_groups())),
                        "parallelism": "dp%d" % world,
                        "units_per_step": N * T * world},
+            "ranks_seen": seen, "collectives": (("rccl" if dist.get_backend() == "nccl" else dist.get_backend())
+                                                if collectives else None),
+            "allreduce_bytes_per_window": (4 * model.net.grads.numel()) if collectives else 0,
+            "windows": windows, "hbm_copy_peak": copy_peak,
             "roofline": roof, "kernels": kernels, "cpu_baseline": cpu, "params_finite": finite,
         }
-        print(json.dumps(out))
-    if world > 1:
+        print(json.dumps(out), flush=True)
+    if collectives:
         dist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main()
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    main(args)

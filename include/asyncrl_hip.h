@@ -296,6 +296,14 @@ int arl_returns_lossgrad(const float* rewards, const uint8_t* dones, const float
                          int keep_loss_scale_same, int clip_reward, float* dlogits, float* dv, float* loss,
                          void* stream);
 
+/* ------------------------------------------------------------------ measurement */
+
+/* Device-to-device copy of `bytes` (a multiple of 16, 16-byte aligned
+ * buffers) by a grid of `blocks` 256-thread workgroups, 16-byte loads: the HBM
+ * stream-copy peak the bench reports beside the 8 TB/s spec (SURVEY 8(d);
+ * no reference counterpart). */
+int arl_stream_copy(const void* src, void* dst, int64_t bytes, int blocks, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
