@@ -55,6 +55,7 @@ SIGNATURES = {
     "arl_observe_rgb": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_i64, c_int, c_int,
                                 c_void_p]),
     "arl_observe_stack": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p]),
+    "arl_observe_states": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p]),
     "arl_truncate_window": (c_int, [c_void_p, c_int, c_void_p]),
     "arl_net_set_loss": (c_int, [c_void_p, c_double, c_int]),
     "arl_net_set_norm_fold": (c_int, [c_void_p, c_int]),
@@ -97,6 +98,7 @@ ARCH_LSTM = 1
 ARCH_FF_NATURE = 2   # A3CFF with NatureDQNHead (dqn_head.py:6-28)
 ARCH_RGB = 16        # flag for FF / LSTM: the ViZDoom models (train_a3c_doom.py:25-63), RGB screens
 ARCH_STACK = 32      # flag for FF / LSTM: observations are whole 4-screen stacks (ALE.state, ale.py:91-94)
+ARCH_STATES = 64     # flag for FF / LSTM: observations are f32 (4, 84, 84) states, phi's output (a3c.py:34,73)
 FWD_KEEP_STATE = 16  # arl_forward_states mode bit: LSTM keep_same_state (a3c_ale.py:57-60)
 ABI_VERSION = 2
 ACT_CONV_ONLY = 4      # arl_act_envs mode bits (env-group staggering)

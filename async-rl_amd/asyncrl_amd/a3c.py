@@ -9,17 +9,20 @@ Two ways in, one set of kernels:
 
 * `A3C.act(state, reward, is_state_terminal) -> int | None` on a one-env model
   (the default for n_envs = 1) is the reference's contract call for call
-  (a3c.py:67-167): `state` is ALE.state (4 uint8 84x84 screens, ale.py:91-94)
-  or anything the `phi` plugin maps to dqn_phi's image of such screens; the
+  (a3c.py:67-167).  The model sees phi(state) (a3c.py:73; phi is the identity
+  by default, a3c.py:34): with phi = asyncrl_amd.dqn_phi, `state` is ALE.state
+  (4 uint8 84x84 screens, ale.py:91-94), kept as uint8 and scaled by the conv
+  kernels (bit-exact dqn_phi); with any other phi (or none) the float32
+  (4, 84, 84) value phi returns is the conv input (an ARCH_STATES ring).  The
   window restarts at every update (t_start = t, a3c.py:152); a terminal call
   runs the R = 0 update over the steps since the last one, resets the
   recurrent state and returns None (a3c.py:77-83,165-167); a full window
   bootstraps with v(s) at pre-update parameters and acts on s with the
   post-update ones (a3c.py:85,156); pi_loss_coef, v_loss_coef and
   keep_loss_scale_same scale the losses as at a3c.py:110-121.  The frames
-  live in an ARCH_STACK ring (one whole stack per slot); the update is the
-  same device learner as the batched path, restricted to the window's steps
-  (arl_truncate_window).
+  live in an ARCH_STACK (uint8) or ARCH_STATES (f32) ring, one whole stack
+  per slot; the update is the same device learner as the batched path,
+  restricted to the window's steps (arl_truncate_window).
 
 * `A3C.act_batch(pairs, reward, is_state_terminal)` / `run_window(...)` on an
   n-env model: the envs step in lockstep, phi runs on the GPU
@@ -41,7 +44,8 @@ import numpy as np
 import torch
 
 from ._lib import (ACT_AFTER_CONV, ACT_CONV_ONLY, ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, ARCH_STACK,
-                   LEARN_CONV, RESIZE_SCALAR)
+                   ARCH_STATES, LEARN_CONV, RESIZE_SCALAR)
+from .dqn_phi import dqn_phi as _device_dqn_phi
 from .distributed import allreduce_grads, dist_initialized, world_info
 from .net import DeviceNet, init_like_torch
 from . import serializers
@@ -53,9 +57,6 @@ STAGGER = os.environ.get("ARL_GROUP_STAGGER", "1") != "0"
 OVERLAP_ALLREDUCE = os.environ.get("ARL_OVERLAP_ALLREDUCE", "1") != "0"
 # one rank: GradientClipping's norm from the learner's conv reduce (ARL_NORM_FOLD=0: grad_sqnorm launch)
 NORM_FOLD = os.environ.get("ARL_NORM_FOLD", "1") != "0"
-
-_PHI_LUT = np.arange(256, dtype=np.float32) / np.float32(255.0)   # dqn_phi.py:14-16, per uint8 value
-
 
 def _to_device_f32(state, device) -> torch.Tensor:
     t = state if torch.is_tensor(state) else torch.from_numpy(np.ascontiguousarray(np.asarray(state, np.float32)))
@@ -69,9 +70,12 @@ class A3CModel:
     """a3c.py:15-24.
 
     frames: "stacks" -- observations are whole ALE.state stacks (the A3C.act
-    drop-in; default for n_envs = 1), or "pairs" -- raw (frame 4, frame 3)
-    pairs whose phi runs on the GPU (the batched hot path; default for
-    n_envs > 1).  RGB (Doom) and Nature models take their own inputs."""
+    drop-in with phi = dqn_phi; default for n_envs = 1), "states" -- float32
+    (4, 84, 84) states, whatever A3C's phi plugin returns (A3C switches a
+    one-env model to it for any phi but asyncrl_amd.dqn_phi), or "pairs" --
+    raw (frame 4, frame 3) pairs whose phi runs on the GPU (the batched hot
+    path; default for n_envs > 1).  RGB (Doom) and Nature models take their
+    own inputs."""
 
     arch = ARCH_FF
 
@@ -82,16 +86,30 @@ class A3CModel:
         stackable = arch in (ARCH_FF, ARCH_LSTM)
         if frames is None:
             frames = "stacks" if (n_envs == 1 and stackable) else "pairs"
-        if frames not in ("stacks", "pairs"):
-            raise ValueError("frames must be 'stacks' or 'pairs'")
-        if frames == "stacks":
-            if not stackable:
-                raise ValueError("frames='stacks' applies to the NIPS-head FF / LSTM models")
-            arch |= ARCH_STACK
+        if frames not in ("stacks", "states", "pairs"):
+            raise ValueError("frames must be 'stacks', 'states' or 'pairs'")
+        if frames != "pairs" and not stackable:
+            raise ValueError(f"frames={frames!r} applies to the NIPS-head FF / LSTM models")
+        arch |= {"stacks": ARCH_STACK, "states": ARCH_STATES, "pairs": 0}[frames]
         self.frames = frames
         self.net = DeviceNet(arch, n_actions, n_envs, t_max, env_offset=env_offset, seed=seed, device=device)
         if init_seed is not None:
             self.net.load_params(init_like_torch(self.arch, n_actions, np.random.default_rng(init_seed)))
+
+    def set_frames(self, frames: str):
+        """Rebuild the device net for another observation layout ("stacks"
+        / "states"), keeping the parameters and the RMSProp statistics."""
+        if frames == self.frames:
+            return
+        if frames not in ("stacks", "states") or self.frames not in ("stacks", "states"):
+            raise ValueError("set_frames switches between 'stacks' and 'states' only")
+        old = self.net
+        arch = self.arch | (ARCH_STACK if frames == "stacks" else ARCH_STATES)
+        net = DeviceNet(arch, self.n_actions, old.n_envs, old.t_max, env_offset=old.env_offset, seed=old.seed,
+                        device=old.device)
+        net.params.copy_(old.params)
+        net.ms.copy_(old.ms)
+        self.net, self.frames = net, frames
 
     def pi_and_v(self, state, keep_same_state: bool = False, deterministic: bool = False):
         """a3c_ale.py:38-40 / 55-63: state (n, C, 84, 84) float32 (dqn_phi
@@ -187,8 +205,12 @@ class A3C:
         self.resize_mode = resize_mode
         self.pg = process_group
         self.world, self.rank = world_info(process_group)
+        if model.frames in ("stacks", "states") and model.net.n_envs == 1:
+            # a3c.py:73 feeds phi(state) to the model: uint8 screens for the device dqn_phi
+            # (bit-exact scaling in the conv kernels), phi's f32 output for any other phi
+            model.set_frames("stacks" if phi is _device_dqn_phi else "states")
         self.net = model.net
-        self.single = self.net.stack and self.net.n_envs == 1
+        self.single = (self.net.stack or self.net.states) and self.net.n_envs == 1
         self.collectives = self.world > 1 if collectives is None else bool(collectives)
         if self.single and self.collectives:
             raise ValueError("A3C: the one-env act() drop-in updates at its own terminals, so ranks cannot "
@@ -210,9 +232,10 @@ class A3C:
         if self.single:
             dev = self.net.device
             pin = dev.type == "cuda"
-            self._h_stack = torch.empty((1, 4, 84, 84), dtype=torch.uint8, pin_memory=pin)
+            sdt = torch.float32 if self.net.states else torch.uint8
+            self._h_stack = torch.empty((1, 4, 84, 84), dtype=sdt, pin_memory=pin)
             self._h_rd = torch.zeros(2, dtype=torch.float32, pin_memory=pin)
-            self._d_stack = torch.empty((1, 4, 84, 84), dtype=torch.uint8, device=dev)
+            self._d_stack = torch.empty((1, 4, 84, 84), dtype=sdt, device=dev)
             self._d_rd = torch.zeros(2, dtype=torch.float32, device=dev)
             self._d_done = torch.zeros(2, dtype=torch.uint8, device=dev)   # [0] = 0, [1] = 1
             self._d_done[1] = 1
@@ -277,7 +300,7 @@ class A3C:
             self._copied.synchronize()                  # the pinned buffers' last upload has landed
         self._h_rd[0] = r
         if not terminal:
-            self._h_stack[0].numpy()[...] = self._screens(state)
+            self._h_stack[0].numpy()[...] = self._phi_input(state)
             self._d_stack.copy_(self._h_stack, non_blocking=True)
         self._d_rd.copy_(self._h_rd, non_blocking=True)
         if net.device.type == "cuda":
@@ -306,30 +329,26 @@ class A3C:
         self.t += 1
         return int(net.step_outputs(slot)["actions"][0].item())
 
-    def _screens(self, state) -> np.ndarray:
-        """The (4, 84, 84) uint8 screens behind phi(state): the conv kernels
-        read uint8 planes and apply dqn_phi's /255 themselves (bit-exact).
-        phi=None or dqn_phi: `state` is the list of 4 screens (dqn_phi.py:12-13
-        asserts); another phi must return uint8 screens, or float32 values
-        that are exactly dqn_phi's image of uint8 screens."""
-        phi = self.phi
-        if phi is None or getattr(phi, "__name__", "") == "dqn_phi":
+    def _phi_input(self, state) -> np.ndarray:
+        """What the ring stores for phi(state) (a3c.py:73).  phi = dqn_phi
+        (the device one): the 4 uint8 screens themselves (dqn_phi.py:12-13
+        asserts) -- the conv kernels apply the /255.  Any other phi, or none
+        (the identity, a3c.py:34): phi's output, which must be float32 (4,
+        84, 84) (or (1, 4, 84, 84)) as Chainer's Convolution2D takes it."""
+        if self.net.stack:
             x = np.asarray(state)
             if x.shape != (4, 84, 84) or x.dtype != np.uint8:
-                raise ValueError("A3C.act: state must be 4 uint8 84x84 screens (dqn_phi.py:12-13)")
+                raise ValueError("A3C.act: with phi=dqn_phi, state must be 4 uint8 84x84 screens (dqn_phi.py:12-13)")
             return x
-        x = phi(state)
+        x = state if self.phi is None else self.phi(state)
         x = x.detach().cpu().numpy() if torch.is_tensor(x) else np.asarray(x)
         x = x.reshape(x.shape[-3:]) if x.ndim == 4 and x.shape[0] == 1 else x
         if x.shape != (4, 84, 84):
             raise ValueError(f"A3C.act: phi(state) has shape {x.shape}, need (4, 84, 84)")
-        if x.dtype == np.uint8:
-            return x
-        u = np.clip(np.rint(np.asarray(x, np.float64) * 255.0), 0, 255).astype(np.uint8)
-        if x.dtype != np.float32 or not np.array_equal(_PHI_LUT[u], x):
-            raise ValueError("A3C.act: phi(state) is not dqn_phi's image of uint8 screens; the device "
-                             "learner reads observations as uint8 planes")
-        return u
+        if x.dtype != np.float32:
+            raise ValueError(f"A3C.act: phi(state) is {x.dtype}; the model takes float32 input "
+                             "(use phi=asyncrl_amd.dqn_phi for uint8 ALE screens)")
+        return x
 
     def act_batch(self, pairs: torch.Tensor, reward=None, is_state_terminal=None) -> torch.Tensor:
         """a3c.py:67-167, lockstep-batched.  pairs: (n, 2, 210, 160, 3) uint8

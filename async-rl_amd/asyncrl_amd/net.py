@@ -15,7 +15,7 @@ import os
 import numpy as np
 import torch
 
-from ._lib import (ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, ARCH_STACK, ENV_GROUP_ALIGN, FWD_KEEP_STATE,
+from ._lib import (ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, ARCH_STACK, ARCH_STATES, ENV_GROUP_ALIGN, FWD_KEEP_STATE,
                    LEARN_CONV, LEARN_FC_REDUCE, LEARN_GATES_REDUCE, LEARN_HEADS_DW, LEARN_RETURNS, LEARN_TRUNK,
                    RESIZE_SCALAR, check, lib, ptr, stream_handle)
 
@@ -26,7 +26,7 @@ def param_shapes(arch: int, n_actions: int):
     Nature head dqn_head.py:16-20 with 512-wide policy / value heads; the
     RGB flag: NIPSDQNHead(n_input_channels=3), train_a3c_doom.py:28,46)."""
     c_in = 3 if arch & ARCH_RGB else 4
-    arch &= ~(ARCH_RGB | ARCH_STACK)
+    arch &= ~(ARCH_RGB | ARCH_STACK | ARCH_STATES)
     if arch == ARCH_FF_NATURE:
         return [("0/0/W", (32, 4, 8, 8)), ("0/0/b", (32,)), ("0/1/W", (64, 32, 4, 4)), ("0/1/b", (64,)),
                 ("0/2/W", (64, 64, 3, 3)), ("0/2/b", (64,)), ("0/3/W", (512, 3136)), ("0/3/b", (512,)),
@@ -72,7 +72,8 @@ class DeviceNet:
         self.arch, self.n_actions, self.n_envs, self.t_max = arch, n_actions, n_envs, t_max
         self.rgb = bool(arch & ARCH_RGB)
         self.stack = bool(arch & ARCH_STACK)
-        self.base_arch = arch & ~(ARCH_RGB | ARCH_STACK)
+        self.states = bool(arch & ARCH_STATES)
+        self.base_arch = arch & ~(ARCH_RGB | ARCH_STACK | ARCH_STATES)
         self.env_offset, self.seed = env_offset, seed
         h = ctypes.c_void_p()
         check(lib.arl_net_create(ctypes.byref(h), arch, n_actions, n_envs, t_max, env_offset, seed),
@@ -144,7 +145,7 @@ class DeviceNet:
         """pair_pool: (pool_len, n, 2, 210, 160, 3) uint8 frame pairs; for an
         RGB net (arch | ARCH_RGB) the screens (pool_len, n, H, W, 3) instead.
         envs=(e0, ne): only envs [e0, e0 + ne) (arl_observe_envs)."""
-        if self.stack and envs is None:
+        if (self.stack or self.states) and envs is None:
             self.observe_stack(t, pair_pool, reward_pool, done_pool, pool_len, force_reset, stream)
             return
         if envs is not None:
@@ -165,8 +166,15 @@ class DeviceNet:
     def observe_stack(self, t: int, stack_pool=None, reward_pool=None, done_pool=None, pool_len: int = 1,
                       force_reset: bool = False, stream=None):
         """ARCH_STACK nets: stack_pool (pool_len, n, 4, 84, 84) uint8 whole
-        frame stacks (arl_observe_stack); None ingests only the reward / done
-        of step t (a terminal observation)."""
+        frame stacks (arl_observe_stack); ARCH_STATES nets: (pool_len, n, 4,
+        84, 84) f32 states, phi's output (arl_observe_states).  None ingests
+        only the reward / done of step t (a terminal observation)."""
+        if self.states:
+            if stack_pool is not None and stack_pool.dtype != torch.float32:
+                raise ValueError("observe_stack: an ARCH_STATES net takes float32 states")
+            check(lib.arl_observe_states(self._h, t, ptr(stack_pool), ptr(reward_pool), ptr(done_pool), pool_len,
+                                         int(force_reset), stream_handle(stream)), "arl_observe_states")
+            return
         check(lib.arl_observe_stack(self._h, t, ptr(stack_pool), ptr(reward_pool), ptr(done_pool), pool_len,
                                     int(force_reset), stream_handle(stream)), "arl_observe_stack")
 
@@ -200,7 +208,7 @@ class DeviceNet:
         """observe + act of a step as one launch (arl_observe_act_envs): frame-pair
         nets with the NIPS head, when enabled (ARL_FUSE_OBS=1 or the instance
         attribute fuse_obs = True)."""
-        return getattr(self, "fuse_obs", FUSE_OBS) and not (self.rgb or self.stack or self.arch == ARCH_FF_NATURE)
+        return getattr(self, "fuse_obs", FUSE_OBS) and not (self.rgb or self.stack or self.states or self.arch == ARCH_FF_NATURE)
 
     def observe_act(self, t: int, pair_pool: torch.Tensor, reward_pool=None, done_pool=None, pool_len: int = 1,
                     force_reset: bool = False, resize_mode: int = RESIZE_SCALAR, mode: int = 1, stream=None,
@@ -224,7 +232,7 @@ class DeviceNet:
     def env_groups(self, groups: int):
         """Split the envs into <= `groups` contiguous ranges (e0, ne) with e0 a
         multiple of ENV_GROUP_ALIGN; [(0, n_envs)] when they do not split."""
-        if groups <= 1 or self.arch == ARCH_FF_NATURE:
+        if groups <= 1 or self.arch == ARCH_FF_NATURE or self.states:
             return [(0, self.n_envs)]
         per = -(-self.n_envs // groups)
         per = -(-per // ENV_GROUP_ALIGN) * ENV_GROUP_ALIGN

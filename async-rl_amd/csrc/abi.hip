@@ -164,7 +164,7 @@ static int ring_args(arl_net* h, int t, const uint8_t* pool, const float* reward
                      int64_t pool_len, int force_reset, int mode, int H, int W, int e0, int ne, arl::RingArgs& a) {
   arl::Net& n = h->net;
   if (t < 0 || t > n.T) return fail(ARL_EINVAL, "observe: t out of [0, t_max]");
-  if ((!pool && n.layout != arl::FRAMES_STACK) || pool_len < 1)
+  if ((!pool && n.layout != arl::FRAMES_STACK && n.layout != arl::FRAMES_STATES) || pool_len < 1)
     return fail(ARL_EINVAL, "observe: need the frame pool and pool_len >= 1");
   if (!aligned(pool, 16)) return fail(ARL_EINVAL, "observe: the frame pool must be 16-byte aligned");
   if (n.N > 65535) return fail(ARL_EINVAL, "observe: n_envs > 65535");
@@ -187,6 +187,7 @@ static int ring_args(arl_net* h, int t, const uint8_t* pool, const float* reward
   a.W = W;
   a.e0 = e0;
   a.ne = ne;
+  a.esize = n.layout == arl::FRAMES_STATES ? 4 : 1;
   return 0;
 }
 
@@ -197,7 +198,7 @@ static int observe_common(arl_net* h, int t, const uint8_t* pool, const float* r
   if (int rc = ring_args(h, t, pool, reward_pool, done_pool, pool_len, force_reset, mode, H, W, e0, ne, a)) return rc;
   const arl::Net& n = h->net;
   return hip_status(n.layout == arl::FRAMES_RGB     ? arl::launch_rgb_ring(a, S(s))
-                    : n.layout == arl::FRAMES_STACK ? arl::launch_stack_ring(a, S(s))
+                    : (n.layout == arl::FRAMES_STACK || n.layout == arl::FRAMES_STATES) ? arl::launch_stack_ring(a, S(s))
                                                     : arl::launch_phi_ring(a, S(s)),
                     "observe");
 }
@@ -207,6 +208,7 @@ int arl_observe(arl_net* h, int t, const uint8_t* pair_pool, const float* reward
   NEED_BOUND(h);
   if (h->net.rgb) return fail(ARL_ESTATE, "observe: RGB net, use arl_observe_rgb");
   if (h->net.stack) return fail(ARL_ESTATE, "observe: ARL_ARCH_STACK net, use arl_observe_stack");
+  if (h->net.states) return fail(ARL_ESTATE, "observe: ARL_ARCH_STATES net, use arl_observe_states");
   if (mode < 0 || mode > (ARL_RESIZE_SIMD | ARL_RESIZE_CROP)) return fail(ARL_EINVAL, "bad resize_mode");
   return observe_common(h, t, pair_pool, reward_pool, done_pool, pool_len, force_reset, mode, 0, 0, s);
 }
@@ -226,6 +228,15 @@ int arl_observe_stack(arl_net* h, int t, const uint8_t* stack_pool, const float*
   if (!h->net.stack) return fail(ARL_ESTATE, "observe_stack: net was not created with ARL_ARCH_STACK");
   if (!stack_pool && t < 1) return fail(ARL_EINVAL, "observe_stack: a frameless observation needs t >= 1");
   return observe_common(h, t, stack_pool, reward_pool, done_pool, pool_len, force_reset, 0, 0, 0, s);
+}
+
+int arl_observe_states(arl_net* h, int t, const float* state_pool, const float* reward_pool,
+                       const uint8_t* done_pool, int64_t pool_len, int force_reset, void* s) {
+  NEED_BOUND(h);
+  if (!h->net.states) return fail(ARL_ESTATE, "observe_states: net was not created with ARL_ARCH_STATES");
+  if (!state_pool && t < 1) return fail(ARL_EINVAL, "observe_states: a stateless observation needs t >= 1");
+  return observe_common(h, t, reinterpret_cast<const uint8_t*>(state_pool), reward_pool, done_pool, pool_len,
+                        force_reset, 0, 0, 0, s);
 }
 
 int arl_truncate_window(arl_net* h, int t_len, void* s) {
@@ -269,8 +280,8 @@ int arl_act_mode(arl_net* h, int t, int mode, void* s) {
 static int check_env_range(const arl::Net& n, int e0, int ne) {
   if (ne < 1 || e0 < 0 || e0 > n.N - ne) return fail(ARL_EINVAL, "env range [e0, e0 + ne) outside [0, n_envs)");
   if (e0 % ARL_ENV_GROUP_ALIGN) return fail(ARL_EINVAL, "env range: e0 must be a multiple of ARL_ENV_GROUP_ALIGN");
-  if (n.arch == arl::ARCH_FF_NATURE && (e0 != 0 || ne != n.N))
-    return fail(ARL_EINVAL, "env range: the Nature head runs all envs in one launch");
+  if ((n.arch == arl::ARCH_FF_NATURE || n.states) && (e0 != 0 || ne != n.N))
+    return fail(ARL_EINVAL, "env range: Nature-head and ARL_ARCH_STATES nets run all envs in one launch");
   return 0;
 }
 
@@ -281,7 +292,7 @@ int arl_observe_envs(arl_net* h, int t, int e0, int ne, const uint8_t* pool, int
   if (h->net.rgb) {
     if (mode < 0 || mode > ARL_RESIZE_SIMD) return fail(ARL_EINVAL, "observe_rgb: resize_mode must be 0 or 1");
     if (int rc = check_rgb_dims(H, W)) return rc;
-  } else if (h->net.stack) {
+  } else if (h->net.stack || h->net.states) {
     H = W = mode = 0;
   } else {
     if (mode < 0 || mode > (ARL_RESIZE_SIMD | ARL_RESIZE_CROP)) return fail(ARL_EINVAL, "bad resize_mode");
@@ -306,7 +317,7 @@ int arl_observe_act_envs(arl_net* h, int t, int e0, int ne, const uint8_t* pair_
                          void* s) {
   NEED_BOUND(h);
   const arl::Net& n = h->net;
-  if (n.rgb || n.stack || n.arch == arl::ARCH_FF_NATURE)
+  if (n.rgb || n.stack || n.states || n.arch == arl::ARCH_FF_NATURE)
     return fail(ARL_ESTATE, "observe_act: frame-pair nets with the NIPS head only (use arl_observe + arl_act)");
   if (ne < 0) {
     e0 = 0;

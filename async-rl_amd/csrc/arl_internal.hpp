@@ -22,11 +22,16 @@ constexpr int ARCH_RGB = 16;
 // arch flag: observations are whole 4-screen stacks (ale.py:91-94 ALE.state), one per ring slot
 // (frames (R, n, 4, 84, 84)) -- the layout of the reference-semantics A3C.act drop-in
 constexpr int ARCH_STACK = 32;
+// arch flag: observations are float32 (4, 84, 84) states -- whatever the A3C phi plugin returns
+// (a3c.py:34,50,73; identity by default), one per ring slot (frames (R, n, 4, 84, 84) f32); the
+// convs run on the generic implicit-GEMM template (states.hip)
+constexpr int ARCH_STATES = 64;
 // frame layout of the ring, as the conv kernels read it (conv input plane c of window step t):
 //   FRAMES_RING  one screen per slot, plane c = slot (k - 3 + c) % R   (k = ctl[STEP] + t)
 //   FRAMES_RGB   three planes per slot [0, R, G, B] of slot k % R
 //   FRAMES_STACK four planes per slot, plane c of slot k % R
-enum FrameLayout { FRAMES_RING = 0, FRAMES_RGB = 1, FRAMES_STACK = 2 };
+//   FRAMES_STATES four f32 planes per slot (ARCH_STATES), plane c of slot k % R
+enum FrameLayout { FRAMES_RING = 0, FRAMES_RGB = 1, FRAMES_STACK = 2, FRAMES_STATES = 3 };
 
 constexpr int PLANE = 84 * 84;         // 7056 B per screen
 constexpr int PAIR = 2 * 210 * 160 * 3; // 201,600 B per frame pair
@@ -57,13 +62,14 @@ struct RingArgs {
   int n, R, t, mode, force_reset;
   int H = 0, W = 0;           // RGB nets: pair_pool is an image pool (pool_len, n, H, W, 3)
   int e0 = 0, ne = -1;        // env range of this launch: e0 + blockIdx.y, ne envs (-1: all n)
+  int esize = 1;              // stack_ring_kernel: bytes per stack element (1 uint8 screens, 4 f32 states)
 };
 
 // RGB (Doom) observations, train_a3c_doom.py:21-23 / doom_env.py:47
 constexpr int RGB_MAX_W = 2048;   // staged source rows: 12 x W x 3 bytes of LDS
 hipError_t launch_rgb_phi(const uint8_t* imgs, int64_t n, int H, int W, float* out, int mode, hipStream_t s);
 hipError_t launch_rgb_ring(const RingArgs& a, hipStream_t s);
-hipError_t launch_stack_ring(const RingArgs& a, hipStream_t s);   // ARCH_STACK nets
+hipError_t launch_stack_ring(const RingArgs& a, hipStream_t s);   // ARCH_STACK / ARCH_STATES nets
 
 hipError_t launch_current_screen(const uint8_t* cur, const uint8_t* prev, uint8_t* out, int64_t n,
                                  int mode, hipStream_t s);
@@ -85,6 +91,7 @@ struct Net {
   int arch, A, N, T, R;
   bool rgb = false;        // ARCH_RGB: 3 planes per obs step in the ring, conv1 W (16, 3, 8, 8)
   bool stack = false;      // ARCH_STACK: 4 planes (a whole stack) per obs step in the ring
+  bool states = false;     // ARCH_STATES: 4 f32 planes (phi's output) per obs step in the ring
   int layout = FRAMES_RING;
   // loss options (a3c.py:110-121): pi_loss_coef, keep_loss_scale_same (arl_net_set_loss)
   float pi_coef = 1.f;
@@ -110,7 +117,7 @@ struct Net {
   int64_t w_ctl, w_frames, w_nvalid, w_reset, w_rewards, w_dones, w_a1, w_a2, w_hfc, w_gates, w_hbuf,
       w_cbuf, w_logits, w_probs, w_logp, w_v, w_ent, w_logpa, w_act, w_dlogits, w_dv, w_dh, w_dfc,
       w_dG, w_dhn, w_dcn, w_da2, w_slab, w_norm, w_loss, w_tick, w_fcb_part = 0, w_fcb_tick = 0;
-  int64_t w_a3 = 0, w_da1 = 0, w_da3 = 0;   // Nature head only
+  int64_t w_a3 = 0, w_da1 = 0, w_da3 = 0;   // Nature head only (w_da1 also ARCH_STATES)
   // LSTM recurrent state of pi_and_v on explicit states (A3CLSTM.pi_and_v, a3c_ale.py:55-63):
   // h, c (n, 256), the step's outputs hn, cn, and reset flags (1 = state is None)
   int64_t w_eval_h = 0, w_eval_c = 0, w_eval_hn = 0, w_eval_cn = 0, w_eval_reset = 0;
@@ -157,6 +164,13 @@ hipError_t nature_act(Net& net, int t, int mode, hipStream_t s);
 hipError_t nature_forward_f32(Net& net, const float* x, int n, int mode, hipStream_t s);
 hipError_t nature_learn(Net& net, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s);
 hipError_t nature_stage(Net& net, int stage, int t, hipStream_t s);
+
+// ARCH_STATES nets (states.hip): conv1 + conv2 forward of window slot t from the f32
+// state ring (all envs), and the conv backward of the window (conv2 dW / db,
+// da1, conv1 dW / db) on the generic GEMM, gradients straight into net.g
+hipError_t states_conv_fwd(const Net& net, int t, float* a1, float* a2, hipStream_t s);
+hipError_t states_conv_bwd(Net& net, hipStream_t s);
+int64_t states_slab_floats(const Net& net);
 
 // shared pieces of the heads' backward (net.hip)
 hipError_t launch_heads_bwd(const float* dl, const float* dv, const float* Wpi, const float* Wv, int A, int H,

@@ -32,7 +32,78 @@ struct OnesColB {       // B(s, j) = j < K ? X[s][j] : 1   (bias gradient column
   }
 };
 
+// im2col of an f32 activation tensor x[s][IC][IH][IH] for a KS x KS, stride ST
+// convolution with OH x OH outputs: A(m, k), m = s*OH*OH + p, k = ic*KS*KS + ky*KS + kx
+template <int IC, int IH, int KS, int ST, int OH>
+struct Im2col {
+  const float* __restrict__ x;
+  __device__ float load(int m, int k) const {
+    constexpr int OP = OH * OH, KK = KS * KS;
+    const int s = m / OP, p = m - s * OP, oy = p / OH, ox = p - oy * OH;
+    const int ic = k / KK, r = k - ic * KK, ky = r / KS, kx = r - ky * KS;
+    return x[((int64_t)s * IC + ic) * (IH * IH) + (ST * oy + ky) * IH + ST * ox + kx];
+  }
+};
+
+// B(m, j) = j < K ? X(m, j) : 1 -- weight-gradient operand with the bias column
+template <class X>
+struct OnesCol {
+  X x; int K;
+  __device__ float load(int m, int j) const { return j < K ? x.load(m, j) : 1.f; }
+  __device__ float4 load4n(int m, int j) const {   // only instantiated for X with load4
+    if (j + 3 < K) return x.load4(m, j);
+    return make_float4(load(m, j), load(m, j + 1), load(m, j + 2), load(m, j + 3));
+  }
+};
+
+// A(oc, m) = dy[s][oc][p], m = s*P + p (output gradient of a conv, transposed)
+struct ConvDyT {
+  const float* __restrict__ dy; int OC, P;
+  __device__ float load(int oc, int m) const {
+    const int s = m / P, p = m - s * P;
+    return dy[((int64_t)s * OC + oc) * P + p];
+  }
+  __device__ float4 load4(int oc, int m) const {   // P % 4 == 0 only (conv1: 400)
+    const int s = m / P, p = m - s * P;
+    return *reinterpret_cast<const float4*>(dy + ((int64_t)s * OC + oc) * P + p);
+  }
+};
+
+// stride-2, 4x4 transposed conv from OC channels of 9 x 9 back to IC channels of
+// 20 x 20 (the second conv of both DQN heads, dqn_head.py:17,42) for one output
+// parity class (py, px): y = 2 qy + py, x = 2 qx + px, qy, qx in [0, 10); k =
+// oc*4 + jy*2 + jx covers exactly the taps ky = py + 2 jy, kx = px + 2 jx that
+// reach (y, x) from oy = qy - jy, ox = qx - jx.
+template <int OC, int IC>
+struct ConvT2ClassA {
+  const float* __restrict__ dy; int py, px;
+  __device__ float load(int m, int k) const {
+    const int s = m / 100, q = m - s * 100, qy = q / 10, qx = q - qy * 10;
+    const int oc = k >> 2, jy = (k >> 1) & 1, jx = k & 1;
+    const int oy = qy - jy, ox = qx - jx;
+    if (oy < 0 || oy >= 9 || ox < 0 || ox >= 9) return 0.f;
+    return dy[((int64_t)s * OC + oc) * 81 + oy * 9 + ox];
+  }
+};
+template <int OC, int IC>
+struct ConvT2ClassW {
+  const float* __restrict__ w; int py, px;
+  __device__ float load(int k, int ic) const {
+    const int oc = k >> 2, ky = py + 2 * ((k >> 1) & 1), kx = px + 2 * (k & 1);
+    return w[(((int64_t)oc * IC + ic) * 4 + ky) * 4 + kx];
+  }
+};
+
 // ---------------------------------------------------------------- epilogues
+template <int IC>
+struct EpiT2Class {     // da1 of one parity class of ConvT2ClassA, times (a1 > 0)
+  float* __restrict__ out; const float* __restrict__ mask; int py, px;
+  __device__ void store(int m, int ic, float v, int) const {
+    const int s = m / 100, q = m - s * 100, qy = q / 10, qx = q - qy * 10;
+    const int64_t i = ((int64_t)s * IC + ic) * 400 + (2 * qy + py) * 20 + 2 * qx + px;
+    out[i] = mask[i] > 0.f ? v : 0.f;
+  }
+};
 struct EpiConv {        // out[s][n][p] = relu(v + b[n]); m = s*P + p
   float* __restrict__ out; const float* __restrict__ b; int OC, P;
   __device__ void store(int m, int n, float v, int) const {

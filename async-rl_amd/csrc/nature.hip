@@ -67,43 +67,6 @@ struct RingIm2col {
   }
 };
 
-// im2col of an f32 activation tensor x[s][IC][IH][IH] for a KS x KS, stride ST
-// convolution with OH x OH outputs: A(m, k), m = s*OH*OH + p, k = ic*KS*KS + ky*KS + kx
-template <int IC, int IH, int KS, int ST, int OH>
-struct Im2col {
-  const float* __restrict__ x;
-  __device__ float load(int m, int k) const {
-    constexpr int OP = OH * OH, KK = KS * KS;
-    const int s = m / OP, p = m - s * OP, oy = p / OH, ox = p - oy * OH;
-    const int ic = k / KK, r = k - ic * KK, ky = r / KS, kx = r - ky * KS;
-    return x[((int64_t)s * IC + ic) * (IH * IH) + (ST * oy + ky) * IH + ST * ox + kx];
-  }
-};
-
-// B(m, j) = j < K ? X(m, j) : 1 -- weight-gradient operand with the bias column
-template <class X>
-struct OnesCol {
-  X x; int K;
-  __device__ float load(int m, int j) const { return j < K ? x.load(m, j) : 1.f; }
-  __device__ float4 load4n(int m, int j) const {   // only instantiated for X with load4
-    if (j + 3 < K) return x.load4(m, j);
-    return make_float4(load(m, j), load(m, j + 1), load(m, j + 2), load(m, j + 3));
-  }
-};
-
-// A(oc, m) = dy[s][oc][p], m = s*P + p (output gradient of a conv, transposed)
-struct ConvDyT {
-  const float* __restrict__ dy; int OC, P;
-  __device__ float load(int oc, int m) const {
-    const int s = m / P, p = m - s * P;
-    return dy[((int64_t)s * OC + oc) * P + p];
-  }
-  __device__ float4 load4(int oc, int m) const {   // P % 4 == 0 only (conv1: 400)
-    const int s = m / P, p = m - s * P;
-    return *reinterpret_cast<const float4*>(dy + ((int64_t)s * OC + oc) * P + p);
-  }
-};
-
 // stride-1 transposed conv (conv3 backward): A(m, k) = dy[s][oc][y-ky][x-kx],
 // m = s*IH*IH + y*IH + x, k = oc*KS*KS + ky*KS + kx
 template <int OC, int OH, int KS, int IH>
@@ -127,28 +90,6 @@ struct ConvTW {
   }
 };
 
-// stride-2, 4x4 transposed conv (conv2 backward) for one output parity class
-// (py, px): y = 2 qy + py, x = 2 qx + px, qy, qx in [0, 10); k = oc*4 + jy*2 + jx
-// covers exactly the taps ky = py + 2 jy, kx = px + 2 jx that reach (y, x) from
-// oy = qy - jy, ox = qx - jx.
-struct ConvT2ClassA {
-  const float* __restrict__ dy; int py, px;
-  __device__ float load(int m, int k) const {
-    const int s = m / 100, q = m - s * 100, qy = q / 10, qx = q - qy * 10;
-    const int oc = k >> 2, jy = (k >> 1) & 1, jx = k & 1;
-    const int oy = qy - jy, ox = qx - jx;
-    if (oy < 0 || oy >= 9 || ox < 0 || ox >= 9) return 0.f;
-    return dy[((int64_t)s * NC2 + oc) * NP2 + oy * 9 + ox];
-  }
-};
-struct ConvT2ClassW {
-  const float* __restrict__ w; int py, px;
-  __device__ float load(int k, int ic) const {
-    const int oc = k >> 2, ky = py + 2 * ((k >> 1) & 1), kx = px + 2 * (k & 1);
-    return w[(((int64_t)oc * NC1 + ic) * 4 + ky) * 4 + kx];
-  }
-};
-
 // out[s][n][p] = mask > 0 ? v : 0  (ReLU backward into a conv activation layout)
 struct EpiConvMask {
   float* __restrict__ out; const float* __restrict__ mask; int OC, P;
@@ -158,15 +99,6 @@ struct EpiConvMask {
     out[i] = mask[i] > 0.f ? v : 0.f;
   }
 };
-struct EpiT2Class {
-  float* __restrict__ out; const float* __restrict__ mask; int py, px;
-  __device__ void store(int m, int ic, float v, int) const {
-    const int s = m / 100, q = m - s * 100, qy = q / 10, qx = q - qy * 10;
-    const int64_t i = ((int64_t)s * NC1 + ic) * NP1 + (2 * qy + py) * 20 + 2 * qx + px;
-    out[i] = mask[i] > 0.f ? v : 0.f;
-  }
-};
-
 #define ARL_TRY(x) do { hipError_t _e = (x); if (_e != hipSuccess) return _e; } while (0)
 
 struct NPlans {
@@ -266,8 +198,8 @@ hipError_t conv_bwd(Net& net, hipStream_t s) {
   ARL_TRY(launch_reduce_grad(slab, pl.c2_w, NC2, NC1 * 16 + 1, MapDense{G, net.o_c2W, net.o_c2b, -1, NC1 * 16}, s));
   for (int cls = 0; cls < 4; ++cls) {
     const int py = cls >> 1, px = cls & 1;
-    ARL_TRY((launch_gemm<64, 32, 32, 2, 2, GS, GS>(ConvT2ClassA{da2, py, px}, ConvT2ClassW{P + net.o_c2W, py, px},
-                                                   EpiT2Class{da1, a1, py, px}, S * 100, NC1, NC2 * 4, 1, s)));
+    ARL_TRY((launch_gemm<64, 32, 32, 2, 2, GS, GS>(ConvT2ClassA<NC2, NC1>{da2, py, px}, ConvT2ClassW<NC2, NC1>{P + net.o_c2W, py, px},
+                                                   EpiT2Class<NC1>{da1, a1, py, px}, S * 100, NC1, NC2 * 4, 1, s)));
   }
   // conv1: dW1 / db1 straight from the frame ring (the window's T steps)
   RingIm2col ring{net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl), n,

@@ -285,17 +285,19 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
               std::string& err) {
   const bool rgb = (arch & ARCH_RGB) != 0;
   const bool stk = (arch & ARCH_STACK) != 0;
-  arch &= ~(ARCH_RGB | ARCH_STACK);
-  if ((rgb || stk) && arch == ARCH_FF_NATURE) {
-    err = "ARCH_RGB / ARCH_STACK apply to the NIPS head (FF or LSTM) only";
+  const bool sts = (arch & ARCH_STATES) != 0;
+  arch &= ~(ARCH_RGB | ARCH_STACK | ARCH_STATES);
+  if ((rgb || stk || sts) && arch == ARCH_FF_NATURE) {
+    err = "ARCH_RGB / ARCH_STACK / ARCH_STATES apply to the NIPS head (FF or LSTM) only";
     return false;
   }
-  if (rgb && stk) { err = "ARCH_RGB and ARCH_STACK are exclusive"; return false; }
+  if ((int)rgb + (int)stk + (int)sts > 1) { err = "ARCH_RGB, ARCH_STACK and ARCH_STATES are exclusive"; return false; }
   net.rgb = rgb;
   net.stack = stk;
-  net.layout = rgb ? FRAMES_RGB : stk ? FRAMES_STACK : FRAMES_RING;
+  net.states = sts;
+  net.layout = rgb ? FRAMES_RGB : stk ? FRAMES_STACK : sts ? FRAMES_STATES : FRAMES_RING;
   if (arch != ARCH_FF && arch != ARCH_LSTM && arch != ARCH_FF_NATURE) {
-    err = "arch must be 0 (FF), 1 (LSTM) or 2 (FF, Nature head), optionally | 16 (RGB) or | 32 (STACK)";
+    err = "arch must be 0 (FF), 1 (LSTM) or 2 (FF, Nature head), optionally | 16 (RGB), | 32 (STACK) or | 64 (STATES)";
     return false;
   }
   if (n_actions < 1 || n_actions > MAXA) { err = "n_actions must be in [1, 32]"; return false; }
@@ -362,6 +364,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   slab = std::max(slab, conv_bwd_slab_floats((int)S));
   if (arch == ARCH_LSTM) slab = std::max(slab, (int64_t)BPTT_SPLIT * HID * n);
   if (NAT) slab = nature_slab_floats(net);
+  if (sts) slab = std::max(slab, states_slab_floats(net));
   net.slab_floats = slab;
   net.bufs.clear();
   int64_t wo = 0;
@@ -373,7 +376,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   };
   const bool L = arch == ARCH_LSTM;
   net.w_ctl = buf("ctl", CTL_SIZE * 8);
-  net.w_frames = buf("frames", (int64_t)net.R * n * PLANE * (rgb ? 3 : stk ? 4 : 1));
+  net.w_frames = buf("frames", (int64_t)net.R * n * PLANE * (rgb ? 3 : stk ? 4 : sts ? 16 : 1));
   net.w_nvalid = buf("nvalid", (int64_t)net.R * n);
   net.w_reset = buf("reset", T1 * n);
   net.w_rewards = buf("rewards", S * 4);
@@ -401,7 +404,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   net.w_dhn = buf("dhn", L ? n * HID * 4 : 0);
   net.w_dcn = buf("dcn", L ? n * HID * 4 : 0);
   net.w_da2 = buf("da2", S * nA2 * 4);
-  net.w_da1 = buf("da1", NAT ? S * NA1 * 4 : 0);
+  net.w_da1 = buf("da1", NAT ? S * NA1 * 4 : sts ? S * A1 * 4 : 0);
   net.w_da3 = buf("da3", NAT ? S * NA3 * 4 : 0);
   net.w_slab = buf("slab", slab * 4);
   if (!NAT) {   // per-job weight-gradient slabs of the NIPS learner
@@ -468,6 +471,9 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne, con
     if (net.layout != FRAMES_RING || (part & ACT_AFTER_CONV) || obs->e0 != e0 || obs->ne != ne)
       return hipErrorInvalidValue;
     ARL_TRY(launch_phi_conv_fwd(*obs, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W, P + net.o_c2b, a1, a2, s));
+  } else if (!(part & ACT_AFTER_CONV) && net.states) {
+    if (e0 != 0 || ne != n) return hipErrorInvalidValue;   // one launch over all envs
+    ARL_TRY(states_conv_fwd(net, t, a1, a2, s));
   } else if (!(part & ACT_AFTER_CONV))
     ARL_TRY(launch_conv_fwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
                             net.at<int64_t>(net.w_ctl), n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W,
@@ -587,6 +593,11 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
   for (int part = 0; part < LEARN_CONV; ++part) ARL_TRY(net_learn_part(net, part, gamma, beta, vcoef, clip_reward, s));
   // the conv part last; with norm_fold its slab reduce also leaves the clip norm's partials
   // (every other gradient tensor is final by now: one stream)
+  if (net.states) {   // the generic-GEMM conv backward has no folded norm: the update runs grad_sqnorm
+    ARL_TRY(states_conv_bwd(net, s));
+    net.norm_ready = false;
+    return hipSuccess;
+  }
   const NormFold nf = norm_fold_args(net);
   ARL_TRY(launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl),
                           net.N, net.R, net.T * net.N, net.at<float>(net.w_a1), net.at<float>(net.w_da2),
@@ -656,6 +667,7 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
   const float* a2 = net.at<float>(net.w_a2);
   const float* a1 = net.at<float>(net.w_a1);
   float* da2 = net.at<float>(net.w_da2);
+  if (part == LEARN_CONV && net.states) return states_conv_bwd(net, s);
   if (part == LEARN_CONV)
     // fused conv backward per sample (conv_bwd.hip): conv2 dW/db,
     // da1 = conv_transpose(da2, W2) * (a1 > 0) kept in LDS, conv1 dW/db
@@ -732,6 +744,11 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
   float* slab = net.at<float>(net.w_slab);
   float* a2 = net.at<float>(net.w_a2);
   float* hfc = net.at<float>(net.w_hfc);
+  if (net.states && (stage == STAGE_CONV_FWD || stage == STAGE_CONV_BWD || stage == STAGE_CONV_REDUCE)) {
+    if (stage == STAGE_CONV_FWD)
+      return states_conv_fwd(net, t, net.at<float>(net.w_a1) + (int64_t)t * n * A1, a2 + (int64_t)t * n * A2, s);
+    return stage == STAGE_CONV_BWD ? states_conv_bwd(net, s) : hipSuccess;   // (no separate slab reduce)
+  }
   switch (stage) {
     case STAGE_CONV_FWD:
       return launch_conv_fwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),

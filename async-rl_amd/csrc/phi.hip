@@ -265,7 +265,7 @@ rgb_ring_kernel(RingArgs a) {
 
 // In-loop ring for ARCH_STACK nets: the env's whole 4-screen stack of obs step
 // k (ale.py:91-94 ALE.state, oldest first) goes to slot k % R (frames (R, n,
-// 4, 84, 84)); nvalid = 4; the reward / done / reset bookkeeping of
+// 4, 84, 84)); ARCH_STATES nets: the same with phi's f32 state (esize 4); nvalid = 4; the reward / done / reset bookkeeping of
 // phi_ring_kernel.  pair_pool == null: bookkeeping only (a terminal
 // observation, whose state a3c.py:72-73 never reads).  One workgroup per env,
 // 16-byte copies.
@@ -276,9 +276,10 @@ stack_ring_kernel(RingArgs a) {
   const int slot = (int)(k % a.R);
   const int64_t pidx = k % a.pool_len;
   if (a.pair_pool != nullptr) {
-    constexpr int V = 4 * PLANE / 16;   // 1764 uint4 per stack
-    const uint4* src = reinterpret_cast<const uint4*>(a.pair_pool + (pidx * a.n + e) * (int64_t)(4 * PLANE));
-    uint4* dst = reinterpret_cast<uint4*>(a.frames + ((int64_t)slot * a.n + e) * (4 * PLANE));
+    const int64_t sb = (int64_t)4 * PLANE * a.esize;   // bytes per stack (uint8 screens / f32 states)
+    const int V = (int)(sb / 16);                       // 1764 / 7056 uint4
+    const uint4* src = reinterpret_cast<const uint4*>(a.pair_pool + (pidx * a.n + e) * sb);
+    uint4* dst = reinterpret_cast<uint4*>(a.frames + ((int64_t)slot * a.n + e) * sb);
     for (int i = threadIdx.x; i < V; i += 256) dst[i] = src[i];
   }
   if (threadIdx.x == 0) {

@@ -37,6 +37,9 @@ extern "C" {
 #define ARL_ARCH_STACK 32 /* flag for FF / LSTM: observations are whole 4-screen stacks (ale.py:91-94
                              ALE.state, as A3C.act receives them, a3c.py:67,72-73), one per ring
                              slot; they come through arl_observe_stack */
+#define ARL_ARCH_STATES 64 /* flag for FF / LSTM: observations are float32 (4, 84, 84) states -- the
+                              output of A3C's phi plugin (a3c.py:34,50,73; identity by default) --
+                              one per ring slot; they come through arl_observe_states */
 
 #define ARL_RESIZE_SCALAR 0  /* OpenCV FixedPtCast vertical pass (canonical) */
 #define ARL_RESIZE_SIMD 1    /* OpenCV VResizeLinearVec_32s8u (mulhi) pass */
@@ -129,6 +132,13 @@ int arl_observe_rgb(arl_net* net, int t, const uint8_t* img_pool, int H, int W, 
  * feeds to the model (a3c.py:72-73, 165-167). */
 int arl_observe_stack(arl_net* net, int t, const uint8_t* stack_pool, const float* reward_pool,
                       const uint8_t* done_pool, int64_t pool_len, int force_reset, void* stream);
+
+/* arl_observe for an ARL_ARCH_STATES net: state_pool (pool_len, n, 4, 84, 84)
+ * f32 (16-byte aligned), the conv input as phi returns it (a3c.py:73
+ * np.expand_dims(self.phi(state), 0)); NULL (t >= 1): reward / done only, as
+ * arl_observe_stack. */
+int arl_observe_states(arl_net* net, int t, const float* state_pool, const float* reward_pool,
+                       const uint8_t* done_pool, int64_t pool_len, int force_reset, void* stream);
 
 /* The reference's early window end (a3c.py:77-78: an update at a terminal
  * after t_len < t_max steps): window steps [t_len, t_max) carry no loss and

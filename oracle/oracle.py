@@ -837,12 +837,13 @@ class A3CAgent:
     self.calls / self.updates."""
 
     def __init__(self, params, arch, n_actions, t_max=5, gamma=0.99, beta=0.01, pi_loss_coef=1.0,
-                 v_loss_coef=0.5, keep_loss_scale_same=False, clip=40.0, seed=0, clip_reward=True):
+                 v_loss_coef=0.5, keep_loss_scale_same=False, clip=40.0, seed=0, clip_reward=True, phi=None):
         self.p = {k: np.asarray(v, np.float32).copy() for k, v in params.items()}
         self.ms = {k: np.zeros_like(v) for k, v in self.p.items()}
         self.arch, self.A, self.T = arch, n_actions, t_max
         self.gamma, self.beta, self.clip, self.seed = gamma, beta, clip, seed
         self.clip_reward = clip_reward
+        self.phi = phi                    # None: dqn_phi (a3c_ale.py:220); else the model sees phi(state)
         self.loss_kw = dict(pi_loss_coef=pi_loss_coef, keep_loss_scale_same=keep_loss_scale_same, t_max=t_max)
         self.v_loss_coef = v_loss_coef
         self.t = self.t_start = 0
@@ -873,7 +874,12 @@ class A3CAgent:
         T = self.T
         if self.clip_reward:
             reward = float(np.clip(reward, -1, 1))            # a3c.py:69-70
-        x = None if terminal else PHI_LUT[np.asarray(screens, np.uint8)][None]
+        if terminal:
+            x = None
+        elif self.phi is None:
+            x = PHI_LUT[np.asarray(screens, np.uint8)][None]
+        else:
+            x = np.asarray(self.phi(screens), np.float32)[None]   # a3c.py:73
         self.rewards[self.t - 1] = reward                     # a3c.py:75
         if (terminal and self.t_start < self.t) or self.t - self.t_start == T:
             self._update(x, terminal, lr)

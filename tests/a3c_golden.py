@@ -14,7 +14,17 @@ import numpy as np
 import oracle as O
 
 PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "a3c_update_golden.npz")
-VARIANTS = ("ff", "ff_opts", "lstm", "lstm_opts")
+VARIANTS = ("ff", "ff_opts", "lstm", "lstm_opts", "ff_phi", "lstm_phi")
+
+
+def norm_phi(screens):
+    """The *_phi variants' phi (a3c.py:34,50,73 plugin point): the 4 uint8
+    screens to float32 in [-1, 1] -- not dqn_phi's image of them.  The
+    generator hands this very function to the reference's a3c.A3C."""
+    x = np.asarray(screens, dtype=np.float32)
+    x /= np.float32(127.5)
+    x -= np.float32(1.0)
+    return x
 
 
 class Variant:
@@ -22,6 +32,8 @@ class Variant:
         pre = name + "|"
         self.name = name
         self.arch_name = str(z[pre + "arch"])
+        self.phi_name = str(z[pre + "phi"]) if pre + "phi" in z.files else "dqn"
+        self.phi = None if self.phi_name == "dqn" else norm_phi
         self.arch = O.ARCH_FF if self.arch_name == "ff" else O.ARCH_LSTM
         (self.pi_loss_coef, self.v_loss_coef, keep, self.clip, self.beta, self.gamma, T, seed, A,
          init_seed) = z[pre + "kw"]

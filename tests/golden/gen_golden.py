@@ -275,11 +275,16 @@ def gen_rmsprop():
 # reference's ALE wrapper on the scripted fake emulator.
 # --------------------------------------------------------------------------
 A3C_VARIANTS = {
-    # name: (arch, kwargs of a3c.A3C, GradientClipping threshold, beta, n act calls)
-    "ff": ("ff", dict(pi_loss_coef=1.0, v_loss_coef=0.5, keep_loss_scale_same=False), 40.0, 1e-2, 44),
-    "ff_opts": ("ff", dict(pi_loss_coef=0.5, v_loss_coef=1.0, keep_loss_scale_same=True), 0.05, 5e-2, 44),
-    "lstm": ("lstm", dict(pi_loss_coef=1.0, v_loss_coef=0.5, keep_loss_scale_same=False), 40.0, 1e-2, 44),
-    "lstm_opts": ("lstm", dict(pi_loss_coef=0.5, v_loss_coef=0.5, keep_loss_scale_same=True), 0.05, 1e-2, 44),
+    # name: (arch, kwargs of a3c.A3C, GradientClipping threshold, beta, n act calls, phi)
+    # phi: "dqn" = the reference's dqn_phi (a3c_ale.py:220), "norm" = tests/a3c_golden.norm_phi,
+    # a user phi through the plugin point (a3c.py:34,50,73) that is not dqn_phi's image
+    "ff": ("ff", dict(pi_loss_coef=1.0, v_loss_coef=0.5, keep_loss_scale_same=False), 40.0, 1e-2, 44, "dqn"),
+    "ff_opts": ("ff", dict(pi_loss_coef=0.5, v_loss_coef=1.0, keep_loss_scale_same=True), 0.05, 5e-2, 44, "dqn"),
+    "lstm": ("lstm", dict(pi_loss_coef=1.0, v_loss_coef=0.5, keep_loss_scale_same=False), 40.0, 1e-2, 44, "dqn"),
+    "lstm_opts": ("lstm", dict(pi_loss_coef=0.5, v_loss_coef=0.5, keep_loss_scale_same=True), 0.05, 1e-2, 44, "dqn"),
+    "ff_phi": ("ff", dict(pi_loss_coef=1.0, v_loss_coef=0.5, keep_loss_scale_same=False), 40.0, 1e-2, 44, "norm"),
+    "lstm_phi": ("lstm", dict(pi_loss_coef=1.0, v_loss_coef=0.5, keep_loss_scale_same=False), 0.02, 1e-2, 44,
+                 "norm"),
 }
 A3C_T, A3C_GAMMA, A3C_SEED, A3C_LR, A3C_STEPS = 5, 0.99, 1234, 7e-4, 10 ** 4
 A3C_INIT_SEED = 21     # oracle.init_like_torch(arch, A, default_rng(A3C_INIT_SEED)) = theta0
@@ -330,7 +335,8 @@ def gen_a3c():
             self.recs.append((rec.msg, rec.args))
 
     out = {}
-    for vname, (arch, kw, clip, beta, K) in A3C_VARIANTS.items():
+    from a3c_golden import norm_phi                                  # tests/a3c_golden.py
+    for vname, (arch, kw, clip, beta, K, phi_name) in A3C_VARIANTS.items():
         np.random.seed(17)
         env = ale.ALE("fake.rom", seed=3, max_start_nullops=4)       # reference ALE on the fake emulator
         n_actions = env.number_of_actions
@@ -346,7 +352,8 @@ def gen_a3c():
         opt = rmsprop_async.RMSpropAsync(lr=A3C_LR, eps=1e-1, alpha=0.99)
         opt.setup(model)
         opt.add_hook(chainer.optimizer.GradientClipping(clip))
-        agent = a3c.A3C(model, opt, A3C_T, A3C_GAMMA, beta=beta, process_idx=0, phi=dqn_phi, **kw)
+        phi = dqn_phi if phi_name == "dqn" else norm_phi
+        agent = a3c.A3C(model, opt, A3C_T, A3C_GAMMA, beta=beta, process_idx=0, phi=phi, **kw)
         names = [n.lstrip("/") for n, _ in model.namedparams()]
         theta0 = {n.lstrip("/"): p.data.copy() for n, p in model.namedparams()}
 
@@ -430,6 +437,7 @@ def gen_a3c():
         assert U == len(Rs) == len(norms) and U >= 6, (U, len(Rs), len(norms))
         pref = vname + "|"
         out[pref + "arch"] = np.array(arch)
+        out[pref + "phi"] = np.array(phi_name)
         out[pref + "names"] = np.array(names)
         out[pref + "kw"] = np.array([kw["pi_loss_coef"], kw["v_loss_coef"], float(kw["keep_loss_scale_same"]),
                                      clip, beta, A3C_GAMMA, A3C_T, A3C_SEED, n_actions, A3C_INIT_SEED])

@@ -11,7 +11,7 @@ import socket
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for p in (os.path.join(ROOT, "async-rl_amd"), os.path.join(ROOT, "tests")):
+for p in (os.path.join(ROOT, "async-rl_amd"), os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")):
     sys.path.insert(0, p)
 
 import numpy as np  # noqa: E402

@@ -81,3 +81,25 @@ class OracleRgbView(OracleEnvView):
 
     def states_f32(self, k0, T):
         return np.stack([self.state(k0 + t) for t in range(T)]), self.state(k0 + T)
+
+
+def make_state_pools(rng, pool_len, n, p_done=0.15):
+    """ARCH_STATES pools: float32 (pool_len, n, 4, 84, 84) states as a user
+    phi might return them (signed, not an image of uint8 screens); rewards
+    and dones as make_pools."""
+    states = rng.standard_normal((pool_len, n, 4, 84, 84)).astype(np.float32)
+    rewards = rng.choice(np.array([-2.0, -1.0, 0.0, 0.0, 0.0, 1.0, 3.5], np.float32), (pool_len, n))
+    dones = (rng.random((pool_len, n)) < p_done).astype(np.uint8)
+    return states, rewards.astype(np.float32), dones
+
+
+class OracleStatesView(OracleEnvView):
+    """States of an ARCH_STATES net: the pool entry itself (no phi, no stack)."""
+
+    def __init__(self, states, dones):
+        self.states, self.dones = states, dones
+        self.pool_len, self.n = states.shape[0], states.shape[1]
+
+    def states_f32(self, k0, T):
+        P = self.pool_len
+        return np.stack([self.states[(k0 + t) % P] for t in range(T)]), self.states[(k0 + T) % P]

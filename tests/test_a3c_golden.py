@@ -39,7 +39,7 @@ def test_fixture_covers_the_update_paths():
 def test_oracle_agent_replays_reference(name):
     v = load(name)
     ag = O.A3CAgent(v.theta0(), v.arch, v.A, v.T, v.gamma, v.beta, v.pi_loss_coef, v.v_loss_coef, v.keep,
-                    v.clip, v.seed)
+                    v.clip, v.seed, phi=v.phi)
     for k in range(v.n_calls):
         a = ag.act(v.states[k], v.rewards[k], bool(v.terminals[k]), float(v.lr[k]))
         assert (-1 if a is None else a) == v.actions[k], (name, k)

@@ -102,11 +102,11 @@ def test_env_group_split():
     from asyncrl_amd.net import DeviceNet
     for n in (1, 31, 32, 96, 100, 256, 1024):
         for g in (1, 2, 3, 4):
-            rs = DeviceNet.env_groups(SimpleNamespace(n_envs=n, arch=ARCH_FF), g)
+            rs = DeviceNet.env_groups(SimpleNamespace(n_envs=n, arch=ARCH_FF, states=False), g)
             assert rs[0][0] == 0 and sum(ne for _, ne in rs) == n and len(rs) <= g
             assert all(e0 % ENV_GROUP_ALIGN == 0 and ne > 0 for e0, ne in rs)
             assert all(rs[i][0] + rs[i][1] == rs[i + 1][0] for i in range(len(rs) - 1))
-    assert DeviceNet.env_groups(SimpleNamespace(n_envs=256, arch=ARCH_FF), 2) == [(0, 128), (128, 128)]
+    assert DeviceNet.env_groups(SimpleNamespace(n_envs=256, arch=ARCH_FF, states=False), 2) == [(0, 128), (128, 128)]
     assert DeviceNet.env_groups(SimpleNamespace(n_envs=256, arch=ARCH_FF_NATURE), 2) == [(0, 256)]
 
 

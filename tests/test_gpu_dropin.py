@@ -29,8 +29,11 @@ def _agent(v, gpu):
     opt = RMSpropAsync(lr=7e-4, eps=1e-1, alpha=0.99)
     opt.setup(model)
     opt.add_hook(GradientClipping(v.clip))
-    agent = A3C(model, opt, v.T, v.gamma, beta=v.beta, process_idx=0, phi=dqn_phi, pi_loss_coef=v.pi_loss_coef,
+    # dqn_phi variants: the uint8 stack ring; the *_phi variants' user phi: the f32 state ring
+    phi = dqn_phi if v.phi is None else v.phi
+    agent = A3C(model, opt, v.T, v.gamma, beta=v.beta, process_idx=0, phi=phi, pi_loss_coef=v.pi_loss_coef,
                 v_loss_coef=v.v_loss_coef, keep_loss_scale_same=v.keep)
+    assert model.frames == ("stacks" if v.phi is None else "states")
     return agent, model, opt
 
 
@@ -70,10 +73,12 @@ def test_dropin_act_matches_reference_trajectory(gpu, name):
 
 @pytest.mark.gpu
 def test_dropin_phi_plugin(gpu):
-    """The phi plugin (a3c.py:34,50,73): a custom phi returning dqn_phi's
-    float32 image drives the same actions as phi=dqn_phi; a phi whose output
-    is not an image of uint8 screens is refused loudly."""
-    from asyncrl_amd import A3C, A3CFF, RMSpropAsync
+    """The phi plugin (a3c.py:34,50,73): a user phi equal to dqn_phi's
+    arithmetic runs on the f32 state ring and reproduces the reference's
+    dqn_phi trajectory (actions, probabilities, first update's gradient); the
+    default identity phi takes float32 states as they are; a phi whose output
+    Chainer's Convolution2D would not take (uint8, float64) is refused."""
+    from asyncrl_amd import A3C, A3CFF, GradientClipping, RMSpropAsync
     v = load("ff")
 
     def my_phi(screens):   # a user's phi, as in the reference (np.float32 / 255)
@@ -82,12 +87,30 @@ def test_dropin_phi_plugin(gpu):
     model = A3CFF(v.A, t_max=v.T, seed=v.seed, init_seed=None, device=gpu)
     model.net.load_params(v.theta0())
     opt = RMSpropAsync(lr=7e-4, eps=1e-1, alpha=0.99).setup(model)
+    opt.add_hook(GradientClipping(v.clip))
     agent = A3C(model, opt, v.T, v.gamma, beta=v.beta, phi=my_phi)
-    for k in range(12):
+    assert model.frames == "states" and model.net.states
+    u0 = int(v.update_calls[0])
+    for k in range(u0 + 1):
         opt.lr = float(v.lr[k])
         a = agent.act(list(v.states[k]), float(v.rewards[k]), bool(v.terminals[k]))
-        assert (-1 if a is None else a) == v.actions[k]
-    bad = A3C(A3CFF(v.A, t_max=v.T, device=gpu), RMSpropAsync(), v.T, v.gamma, phi=lambda s: my_phi(s) * 0.5 + 1e-3)
+        assert (-1 if a is None else a) == v.actions[k], k
+        if a is not None:
+            o = model.net.step_outputs(agent.t - 1 - agent.t_start)
+            assert rel(o["probs"].cpu().numpy()[0], v.probs[k]) < RTOL, k
+    torch.cuda.synchronize()
+    g = model.net.state_dict(model.net.grads)
+    for n in v.names:
+        ok, err = close_normscaled(v.pick(n, g[n]), v.grad[n][0], RTOL)
+        assert ok, (n, err)
+    # identity phi (the reference's default): float32 states go in as they are
+    ident = A3C(A3CFF(v.A, t_max=v.T, device=gpu), RMSpropAsync(), v.T, v.gamma)
+    assert ident.model.frames == "states"
+    assert isinstance(ident.act(my_phi(list(v.states[0])), 0.0, False), int)
+    with pytest.raises(ValueError):
+        ident.act(np.asarray(v.states[1]), 0.0, False)                 # uint8: not a model input
+    bad = A3C(A3CFF(v.A, t_max=v.T, device=gpu), RMSpropAsync(), v.T, v.gamma,
+              phi=lambda s: my_phi(s).astype(np.float64))
     with pytest.raises(ValueError):
         bad.act(list(v.states[0]), 0.0, False)
 

@@ -12,7 +12,7 @@ import torch
 
 import oracle as O
 from conftest import close_normscaled, golden, grads_match, load_checkpoint
-from sim import OracleEnvView, OracleRgbView, make_pools, make_rgb_pools
+from sim import OracleEnvView, OracleRgbView, OracleStatesView, make_pools, make_rgb_pools, make_state_pools
 
 pytestmark = pytest.mark.gpu
 
@@ -257,13 +257,15 @@ def _run_ff(gpu, N, T, A, seed, kind, windows=2, ckpt=False, arch=O.ARCH_FF, p_d
     rng = np.random.default_rng(seed)
     P = 2 * T + 1
     rgb = bool(arch & O.ARCH_RGB)
-    if rgb:
+    if kind == "states":
+        pairs, rewards, dones = make_state_pools(rng, P, N, p_done=0.15 if p_done is None else p_done)
+    elif rgb:
         pairs, rewards, dones = make_rgb_pools(rng, P, N, *hw, p_done=0.15 if p_done is None else p_done)
     else:
         pairs, rewards, dones = make_pools(rng, P, N, kind) if p_done is None else \
             make_pools(rng, P, N, kind, p_done=p_done)
     Model = A3CFFNature if arch == O.ARCH_FF_NATURE else (DoomA3CFF if rgb else A3CFF)
-    model = Model(A, n_envs=N, t_max=T, seed=99, init_seed=seed, frames="pairs")
+    model = Model(A, n_envs=N, t_max=T, seed=99, init_seed=seed, frames="states" if kind == "states" else "pairs")
     if ckpt:
         model.net.load_params(load_checkpoint())
     opt = RMSpropAsync(lr=7e-4, eps=1e-1, alpha=0.99)
@@ -271,7 +273,8 @@ def _run_ff(gpu, N, T, A, seed, kind, windows=2, ckpt=False, arch=O.ARCH_FF, p_d
     opt.add_hook(GradientClipping(40))
     agent = A3C(model, opt, T, 0.99, beta=1e-2)
     net = model.net
-    view = OracleRgbView(pairs, dones) if rgb else OracleEnvView(pairs, dones)
+    view = OracleStatesView(pairs, dones) if kind == "states" else \
+        OracleRgbView(pairs, dones) if rgb else OracleEnvView(pairs, dones)
     dp, dr, dd = dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu)
     for w in range(windows):
         k0 = w * T
@@ -317,6 +320,13 @@ def test_ff_windows_match_oracle(gpu):
 
 def test_ff_windows_real_checkpoint_palette_frames(gpu):
     _run_ff(gpu, N=5, T=5, A=4, seed=22, kind="palette", ckpt=True)
+
+
+def test_ff_states_windows_match_oracle(gpu):
+    """ARCH_STATES (the phi plugin's f32 state ring, generic-GEMM convs):
+    signed float states that are no image of uint8 screens, 9 envs (ragged
+    against the 64-row conv tiles), two windows with terminals."""
+    _run_ff(gpu, N=9, T=5, A=4, seed=28, kind="states")
 
 
 def test_ff_wide_action_set(gpu):
@@ -437,7 +447,8 @@ def test_lstm_windows_match_oracle(gpu, rgb, N, T, A):
     opt.add_hook(GradientClipping(40))
     agent = A3C(model, opt, T, 0.99)
     net = model.net
-    view = OracleRgbView(pairs, dones) if rgb else OracleEnvView(pairs, dones)
+    view = OracleStatesView(pairs, dones) if kind == "states" else \
+        OracleRgbView(pairs, dones) if rgb else OracleEnvView(pairs, dones)
     dp, dr, dd = dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu)
     st = O.LSTMState(h=np.zeros((N, 256), np.float32), c=np.zeros((N, 256), np.float32),
                      has=np.zeros(N, bool))
