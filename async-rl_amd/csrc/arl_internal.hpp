@@ -172,6 +172,11 @@ hipError_t states_conv_fwd(const Net& net, int t, float* a1, float* a2, hipStrea
 hipError_t states_conv_bwd(Net& net, hipStream_t s);
 int64_t states_slab_floats(const Net& net);
 
+// LSTM gate GEMM + bias (+ the F.lstm cell when cell) for rows [0, n) (lstm.hip)
+hipError_t launch_lstm_gates(const float* x, const float* h, const uint8_t* reset, const float* Wu, const float* Wl,
+                             const float* b, float* gates, const float* c_prev, float* c_out, float* h_out, int n,
+                             bool cell, hipStream_t s);
+
 // shared pieces of the heads' backward (net.hip)
 hipError_t launch_heads_bwd(const float* dl, const float* dv, const float* Wpi, const float* Wv, int A, int H,
                             const float* mask, float* out, int64_t S, hipStream_t s);

@@ -1,0 +1,173 @@
+// The LSTM's gate GEMM with the cell in its epilogue (a3c_ale.py:50-51,62:
+// L.LSTM(256, 256) = upward Linear(256, 1024) + lateral Linear(256, 1024, no
+// bias) -> Chainer 1.8.1 F.lstm; one launch per lockstep step):
+//
+//   gates[m][j] = x[m] . Wu[j] + (reset[m] ? 0 : h[m] . Wl[j]) + b[j]
+//   (a, i, f, o) = gates[m][4u .. 4u + 3]          (interleaved, reshape(n, 256, 4))
+//   c' = tanh(a) sig(i) + sig(f) c,   h' = sig(o) tanh(c')
+//
+// M = n envs, N = 1024 gate columns, K = 512 = [x | h].  Shaped like fc.hip
+// (latency-bound at these sizes: one short chain per workgroup):
+//   * 32 x 64 output tile (16 units x 4 gates) per 512-thread workgroup, 8
+//     waves with one 16 x 16 sub-tile each (exact f32 v_mfma_f32_16x16x4_f32);
+//   * the 96 operand rows (32 of [x | h], 64 of [Wu | Wl]) are staged by
+//     LDS-DMA in four 128-column K chunks through three LDS stages (row stride
+//     33 float4: the 16 rows a ds_read_b128 touches land on distinct bank
+//     quads); chunks 0-2 are issued at once, chunk 3 as soon as stage 0 is free;
+//   * the x and h halves accumulate separately, so a reset row (h = None after
+//     an episode end, a3c.py:166 / a3c_ale.py:65-66) drops the h half at the
+//     epilogue instead of zero-filling staged rows;
+//   * epilogue: the tile through LDS (row stride 68 floats: the four lane
+//     quarters' rows on distinct banks), one (row, unit) per thread: bias, the
+//     gates written for the backward, and the cell -- the arithmetic of
+//     lstm_cell_fwd_kernel (net.hip), op for op.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "arl_internal.hpp"
+
+namespace arl {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+constexpr int LBM = 32, LBN = 64, LT = 512, LW = LT / 64;
+constexpr int LKC = 128;                       // K chunk (columns)
+constexpr int LROWS = LBM + LBN;               // 96 staged rows
+constexpr int LLD = LKC / 4 + 1;               // 33 float4 per staged row (32 used)
+constexpr int LPIECES = (LROWS * LLD + 63) / 64;   // 50 LDS-DMA pieces (64 x 16 B) per chunk
+constexpr int LSTAGE4 = LPIECES * 64;          // float4 per stage (incl. the last piece's overhang)
+constexpr int LSTAGES = 3;
+constexpr int TLD = 68;                        // epilogue tile row stride (floats)
+static_assert(LBM * TLD <= LSTAGE4 * 4, "epilogue tile fits one stage");
+static_assert(GATES % LBN == 0 && LBM * (LBN / 4) == LT, "one (row, unit) per thread");
+// pieces of wave w per chunk (piece it -> wave it % LW): 7 for waves 0, 1, else 6
+__host__ __device__ constexpr int wave_pieces(int w) { return (LPIECES - w + LW - 1) / LW; }
+}  // namespace
+
+__device__ inline void lstm_wait_vm(int n) {   // s_waitcnt vmcnt(n), n wave-uniform
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// LDS-only workgroup barrier (keeps the other chunks' LDS-DMA in flight; see conv_bwd.hip)
+__device__ inline void lstm_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ inline float lstm_sigm(float x) { return __fdiv_rn(1.f, __fadd_rn(1.f, expf(-x))); }
+
+struct LstmGatesArgs {
+  const float* x;        // (n, 256) the upward input (the FC output)
+  const float* h;        // (n, 256) h_prev (ignored on reset rows)
+  const uint8_t* reset;  // (n) 1 = the state is None
+  const float* Wu;       // (1024, 256)
+  const float* Wl;       // (1024, 256)
+  const float* b;        // (1024)
+  float* gates;          // (n, 1024) pre-activations (+ bias), kept for the backward
+  const float* c_prev;   // (n, 256)
+  float* c_out;          // (n, 256) (cell == 0: untouched)
+  float* h_out;          // (n, 256)
+  int n, cell;
+};
+
+__global__ void __launch_bounds__(LT)
+lstm_gates_kernel(LstmGatesArgs a) {
+  __shared__ __attribute__((aligned(16))) float S[LSTAGES * LSTAGE4 * 4];   // 153,600 B
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NTN = GATES / LBN;
+  const int m0 = (blockIdx.x / NTN) * LBM, n0 = (blockIdx.x % NTN) * LBN;
+  const int pw = wave_pieces(wave);
+
+  // ---- staging: chunk c into stage c % 3; slot i -> row i / LLD, float4
+  // column min(i % LLD, 31) (the pad slot re-loads the row's last float4)
+  auto issue = [&](int c) {
+    float* st = S + 4 * LSTAGE4 * (c % LSTAGES);
+    const int kc = (c & 1) * LKC;
+    const float* xa = c < 2 ? a.x : a.h;
+    const float* wb = c < 2 ? a.Wu : a.Wl;
+    for (int it = wave; it < LPIECES; it += LW) {
+      const int i = min(it * 64 + lane, LROWS * LLD - 1);
+      const int r = i / LLD, cc = min(i - r * LLD, LKC / 4 - 1);
+      const float* src = r < LBM ? xa + (int64_t)min(m0 + r, a.n - 1) * HID   // rows past n: any valid row
+                                 : wb + (int64_t)(n0 + r - LBM) * HID;
+      __builtin_amdgcn_global_load_lds(src + kc + 4 * cc, (__attribute__((address_space(3))) void*)(st + 4 * it * 64),
+                                       16, 0, 0);
+    }
+  };
+  const int q = lane >> 4, col = lane & 15;
+  const int ms = wave & 1, ns = wave >> 1;
+  // reset flags of this lane's four C rows, issued first (the oldest loads, so
+  // the counted waits below cover them with chunk 0)
+  uint8_t rs[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) rs[r] = a.reset[min(m0 + ms * 16 + q * 4 + r, a.n - 1)];
+  issue(0);
+  issue(1);
+  issue(2);
+
+  f32x4 accx = {0.f, 0.f, 0.f, 0.f}, acch = accx;
+  auto compute = [&](int c, f32x4& acc) {
+    const float* st = S + 4 * LSTAGE4 * (c % LSTAGES);
+    const float* Ar = st + (ms * 16 + col) * 4 * LLD + 4 * q;
+    const float* Br = st + (LBM + ns * 16 + col) * 4 * LLD + 4 * q;
+#pragma unroll
+    for (int s = 0; s < LKC / 16; ++s) {   // lane quarter q holds k = 16 s + 4 q + r of the chunk
+      const f32x4 av = *reinterpret_cast<const f32x4*>(Ar + 16 * s);
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(Br + 16 * s);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], bv[r], acc, 0, 0, 0);
+    }
+  };
+  // outstanding per wave after issuing chunks 0..2: 3 pw
+  lstm_wait_vm(2 * pw);       // chunk 0 landed (1, 2 in flight)
+  lstm_lds_barrier();
+  compute(0, accx);
+  lstm_wait_vm(pw);           // chunk 1 landed (2 in flight)
+  lstm_lds_barrier();         // also: everyone is done with stage 0
+  issue(3);                   // -> stage 0
+  compute(1, accx);
+  lstm_wait_vm(pw);           // chunk 2 landed (3 in flight)
+  lstm_lds_barrier();
+  compute(2, acch);
+  lstm_wait_vm(0);            // chunk 3 landed
+  lstm_lds_barrier();
+  compute(3, acch);
+
+  // ---- epilogue tile into stage 1 (free since the barrier before chunk 2):
+  // C row q*4 + r, column col of sub-tile (ms, ns)
+  float* T = S + 4 * LSTAGE4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    T[(ms * 16 + q * 4 + r) * TLD + ns * 16 + col] = rs[r] ? accx[r] : __fadd_rn(accx[r], acch[r]);
+  lstm_lds_barrier();
+  const int row = tid >> 4, u = tid & 15, m = m0 + row, n = n0 + 4 * u;
+  if (m >= a.n) return;
+  const float4 bb = *reinterpret_cast<const float4*>(a.b + n);
+  const float4 v = *reinterpret_cast<const float4*>(T + row * TLD + 4 * u);
+  const float4 g = make_float4(__fadd_rn(v.x, bb.x), __fadd_rn(v.y, bb.y), __fadd_rn(v.z, bb.z), __fadd_rn(v.w, bb.w));
+  *reinterpret_cast<float4*>(a.gates + (int64_t)m * GATES + n) = g;
+  if (!a.cell) return;
+  const int64_t i = (int64_t)m * HID + (n >> 2);
+  const float ag = tanhf(g.x), ig = lstm_sigm(g.y), fg = lstm_sigm(g.z), og = lstm_sigm(g.w);
+  const float cp = a.reset[m] ? 0.f : a.c_prev[i];
+  const float c = __fadd_rn(__fmul_rn(ag, ig), __fmul_rn(fg, cp));
+  a.c_out[i] = c;
+  a.h_out[i] = __fmul_rn(og, tanhf(c));
+}
+
+hipError_t launch_lstm_gates(const float* x, const float* h, const uint8_t* reset, const float* Wu, const float* Wl,
+                             const float* b, float* gates, const float* c_prev, float* c_out, float* h_out, int n,
+                             bool cell, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const LstmGatesArgs a{x, h, reset, Wu, Wl, b, gates, c_prev, c_out, h_out, n, cell ? 1 : 0};
+  const unsigned blocks = (unsigned)(((n + LBM - 1) / LBM) * (GATES / LBN));
+  hipLaunchKernelGGL(lstm_gates_kernel, dim3(blocks), dim3(LT), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace arl

@@ -108,6 +108,8 @@ struct EpiResetMask {   // out[m][n] = reset[m] ? 0 : v
   }
 };
 
+#define ARL_TRY(x) do { hipError_t _e = (x); if (_e != hipSuccess) return _e; } while (0)
+
 // ---------------------------------------------------------------- elementwise
 __device__ inline float sigm(float x) { return __fdiv_rn(1.f, __fadd_rn(1.f, expf(-x))); }
 
@@ -162,10 +164,25 @@ static const bool LSTM_SPLIT = [] {
   return e != nullptr && e[0] == '1';
 }();
 
+// ARL_LSTM_GEMM=generic: the round-2 gate GEMM (generic gather template, EpiLstmCell) instead of
+// lstm_gates_kernel (lstm.hip) -- A/B timing only
+static const bool LSTM_GEMM_GENERIC = [] {
+  const char* e = getenv("ARL_LSTM_GEMM");
+  return e != nullptr && e[0] == 'g';
+}();
+
 // gates = [x | h] [Wu ; Wl]^T + b, then the cell: c_out, h_out (rows [0, n))
 template <class AOp, class BOp>
 static hipError_t lstm_gates_cell(const AOp& A, const BOp& B, const float* bias, float* gates, const float* c_prev,
                                   const uint8_t* reset, float* c_out, float* h_out, int n, hipStream_t s) {
+  if (!LSTM_GEMM_GENERIC) {   // lstm.hip: LDS-DMA staged tile, the cell in the epilogue (or its own launch)
+    ARL_TRY(launch_lstm_gates(A.x, A.h, A.reset, B.wu, B.wl, bias, gates, c_prev, c_out, h_out, n, !LSTM_SPLIT, s));
+    if (!LSTM_SPLIT) return hipSuccess;
+    const int64_t cnt = (int64_t)n * HID;
+    hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, gates, c_prev,
+                       reset, c_out, h_out, cnt);
+    return hipGetLastError();
+  }
   if (!LSTM_SPLIT)
     return launch_gemm<32, 64, 32, 2, 2, GK, GK>(A, B, EpiLstmCell{gates, bias, c_prev, reset, c_out, h_out}, n, GATES,
                                                  2 * HID, 1, s);
@@ -427,7 +444,6 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
 }
 
 // ---------------------------------------------------------------- forward
-#define ARL_TRY(x) do { hipError_t _e = (x); if (_e != hipSuccess) return _e; } while (0)
 
 // head after conv1 (conv2 -> fc) for n rows, activations at a1/a2/hfc
 static hipError_t fc_forward(const Net& net, int n, const float* a2, float* hfc, hipStream_t s) {

@@ -447,8 +447,7 @@ def test_lstm_windows_match_oracle(gpu, rgb, N, T, A):
     opt.add_hook(GradientClipping(40))
     agent = A3C(model, opt, T, 0.99)
     net = model.net
-    view = OracleStatesView(pairs, dones) if kind == "states" else \
-        OracleRgbView(pairs, dones) if rgb else OracleEnvView(pairs, dones)
+    view = OracleRgbView(pairs, dones) if rgb else OracleEnvView(pairs, dones)
     dp, dr, dd = dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu)
     st = O.LSTMState(h=np.zeros((N, 256), np.float32), c=np.zeros((N, 256), np.float32),
                      has=np.zeros(N, bool))
