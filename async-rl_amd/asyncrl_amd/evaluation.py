@@ -18,7 +18,9 @@ number k * N + i; the first `n_runs` run numbers are the scores returned, so
 the result does not depend on which env finishes first.
 
 Life loss is not terminal here (the reference's eval ALE), whatever the
-envs were built with: `eval_performance` switches it off for the duration.
+envs were built with: `eval_performance` switches it off for the duration,
+and every env's game restarts at the start of the evaluation.  The envs are
+left partway through episodes when it returns.
 The run uses (and overwrites) the model's lockstep workspace -- frame ring,
 step counter, LSTM state -- so evaluate on a model of its own (copy the
 trained parameters in: `eval_model.net.params.copy_(model.net.params)`).
@@ -33,7 +35,7 @@ import numpy as np
 MODE_SAMPLE, MODE_GREEDY = 1, 2
 
 
-def run_episodes(model, vec_env, n_runs: int, deterministic: bool = True, max_steps: int | None = None,
+def run_episodes(model, vec_env, n_runs: int, deterministic: bool = False, max_steps: int | None = None,
                  stream=None):
     """Run `n_runs` evaluation episodes over `vec_env` (a VecALE with exactly
     model.net.n_envs envs) with the model's lockstep workspace.  Returns
@@ -55,7 +57,10 @@ def run_episodes(model, vec_env, n_runs: int, deterministic: bool = True, max_st
     trace_a, trace_d = [], []
     try:
         for e in vec_env.envs:
+            # a fresh game per env, as the reference builds a fresh ALE per eval run
+            # (a3c_ale.py:75-76): an env left mid-game by training starts over
             e.treat_life_lost_as_terminal = False
+            e.ale.reset_game()
             e.initialize()
         pairs, r, d = vec_env.reset(stream)
         done_eps = [0] * N
@@ -95,11 +100,12 @@ def run_episodes(model, vec_env, n_runs: int, deterministic: bool = True, max_st
     return scores, {"actions": np.array(trace_a), "dones": np.array(trace_d)}
 
 
-def eval_performance(model, vec_env, n_runs: int, deterministic: bool = True, max_steps: int | None = None,
+def eval_performance(model, vec_env, n_runs: int, deterministic: bool = False, max_steps: int | None = None,
                      stream=None):
     """a3c_ale.py:73-89 batched: (mean, median, stdev) of `n_runs` episode
-    scores.  deterministic=True plays most_probable_actions (the demo's
-    mode), False samples from the policy (the training script's eval)."""
+    scores.  By default the action is sampled from the policy, as the
+    training script's eval does (pout.action_indices); deterministic=True
+    plays most_probable_actions (demo_a3c_ale.py:15-30)."""
     if n_runs < 2:
         raise ValueError("Computing stdev requires at least two runs")   # a3c_ale.py:74
     scores, _ = run_episodes(model, vec_env, n_runs, deterministic, max_steps, stream)

@@ -101,8 +101,24 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def cgroup_cpu_quota():
+    """CPUs granted by the cgroup v2 CPU controller (cpu.max "quota period"),
+    or None when unlimited / unreadable.  The GPU box runs a command under a
+    16-CPU quota (cpu.max 1600000 100000) on a 128-core host: processes beyond
+    the quota only time-share it."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota == "max":
+            return None
+        return max(1, int(int(quota) // int(period)))
+    except (OSError, ValueError):
+        return None
+
+
 def host_cores():
-    """(physical cores, logical CPUs, CPUs this process may run on)."""
+    """(physical cores, logical CPUs, CPUs this process may run on: the
+    affinity mask, capped by the cgroup CPU quota)."""
     import os
     try:
         import psutil
@@ -114,34 +130,48 @@ def host_cores():
         avail = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         avail = logical
+    quota = cgroup_cpu_quota()
+    if quota is not None:
+        avail = min(avail, quota)
     return phys or logical, logical, avail
 
 
 def run_parallel(seconds: float = 10.0, t_max: int = 5, n_actions: int = 4, procs: int | None = None,
-                 cap: int = 16, ctx=None):
+                 cap: int | None = None, ctx=None):
     """Leg (ii) of BASELINE.md §2: P independent actor-learner processes in
     the reference's style (async.py:68-90 run_async -- one process per
     core, OMP_NUM_THREADS=1 each, a3c_ale.py:186), P = min(physical cores,
-    CPUs this process may use, cap); the box's CPU share for one GPU is 16,
-    hence the default cap.  Each process owns its parameters (the
-    reference's shared RawArrays add Hogwild write traffic, not arithmetic).
-    Aggregate env-steps/s = sum of steps / the slowest process's time.
-    ctx: a multiprocessing context -- pass a forkserver started before the
-    GPU was touched (bench.py) so no worker is forked from a GPU process."""
+    CPUs this process may use [, cap]).  "May use" includes the cgroup CPU
+    quota: on the GPU box that is 16 CPUs of the 128-core host, so P = 16 is
+    every core the bench can actually run on; more processes would only
+    time-share those 16.  The record also states the per-process rate times
+    the physical core count, labelled as an extrapolation (the reference's
+    P = physical cores, run on the whole host).  Each process owns its
+    parameters (the reference's shared RawArrays add Hogwild write traffic,
+    not arithmetic).  Aggregate env-steps/s = sum of steps / the slowest
+    process's time.  ctx: a multiprocessing context -- pass a forkserver
+    started before the GPU was touched (bench.py) so no worker is forked
+    from a GPU process."""
     import multiprocessing as mp
     phys, logical, avail = host_cores()
-    P = procs if procs else max(1, min(phys, avail, cap))
+    P = procs if procs else max(1, min(phys, avail, cap or phys))
     ctx = ctx if ctx is not None else mp.get_context("forkserver")
     with ctx.Pool(P) as pool:
         res = pool.map(_worker, [(seconds, t_max, n_actions, 1000 + i) for i in range(P)])
     steps = [r["steps"] for r in res]
     rates = [r["value"] for r in res]
     el = max(r["seconds"] for r in res)
+    per_proc = sum(rates) / len(rates)
     return {"value": sum(steps) / el, "unit": "env-steps/s", "cores": P, "kind": "port",
             "sample": f"{P} processes x ~{seconds:.0f} s of the batch-1 A3C-FF actor-learner (NumPy restatement, "
                       f"1 thread each), {sum(steps)} env-steps in total; per-process {min(rates):.1f}-"
                       f"{max(rates):.1f} env-steps/s",
-            "cpu_model": cpu_model(), "physical_cores": phys, "logical_cpus": logical, "cpus_allowed": avail}
+            "cpu_model": cpu_model(), "physical_cores": phys, "logical_cpus": logical, "cpus_allowed": avail,
+            "cgroup_cpu_quota": cgroup_cpu_quota(),
+            "extrapolated_physical_cores": {"value": round(per_proc * phys, 1), "cores": phys,
+                                            "note": "mean per-process rate x physical cores: an estimate of the "
+                                                    "reference-style P = physical-cores run, not a measurement "
+                                                    "(the quota admits only cpus_allowed processes at once)"}}
 
 
 if __name__ == "__main__":

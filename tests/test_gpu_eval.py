@@ -25,6 +25,7 @@ def _serial_replay(params, n, seed, nullops, actions):
                           max_start_nullops=nullops) for i in range(n)]
     for e in envs:
         e.treat_life_lost_as_terminal = False   # ale.ALE(rom, treat_life_lost_as_terminal=False)
+        e.ale.reset_game()                      # a fresh game per eval run (a3c_ale.py:75-76)
         e.initialize()
     stacks = [O.stack_push(None, O.current_screen(e.pair[0], e.pair[1]), True) for e in envs]
     scores = [[] for _ in range(n)]
