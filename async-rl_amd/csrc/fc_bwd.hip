@@ -77,6 +77,19 @@ static_assert(BK * (AJ + AK) <= STAGE && 128 * BK + BK * BN <= STAGE, "stage siz
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
+// XCD-aware job order (ARL_FC_BWD_XCD=0: plain order, A/B timing only).
+// Workgroups are dealt round-robin over the 8 XCDs (b % 8 share one XCD and
+// its L2; which XCD is not fixed, MI355X_MICROARCH.md), so job b of n gets
+// linear work index xcd_order(b, n): every XCD takes one contiguous range of
+// the linear order.  Linear orders put tiles that share an operand next to
+// each other -- job A: the two j tiles of one (range, k tile) a2 slice; job B:
+// the sample tiles of one k tile (one W slice) -- so each slice is fetched
+// into about one L2 instead of all eight.
+__device__ inline int xcd_order(int b, int n) {
+  const int x = b & 7, slot = b >> 3, per = n >> 3, rem = n & 7;
+  return x * per + min(x, rem) + slot;
+}
+
 __device__ inline uint64_t pack2(float lo, float hi) {
   return (uint64_t)__float_as_uint(lo) | ((uint64_t)__float_as_uint(hi) << 32);
 }
@@ -127,6 +140,7 @@ struct FcBwdArgs {
   int abl;            // ARL_FC_BWD_ABL bits (timing experiments only): 1 no MFMA, 2 no staging,
                       // 4 no job A reduction (wrong dW), 8 no job A k loop
   int spin;           // job A reduce: ticket first, the last range waits for the others' partials
+  int xcd;            // XCD-aware job order (xcd_order)
 };
 
 // ---------------------------------------------------------------- job A: dW, db
@@ -153,7 +167,13 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, col = lane & 15;
   const int wm = wave >> 1, wn = wave & 1;   // wave: 64 j x 32 k
-  const int tile = job % NTA, z = job / NTA;
+  int tile = job % NTA, z = job / NTA;
+  if (a.xcd) {   // linear order (z, kt, jt), jt fastest
+    const int lin = xcd_order(job, NTA * a.Z);
+    z = lin / NTA;
+    const int r = lin - z * NTA;
+    tile = (r % NJA) * NKA + r / NJA;
+  }
   const int kt = tile % NKA, jt = tile / NKA;
   const int j0 = jt * AJ, k0 = kt * AK;
   const int r0 = z * a.kpz, r1 = min(a.S, r0 + a.kpz);
@@ -410,7 +430,13 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, col = lane & 15;
   const int wm = wave >> 1, wn = wave & 1;   // wave: 16 MT s x 64 k
-  const int kt = tile % NKB, st = tile / NKB;
+  int kt = tile % NKB, st = tile / NKB;
+  if (a.xcd) {   // linear order (kt, st), st fastest
+    const int nst = (a.S + BMT - 1) / BMT;
+    const int lin = xcd_order(tile, nst * NKB);
+    kt = lin / nst;
+    st = lin - kt * nst;
+  }
   const int s0 = st * BMT, k0 = kt * BN;
   constexpr int NCH = HID / BK;              // 8 chunks of 32 j
   auto issue = [&](int c) {
@@ -659,8 +685,9 @@ hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int 
   const int grid = (only && only[0] == 'a') ? na : (only && only[0] == 'b') ? nb : nc + na + nb;
   // ARL_FC_BWD_SPIN=1: ticket-first job A reduce (the last range's partial is never published)
   static const char* spin = getenv("ARL_FC_BWD_SPIN");
+  static const char* xcd = getenv("ARL_FC_BWD_XCD");
   FcBwdArgs args{dfc, a2, W, S, Z, kpz, gW, gb, da2, part, tick, heads ? *heads : HeadsDW{}, nc, b0,
-                 abl ? atoi(abl) : 0, (spin && atoi(spin) == 1) ? 1 : 0};
+                 abl ? atoi(abl) : 0, (spin && atoi(spin) == 1) ? 1 : 0, (xcd && xcd[0] == '0') ? 0 : 1};
   if (split) hipLaunchKernelGGL((fc_bwd_kernel<2, true>), dim3(grid), dim3(NT), 0, s, args);
   else if (MT == 2) hipLaunchKernelGGL((fc_bwd_kernel<2, false>), dim3(grid), dim3(NT), 0, s, args);
   else hipLaunchKernelGGL((fc_bwd_kernel<4, false>), dim3(grid), dim3(NT), 0, s, args);

@@ -8,9 +8,16 @@ import oracle as O
 def make_pools(rng, pool_len, n, kind="uniform", p_done=0.15):
     """pairs (pool_len, n, 2, 210, 160, 3) uint8 (frame 4, frame 3 of the
     skip); rewards (pool_len, n) f32 incl. out-of-range values (clip test);
-    dones (pool_len, n) uint8."""
+    dones (pool_len, n) uint8.  kind: "uniform" [0, 255]; "palette" sparse
+    palette blocks on black (SURVEY 8(d) variant ii, Breakout- / Space
+    Invaders-shaped); "shaped": palette frames with every 16th env all-255
+    (variant iii, luminance 254) and every 16th env (offset 9) uniform."""
     if kind == "uniform":
         pairs = rng.integers(0, 256, (pool_len, n, 2, 210, 160, 3), dtype=np.uint8)
+    elif kind == "shaped":
+        pairs, _, _ = make_pools(rng, pool_len, n, "palette", p_done)
+        pairs[:, 5::16] = 255
+        pairs[:, 9::16] = rng.integers(0, 256, pairs[:, 9::16].shape, dtype=np.uint8)
     else:
         pairs = np.zeros((pool_len, n, 2, 210, 160, 3), np.uint8)
         pal = rng.integers(0, 256, (16, 3), dtype=np.uint8)

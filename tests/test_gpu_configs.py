@@ -4,7 +4,9 @@ more than one GPU:
 
   C3  A3C LSTM, 1024 envs, A = 6, the default two env groups, two windows
   C4  the per-GPU leg of the 8-GPU config: A3C FF, 512 envs, two env groups
-  C2  A3C FF, 256 envs (the bench's default workload), two windows
+  C2  A3C FF, 256 envs, two windows
+(each on uniform frames and on SURVEY 8(d)'s shaped frames: palette blocks on
+black, all-255 envs and uniform envs in one batch)
   C5  phi_stack over 16,384 frame pairs (a 3.3 GB input whose byte offsets
       pass 2^31)
 
@@ -65,11 +67,11 @@ def _oracle_window(arch, params, states, acts, r, d, boot, st=None, dprev=None, 
     return {k: v.astype(np.float32) for k, v in g.items()}, out
 
 
-def _run_config(gpu, arch, N, A, windows=2, seed=0):
+def _run_config(gpu, arch, N, A, windows=2, seed=0, kind="uniform"):
     from asyncrl_amd import A3C, A3CFF, A3CLSTM, GradientClipping, RMSpropAsync
     rng = np.random.default_rng(seed)
     T, P = 5, 6          # pool of 6 steps, reused cyclically by the second window
-    pairs, rewards, dones = make_pools(rng, P, N, "uniform", p_done=0.1)
+    pairs, rewards, dones = make_pools(rng, P, N, kind, p_done=0.1)
     Model = A3CLSTM if arch == O.ARCH_LSTM else A3CFF
     model = Model(A, n_envs=N, t_max=T, seed=77, init_seed=seed + 1, frames="pairs", device=gpu)
     opt = RMSpropAsync(lr=7e-4, eps=1e-1, alpha=0.99).setup(model)
@@ -120,6 +122,13 @@ def test_c3_lstm_1024_envs_two_groups(gpu):
     assert len(groups) == 2
 
 
+def test_c3_lstm_1024_envs_shaped_frames(gpu):
+    """C3 on SURVEY 8(d)'s shaped frames: sparse palette blocks on black
+    (conv pre-activations tie at zero: the tie-aware ReLU masks), all-255 envs
+    and uniform envs mixed in one batch."""
+    _run_config(gpu, O.ARCH_LSTM, 1024, 6, seed=13, kind="shaped")
+
+
 def test_c4_leg_ff_512_envs_two_groups(gpu):
     groups = _run_config(gpu, O.ARCH_FF, 512, 4, seed=4)
     assert len(groups) == 2
@@ -127,6 +136,14 @@ def test_c4_leg_ff_512_envs_two_groups(gpu):
 
 def test_c2_ff_256_envs(gpu):
     _run_config(gpu, O.ARCH_FF, 256, 4, seed=2)
+
+
+def test_c2_ff_256_envs_shaped_frames(gpu):
+    _run_config(gpu, O.ARCH_FF, 256, 4, seed=12, kind="shaped")
+
+
+def test_c4_leg_ff_512_envs_shaped_frames(gpu):
+    _run_config(gpu, O.ARCH_FF, 512, 4, seed=14, kind="shaped")
 
 
 def test_c5_phi_stack_16384_pairs(gpu):
