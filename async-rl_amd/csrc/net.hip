@@ -73,12 +73,27 @@ struct LstmGateB {      // B(k, j) = [Wu^T ; Wl^T]
                    : *reinterpret_cast<const float4*>(wl + (int64_t)j * HID + k - HID);
   }
 };
-struct LstmWB {         // B(s, j) = [x (256) | 1 | h_prev (256, 0 after reset)]
+struct LstmWB {         // B(s, j) = [x (256) | h_prev (256, 0 after reset) | 1]: the gate weight gradient's
+                        // operand (upward W, lateral W, then the ones column for the upward bias)
   const float* __restrict__ x; const float* __restrict__ h; const uint8_t* __restrict__ reset;
   __device__ float load(int s, int j) const {
     if (j < HID) return x[(int64_t)s * HID + j];
-    if (j == HID) return 1.f;
-    return reset[s] ? 0.f : h[(int64_t)s * HID + j - HID - 1];
+    if (j < 2 * HID) return reset[s] ? 0.f : h[(int64_t)s * HID + j - HID];
+    return 1.f;
+  }
+  // 4 consecutive j (j % 4 == 0, j + 3 < 2 HID): one 16-byte load of x or h
+  __device__ float4 load4n(int s, int j) const {
+    if (j < HID) return *reinterpret_cast<const float4*>(x + (int64_t)s * HID + j);
+    if (reset[s]) return make_float4(0.f, 0.f, 0.f, 0.f);
+    return *reinterpret_cast<const float4*>(h + (int64_t)s * HID + j - HID);
+  }
+};
+struct MapLstmW {       // LstmWB's column order -> the flat gradient: upward W, lateral W, upward b
+  float* g; int64_t oU, oL, ob;
+  __device__ void put(int m, int n, float v) const {
+    if (n < HID) g[oU + (int64_t)m * HID + n] = v;
+    else if (n < 2 * HID) g[oL + (int64_t)m * HID + (n - HID)] = v;
+    else g[ob + m] = v;
   }
 };
 
@@ -675,7 +690,7 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
   float* slab_l = net.at<float>(net.w_slab_lstm);
   if (part == LEARN_GATES_REDUCE)
     return L ? launch_reduce_grad(slab_l, pl.lstm_w, GATES, 2 * HID + 1,
-                                  MapDense{G, net.o_luW, net.o_lub, net.o_llW, HID}, s)
+                                  MapLstmW{G, net.o_luW, net.o_llW, net.o_lub}, s)
              : hipSuccess;
   if (part == LEARN_FC_REDUCE)   // the FC weight gradient is written by fc_bwd_kernel (LEARN_TRUNK)
     return FC_BWD_GEMM ? launch_reduce_grad(slab_f, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s)
@@ -732,7 +747,7 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
       }
     }
     // gate weight gradients and dfc = (dG Wu) * (hfc > 0): independent, one launch
-    ARL_TRY((launch_gemm2<64, 64, 32, 2, 2, GM, GS, GK, GM>(
+    ARL_TRY((launch_gemm2<64, 64, 32, 2, 2, GM, GM, GK, GM>(
         gemm_job<64, 32>(ColMajor{dG, GATES}, LstmWB{hfc, hbuf, rs}, EpiSlab{slab_l, GATES, 2 * HID + 1}, GATES,
                          2 * HID + 1, S, pl.lstm_w, 64),
         gemm_job<64, 32>(RowMajor{dG, GATES}, RowMajor{P + net.o_luW, HID}, EpiMask{dfc, hfc, HID}, S, HID, GATES, 1,
