@@ -82,7 +82,7 @@ SIGNATURES = {
     "arl_returns_lossgrad": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_i64,
                                      c_int, c_double, c_double, c_double, c_double, c_int, c_int, c_void_p,
                                      c_void_p, c_void_p, c_void_p]),
-    "arl_stream_copy": (c_int, [c_void_p, c_void_p, c_i64, c_int, c_void_p]),
+    "arl_stream_copy": (c_int, [c_void_p, c_void_p, c_i64, c_int, c_int, c_void_p]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

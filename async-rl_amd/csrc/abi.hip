@@ -434,12 +434,13 @@ int arl_returns_lossgrad(const float* rewards, const uint8_t* dones, const float
                     "returns");
 }
 
-int arl_stream_copy(const void* src, void* dst, int64_t bytes, int blocks, void* s) {
+int arl_stream_copy(const void* src, void* dst, int64_t bytes, int blocks, int mode, void* s) {
   if (bytes < 0 || (bytes > 0 && (!src || !dst))) return fail(ARL_EINVAL, "stream_copy: null pointer / bytes < 0");
   if (bytes % 16 || !aligned(src, 16) || !aligned(dst, 16)) return fail(ARL_EINVAL, "stream_copy: 16-byte units");
   if (blocks < 1 || blocks > 65535) return fail(ARL_EINVAL, "stream_copy: blocks out of [1, 65535]");
+  if (mode < 0 || mode > 1) return fail(ARL_EINVAL, "stream_copy: mode must be 0 or 1");
   if (bytes == 0) return ARL_OK;
-  return hip_status(arl::launch_stream_copy(src, dst, bytes, blocks, S(s)), "stream_copy");
+  return hip_status(arl::launch_stream_copy(src, dst, bytes, blocks, mode, S(s)), "stream_copy");
 }
 
 }  // extern "C"

@@ -271,7 +271,7 @@ hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double
                           int64_t total_steps, int64_t n_total, int t_max, hipStream_t s,
                           const AdvanceArgs* adv = nullptr);
 hipError_t launch_grad_sqnorm(const float* g, int64_t n, double* partials, int blocks, hipStream_t s);
-hipError_t launch_stream_copy(const void* src, void* dst, int64_t bytes, int blocks, hipStream_t s);
+hipError_t launch_stream_copy(const void* src, void* dst, int64_t bytes, int blocks, int mode, hipStream_t s);
 hipError_t launch_policy(const float* h, int64_t n, const float* Wpi, const float* bpi, const float* Wv,
                          const float* bv, int A, uint64_t seed, const int64_t* ctl, int64_t step_off,
                          int env_offset, int mode, float* logits, float* probs, float* logp, float* v,

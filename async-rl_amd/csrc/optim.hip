@@ -186,8 +186,12 @@ hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double
 }
 
 // HBM stream-copy peak (measurement only; SURVEY 8(d) "also report vs the
-// measured stream-copy peak"): 16-byte loads, four in flight per lane before
-// the first store, grid-stride over the buffer.
+// measured stream-copy peak").  Two forms, the bench keeps the faster:
+//   mode 0: grid-stride, four 16-byte loads in flight per lane before the
+//           first store (addresses one grid apart);
+//   mode 1: each workgroup copies contiguous 64 KB blocks (block-stride over
+//           the buffer), every lane 4 consecutive-in-wave 16-byte loads in
+//           flight, non-temporal loads / stores (a once-read stream).
 __global__ void __launch_bounds__(256)
 stream_copy_kernel(const float4* __restrict__ src, float4* __restrict__ dst, int64_t n4) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -202,9 +206,32 @@ stream_copy_kernel(const float4* __restrict__ src, float4* __restrict__ dst, int
   for (; i < n4; i += stride) dst[i] = src[i];
 }
 
-hipError_t launch_stream_copy(const void* src, void* dst, int64_t bytes, int blocks, hipStream_t s) {
-  hipLaunchKernelGGL(stream_copy_kernel, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const float4*>(src),
-                     reinterpret_cast<float4*>(dst), bytes / 16);
+typedef float cp_f32x4 __attribute__((ext_vector_type(4)));
+
+__global__ void __launch_bounds__(256)
+stream_copy_blocks_kernel(const cp_f32x4* __restrict__ src, cp_f32x4* __restrict__ dst, int64_t n4) {
+  constexpr int U = 16;                         // 16-byte vectors per lane per block: 256 x 16 x 16 B = 64 KB
+  const int64_t nblk = n4 / (256 * U);
+  for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const cp_f32x4* s = src + b * (256 * U) + threadIdx.x;
+    cp_f32x4* d = dst + b * (256 * U) + threadIdx.x;
+    cp_f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(s + 256 * u);
+#pragma unroll
+    for (int u = 0; u < U; ++u) __builtin_nontemporal_store(v[u], d + 256 * u);
+  }
+  for (int64_t i = nblk * (256 * U) + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
+    dst[i] = src[i];
+}
+
+hipError_t launch_stream_copy(const void* src, void* dst, int64_t bytes, int blocks, int mode, hipStream_t s) {
+  const float4* a = reinterpret_cast<const float4*>(src);
+  float4* b = reinterpret_cast<float4*>(dst);
+  if (mode == 1)
+    hipLaunchKernelGGL(stream_copy_blocks_kernel, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const cp_f32x4*>(src),
+                       reinterpret_cast<cp_f32x4*>(dst), bytes / 16);
+  else hipLaunchKernelGGL(stream_copy_kernel, dim3(blocks), dim3(256), 0, s, a, b, bytes / 16);
   return hipGetLastError();
 }
 

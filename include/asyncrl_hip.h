@@ -311,8 +311,9 @@ int arl_returns_lossgrad(const float* rewards, const uint8_t* dones, const float
 /* Device-to-device copy of `bytes` (a multiple of 16, 16-byte aligned
  * buffers) by a grid of `blocks` 256-thread workgroups, 16-byte loads: the HBM
  * stream-copy peak the bench reports beside the 8 TB/s spec (SURVEY 8(d);
- * no reference counterpart). */
-int arl_stream_copy(const void* src, void* dst, int64_t bytes, int blocks, void* stream);
+ * no reference counterpart).  mode 0: grid-stride, 4 loads in flight per lane;
+ * mode 1: 64 KB blocks per workgroup, 16 non-temporal loads in flight per lane. */
+int arl_stream_copy(const void* src, void* dst, int64_t bytes, int blocks, int mode, void* stream);
 
 #ifdef __cplusplus
 }
