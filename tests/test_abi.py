@@ -121,3 +121,20 @@ def test_env_range_validation_without_device():
         assert lib.arl_observe_envs(h, 0, 0, 32, None, 0, 0, None, None, 1, 0, 0, None) == 3
     finally:
         lib.arl_net_destroy(h)
+
+
+def test_bench_launcher_propagates_rank_failure():
+    """`python bench.py --gpus 2` without WORLD_SIZE starts two rank processes
+    itself (bench.launch_ranks, the reference's run_async shape); when a rank
+    fails -- here: no GPU in this container -- the launcher stops the other,
+    reports it and exits non-zero instead of hanging."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                        "--cpu-seconds", "0"], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode != 0
+    assert "a rank failed" in r.stderr, r.stderr[-2000:]
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
