@@ -173,6 +173,9 @@ hipError_t states_conv_bwd(Net& net, hipStream_t s);
 int64_t states_slab_floats(const Net& net);
 
 // LSTM gate GEMM + bias (+ the F.lstm cell when cell) for rows [0, n) (lstm.hip)
+hipError_t launch_lstm_bptt(const float* dG, const float* Wl, const uint8_t* rs_t, const float* gates, const float* c_t,
+                            const float* c_prev, const uint8_t* rs, const float* dH, float* dcn, float* dG_out,
+                            float* dhn, int n, bool cell, hipStream_t s);
 hipError_t launch_lstm_gates(const float* x, const float* h, const uint8_t* reset, const float* Wu, const float* Wl,
                              const float* b, float* gates, const float* c_prev, float* c_out, float* h_out, int n,
                              bool cell, hipStream_t s);

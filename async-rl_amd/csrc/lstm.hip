@@ -170,4 +170,183 @@ hipError_t launch_lstm_gates(const float* x, const float* h, const uint8_t* rese
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Truncated BPTT step of the LSTM backward (a3c.py:129-130 through Chainer
+// F.lstm; unchain_backward at the window edge, a3c_ale.py:68-70), one launch
+// per step t >= 1:
+//
+//   dh[m][u]  = sum_j dG_t[m][j] Wl[j][u]        (the lateral Linear's input gradient)
+//   dh[m][u]  = 0 where the env reset at step t   (h_{t-1} was None, a3c.py:166)
+//   cell = 1: F.lstm backward of step t-1 for (m, u) with dh + dH_{t-1} (the
+//             heads' share): dG_{t-1} (4 interleaved gates) and the carried dc
+//             -- lstm_cell_bwd_elem's arithmetic (net.hip), op for op;
+//   cell = 0: dhn[m][u] = dh only (the split path's separate cell launch reads it).
+//
+// M = n envs, N = 256 units, K = 1024 gates.  32 x 32 tile per 512-thread
+// workgroup; 8 waves = 4 sub-tiles of 16 x 16 x 2 K halves (exact f32
+// v_mfma_f32_16x16x4_f32), the halves summed in a fixed order in LDS.  K is
+// staged by LDS-DMA in eight 128-column chunks through four LDS stages (three
+// chunks in flight, one barrier a chunk): dG_t rows (row stride 33 float4)
+// and Wl rows j (32 units + a pad float4, read one float per lane).  The
+// epilogue's operands are loaded before the K loop.
+namespace {
+constexpr int BBM = 32, BBN = 32, BT = 512, BW = BT / 64;
+constexpr int BKC = 128;                                 // K chunk
+constexpr int BNCH = GATES / BKC;                        // 8 chunks
+constexpr int BA_LD = BKC / 4 + 1;                       // 33 float4 per dG row
+constexpr int BB_LD = BBN / 4 + 1;                       // 9 float4 per Wl row
+constexpr int BA_PC = (BBM * BA_LD + 63) / 64;           // 17 pieces
+constexpr int BB_PC = (BKC * BB_LD + 63) / 64;           // 18 pieces
+constexpr int BPIECES = BA_PC + BB_PC;                   // 35 pieces a chunk
+constexpr int BSTAGE4 = BPIECES * 64;                    // float4 per stage
+constexpr int BSTAGES = 4;
+constexpr int BTLD = BBN + 4;                            // epilogue half-sum row stride (floats)
+static_assert(2 * BBM * BTLD <= BSTAGE4 * 4, "epilogue halves fit one stage");
+static_assert(BBM * BBN == 2 * BT, "two (row, unit) pairs per thread");
+__host__ __device__ constexpr int bptt_pieces(int w) { return (BPIECES - w + BW - 1) / BW; }
+}  // namespace
+
+struct LstmBpttArgs {
+  const float* dG;       // (n, 1024) dG_t
+  const float* Wl;       // (1024, 256)
+  const uint8_t* rs_t;   // (n) reset at step t
+  // step t - 1 (cell = 1)
+  const float* gates;    // (n, 1024)
+  const float* c_t;      // (n, 256) c after step t - 1
+  const float* c_prev;   // (n, 256) c before step t - 1
+  const uint8_t* rs;     // (n) reset at step t - 1
+  const float* dH;       // (n, 256) the heads' dL/dh of step t - 1
+  float* dcn;            // (n, 256) carried dc: in from step t, out to step t - 2
+  float* dG_out;         // (n, 1024) dG_{t-1}
+  float* dhn;            // (n, 256) cell = 0: the masked dh
+  int n, cell;
+};
+
+__device__ inline void bptt_wait_vm(int n) {   // s_waitcnt vmcnt(n), n wave-uniform
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+__global__ void __launch_bounds__(BT)
+lstm_bptt_kernel(LstmBpttArgs a) {
+  __shared__ __attribute__((aligned(16))) float S[BSTAGES * BSTAGE4 * 4];   // 143,360 B
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NTN = HID / BBN;
+  const int m0 = (blockIdx.x / NTN) * BBM, u0 = (blockIdx.x % NTN) * BBN;
+  const int pw = bptt_pieces(wave);
+
+  // the epilogue's operands first (the oldest loads: the counted waits cover them)
+  int em[2], eu[2];
+  float4 eg[2];
+  float ec[2], ep[2], eh[2], ed[2];
+  uint8_t ers[2], erst[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int pr = tid + BT * i;              // (row, unit) pair: 32 rows x 32 units
+    em[i] = min(m0 + pr / BBN, a.n - 1);
+    eu[i] = u0 + pr % BBN;
+    const int64_t e = (int64_t)em[i] * HID + eu[i];
+    erst[i] = a.rs_t[em[i]];
+    if (a.cell) {
+      eg[i] = reinterpret_cast<const float4*>(a.gates)[e];
+      ec[i] = a.c_t[e];
+      ep[i] = a.c_prev[e];
+      eh[i] = a.dH[e];
+      ed[i] = a.dcn[e];
+      ers[i] = a.rs[em[i]];
+    }
+  }
+
+  auto issue = [&](int c) {
+    float* st = S + 4 * BSTAGE4 * (c % BSTAGES);
+    const int kc = c * BKC;
+    for (int it = wave; it < BPIECES; it += BW) {
+      const float* src;
+      if (it < BA_PC) {                       // dG_t rows m0.. (rows past n: a valid row, never stored)
+        const int i = min(it * 64 + lane, BBM * BA_LD - 1);
+        const int r = i / BA_LD, cc = min(i - r * BA_LD, BKC / 4 - 1);
+        src = a.dG + (int64_t)min(m0 + r, a.n - 1) * GATES + kc + 4 * cc;
+      } else {                                // Wl rows kc.., units u0..u0+31
+        const int i = min((it - BA_PC) * 64 + lane, BKC * BB_LD - 1);
+        const int r = i / BB_LD, cc = min(i - r * BB_LD, BBN / 4 - 1);
+        src = a.Wl + (int64_t)(kc + r) * HID + u0 + 4 * cc;
+      }
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(st + 4 * it * 64), 16, 0, 0);
+    }
+  };
+  issue(0);
+  issue(1);
+  issue(2);
+
+  const int q = lane >> 4, col = lane & 15;
+  const int sub = wave & 3, kh = wave >> 2;   // sub-tile (ms, ns), K half of each chunk
+  const int ms = sub & 1, ns = sub >> 1;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < BNCH; ++c) {
+    bptt_wait_vm(min(2, BNCH - 1 - c) * pw);  // chunk c landed (up to two later ones in flight)
+    lstm_lds_barrier();                       // ... for every wave, and stage (c + 3) % 4 is free
+    if (c + 3 < BNCH) issue(c + 3);
+    const float* st = S + 4 * BSTAGE4 * (c % BSTAGES);
+    const float* Ar = st + (ms * 16 + col) * 4 * BA_LD + 4 * q;
+    const float* Bs = st + 4 * 64 * BA_PC + ns * 16 + col;
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {          // k = 16 s + 4 q + r of the chunk, s = 4 kh + s4
+      const int s = 4 * kh + s4;
+      const f32x4 av = *reinterpret_cast<const f32x4*>(Ar + 16 * s);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], Bs[(16 * s + 4 * q + r) * 4 * BB_LD], acc, 0, 0, 0);
+    }
+  }
+  // ---- the two K halves: into stage 0 (free: chunk 4's stage, done two chunks ago), fixed order
+  lstm_lds_barrier();
+  float* T = S;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) T[(kh * BBM + ms * 16 + q * 4 + r) * BTLD + ns * 16 + col] = acc[r];
+  lstm_lds_barrier();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int pr = tid + BT * i, row = pr / BBN, u = pr % BBN;
+    if (m0 + row >= a.n) continue;
+    float dh = __fadd_rn(T[row * BTLD + u], T[(BBM + row) * BTLD + u]);
+    if (erst[i]) dh = 0.f;
+    const int64_t e = (int64_t)em[i] * HID + eu[i];
+    if (!a.cell) {
+      a.dhn[e] = dh;
+      continue;
+    }
+    // lstm_cell_bwd_elem (net.hip) with dh + dH, not first
+    const float dht = __fadd_rn(eh[i], dh);
+    const float4 g = eg[i];
+    const float ag = tanhf(g.x), ig = lstm_sigm(g.y), fg = lstm_sigm(g.z), og = lstm_sigm(g.w);
+    const float tc = tanhf(ec[i]);
+    float dc = __fmul_rn(__fmul_rn(dht, og), __fsub_rn(1.f, __fmul_rn(tc, tc)));
+    dc = __fadd_rn(dc, ed[i]);
+    const float cp = ers[i] ? 0.f : ep[i];
+    float4 d;
+    d.x = __fmul_rn(__fmul_rn(dc, ig), __fsub_rn(1.f, __fmul_rn(ag, ag)));
+    d.y = __fmul_rn(__fmul_rn(__fmul_rn(dc, ag), ig), __fsub_rn(1.f, ig));
+    d.z = __fmul_rn(__fmul_rn(__fmul_rn(dc, cp), fg), __fsub_rn(1.f, fg));
+    d.w = __fmul_rn(__fmul_rn(__fmul_rn(dht, tc), og), __fsub_rn(1.f, og));
+    reinterpret_cast<float4*>(a.dG_out)[e] = d;
+    a.dcn[e] = ers[i] ? 0.f : __fmul_rn(dc, fg);
+  }
+}
+
+hipError_t launch_lstm_bptt(const float* dG, const float* Wl, const uint8_t* rs_t, const float* gates, const float* c_t,
+                            const float* c_prev, const uint8_t* rs, const float* dH, float* dcn, float* dG_out,
+                            float* dhn, int n, bool cell, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const LstmBpttArgs a{dG, Wl, rs_t, gates, c_t, c_prev, rs, dH, dcn, dG_out, dhn, n, cell ? 1 : 0};
+  const unsigned blocks = (unsigned)(((n + BBM - 1) / BBM) * (HID / BBN));
+  hipLaunchKernelGGL(lstm_bptt_kernel, dim3(blocks), dim3(BT), 0, s, a);
+  return hipGetLastError();
+}
+
 }  // namespace arl

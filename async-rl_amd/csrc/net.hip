@@ -181,6 +181,12 @@ static const bool LSTM_SPLIT = [] {
 
 // ARL_LSTM_GEMM=generic: the round-2 gate GEMM (generic gather template, EpiLstmCell) instead of
 // lstm_gates_kernel (lstm.hip) -- A/B timing only
+// ARL_LSTM_BPTT=generic: the BPTT step as the split-K GEMM + reduce/cell
+// launches (the A/B arm for lstm.hip's fused lstm_bptt_kernel)
+static const bool LSTM_BPTT_GENERIC = [] {
+  const char* e = getenv("ARL_LSTM_BPTT");
+  return e != nullptr && e[0] == 'g';
+}();
 static const bool LSTM_GEMM_GENERIC = [] {
   const char* e = getenv("ARL_LSTM_GEMM");
   return e != nullptr && e[0] == 'g';
@@ -732,7 +738,12 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
                            t == T - 1 ? 1 : 0, cnt);
         ARL_TRY(hipGetLastError());
       }
-      if (t > 0) {
+      if (t > 0 && !LSTM_BPTT_GENERIC) {   // lstm.hip: dh GEMM + mask + step t-1's cell in one launch
+        const int64_t op = o - n;
+        ARL_TRY(launch_lstm_bptt(dG + o * GATES, P + net.o_llW, rs + o, gates + op * GATES, cbuf + (op + n) * HID,
+                                 cbuf + op * HID, rs + op, dH + op * HID, dcn, dG + op * GATES, dhn, n, !LSTM_SPLIT,
+                                 s));
+      } else if (t > 0) {
         ARL_TRY((launch_gemm<32, 64, 32, 2, 2, GK, GM>(RowMajor{dG + o * GATES, GATES}, RowMajor{P + net.o_llW, HID},
                                                        EpiSlab{slab, n, HID}, n, HID, GATES, BPTT_SPLIT, s)));
         if (LSTM_SPLIT) {
