@@ -53,6 +53,11 @@ from .policy_output import SoftmaxPolicyOutput
 
 # env groups: chain g starts after chain g-1's first kernel (ARL_GROUP_STAGGER=0: together)
 STAGGER = os.environ.get("ARL_GROUP_STAGGER", "1") != "0"
+# env groups: the chains' launches are issued (captured) step-interleaved --
+# step t of chain 0, of chain 1, ..., then step t + 1 -- so a graph replay
+# hands every chain's first launches to the device early; ARL_GROUP_ORDER=chain
+# issues chain 0 whole, then chain 1, ... (the A arm)
+GROUP_ORDER = os.environ.get("ARL_GROUP_ORDER", "interleave")
 # > 1 rank: split the gradient all-reduce around the conv backward (ARL_OVERLAP_ALLREDUCE=0: one call)
 OVERLAP_ALLREDUCE = os.environ.get("ARL_OVERLAP_ALLREDUCE", "1") != "0"
 # one rank: GradientClipping's norm from the learner's conv reduce (ARL_NORM_FOLD=0: grad_sqnorm launch)
@@ -401,12 +406,29 @@ class A3C:
             side = self._side_streams(len(groups) - 1)
             for s in side:
                 s.wait_stream(main)                  # fork before any chain is issued
-            started = None
-            for g, envs in enumerate(groups):
-                s = main if g == 0 else side[g - 1]
-                if started is not None:
-                    s.wait_event(started)            # stagger: after chain g-1's first kernel
-                started = self._forward_chain(pair_pool, reward_pool, done_pool, pool_len, first, s, envs)
+            chains = [self._chain_steps(pair_pool, reward_pool, done_pool, pool_len, first,
+                                        main if g == 0 else side[g - 1], envs) for g, envs in enumerate(groups)]
+            started = [None] * len(chains)
+            if GROUP_ORDER == "chain":
+                for g, c in enumerate(chains):
+                    if g > 0 and started[g - 1] is not None:
+                        side[g - 1].wait_event(started[g - 1])   # stagger: after chain g-1's first kernel
+                    for ev in c:
+                        if ev is not None:
+                            started[g] = ev
+            else:
+                live = list(range(len(chains)))
+                step = 0
+                while live:
+                    for g in list(live):
+                        if step == 0 and g > 0 and started[g - 1] is not None:
+                            side[g - 1].wait_event(started[g - 1])   # stagger: after chain g-1's first kernel
+                        ev = next(chains[g], StopIteration)
+                        if ev is StopIteration:
+                            live.remove(g)
+                        elif ev is not None:
+                            started[g] = ev
+                    step += 1
             for s in side:
                 main.wait_stream(s)
             stream = main
@@ -425,9 +447,15 @@ class A3C:
     def _forward_chain(self, pair_pool, reward_pool, done_pool, pool_len, first, stream, envs):
         """T x (observe, act) + the bootstrap observe / act for envs (all if
         None) on `stream`; each observe + act is one launch shorter where the
-        net fuses them (DeviceNet.observe_act).  For an env group, returns an
-        event recorded after the chain's first kernel (the first conv launch,
-        with or without its observation)."""
+        net fuses them (DeviceNet.observe_act)."""
+        for _ in self._chain_steps(pair_pool, reward_pool, done_pool, pool_len, first, stream, envs):
+            pass
+
+    def _chain_steps(self, pair_pool, reward_pool, done_pool, pool_len, first, stream, envs):
+        """_forward_chain as a generator that yields after each step's
+        launches: for an env group, the first yield is an event recorded after
+        the chain's first kernel (the first conv launch, with or without its
+        observation), later ones None."""
         net, T = self.net, self.t_max
         ev = None
         stagger = envs is not None and STAGGER
@@ -440,6 +468,7 @@ class A3C:
                     ev = torch.cuda.Event()
                     ev.record(stream)
                     net.act(t, stream=stream, envs=envs)
+                    yield ev
                     continue
                 if obs:
                     net.observe_act(t, pair_pool, reward_pool, done_pool, pool_len, force_reset=(t == 0),
@@ -449,13 +478,14 @@ class A3C:
                 ev = torch.cuda.Event()
                 ev.record(stream)
                 net.act(t, mode=1 | ACT_AFTER_CONV, stream=stream, envs=envs)
+                yield ev
                 continue
             if obs:
                 net.observe_act(t, pair_pool, reward_pool, done_pool, pool_len, force_reset=(t == 0),
                                 resize_mode=self.resize_mode, stream=stream, envs=envs)
             else:
                 net.act(t, stream=stream, envs=envs)
-        return ev
+            yield None
 
     def finish_window(self, stream=None, conv=None):
         """The rest of a window after run_window(split_update=True): [the conv
