@@ -178,7 +178,8 @@ hipError_t launch_lstm_bptt(const float* dG, const float* Wl, const uint8_t* rs_
                             float* dhn, int n, bool cell, hipStream_t s);
 hipError_t launch_lstm_gates(const float* x, const float* h, const uint8_t* reset, const float* Wu, const float* Wl,
                              const float* b, float* gates, const float* c_prev, float* c_out, float* h_out, int n,
-                             bool cell, hipStream_t s);
+                             bool cell, hipStream_t s, const float* fc_slab = nullptr, const float* fc_b = nullptr,
+                             float* hfc = nullptr);
 
 // shared pieces of the heads' backward (net.hip)
 hipError_t launch_heads_bwd(const float* dl, const float* dv, const float* Wpi, const float* Wv, int A, int H,

@@ -33,27 +33,30 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 namespace {
 constexpr int LBM = 32, LBN = 64, LT = 512, LW = LT / 64;
 constexpr int LKC = 128;                       // K chunk (columns)
-constexpr int LROWS = LBM + LBN;               // 96 staged rows
+constexpr int LROWS = LBN + LBM;               // 96 staged rows: 64 of [Wu | Wl], then 32 of [x | h]
 constexpr int LLD = LKC / 4 + 1;               // 33 float4 per staged row (32 used)
 constexpr int LPIECES = (LROWS * LLD + 63) / 64;   // 50 LDS-DMA pieces (64 x 16 B) per chunk
+constexpr int LWPIECES = LBN * LLD / 64;       // 33: the W rows alone (XRED x chunks)
 constexpr int LSTAGE4 = LPIECES * 64;          // float4 per stage (incl. the last piece's overhang)
 constexpr int LSTAGES = 3;
 constexpr int TLD = 68;                        // epilogue tile row stride (floats)
+static_assert(LBN * LLD % 64 == 0, "the A rows start on a piece boundary");
 static_assert(LBM * TLD <= LSTAGE4 * 4, "epilogue tile fits one stage");
 static_assert(GATES % LBN == 0 && LBM * (LBN / 4) == LT, "one (row, unit) per thread");
-// pieces of wave w per chunk (piece it -> wave it % LW): 7 for waves 0, 1, else 6
-__host__ __device__ constexpr int wave_pieces(int w) { return (LPIECES - w + LW - 1) / LW; }
+// every wave issues the same number of pieces per chunk (pieces past the end
+// repeat the last one: the same bytes to the same LDS slots), so the counted
+// waits below are compile-time constants and the compiler's own wait for
+// the XRED partial loads counts exactly the DMA issued after them
+constexpr int LPW = (LPIECES + LW - 1) / LW;   // 7
+constexpr int LWPW = (LWPIECES + LW - 1) / LW; // 5
+constexpr int XRJ = LBM * HID / 4 / LT;        // XRED: float4 of the x tile per thread (4)
 }  // namespace
 
-__device__ inline void lstm_wait_vm(int n) {   // s_waitcnt vmcnt(n), n wave-uniform
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
+// s_waitcnt vmcnt(n) for the compile-time counts of the LSTM kernels
+template <int N>
+__device__ inline void lstm_wait_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 // LDS-only workgroup barrier (keeps the other chunks' LDS-DMA in flight; see conv_bwd.hip)
@@ -62,7 +65,7 @@ __device__ inline void lstm_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n
 __device__ inline float lstm_sigm(float x) { return __fdiv_rn(1.f, __fadd_rn(1.f, expf(-x))); }
 
 struct LstmGatesArgs {
-  const float* x;        // (n, 256) the upward input (the FC output)
+  const float* x;        // (n, 256) the upward input (the FC output); XRED: unused
   const float* h;        // (n, 256) h_prev (ignored on reset rows)
   const uint8_t* reset;  // (n) 1 = the state is None
   const float* Wu;       // (1024, 256)
@@ -72,29 +75,43 @@ struct LstmGatesArgs {
   const float* c_prev;   // (n, 256)
   float* c_out;          // (n, 256) (cell == 0: untouched)
   float* h_out;          // (n, 256)
+  // XRED: x = relu(sum_z slab[z] + fc_b) formed here from the FC forward's
+  // split-K partials (fc.hip, tickets == nullptr), summed in split order
+  // 0..7 from 0.f like fc_fwd_kernel's last arriver (bit-identical hfc);
+  // the column-tile-0 workgroups write it to hfc for the backward
+  const float* slab;     // (FC_SPLIT, n, 256)
+  const float* fc_b;     // (256)
+  float* hfc;            // (n, 256)
   int n, cell;
 };
 
+template <bool XRED>
 __global__ void __launch_bounds__(LT)
 lstm_gates_kernel(LstmGatesArgs a) {
   __shared__ __attribute__((aligned(16))) float S[LSTAGES * LSTAGE4 * 4];   // 153,600 B
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NTN = GATES / LBN;
   const int m0 = (blockIdx.x / NTN) * LBM, n0 = (blockIdx.x % NTN) * LBN;
-  const int pw = wave_pieces(wave);
 
   // ---- staging: chunk c into stage c % 3; slot i -> row i / LLD, float4
-  // column min(i % LLD, 31) (the pad slot re-loads the row's last float4)
+  // column min(i % LLD, 31) (the pad slot re-loads the row's last float4);
+  // rows 0..63 are W rows n0.., rows 64..95 env rows m0.. (XRED chunks 0, 1:
+  // the W rows only, the x rows are written from registers)
   auto issue = [&](int c) {
     float* st = S + 4 * LSTAGE4 * (c % LSTAGES);
     const int kc = (c & 1) * LKC;
     const float* xa = c < 2 ? a.x : a.h;
     const float* wb = c < 2 ? a.Wu : a.Wl;
-    for (int it = wave; it < LPIECES; it += LW) {
+    const bool wonly = XRED && c < 2;
+    const int np = wonly ? LWPIECES : LPIECES;
+#pragma unroll
+    for (int j = 0; j < LPW; ++j) {
+      if (wonly && j >= LWPW) break;   // uniform: c is a compile-time constant at every call
+      const int it = min(wave + LW * j, np - 1);
       const int i = min(it * 64 + lane, LROWS * LLD - 1);
       const int r = i / LLD, cc = min(i - r * LLD, LKC / 4 - 1);
-      const float* src = r < LBM ? xa + (int64_t)min(m0 + r, a.n - 1) * HID   // rows past n: any valid row
-                                 : wb + (int64_t)(n0 + r - LBM) * HID;
+      const float* src = r < LBN ? wb + (int64_t)(n0 + r) * HID
+                                 : xa + (int64_t)min(m0 + r - LBN, a.n - 1) * HID;   // rows past n: any valid row
       __builtin_amdgcn_global_load_lds(src + kc + 4 * cc, (__attribute__((address_space(3))) void*)(st + 4 * it * 64),
                                        16, 0, 0);
     }
@@ -106,15 +123,12 @@ lstm_gates_kernel(LstmGatesArgs a) {
   uint8_t rs[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) rs[r] = a.reset[min(m0 + ms * 16 + q * 4 + r, a.n - 1)];
-  issue(0);
-  issue(1);
-  issue(2);
-
+  typedef float xf4 __attribute__((ext_vector_type(4)));
   f32x4 accx = {0.f, 0.f, 0.f, 0.f}, acch = accx;
   auto compute = [&](int c, f32x4& acc) {
     const float* st = S + 4 * LSTAGE4 * (c % LSTAGES);
-    const float* Ar = st + (ms * 16 + col) * 4 * LLD + 4 * q;
-    const float* Br = st + (LBM + ns * 16 + col) * 4 * LLD + 4 * q;
+    const float* Ar = st + (LBN + ms * 16 + col) * 4 * LLD + 4 * q;
+    const float* Br = st + (ns * 16 + col) * 4 * LLD + 4 * q;
 #pragma unroll
     for (int s = 0; s < LKC / 16; ++s) {   // lane quarter q holds k = 16 s + 4 q + r of the chunk
       const f32x4 av = *reinterpret_cast<const f32x4*>(Ar + 16 * s);
@@ -123,18 +137,70 @@ lstm_gates_kernel(LstmGatesArgs a) {
       for (int r = 0; r < 4; ++r) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], bv[r], acc, 0, 0, 0);
     }
   };
-  // outstanding per wave after issuing chunks 0..2: 3 pw
-  lstm_wait_vm(2 * pw);       // chunk 0 landed (1, 2 in flight)
-  lstm_lds_barrier();
-  compute(0, accx);
-  lstm_wait_vm(pw);           // chunk 1 landed (2 in flight)
-  lstm_lds_barrier();         // also: everyone is done with stage 0
-  issue(3);                   // -> stage 0
-  compute(1, accx);
-  lstm_wait_vm(pw);           // chunk 2 landed (3 in flight)
+  xf4 xo[XRED ? XRJ : 1];
+  if constexpr (XRED) {
+    // chunks 0-2 go out first (chunks 0, 1: the W rows only), then the x
+    // tile's FC partials and bias (float4 idx = tid + 512 j: row idx / 64,
+    // float4 column idx % 64), summed as they land; every operand is in
+    // flight at once, so waiting for all of it before chunk 0's MFMAs costs
+    // little (the staging is latency-bound), and the compiler's own waits for
+    // the partials (it does not count LDS-DMA) stay correct whatever order
+    // it issues them in
+    issue(0);
+    issue(1);
+    issue(2);
+    // (scheduling barriers: every DMA piece, then every partial load, issued
+    // before the first add -- one wait for all of them)
+    __builtin_amdgcn_sched_barrier(0);
+    xf4 p[XRJ][FC_SPLIT], b[XRJ];
+#pragma unroll
+    for (int j = 0; j < XRJ; ++j) {
+      const int idx = tid + LT * j, row = idx >> 6, c4 = idx & 63;
+      const int64_t m = min(m0 + row, a.n - 1);
+#pragma unroll
+      for (int z = 0; z < FC_SPLIT; ++z)
+        p[j][z] = *reinterpret_cast<const xf4*>(a.slab + ((int64_t)z * a.n + m) * HID + 4 * c4);
+      b[j] = *reinterpret_cast<const xf4*>(a.fc_b + 4 * c4);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < XRJ; ++j) {
+      xf4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int z = 0; z < FC_SPLIT; ++z)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] = __fadd_rn(acc[e], p[j][z][e]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) xo[j][e] = fmaxf(__fadd_rn(acc[e], b[j][e]), 0.f);
+    }
+    lstm_wait_vm<0>();        // chunks 0-2 landed
+#pragma unroll
+    for (int j = 0; j < XRJ; ++j) {
+      const int idx = tid + LT * j, row = idx >> 6, c4 = idx & 63;
+      *reinterpret_cast<xf4*>(S + 4 * (LSTAGE4 * (c4 >> 5) + (LBN + row) * LLD + (c4 & 31))) = xo[j];
+    }
+    lstm_lds_barrier();       // chunks 0-2 and every wave's x rows in LDS
+    compute(0, accx);
+    lstm_lds_barrier();       // everyone is done with stage 0
+    issue(3);                 // -> stage 0
+    compute(1, accx);
+  } else {
+    issue(0);
+    issue(1);
+    issue(2);
+    // outstanding per wave after issuing chunks 0..2: 3 LPW
+    lstm_wait_vm<2 * LPW>();  // chunk 0 landed (1, 2 in flight)
+    lstm_lds_barrier();
+    compute(0, accx);
+    lstm_wait_vm<LPW>();      // chunk 1 landed (2 in flight)
+    lstm_lds_barrier();       // also: everyone is done with stage 0
+    issue(3);                 // -> stage 0
+    compute(1, accx);
+    lstm_wait_vm<LPW>();      // chunk 2 landed (3 in flight)
+  }
   lstm_lds_barrier();
   compute(2, acch);
-  lstm_wait_vm(0);            // chunk 3 landed
+  lstm_wait_vm<0>();          // chunk 3 landed
   lstm_lds_barrier();
   compute(3, acch);
 
@@ -144,6 +210,15 @@ lstm_gates_kernel(LstmGatesArgs a) {
 #pragma unroll
   for (int r = 0; r < 4; ++r)
     T[(ms * 16 + q * 4 + r) * TLD + ns * 16 + col] = rs[r] ? accx[r] : __fadd_rn(accx[r], acch[r]);
+  if constexpr (XRED) {
+    if (n0 == 0) {   // hfc for the backward, from the column-tile-0 workgroups
+#pragma unroll
+      for (int j = 0; j < XRJ; ++j) {
+        const int idx = tid + LT * j, row = idx >> 6, c4 = idx & 63;
+        if (m0 + row < a.n) *reinterpret_cast<xf4*>(a.hfc + (int64_t)(m0 + row) * HID + 4 * c4) = xo[j];
+      }
+    }
+  }
   lstm_lds_barrier();
   const int row = tid >> 4, u = tid & 15, m = m0 + row, n = n0 + 4 * u;
   if (m >= a.n) return;
@@ -162,11 +237,17 @@ lstm_gates_kernel(LstmGatesArgs a) {
 
 hipError_t launch_lstm_gates(const float* x, const float* h, const uint8_t* reset, const float* Wu, const float* Wl,
                              const float* b, float* gates, const float* c_prev, float* c_out, float* h_out, int n,
-                             bool cell, hipStream_t s) {
+                             bool cell, hipStream_t s, const float* fc_slab, const float* fc_b, float* hfc) {
   if (n <= 0) return hipSuccess;
-  const LstmGatesArgs a{x, h, reset, Wu, Wl, b, gates, c_prev, c_out, h_out, n, cell ? 1 : 0};
+  const LstmGatesArgs a{x, h, reset, Wu, Wl, b, gates, c_prev, c_out, h_out, fc_slab, fc_b, hfc, n, cell ? 1 : 0};
   const unsigned blocks = (unsigned)(((n + LBM - 1) / LBM) * (GATES / LBN));
-  hipLaunchKernelGGL(lstm_gates_kernel, dim3(blocks), dim3(LT), 0, s, a);
+  if (fc_slab != nullptr) {
+    if (fc_b == nullptr || hfc == nullptr) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(lstm_gates_kernel<true>, dim3(blocks), dim3(LT), 0, s, a);
+  } else {
+    if (x == nullptr) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(lstm_gates_kernel<false>, dim3(blocks), dim3(LT), 0, s, a);
+  }
   return hipGetLastError();
 }
 

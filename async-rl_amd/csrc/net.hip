@@ -191,6 +191,12 @@ static const bool LSTM_GEMM_GENERIC = [] {
   const char* e = getenv("ARL_LSTM_GEMM");
   return e != nullptr && e[0] == 'g';
 }();
+// ARL_LSTM_XRED=0: the FC forward's ticket reduce writes hfc and the gate kernel stages it
+// (the A arm for the reduce in the gate kernel's staging)
+static const bool LSTM_XRED = [] {
+  const char* e = getenv("ARL_LSTM_XRED");
+  return e == nullptr || e[0] != '0';
+}();
 
 // gates = [x | h] [Wu ; Wl]^T + b, then the cell: c_out, h_out (rows [0, n))
 template <class AOp, class BOp>
@@ -529,10 +535,30 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne, con
                                              net.at<float>(net.w_logpa) + o),
                             s);
   }
+  // LSTM: the FC's split-K partials only, their reduce + bias + relu in the gate kernel's
+  // staging (lstm.hip XRED); ARL_LSTM_XRED=0 / the generic gate GEMM: the FC's ticket reduce
+  const bool xred = !LSTM_GEMM_GENERIC && LSTM_XRED;
   ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab,
-                        net.at<int>(net.w_tick) + fc_fwd_tiles(e0), hfc, s));
+                        xred ? nullptr : net.at<int>(net.w_tick) + fc_fwd_tiles(e0), xred ? nullptr : hfc, s));
   const float* hpol = hfc;
-  if (net.arch == ARCH_LSTM) {
+  if (xred) {
+    const int64_t r0 = (int64_t)t * n + e0;
+    const float* hprev = net.at<float>(net.w_hbuf) + r0 * HID;
+    float* hout = net.at<float>(net.w_hbuf) + (r0 + n) * HID;
+    float* cout = net.at<float>(net.w_cbuf) + (r0 + n) * HID;
+    const uint8_t* rs = net.at<uint8_t>(net.w_reset) + r0;
+    float* gates = net.at<float>(net.w_gates) + r0 * GATES;
+    const float* cprev = net.at<float>(net.w_cbuf) + r0 * HID;
+    ARL_TRY(launch_lstm_gates(nullptr, hprev, rs, P + net.o_luW, P + net.o_llW, P + net.o_lub, gates, cprev, cout,
+                              hout, ne, !LSTM_SPLIT, s, fc_slab, P + net.o_fcb, hfc));
+    if (LSTM_SPLIT) {
+      const int64_t cnt = (int64_t)ne * HID;
+      hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, gates, cprev,
+                         rs, cout, hout, cnt);
+      ARL_TRY(hipGetLastError());
+    }
+    hpol = hout;
+  } else if (net.arch == ARCH_LSTM) {
     const int64_t r0 = (int64_t)t * n + e0;
     float* gates = net.at<float>(net.w_gates) + r0 * GATES;
     const float* hprev = net.at<float>(net.w_hbuf) + r0 * HID;
