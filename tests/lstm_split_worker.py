@@ -1,8 +1,9 @@
 """Runs two LSTM windows (eager + graph-captured) and one pi_and_v call and
 saves actions, values, hidden states, gradients and parameters to an .npz
-(argv[1]); test_gpu_parity.test_lstm_fused_cell_identical runs it with
-ARL_LSTM_SPLIT=0 / 1 (cell fused into the gate GEMM / BPTT reduce, or
-separate launches) and compares the files bitwise."""
+(argv[1]); test_gpu_parity.test_lstm_fused_cell_identical runs it under
+the LSTM knobs (ARL_LSTM_SPLIT, ARL_LSTM_XRED, ARL_GROUP_ORDER) and compares
+the files bitwise.  argv[2] == "one": a single window, its gradients only
+(test_lstm_bptt_kernel_matches_generic)."""
 import os
 import sys
 
@@ -15,7 +16,7 @@ from sim import make_pools  # noqa: E402
 from asyncrl_amd import A3C, A3CLSTM, GradientClipping, RMSpropAsync  # noqa: E402
 
 
-def main(out):
+def main(out, one=False):
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(123)
     N, T, P = 72, 5, 7
@@ -26,7 +27,12 @@ def main(out):
     o = RMSpropAsync(lr=7e-4, eps=0.1, alpha=0.99).setup(m)
     o.add_hook(GradientClipping(40))
     ag = A3C(m, o, T, 0.99)
-    ag.run_window(dp, dr, dd, P, first=True, env_groups=2)
+    ag.run_window(dp, dr, dd, P, first=True, env_groups=2, split_update=one)
+    if one:
+        torch.cuda.synchronize()
+        np.savez(out, grads=ag.net.grads.detach().cpu().numpy(),
+                 hbuf=ag.net.buffer("hbuf", torch.float32).detach().cpu().numpy())
+        return
     ag.run_window(dp, dr, dd, P, env_groups=1)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -49,4 +55,4 @@ def main(out):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], len(sys.argv) > 2 and sys.argv[2] == "one")

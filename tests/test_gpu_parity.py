@@ -686,23 +686,49 @@ def test_fused_observe_identical(gpu, arch, N, groups, resize_mode):
 
 
 def test_lstm_fused_cell_identical(gpu, tmp_path):
-    """The LSTM cell fused into the gate GEMM's epilogue (forward, act and
-    pi_and_v) and into the BPTT reduce (backward) gives the same bits as the
-    cell as separate launches (ARL_LSTM_SPLIT=1): hidden / cell states, gates,
-    actions, values, gradients, parameters."""
+    """The LSTM cell fused into the gate kernel's epilogue (forward, act and
+    pi_and_v) and into the BPTT step (backward) gives the same bits as the
+    cell as separate launches (ARL_LSTM_SPLIT=1); so do the FC forward's
+    ticket reduce instead of the reduce in the gate kernel's staging
+    (ARL_LSTM_XRED=0) and the env-group chains issued chain by chain
+    (ARL_GROUP_ORDER=chain): hidden / cell states, gates, actions, values,
+    gradients, parameters."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     outs = []
-    for split in ("0", "1"):
-        f = str(tmp_path / f"lstm_{split}.npz")
-        env = dict(os.environ, ARL_LSTM_SPLIT=split)
+    for extra in ({}, {"ARL_LSTM_SPLIT": "1"}, {"ARL_LSTM_XRED": "0"}, {"ARL_GROUP_ORDER": "chain"}):
+        f = str(tmp_path / f"lstm_{len(outs)}.npz")
+        env = dict(os.environ, **extra)
         subprocess.run([sys.executable, os.path.join(here, "lstm_split_worker.py"), f], env=env, check=True,
                        timeout=240)
         outs.append(np.load(f))
     assert int((outs[0]["hbuf"] != 0).sum()) > 0
-    for k in outs[0].files:
-        assert np.array_equal(outs[0][k], outs[1][k]), k
+    for o in outs[1:]:
+        for k in outs[0].files:
+            assert np.array_equal(outs[0][k], o[k]), k
+
+
+def test_lstm_bptt_kernel_matches_generic(gpu, tmp_path):
+    """The fused BPTT step (lstm.hip lstm_bptt_kernel: dh GEMM in two K
+    halves, reset mask, the previous step's cell backward) against the
+    split-K GEMM + f64 reduce + cell launches (ARL_LSTM_BPTT=generic): same
+    forward bits, window gradients within 1e-5 of each tensor's scale (both
+    sum exact f32 products; only the order differs)."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    outs = []
+    for extra in ({}, {"ARL_LSTM_BPTT": "generic"}):
+        f = str(tmp_path / f"bptt_{len(outs)}.npz")
+        env = dict(os.environ, **extra)
+        subprocess.run([sys.executable, os.path.join(here, "lstm_split_worker.py"), f, "one"], env=env, check=True,
+                       timeout=240)
+        outs.append(np.load(f))
+    assert np.array_equal(outs[0]["hbuf"], outs[1]["hbuf"])
+    assert float(np.abs(outs[0]["grads"]).max()) > 0
+    ok, err = close_normscaled(outs[1]["grads"], outs[0]["grads"], 1e-5)
+    assert ok, err
 
 
 def test_fc_bwd_variants(gpu, tmp_path):
