@@ -244,7 +244,7 @@ class DeviceNet:
         return out
 
     STAGES = {"conv_fwd": 1, "fc_fwd": 2, "policy": 3, "fc_bwd": 4, "conv_bwd": 5, "returns": 6, "conv_reduce": 7,
-              "grad_sqnorm": 8}
+              "grad_sqnorm": 8, "lstm_gates": 9, "lstm_bptt": 10, "lstm_wgrad": 11}
 
     def run_stage(self, stage: str, t: int = 0, stream=None):
         """One window stage alone on the current workspace (timing / profiling)."""

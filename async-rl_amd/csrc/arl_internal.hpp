@@ -152,7 +152,8 @@ hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_tot
                         float clip, hipStream_t s, bool advance = false);
 hipError_t net_advance(Net& net, hipStream_t s);
 enum Stage { STAGE_CONV_FWD = 1, STAGE_FC_FWD = 2, STAGE_POLICY = 3, STAGE_FC_BWD = 4, STAGE_CONV_BWD = 5,
-             STAGE_RETURNS = 6, STAGE_CONV_REDUCE = 7, STAGE_GRAD_SQNORM = 8 };
+             STAGE_RETURNS = 6, STAGE_CONV_REDUCE = 7, STAGE_GRAD_SQNORM = 8,
+             STAGE_LSTM_GATES = 9, STAGE_LSTM_BPTT = 10, STAGE_LSTM_WGRAD = 11 };
 hipError_t net_stage(Net& net, int stage, int t, hipStream_t s);
 // keep: LSTM keep_same_state (the pi_and_v recurrent state is not advanced)
 hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_t s, bool keep = false);

@@ -675,6 +675,22 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
 // stream once LEARN_RETURNS is done, and LEARN_GATES_REDUCE / LEARN_FC_REDUCE
 // once LEARN_TRUNK is done, concurrently with the rest: nothing on the
 // critical path (dh -> FC -> conv backward) reads what they write.
+// LSTM gate weight gradients ([x | h | 1] operand, reset rows' h dropped) into
+// the LSTM slab and dfc = (dG Wu) * (hfc > 0), one dual-GEMM launch
+static hipError_t lstm_wgrad(Net& net, hipStream_t s) {
+  const int n = net.N, S = net.T * n;
+  const Plans pl = make_plans(net);
+  const float* dG = net.at<float>(net.w_dG);
+  const float* hfc = net.at<float>(net.w_hfc);
+  return launch_gemm2<64, 64, 32, 2, 2, GM, GM, GK, GM>(
+      gemm_job<64, 32>(ColMajor{dG, GATES}, LstmWB{hfc, net.at<float>(net.w_hbuf), net.at<uint8_t>(net.w_reset)},
+                       EpiSlab{net.at<float>(net.w_slab_lstm), GATES, 2 * HID + 1}, GATES, 2 * HID + 1, S, pl.lstm_w,
+                       64),
+      gemm_job<64, 32>(RowMajor{dG, GATES}, RowMajor{net.p + net.o_luW, HID}, EpiMask{net.at<float>(net.w_dfc), hfc, HID},
+                       S, HID, GATES, 1, 64),
+      s);
+}
+
 hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s) {
   if (net.arch == ARCH_FF_NATURE) return hipErrorInvalidValue;
   if (part == LEARN_RETURNS) net.norm_ready = false;   // a new gradient: no folded norm until net_learn's reduce
@@ -744,7 +760,6 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
   if (L) {
     const float* gates = net.at<float>(net.w_gates);
     const float* cbuf = net.at<float>(net.w_cbuf);
-    const float* hbuf = net.at<float>(net.w_hbuf);
     const uint8_t* rs = net.at<uint8_t>(net.w_reset);
     float* dG = net.at<float>(net.w_dG);
     float* dhn = net.at<float>(net.w_dhn);
@@ -784,12 +799,7 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
       }
     }
     // gate weight gradients and dfc = (dG Wu) * (hfc > 0): independent, one launch
-    ARL_TRY((launch_gemm2<64, 64, 32, 2, 2, GM, GM, GK, GM>(
-        gemm_job<64, 32>(ColMajor{dG, GATES}, LstmWB{hfc, hbuf, rs}, EpiSlab{slab_l, GATES, 2 * HID + 1}, GATES,
-                         2 * HID + 1, S, pl.lstm_w, 64),
-        gemm_job<64, 32>(RowMajor{dG, GATES}, RowMajor{P + net.o_luW, HID}, EpiMask{dfc, hfc, HID}, S, HID, GATES, 1,
-                         64),
-        s)));
+    ARL_TRY(lstm_wgrad(net, s));
   }
   // 3. FC: dW + db straight into the gradient and da2 = (dfc W) * (a2 > 0),
   //    one launch (fc_bwd.hip)
@@ -823,8 +833,8 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
                              net.at<int64_t>(net.w_ctl), n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W,
                              P + net.o_c2b, net.at<float>(net.w_a1) + (int64_t)t * n * A1, a2 + (int64_t)t * n * A2,
                              s, net.layout);
-    case STAGE_FC_FWD:   // as in net_act: FF runs the partials-only FC, its reduce is in the policy stage
-      if (net.arch != ARCH_LSTM)
+    case STAGE_FC_FWD:   // as in net_act: FF (and the LSTM's XRED gate kernel) reduce the partials downstream
+      if (net.arch != ARCH_LSTM || (!LSTM_GEMM_GENERIC && LSTM_XRED))
         return launch_fc_fwd(a2 + (int64_t)t * n * A2, n, P + net.o_fcW, P + net.o_fcb, slab, nullptr, nullptr, s);
       return fc_forward(net, n, a2 + (int64_t)t * n * A2, hfc + (int64_t)t * n * HID, s);
     case STAGE_POLICY: {
@@ -867,6 +877,31 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
                                 norm_fold_args(net));   // as arl_learn launches it
     case STAGE_GRAD_SQNORM:
       return launch_grad_sqnorm(net.g, net.param_floats, net.at<double>(net.w_norm), net.norm_blocks, s);
+    case STAGE_LSTM_GATES: {   // as net_act's LSTM step over all envs
+      if (net.arch != ARCH_LSTM) return hipErrorInvalidValue;
+      const int64_t r0 = (int64_t)t * n;
+      const bool xred = !LSTM_GEMM_GENERIC && LSTM_XRED;
+      return launch_lstm_gates(xred ? nullptr : hfc + r0 * HID, net.at<float>(net.w_hbuf) + r0 * HID,
+                               net.at<uint8_t>(net.w_reset) + r0, P + net.o_luW, P + net.o_llW, P + net.o_lub,
+                               net.at<float>(net.w_gates) + r0 * GATES, net.at<float>(net.w_cbuf) + r0 * HID,
+                               net.at<float>(net.w_cbuf) + (r0 + n) * HID, net.at<float>(net.w_hbuf) + (r0 + n) * HID,
+                               n, true, s, xred ? slab : nullptr, xred ? P + net.o_fcb : nullptr,
+                               xred ? hfc + r0 * HID : nullptr);
+    }
+    case STAGE_LSTM_BPTT: {    // the BPTT step t -> t - 1 (t = T - 1 when t is 0)
+      if (net.arch != ARCH_LSTM || net.T < 2) return hipErrorInvalidValue;
+      const int tt = t > 0 && t < net.T ? t : net.T - 1;
+      const int64_t o = (int64_t)tt * n, op = o - n;
+      float* dG = net.at<float>(net.w_dG);
+      const float* cbuf = net.at<float>(net.w_cbuf);
+      const uint8_t* rs = net.at<uint8_t>(net.w_reset);
+      return launch_lstm_bptt(dG + o * GATES, P + net.o_llW, rs + o, net.at<float>(net.w_gates) + op * GATES,
+                              cbuf + (op + n) * HID, cbuf + op * HID, rs + op, net.at<float>(net.w_dh) + op * HID,
+                              net.at<float>(net.w_dcn), dG + op * GATES, net.at<float>(net.w_dhn), n, true, s);
+    }
+    case STAGE_LSTM_WGRAD:
+      if (net.arch != ARCH_LSTM) return hipErrorInvalidValue;
+      return lstm_wgrad(net, s);
     default:
       return hipErrorInvalidValue;
   }

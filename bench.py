@@ -58,6 +58,14 @@ FC_FWD_FLOP_PER_ENV = 2 * 2592 * 256                                     # 1,327
 CONV_BWD_FLOP_PER_SAMPLE = 2 * (32 * 256 * 81 + 81 * 32 * 256 + 400 * 16 * 256)   # dW2 + convT + dW1
 HID_BYTES = 256 * 4
 FC_SPLIT = 8                                # fc.hip split-K (partial slabs read by policy_fc_kernel)
+# LSTM (a3c_ale.py:50-51,62; L.LSTM(256, 256)): gates = [x | h] [Wu ; Wl]^T (K = 512, N = 1024);
+# BPTT dh = dG Wl (K = 1024, N = 256); gate weight gradients [x | h | 1]^T dG (513 x 1024 per
+# sample) + dfc = dG Wu (K = 1024, N = 256)
+LSTM_GATES_FLOP_PER_ENV = 2 * 512 * 1024
+LSTM_BPTT_FLOP_PER_ENV = 2 * 1024 * 256
+LSTM_WGRAD_FLOP_PER_SAMPLE = 2 * 513 * 1024 + 2 * 1024 * 256
+# the gate kernel forms x from the FC's split-K partials unless ARL_LSTM_XRED=0 (net.hip)
+LSTM_XRED = os.environ.get("ARL_LSTM_XRED", "1")[:1] != "0"
 # ViZDoom models (train_a3c_doom.py:28,46): conv1 K = 3 * 64 (the kernels' zero input plane is not counted)
 DOOM_CONV_FWD_FLOP_PER_ENV = 2 * (400 * 16 * 192 + 81 * 32 * 256)
 DOOM_CONV_BWD_FLOP_PER_SAMPLE = 2 * (32 * 256 * 81 + 81 * 32 * 256 + 400 * 16 * 192)
@@ -557,8 +565,8 @@ def main(a):
             ("conv_fwd", "gemm_kernel x3 (implicit-GEMM convs)" if nat else "conv_fwd_kernel<false>",
              lambda i: net.run_stage("conv_fwd", i % T, stream=stream), 1 if fused else T + 1, "mfma",
              N * conv_fwd_flop),
-            ("fc_fwd", "gemm_kernel + reduce_grad_kernel" if nat else "fc_fwd_kernel" if lstm else
-             "fc_fwd_kernel (split-K partials)",
+            ("fc_fwd", "gemm_kernel + reduce_grad_kernel" if nat else
+             "fc_fwd_kernel (split-K partials)" if (not lstm or LSTM_XRED) else "fc_fwd_kernel",
              lambda i: net.run_stage("fc_fwd", i % T, stream=stream), T + 1, "mfma", N * fc_fwd_flop),
             # FF NIPS / Doom FF: the FC split-K reduce + bias + relu runs in the policy launch
             # (policy_fc_kernel): it also reads the 8 partial slabs and writes h
@@ -569,6 +577,17 @@ def main(a):
              lambda i: net.run_stage("fc_bwd", 0, stream=stream), 1, "mfma", 2 * fc_fwd_flop * S),
             ("conv_bwd", "gemm_kernel x9 + reduce_grad_kernel x3" if nat else "conv_bwd_kernel",
              lambda i: net.run_stage("conv_bwd", 0, stream=stream), 1, "mfma", S * conv_bwd_flop),
+            # LSTM: the gate kernel (LSTM_XRED: it also forms x from the FC's partials), the
+            # truncated-BPTT steps, the gate weight gradients + dfc (a3c_ale.py:50-51,62)
+            ("lstm_gates", "lstm_gates_kernel" + ("<true> (FC reduce + gates + cell)" if LSTM_XRED else "<false>"),
+             lambda i: net.run_stage("lstm_gates", i % T, stream=stream), T + 1, "mfma",
+             N * LSTM_GATES_FLOP_PER_ENV) if lstm and not doom else None,
+            ("lstm_bptt", "lstm_bptt_kernel (dh GEMM + cell backward)",
+             lambda i: net.run_stage("lstm_bptt", T - 1 - i % (T - 1), stream=stream), T - 1, "mfma",
+             N * LSTM_BPTT_FLOP_PER_ENV) if lstm and not doom and T > 1 else None,
+            ("lstm_wgrad", "gemm2_kernel (gate dW + dfc)",
+             lambda i: net.run_stage("lstm_wgrad", stream=stream), 1, "mfma",
+             S * LSTM_WGRAD_FLOP_PER_SAMPLE) if lstm and not doom else None,
             ("rmsprop", "rmsprop_kernel", lambda i: net.optimize(lr0=1e-12, clip=0.0, stream=stream), 1, "hbm",
              net.n_params * RMSPROP_BYTES_PER_PARAM),
             # the learner's small HBM-bound launches (NIPS heads): returns + loss gradient + heads dh,

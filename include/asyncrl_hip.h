@@ -249,7 +249,10 @@ enum {
   ARL_STAGE_RETURNS = 6,    /* n-step returns + loss gradient + heads dh (gamma 0.99, beta 0.01, v coef 0.5,
                                clipped rewards): the learner's first launch */
   ARL_STAGE_CONV_REDUCE = 7,  /* the conv backward's slab reduce into the conv gradients */
-  ARL_STAGE_GRAD_SQNORM = 8   /* squared-norm partials of the whole gradient (GradientClipping) */
+  ARL_STAGE_GRAD_SQNORM = 8,  /* squared-norm partials of the whole gradient (GradientClipping) */
+  ARL_STAGE_LSTM_GATES = 9,   /* LSTM: the gate kernel of slot t (cell in its epilogue) */
+  ARL_STAGE_LSTM_BPTT = 10,   /* LSTM: one truncated-BPTT step (dh GEMM + the previous step's cell backward) */
+  ARL_STAGE_LSTM_WGRAD = 11   /* LSTM: the gate weight gradients + dfc (one dual-GEMM launch) */
 };
 int arl_run_stage(arl_net* net, int stage, int t, void* stream);
 
