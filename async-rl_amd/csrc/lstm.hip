@@ -129,12 +129,22 @@ lstm_gates_kernel(LstmGatesArgs a) {
     const float* st = S + 4 * LSTAGE4 * (c % LSTAGES);
     const float* Ar = st + (LBN + ms * 16 + col) * 4 * LLD + 4 * q;
     const float* Br = st + (ns * 16 + col) * 4 * LLD + 4 * q;
+    // lane quarter q holds k = 16 s + 4 q + r of the chunk; the fragments of
+    // four s read first (one LDS wait), then their 16 MFMAs back to back
 #pragma unroll
-    for (int s = 0; s < LKC / 16; ++s) {   // lane quarter q holds k = 16 s + 4 q + r of the chunk
-      const f32x4 av = *reinterpret_cast<const f32x4*>(Ar + 16 * s);
-      const f32x4 bv = *reinterpret_cast<const f32x4*>(Br + 16 * s);
+    for (int s0 = 0; s0 < LKC / 16; s0 += 4) {
+      f32x4 av[4], bv[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], bv[r], acc, 0, 0, 0);
+      for (int s = 0; s < 4; ++s) {
+        av[s] = *reinterpret_cast<const f32x4*>(Ar + 16 * (s0 + s));
+        bv[s] = *reinterpret_cast<const f32x4*>(Br + 16 * (s0 + s));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s][r], bv[s][r], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
   xf4 xo[XRED ? XRJ : 1];
@@ -374,16 +384,24 @@ lstm_bptt_kernel(LstmBpttArgs a) {
     lstm_lds_barrier();                       // ... for every wave, and stage (c + 3) % 4 is free
     if (c + 3 < BNCH) issue(c + 3);
     const float* st = S + 4 * BSTAGE4 * (c % BSTAGES);
-    const float* Ar = st + (ms * 16 + col) * 4 * BA_LD + 4 * q;
-    const float* Bs = st + 4 * 64 * BA_PC + ns * 16 + col;
+    const float* Ar = st + (ms * 16 + col) * 4 * BA_LD + 4 * q + 64 * kh;
+    const float* Bs = st + 4 * 64 * BA_PC + ns * 16 + col + (64 * kh + 4 * q) * 4 * BB_LD;
+    // k = 16 s + 4 q + r of the chunk, s = 4 kh + s4: every fragment of the
+    // chunk read first (one LDS wait), then the 16 MFMAs back to back
+    f32x4 av[4];
+    float bv[4][4];
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {          // k = 16 s + 4 q + r of the chunk, s = 4 kh + s4
-      const int s = 4 * kh + s4;
-      const f32x4 av = *reinterpret_cast<const f32x4*>(Ar + 16 * s);
+    for (int s4 = 0; s4 < 4; ++s4) {
+      av[s4] = *reinterpret_cast<const f32x4*>(Ar + 16 * s4);
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], Bs[(16 * s + 4 * q + r) * 4 * BB_LD], acc, 0, 0, 0);
+      for (int r = 0; r < 4; ++r) bv[s4][r] = Bs[(16 * s4 + r) * 4 * BB_LD];
     }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s4][r], bv[s4][r], acc, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
   // ---- the two K halves: into stage 0 (free: chunk 4's stage, done two chunks ago), fixed order
   lstm_lds_barrier();
