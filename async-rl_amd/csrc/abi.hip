@@ -155,6 +155,7 @@ int arl_net_reset(arl_net* h, void* s) {
     e = hipMemsetAsync(n.ws + n.w_hbuf, 0, (size_t)(n.T + 2) * n.N * arl::HID * 4, S(s));
     if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_cbuf, 0, (size_t)(n.T + 2) * n.N * arl::HID * 4, S(s));
     if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_eval_reset, 1, (size_t)n.N, S(s));
+    if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_zero, 0, arl::ZERO_ROW_FLOATS * 4, S(s));
   }
   return hip_status(e, "net_reset");
 }
@@ -336,9 +337,11 @@ int arl_observe_act_envs(arl_net* h, int t, int e0, int ne, const uint8_t* pair_
 
 int arl_run_stage(arl_net* h, int stage, int t, void* s) {
   NEED_BOUND(h);
-  if (stage < ARL_STAGE_CONV_FWD || stage > ARL_STAGE_GRAD_SQNORM) return fail(ARL_EINVAL, "run_stage: unknown stage");
+  if (stage < ARL_STAGE_CONV_FWD || stage > ARL_STAGE_LSTM_WGRAD) return fail(ARL_EINVAL, "run_stage: unknown stage");
   if (stage >= ARL_STAGE_RETURNS && h->net.arch == arl::ARCH_FF_NATURE)
     return fail(ARL_EINVAL, "run_stage: returns / conv reduce / grad sqnorm stages are NIPS-head only");
+  if (stage >= ARL_STAGE_LSTM_GATES && h->net.arch != arl::ARCH_LSTM)
+    return fail(ARL_EINVAL, "run_stage: the LSTM stages need an LSTM net");
   if (t < 0 || t > h->net.T) return fail(ARL_EINVAL, "run_stage: t out of [0, t_max]");
   return hip_status(arl::net_stage(h->net, stage, t, S(s)), "run_stage");
 }

@@ -41,6 +41,7 @@ constexpr int A1 = C1_OC * C1_P;       // 6400
 constexpr int A2 = C2_OC * C2_P;       // 2592
 constexpr int HID = 256;
 constexpr int GATES = 4 * HID;
+constexpr int ZERO_ROW_FLOATS = 64;     // LSTM: the zero row a reset sample's h_prev is DMA'd from (fc_bwd.hip)
 constexpr int MAXA = 32;               // max actions supported by the policy kernel
 // NatureDQNHead (dqn_head.py:6-28): 4->32 k8 s4 (20x20), 32->64 k4 s2 (9x9),
 // 64->64 k3 s1 (7x7), Linear 3136 -> 512
@@ -116,7 +117,7 @@ struct Net {
   int64_t ws_bytes;
   int64_t w_ctl, w_frames, w_nvalid, w_reset, w_rewards, w_dones, w_a1, w_a2, w_hfc, w_gates, w_hbuf,
       w_cbuf, w_logits, w_probs, w_logp, w_v, w_ent, w_logpa, w_act, w_dlogits, w_dv, w_dh, w_dfc,
-      w_dG, w_dhn, w_dcn, w_da2, w_slab, w_norm, w_loss, w_tick, w_fcb_part = 0, w_fcb_tick = 0;
+      w_dG, w_dhn, w_dcn, w_da2, w_slab, w_norm, w_loss, w_tick, w_fcb_part = 0, w_fcb_tick = 0, w_zero = 0;
   int64_t w_a3 = 0, w_da1 = 0, w_da3 = 0;   // Nature head only (w_da1 also ARCH_STATES)
   // LSTM recurrent state of pi_and_v on explicit states (A3CLSTM.pi_and_v, a3c_ale.py:55-63):
   // h, c (n, 256), the step's outputs hn, cn, and reset flags (1 = state is None)
@@ -249,7 +250,11 @@ struct HeadsDW {
 };
 hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int S, float* gW, float* gb, float* da2,
                          float* part, int* tick, hipStream_t s, const HeadsDW* heads = nullptr);
-int64_t fc_bwd_part_floats(int S);   // workspace of its in-launch split reduction
+// LSTM gate weight gradients (upward W / b, lateral W) + dfc = (dG Wu) * (hfc > 0), the same kernel
+hipError_t launch_lstm_wgrad(const float* dG, const float* hfc, const float* hprev, const uint8_t* reset,
+                             const float* zero, const float* Wu, int S, float* gWu, float* gWl, float* gbu, float* dfc,
+                             float* part, int* tick, hipStream_t s);
+int64_t fc_bwd_part_floats(int S);   // workspace of its in-launch split reduction (both launches)
 int fc_bwd_tickets();                 // int counters, zero before the first launch (re-armed by it)
 hipError_t launch_policy_args(const float* h, int64_t n, const PolicyArgs& pa, hipStream_t s, int hid);
 // policy arguments of a forward on explicit states (arl_forward_states): slot

@@ -65,15 +65,44 @@ constexpr int NW = NT / 64;
 constexpr int BK = 32;                  // K chunk (rows of a stage)
 constexpr int STAGE = 8192;             // floats per LDS stage
 constexpr int AJ = 128, AK = 64;        // job A tile: 128 j x 64 k
-constexpr int NJA = HID / AJ;           // 2
-constexpr int NKA = (A2 + AK - 1) / AK; // 41 (the last one half full)
-constexpr int NTA = NJA * NKA;          // 82 job A tiles per range
 constexpr int BN = 128;                 // job B tile: 32 MT samples x 128 k
-constexpr int NKB = (A2 + BN - 1) / BN; // 21 (the last one a quarter full)
 constexpr int PART = AJ * AK + AJ;      // floats per published partial (dW tile + db)
 constexpr int FLUSH = 4;                // job A: f32 MFMA sums over 4 chunks (128 samples), then f64
-static_assert(HID % AJ == 0 && HID % BK == 0 && A2 % 4 == 0 && A2 % AK == 32, "tiles");
 static_assert(BK * (AJ + AK) <= STAGE && 128 * BK + BK * BN <= STAGE, "stage size");
+
+// The two layers this kernel serves (the same dual-GEMM shape):
+//   dW[j][k] = sum_s dY[s][j] X[s][k] (+ db[j] = sum_s dY[s][j]),
+//   dX[s][k] = (sum_j dY[s][j] W[j][k]) * (mask[s][k] > 0)
+// ShapeFC: Linear(2592, 256) of the NIPS head (dqn_head.py:43): dY = dfc (S x
+//   256), X = a2 (S x 2592), W (256 x 2592), mask = a2, dX = da2.
+// ShapeLSTM: the gate weights of L.LSTM(256, 256) (a3c_ale.py:50-51,62;
+//   Chainer's LSTM gates = upward(x) + lateral(h)): dY = dG (S x 1024), X =
+//   [x | h_prev] (S x 512; h_prev rows of samples whose env reset at that step
+//   read 0, as the forward saw them), dW = [upward W | lateral W], db = the
+//   upward bias; dX = dfc = (dG Wu) * (hfc > 0).  Replaces the generic dual
+//   GEMM + slab reduce of round 2 (ARL_LSTM_WGRAD=gemm keeps it).
+struct ShapeFC {
+  static constexpr int J = HID, KW = A2, KW1 = A2, NB = A2;
+  static constexpr bool kLstm = false;
+};
+struct ShapeLSTM {
+  static constexpr int J = GATES, KW = 2 * HID, KW1 = HID, NB = HID;
+  static constexpr bool kLstm = true;
+};
+template <class SH>
+struct Dims {
+  static constexpr int NJA = SH::J / AJ;              // FC 2, LSTM 8
+  static constexpr int NKA = (SH::KW + AK - 1) / AK;  // FC 41 (the last one half full), LSTM 8
+  static constexpr int NTA = NJA * NKA;               // job A tiles per range: FC 82, LSTM 64
+  static constexpr int NKB = (SH::NB + BN - 1) / BN;  // FC 21 (the last one a quarter full), LSTM 2
+  static constexpr int NCHB = SH::J / BK;             // job B K chunks: FC 8, LSTM 32
+  static_assert(SH::J % AJ == 0 && SH::J % BK == 0 && SH::KW % 4 == 0 && SH::NB % 4 == 0, "tiles");
+  static_assert(SH::KW1 % AK == 0 || SH::KW1 == SH::KW, "a k tile never straddles the two dW blocks");
+};
+static_assert(A2 % AK == 32, "FC: the last job A k tile is half full");
+constexpr int NTA_MAX = Dims<ShapeFC>::NTA;
+static_assert(Dims<ShapeLSTM>::NTA <= NTA_MAX, "ticket / partial workspace");
+constexpr int RST_MAX = 1024;           // LSTM job A: reset flags of a sample range, staged in LDS
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -104,8 +133,10 @@ __device__ inline void barrier_lds() {
 // tile row r = global row min(row0 + r, rmax); logical 16-byte chunk c of
 // row r lands at physical chunk c ^ key(r).  Wave w issues the 1 KB pieces
 // w, w + NW, ...
-template <int R, int WC, int KEY>
-__device__ inline void stage_tile(float* dst, const float* __restrict__ g, int64_t ld, int row0, int rmax, int col0) {
+// ZR (LSTM h_prev): rows whose flag zr[row - zbase] is set (LDS) read the zero row instead.
+template <int R, int WC, int KEY, bool ZR = false>
+__device__ inline void stage_tile(float* dst, const float* __restrict__ g, int64_t ld, int row0, int rmax, int col0,
+                                  const uint8_t* zr = nullptr, int zbase = 0, const float* zero = nullptr) {
   constexpr int CPR = WC / 4;                 // chunks per row
   constexpr int NI = R * WC * 4 / 1024;       // 1 KB pieces
   static_assert(NI % NW == 0, "whole pieces per wave");
@@ -120,18 +151,22 @@ __device__ inline void stage_tile(float* dst, const float* __restrict__ g, int64
     else if constexpr (KEY == 2) key = (r >> 1) & 7;
     const int row = min(row0 + r, rmax);
     const float* src = g + (int64_t)row * ld + col0 + 4 * (pc ^ key);
+    if constexpr (ZR) {
+      if (zr[row - zbase]) src = zero + 4 * (pc ^ key);
+    }
     __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(dst + it * 256), 16, 0, 0);
   }
 }
 
 struct FcBwdArgs {
-  const float* dfc;   // (S, 256)
-  const float* a2;    // (S + 1, 2592): job A's last k tile reads 32 floats past a row's end
-  const float* W;     // (256, 2592) followed by more parameters
+  const float* dfc;   // dY: (S, 256) FC / dG (S, 1024) LSTM
+  const float* a2;    // X (FC: (S + 1, 2592): job A's last k tile reads 32 floats past a row's end);
+                      // LSTM: x = hfc (S, 256), also the ReLU mask of both
+  const float* W;     // (256, 2592) followed by more parameters / LSTM Wu (1024, 256)
   int S, Z, kpz;      // job A: Z sample ranges of kpz samples (multiple of BK)
-  float* gW;          // (256, 2592)
-  float* gb;          // (256)
-  float* da2;         // (S, 2592)
+  float* gW;          // (256, 2592) / LSTM upward W (1024, 256)
+  float* gb;          // (256) / LSTM upward b (1024)
+  float* da2;         // dX: (S, 2592) / LSTM dfc (S, 256)
   float* part;        // (NTA, Z, PART) published job A partials (slot z = range z)
   int* tick;          // (2 NTA): arrival tickets per tile, then ready counts (spin)
   HeadsDW hd;         // job C (hd.dl null: none)
@@ -141,6 +176,11 @@ struct FcBwdArgs {
                       // 4 no job A reduction (wrong dW), 8 no job A k loop
   int spin;           // job A reduce: ticket first, the last range waits for the others' partials
   int xcd;            // XCD-aware job order (xcd_order)
+  // LSTM only
+  const float* hprev;      // h_prev (S, 256): the carry-in h of each sample's step (hbuf slot t)
+  const uint8_t* reset;    // (S): the env reset at that step (its h_prev reads 0)
+  const float* zero;       // >= 64 zero floats (the DMA source of a reset row)
+  float* gW2;              // lateral W (1024, 256)
 };
 
 // ---------------------------------------------------------------- job A: dW, db
@@ -162,8 +202,10 @@ __device__ inline void publish_dw(const FcBwdArgs& a, int tile, int z, const dou
       __hip_atomic_store(dst + AJ * AK + wm * 64 + 4 * col + t, (float)sb[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool SPLIT>
-__device__ void job_dw(const FcBwdArgs& a, int job, float* lds) {
+template <bool SPLIT, class SH>
+__device__ void job_dw(const FcBwdArgs& a, int job, float* lds, uint8_t* rst) {
+  using D = Dims<SH>;
+  constexpr int NTA = D::NTA;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, col = lane & 15;
   const int wm = wave >> 1, wn = wave & 1;   // wave: 64 j x 32 k
@@ -172,13 +214,23 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds) {
     const int lin = xcd_order(job, NTA * a.Z);
     z = lin / NTA;
     const int r = lin - z * NTA;
-    tile = (r % NJA) * NKA + r / NJA;
+    tile = (r % D::NJA) * D::NKA + r / D::NJA;
   }
-  const int kt = tile % NKA, jt = tile / NKA;
+  const int kt = tile % D::NKA, jt = tile / D::NKA;
   const int j0 = jt * AJ, k0 = kt * AK;
   const int r0 = z * a.kpz, r1 = min(a.S, r0 + a.kpz);
   const bool bias = kt == 0 && wn == 0;
   const int nchunks = (a.abl & 8) ? 0 : max(0, (r1 - r0 + BK - 1) / BK);
+  // X columns of this k tile: FC a2; LSTM x = hfc (k < 256) or h_prev (k >= 256, the
+  // range's reset flags staged in LDS first: a reset sample's row is DMA'd from the zero row)
+  const bool hpart = SH::kLstm && k0 >= SH::KW1;   // block-uniform
+  const float* xsrc = hpart ? a.hprev : a.a2;
+  constexpr int XLD = SH::kLstm ? HID : A2;
+  const int xc0 = hpart ? k0 - SH::KW1 : k0;
+  if (hpart) {
+    for (int i = tid; i < r1 - r0; i += NT) rst[i] = a.reset[r0 + i];
+    __syncthreads();
+  }
   // m-tile t: rows j = wm*64 + 4 col + t; n-tile u: cols k = wn*32 + 2 col + u
   double s[4][2][4], sb[4];
 #pragma unroll
@@ -192,8 +244,11 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds) {
   auto issue = [&](int c) {
     if (a.abl & 2) return;
     float* st = lds + (c & 1) * STAGE;
-    stage_tile<BK, AJ, 0>(st, a.dfc, HID, r0 + c * BK, r1 - 1, j0);         // dfc[s][j0 .. j0+127]
-    stage_tile<BK, AK, 1>(st + BK * AJ, a.a2, A2, r0 + c * BK, r1 - 1, k0);  // a2[s][k0 .. k0+63]
+    stage_tile<BK, AJ, 0>(st, a.dfc, SH::J, r0 + c * BK, r1 - 1, j0);       // dY[s][j0 .. j0+127]
+    if (SH::kLstm && hpart)
+      stage_tile<BK, AK, 1, true>(st + BK * AJ, xsrc, XLD, r0 + c * BK, r1 - 1, xc0, rst, r0, a.zero);
+    else
+      stage_tile<BK, AK, 1>(st + BK * AJ, xsrc, XLD, r0 + c * BK, r1 - 1, xc0);   // X[s][k0 .. k0+63]
   };
   const int nb = wn * 32 + 2 * col;
   f32x4 acc[4][2], bs;
@@ -400,7 +455,9 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds) {
     }
   }
   const int k = k0 + wn * 32 + 2 * col;
-  if (k < A2) {   // the last k tile is half full (k even, A2 even: a pair is all in or out)
+  if (k < SH::KW) {   // FC: the last k tile is half full (k even, A2 even: a pair is all in or out)
+    // LSTM: k < 256 the upward W, else the lateral W (a k tile never straddles the two)
+    float* gw = hpart ? a.gW2 + (k - SH::KW1) : a.gW + k;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -409,7 +466,7 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds) {
         float2 w;
         w.x = (float)o[t][0][e];
         w.y = (float)o[t][1][e];
-        *reinterpret_cast<float2*>(a.gW + (int64_t)j * A2 + k) = w;
+        *reinterpret_cast<float2*>(gw + (int64_t)j * SH::KW1) = w;
       }
   }
   if (bias && q == 0)
@@ -423,8 +480,10 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds) {
 
 // ---------------------------------------------------------------- job B: da2
 // MT m-tiles per wave: workgroup tiles of BMT = 32 MT samples x 128 k
-template <int MT, bool SPLIT>
+template <int MT, bool SPLIT, class SH>
 __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
+  using D = Dims<SH>;
+  constexpr int NKB = D::NKB, NB = SH::NB;
   constexpr int BMT = 32 * MT;
   constexpr int PIECES = (BMT * BK + BK * BN) / 256 / NW;   // LDS-DMA pieces per wave per chunk
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -438,12 +497,12 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
     st = lin - kt * nst;
   }
   const int s0 = st * BMT, k0 = kt * BN;
-  constexpr int NCH = HID / BK;              // 8 chunks of 32 j
+  constexpr int NCH = D::NCHB;               // chunks of 32 j: FC 8, LSTM 32
   auto issue = [&](int c) {
     if (a.abl & 2) return;
     float* sg = lds + (c & 1) * STAGE;
-    stage_tile<BMT, BK, 2>(sg, a.dfc + c * BK, HID, s0, a.S - 1, 0);                    // dfc[s][j]
-    stage_tile<BK, BN, 0>(sg + BMT * BK, a.W + (int64_t)c * BK * A2, A2, 0, BK - 1, k0);  // W[j][k0..k0+127]
+    stage_tile<BMT, BK, 2>(sg, a.dfc + c * BK, SH::J, s0, a.S - 1, 0);                  // dY[s][j]
+    stage_tile<BK, BN, 0>(sg + BMT * BK, a.W + (int64_t)c * BK * NB, NB, 0, BK - 1, k0);  // W[j][k0..k0+127]
   };
   f32x4 acc[MT][4];                          // m-tile i: rows 16 i + col; n-tile u: cols 4 col + u
   f32x4 sml[SPLIT ? MT : 1][4];              // split path: the 5 small terms (acc: the h.h term)
@@ -460,16 +519,16 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
   // load round trip is left for the epilogue.  Out-of-range rows / columns
   // read 0 through the buffer's range check.
   const int k = k0 + wn * 64 + 4 * col;
-  const bool kin = k < A2;                   // A2 % 4 == 0: a 4-run is all in or all out
+  const bool kin = k < NB;                   // NB % 4 == 0: a 4-run is all in or all out
   const int rows = min(BMT, a.S - s0);
-  const __amdgpu_buffer_rsrc_t msk = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.a2) + (int64_t)s0 * A2,
-                                                                       0, rows * A2 * 4, BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t msk = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.a2) + (int64_t)s0 * NB,
+                                                                       0, rows * NB * 4, BUF_DWORD3);
   unsigned mb[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) mb[i] = 0u;
   f32x4 mraw[4];
   issue(0);
-#pragma unroll
+#pragma unroll 8
   for (int c = 0; c < NCH; ++c) {
     if (c + 1 < NCH) issue(c + 1);
     if (c >= 1 && c <= MT) {   // the band loaded one chunk ago (the compiler's own vmcnt wait)
@@ -483,7 +542,7 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
       for (int e = 0; e < 4; ++e) {
         const int row = wm * 16 * MT + 16 * c + 4 * q + e;
         mraw[e] = __builtin_bit_cast(
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(msk, kin ? (row * A2 + k) * 4 : OOB, 0, 0));
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(msk, kin ? (row * NB + k) * 4 : OOB, 0, 0));
       }
     }
     // this chunk's DMA done: the next chunk's PIECES a wave and this chunk's mask band may still fly
@@ -555,7 +614,7 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
   // out-of-range lanes (s >= S, k >= A2) the buffer's range check drops -- no
   // per-store branch, so no store waits for the one before it.
   const __amdgpu_buffer_rsrc_t out =
-      __builtin_amdgcn_make_buffer_rsrc(a.da2 + (int64_t)s0 * A2, 0, rows * A2 * 4, BUF_DWORD3);
+      __builtin_amdgcn_make_buffer_rsrc(a.da2 + (int64_t)s0 * NB, 0, rows * NB * 4, BUF_DWORD3);
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -568,7 +627,7 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
         if constexpr (SPLIT) v += sml[i][u][e];
         o[u] = (mb[i] >> (4 * e + u)) & 1u ? v : 0.f;
       }
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), out, kin ? (row * A2 + k) * 4 : OOB, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), out, kin ? (row * NB + k) * 4 : OOB, 0, 0);
     }
 }
 
@@ -635,15 +694,16 @@ __device__ void job_heads(const FcBwdArgs& a, int jt, float* lds) {
   }
 }
 
-template <int MT, bool SPLIT>
+template <int MT, bool SPLIT, class SH>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2)))
 fc_bwd_kernel(FcBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];   // 64 KB, the only LDS object
+  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];   // 64 KB
+  __shared__ uint8_t rst[SH::kLstm ? RST_MAX : 4];                 // LSTM: a range's reset flags
   const int b = a.b0 + blockIdx.x;
-  const int na = NTA * a.Z;
+  const int na = Dims<SH>::NTA * a.Z;
   if (b < a.nc) job_heads(a, b, lds);   // first: the smallest, longest-latency jobs
-  else if (b < a.nc + na) job_dw<SPLIT>(a, b - a.nc, lds);
-  else job_da2<MT, SPLIT>(a, b - a.nc - na, lds);
+  else if (b < a.nc + na) job_dw<SPLIT, SH>(a, b - a.nc, lds, rst);
+  else job_da2<MT, SPLIT, SH>(a, b - a.nc - na, lds);
 }
 
 // ~800 samples per job A range, at most 16 ranges (bf16-split steps, sweep in
@@ -653,10 +713,15 @@ int fc_bwd_ranges(int S) {
   if (zs) return std::max(1, std::min(16, atoi(zs)));
   return std::max(1, std::min(16, (S + 400) / 800));
 }
+// LSTM: the same, with no range longer than the LDS reset table
+int lstm_wgrad_ranges(int S) { return std::max(fc_bwd_ranges(S), (S + RST_MAX - 1) / RST_MAX); }
+int range_len(int S, int Z) { return ((S + Z - 1) / Z + BK - 1) / BK * BK; }
 }  // namespace
 
-int64_t fc_bwd_part_floats(int S) { return (int64_t)NTA * fc_bwd_ranges(S) * PART; }
-int fc_bwd_tickets() { return 2 * NTA; }   // arrival tickets, then ready counts (ARL_FC_BWD_SPIN)
+int64_t fc_bwd_part_floats(int S) {
+  return (int64_t)std::max(Dims<ShapeFC>::NTA * fc_bwd_ranges(S), Dims<ShapeLSTM>::NTA * lstm_wgrad_ranges(S)) * PART;
+}
+int fc_bwd_tickets() { return 2 * NTA_MAX; }   // arrival tickets, then ready counts (ARL_FC_BWD_SPIN)
 
 // Job A's last k tile stages a2 columns 2560..2623 and job B's last one W
 // columns 2560..2687: the floats past a row's end are the next row's (a2 has
@@ -666,8 +731,7 @@ hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int 
                          float* part, int* tick, hipStream_t s, const HeadsDW* heads) {
   if (S <= 0) return hipSuccess;
   const int Z = fc_bwd_ranges(S);
-  int kpz = (S + Z - 1) / Z;
-  kpz = (kpz + BK - 1) / BK * BK;
+  const int kpz = range_len(S, Z);
   // ARL_FC_BWD_F32=1: the exact-f32 16x16x4 MFMA steps instead of the bf16 splits (A/B timing).
   // Job B tiles: 64 samples (2 m-tiles a wave) on the split path, whose small-term
   // accumulators leave no room for 4 m-tiles; 128 on the f32 path unless ARL_FC_BWD_BM=64.
@@ -675,7 +739,8 @@ hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int 
   static const char* bm = getenv("ARL_FC_BWD_BM");
   const bool split = !(f32 && atoi(f32) == 1);
   const int MT = (split || (bm && atoi(bm) == 64)) ? 2 : 4, BMT = 32 * MT;
-  const int na = NTA * Z, nb = ((S + BMT - 1) / BMT) * NKB;
+  using D = Dims<ShapeFC>;
+  const int na = D::NTA * Z, nb = ((S + BMT - 1) / BMT) * D::NKB;
   // ARL_FC_BWD_JOBS=a / b: launch one job alone; ARL_FC_BWD_ABL: ablations (timing experiments only)
   static const char* only = getenv("ARL_FC_BWD_JOBS");
   static const char* abl = getenv("ARL_FC_BWD_ABL");
@@ -687,10 +752,31 @@ hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int 
   static const char* spin = getenv("ARL_FC_BWD_SPIN");
   static const char* xcd = getenv("ARL_FC_BWD_XCD");
   FcBwdArgs args{dfc, a2, W, S, Z, kpz, gW, gb, da2, part, tick, heads ? *heads : HeadsDW{}, nc, b0,
-                 abl ? atoi(abl) : 0, (spin && atoi(spin) == 1) ? 1 : 0, (xcd && xcd[0] == '0') ? 0 : 1};
-  if (split) hipLaunchKernelGGL((fc_bwd_kernel<2, true>), dim3(grid), dim3(NT), 0, s, args);
-  else if (MT == 2) hipLaunchKernelGGL((fc_bwd_kernel<2, false>), dim3(grid), dim3(NT), 0, s, args);
-  else hipLaunchKernelGGL((fc_bwd_kernel<4, false>), dim3(grid), dim3(NT), 0, s, args);
+                 abl ? atoi(abl) : 0, (spin && atoi(spin) == 1) ? 1 : 0, (xcd && xcd[0] == '0') ? 0 : 1,
+                 nullptr, nullptr, nullptr, nullptr};
+  if (split) hipLaunchKernelGGL((fc_bwd_kernel<2, true, ShapeFC>), dim3(grid), dim3(NT), 0, s, args);
+  else if (MT == 2) hipLaunchKernelGGL((fc_bwd_kernel<2, false, ShapeFC>), dim3(grid), dim3(NT), 0, s, args);
+  else hipLaunchKernelGGL((fc_bwd_kernel<4, false, ShapeFC>), dim3(grid), dim3(NT), 0, s, args);
+  return hipGetLastError();
+}
+
+// LSTM gate weight gradients + dfc in one launch (ShapeLSTM above): job A
+// writes the upward W / b and lateral W gradients straight into the flat
+// gradient, job B dfc = (dG Wu) * (hfc > 0).  zero: >= 64 zero floats.
+hipError_t launch_lstm_wgrad(const float* dG, const float* hfc, const float* hprev, const uint8_t* reset,
+                             const float* zero, const float* Wu, int S, float* gWu, float* gWl, float* gbu, float* dfc,
+                             float* part, int* tick, hipStream_t s) {
+  if (S <= 0) return hipSuccess;
+  const int Z = lstm_wgrad_ranges(S);
+  const int kpz = range_len(S, Z);
+  if (kpz > RST_MAX) return hipErrorInvalidValue;
+  using D = Dims<ShapeLSTM>;
+  constexpr int BMT = 64;
+  const int na = D::NTA * Z, nb = ((S + BMT - 1) / BMT) * D::NKB;
+  static const char* xcd = getenv("ARL_FC_BWD_XCD");
+  FcBwdArgs args{dG, hfc, Wu, S, Z, kpz, gWu, gbu, dfc, part, tick, HeadsDW{}, 0, 0, 0, 0,
+                 (xcd && xcd[0] == '0') ? 0 : 1, hprev, reset, zero, gWl};
+  hipLaunchKernelGGL((fc_bwd_kernel<2, true, ShapeLSTM>), dim3(na + nb), dim3(NT), 0, s, args);
   return hipGetLastError();
 }
 

@@ -197,6 +197,12 @@ static const bool LSTM_XRED = [] {
   const char* e = getenv("ARL_LSTM_XRED");
   return e == nullptr || e[0] != '0';
 }();
+// ARL_LSTM_WGRAD=gemm: the gate weight gradients + dfc as the round-2 generic dual GEMM into the LSTM
+// slab (+ the LEARN_GATES_REDUCE reduce) instead of fc_bwd.hip's ShapeLSTM kernel -- A/B timing only
+static const bool LSTM_WGRAD_GEMM = [] {
+  const char* e = getenv("ARL_LSTM_WGRAD");
+  return e != nullptr && e[0] == 'g';
+}();
 
 // gates = [x | h] [Wu ; Wl]^T + b, then the cell: c_out, h_out (rows [0, n))
 template <class AOp, class BOp>
@@ -466,6 +472,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   net.w_eval_hn = buf("eval_hn", L ? n * HID * 4 : 0);
   net.w_eval_cn = buf("eval_cn", L ? n * HID * 4 : 0);
   net.w_eval_reset = buf("eval_reset", L ? n : 0);
+  net.w_zero = buf("zero_row", L ? ZERO_ROW_FLOATS * 4 : 0);
   net.ws_bytes = wo;
   return true;
 }
@@ -682,6 +689,11 @@ static hipError_t lstm_wgrad(Net& net, hipStream_t s) {
   const Plans pl = make_plans(net);
   const float* dG = net.at<float>(net.w_dG);
   const float* hfc = net.at<float>(net.w_hfc);
+  if (!LSTM_WGRAD_GEMM)   // straight into the gradient (no slab, no LEARN_GATES_REDUCE)
+    return launch_lstm_wgrad(dG, hfc, net.at<float>(net.w_hbuf), net.at<uint8_t>(net.w_reset),
+                             net.at<float>(net.w_zero), net.p + net.o_luW, S, net.g + net.o_luW, net.g + net.o_llW,
+                             net.g + net.o_lub, net.at<float>(net.w_dfc), net.at<float>(net.w_fcb_part),
+                             net.at<int>(net.w_fcb_tick), s);
   return launch_gemm2<64, 64, 32, 2, 2, GM, GM, GK, GM>(
       gemm_job<64, 32>(ColMajor{dG, GATES}, LstmWB{hfc, net.at<float>(net.w_hbuf), net.at<uint8_t>(net.w_reset)},
                        EpiSlab{net.at<float>(net.w_slab_lstm), GATES, 2 * HID + 1}, GATES, 2 * HID + 1, S, pl.lstm_w,
@@ -737,7 +749,7 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
   }
   float* slab_l = net.at<float>(net.w_slab_lstm);
   if (part == LEARN_GATES_REDUCE)
-    return L ? launch_reduce_grad(slab_l, pl.lstm_w, GATES, 2 * HID + 1,
+    return (L && LSTM_WGRAD_GEMM) ? launch_reduce_grad(slab_l, pl.lstm_w, GATES, 2 * HID + 1,
                                   MapLstmW{G, net.o_luW, net.o_llW, net.o_lub}, s)
              : hipSuccess;
   if (part == LEARN_FC_REDUCE)   // the FC weight gradient is written by fc_bwd_kernel (LEARN_TRUNK)

@@ -66,6 +66,8 @@ LSTM_BPTT_FLOP_PER_ENV = 2 * 1024 * 256
 LSTM_WGRAD_FLOP_PER_SAMPLE = 2 * 513 * 1024 + 2 * 1024 * 256
 # the gate kernel forms x from the FC's split-K partials unless ARL_LSTM_XRED=0 (net.hip)
 LSTM_XRED = os.environ.get("ARL_LSTM_XRED", "1")[:1] != "0"
+# the gate weight gradients run on fc_bwd.hip's ShapeLSTM kernel unless ARL_LSTM_WGRAD=gemm (net.hip)
+LSTM_WGRAD_GEMM = os.environ.get("ARL_LSTM_WGRAD", "")[:1] == "g"
 # ViZDoom models (train_a3c_doom.py:28,46): conv1 K = 3 * 64 (the kernels' zero input plane is not counted)
 DOOM_CONV_FWD_FLOP_PER_ENV = 2 * (400 * 16 * 192 + 81 * 32 * 256)
 DOOM_CONV_BWD_FLOP_PER_SAMPLE = 2 * (32 * 256 * 81 + 81 * 32 * 256 + 400 * 16 * 192)
@@ -585,7 +587,8 @@ def main(a):
             ("lstm_bptt", "lstm_bptt_kernel (dh GEMM + cell backward)",
              lambda i: net.run_stage("lstm_bptt", T - 1 - i % (T - 1), stream=stream), T - 1, "mfma",
              N * LSTM_BPTT_FLOP_PER_ENV) if lstm and not doom and T > 1 else None,
-            ("lstm_wgrad", "gemm2_kernel (gate dW + dfc)",
+            ("lstm_wgrad", "gemm2_kernel (gate dW + dfc)" if LSTM_WGRAD_GEMM else
+             "fc_bwd_kernel<ShapeLSTM> (gate dW / db + dfc, straight into the gradient)",
              lambda i: net.run_stage("lstm_wgrad", stream=stream), 1, "mfma",
              S * LSTM_WGRAD_FLOP_PER_SAMPLE) if lstm and not doom else None,
             ("rmsprop", "rmsprop_kernel", lambda i: net.optimize(lr0=1e-12, clip=0.0, stream=stream), 1, "hbm",
@@ -656,7 +659,13 @@ def main(a):
         import cpu_baseline  # noqa: E402  (oracle/, CPU baseline leg only)
         cpu = cpu_baseline.run(seconds=a.cpu_seconds, t_max=T, n_actions=4)        # leg (i): 1 process, 1 core
         cpu["cpu_model"] = cpu_baseline.cpu_model()
-        par = cpu_baseline.run_parallel(seconds=a.cpu_seconds, t_max=T, n_actions=4, ctx=mp_ctx)   # leg (ii)
+        # leg (ii) as BASELINE.md §2 states it: P = physical cores, one process each (async.py:68-90);
+        # on a box whose cgroup quota grants fewer CPUs they time-share them, so the quota-sized run
+        # (P = CPUs this process may use) is recorded beside it
+        phys, _, avail = cpu_baseline.host_cores()
+        par = cpu_baseline.run_parallel(seconds=a.cpu_seconds, t_max=T, n_actions=4, procs=phys, ctx=mp_ctx)
+        if avail < phys:
+            par["quota_sized"] = cpu_baseline.run_parallel(seconds=a.cpu_seconds, t_max=T, n_actions=4, ctx=mp_ctx)
         cpu["parallel"] = par
         cpu["gpu_vs_parallel"] = round(value / par["value"], 1)
 

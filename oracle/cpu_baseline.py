@@ -162,16 +162,20 @@ def run_parallel(seconds: float = 10.0, t_max: int = 5, n_actions: int = 4, proc
     rates = [r["value"] for r in res]
     el = max(r["seconds"] for r in res)
     per_proc = sum(rates) / len(rates)
+    shared = (f"; {P} processes time-share the {avail} CPUs this process may use"
+              if P > avail else "")
     return {"value": sum(steps) / el, "unit": "env-steps/s", "cores": P, "kind": "port",
             "sample": f"{P} processes x ~{seconds:.0f} s of the batch-1 A3C-FF actor-learner (NumPy restatement, "
                       f"1 thread each), {sum(steps)} env-steps in total; per-process {min(rates):.1f}-"
-                      f"{max(rates):.1f} env-steps/s",
+                      f"{max(rates):.1f} env-steps/s{shared}",
             "cpu_model": cpu_model(), "physical_cores": phys, "logical_cpus": logical, "cpus_allowed": avail,
             "cgroup_cpu_quota": cgroup_cpu_quota(),
-            "extrapolated_physical_cores": {"value": round(per_proc * phys, 1), "cores": phys,
-                                            "note": "mean per-process rate x physical cores: an estimate of the "
-                                                    "reference-style P = physical-cores run, not a measurement "
-                                                    "(the quota admits only cpus_allowed processes at once)"}}
+            **({"extrapolated_physical_cores": {"value": round(per_proc * phys, 1), "cores": phys,
+                                                "note": "mean per-process rate x physical cores: an estimate of "
+                                                        "the reference-style P = physical-cores run on a whole "
+                                                        "host, not a measurement (the quota admits only "
+                                                        "cpus_allowed processes at once)"}}
+               if P <= avail and P < phys else {})}
 
 
 if __name__ == "__main__":

@@ -2,8 +2,9 @@
 saves actions, values, hidden states, gradients and parameters to an .npz
 (argv[1]); test_gpu_parity.test_lstm_fused_cell_identical runs it under
 the LSTM knobs (ARL_LSTM_SPLIT, ARL_LSTM_XRED, ARL_GROUP_ORDER) and compares
-the files bitwise.  argv[2] == "one": a single window, its gradients only
-(test_lstm_bptt_kernel_matches_generic)."""
+the files bitwise.  argv[2] == "one": a single window, its gradients (flat and per tensor)
+and dfc only (test_lstm_bptt_kernel_matches_generic,
+test_lstm_wgrad_kernel_matches_gemm)."""
 import os
 import sys
 
@@ -30,8 +31,10 @@ def main(out, one=False):
     ag.run_window(dp, dr, dd, P, first=True, env_groups=2, split_update=one)
     if one:
         torch.cuda.synchronize()
+        per = {"g." + k.replace("/", "."): v.detach().cpu().numpy() for k, v in ag.net.state_dict(ag.net.grads).items()}
         np.savez(out, grads=ag.net.grads.detach().cpu().numpy(),
-                 hbuf=ag.net.buffer("hbuf", torch.float32).detach().cpu().numpy())
+                 hbuf=ag.net.buffer("hbuf", torch.float32).detach().cpu().numpy(),
+                 dfc=ag.net.buffer("dfc", torch.float32).detach().cpu().numpy(), **per)
         return
     ag.run_window(dp, dr, dd, P, env_groups=1)
     s = torch.cuda.Stream()

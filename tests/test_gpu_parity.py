@@ -731,6 +731,35 @@ def test_lstm_bptt_kernel_matches_generic(gpu, tmp_path):
     assert ok, err
 
 
+def test_lstm_wgrad_kernel_matches_gemm(gpu, tmp_path):
+    """The LSTM gate weight gradients + dfc on fc_bwd.hip's ShapeLSTM kernel
+    (bf16-split MFMA steps, [x | h_prev] staged by LDS-DMA with reset rows read
+    from a zero row, straight into the gradient) against the round-2 generic
+    exact-f32 dual GEMM + slab reduce (ARL_LSTM_WGRAD=gemm): same forward bits,
+    dfc and every gradient tensor within 1e-5 of its own scale (both are
+    f32-accurate sums; only the order differs)."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    outs = []
+    for extra in ({}, {"ARL_LSTM_WGRAD": "gemm"}):
+        f = str(tmp_path / f"wgrad_{len(outs)}.npz")
+        env = dict(os.environ, **extra)
+        subprocess.run([sys.executable, os.path.join(here, "lstm_split_worker.py"), f, "one"], env=env, check=True,
+                       timeout=240)
+        outs.append(np.load(f))
+    new, old = outs
+    assert np.array_equal(new["hbuf"], old["hbuf"])
+    ok, err = close_normscaled(old["dfc"], new["dfc"], 1e-5)
+    assert ok, ("dfc", err)
+    names = [k for k in new.files if k.startswith("g.")]
+    assert any("lateral" in k for k in names) and any("upward" in k for k in names)
+    for k in names:
+        assert float(np.abs(old[k]).max()) > 0, k
+        ok, err = close_normscaled(old[k], new[k], 1e-5)
+        assert ok, (k, err)
+
+
 def test_fc_bwd_variants(gpu, tmp_path):
     """FC backward knobs at S = 1,280 (two dW ranges): the ticket-first reduce
     (ARL_FC_BWD_SPIN=1) sums the same partials in the same order, so every
