@@ -73,6 +73,22 @@ constexpr int L_XOFS = L_GRAY + G_ROWS * SRC_W;       // int16 xofs[84], xa0[84]
 static_assert(L_XOFS + 5 * DST * 2 <= L_END, "gray rows + tables fit the W2 region");
 constexpr int PHI_TASKS = G_ROWS * 10;                // (row, 16-pixel chunk): 1680
 constexpr int PHI_J = (PHI_TASKS + NT - 1) / NT;      // 4
+
+// LDS layout by envs per workgroup (EPW).  EPW = 1 is the layout above.  EPW = 2
+// (1,024 threads; waves 0-7 take env 0, waves 8-15 env 1, both share the weight
+// planes): conv1 phase  [screens e0 | screens e1 | W1 planes]       138,240 B;
+//          conv2 phase  [a1 planes e0 | a1 planes e1 | W2 planes]  127,488 B
+// (W2 is split into the dead screen / W1 bytes after conv1's barrier).
+template <int EPW>
+struct Lay {
+  static constexpr int XB(int el) { return el * 4 * XB_PLANE; }
+  static constexpr int W1 = EPW * 4 * XB_PLANE;                      // 56,448 / 112,896
+  static constexpr int A1(int el) { return EPW == 1 ? W1 : el * 3 * A1P; }
+  static constexpr int W2 = EPW == 1 ? L_W2 : 2 * 3 * A1P;           // 94,848 / 76,800
+  static constexpr int END = EPW == 1 ? L_END : W1 + 3 * W1P;        // 145,536 / 138,240
+};
+static_assert(Lay<2>::W2 + 3 * W2P <= Lay<2>::END && Lay<2>::END <= 160 * 1024, "EPW 2 layout");
+static_assert(Lay<1>::A1(0) == L_R1 && Lay<1>::END == L_END, "EPW 1 layout");
 }  // namespace
 
 // a1 plane byte offset of (pixel P, ic half h): 16-byte slot 2P + h with its
@@ -93,8 +109,9 @@ struct ConvFwdArgs {
   float* a2;            // (n, 32, 81)
   int layout;           // FrameLayout: FRAMES_RGB = (R, n, 3, 84, 84), planes [0, R, G, B] of slot ks % R;
                         // FRAMES_STACK = (R, n, 4, 84, 84), the 4 planes of slot ks % R
-  int e0;               // first env of this launch (env = e0 + blockIdx.x)
+  int e0;               // first env of this launch (env = e0 + EPW * blockIdx.x + env slot)
   RingArgs ring;        // PHI: the observation (pair pool, bookkeeping); frames / nvalid / ctl / n / R / t as above
+  int e1;               // one past the last env of this launch (EPW = 2: an odd count leaves a slot idle)
 };
 
 // W1 (16, 4, 8, 8) f32 -> the split planes [3][oc][k] in LDS: thread tid
@@ -109,7 +126,7 @@ __device__ inline void w1_load(const float* W1, bool rgb, int tid, float4& w1a, 
   w1a = w1p[0];
   w1b = w1p[1];
 }
-__device__ inline void w1_split_store(uint8_t* lds, int tid, float4 w1a, float4 w1b, bool rgb = false) {
+__device__ inline void w1_split_store(uint8_t* lds, int tid, float4 w1a, float4 w1b, bool rgb = false, int base = L_R1) {
   const int w1oc = tid >> 5, w1k = (8 * tid) & 255;
   if (rgb && w1k < 64) w1a = w1b = make_float4(0.f, 0.f, 0.f, 0.f);
   uint4 ph, pm, pl;
@@ -117,7 +134,7 @@ __device__ inline void w1_split_store(uint8_t* lds, int tid, float4 w1a, float4 
   split3_pack(w1a.z, w1a.w, ph.y, pm.y, pl.y);
   split3_pack(w1b.x, w1b.y, ph.z, pm.z, pl.z);
   split3_pack(w1b.z, w1b.w, ph.w, pm.w, pl.w);
-  uint8_t* d = lds + L_R1 + w1oc * WROW + w1k * 2;
+  uint8_t* d = lds + base + w1oc * WROW + w1k * 2;
   *reinterpret_cast<uint4*>(d) = ph;
   *reinterpret_cast<uint4*>(d + W1P) = pm;
   *reinterpret_cast<uint4*>(d + 2 * W1P) = pl;
@@ -129,7 +146,7 @@ __device__ inline void w2_load(const float* W2, int tid, float4 (&w2v)[4]) {
 #pragma unroll
   for (int ii = 0; ii < 4; ++ii) w2v[ii] = reinterpret_cast<const float4*>(W2)[(w2oc * 16 + 4 * ic4 + ii) * 4 + tg];
 }
-__device__ inline void w2_split_store(uint8_t* lds, int tid, const float4 (&w2v)[4]) {
+__device__ inline void w2_split_store(uint8_t* lds, int tid, const float4 (&w2v)[4], int base = L_W2) {
   const int w2oc = tid >> 4, ic4 = (tid >> 2) & 3, tg = tid & 3;
 #pragma unroll
   for (int tt = 0; tt < 4; ++tt) {
@@ -137,7 +154,7 @@ __device__ inline void w2_split_store(uint8_t* lds, int tid, const float4 (&w2v)
     uint2 ph, pm, pl;
     split3_pack(v0, v1, ph.x, pm.x, pl.x);
     split3_pack(v2, v3, ph.y, pm.y, pl.y);
-    uint8_t* d = lds + L_W2 + w2oc * WROW + ((4 * tg + tt) * 16 + 4 * ic4) * 2;
+    uint8_t* d = lds + base + w2oc * WROW + ((4 * tg + tt) * 16 + 4 * ic4) * 2;
     *reinterpret_cast<uint2*>(d) = ph;
     *reinterpret_cast<uint2*>(d + W2P) = pm;
     *reinterpret_cast<uint2*>(d + 2 * W2P) = pl;
@@ -155,14 +172,21 @@ __device__ inline void px16_store(uint8_t* d, uint4 x) {
   reinterpret_cast<uint4*>(d)[1] = hi;
 }
 
-template <bool PHI>
-__global__ void __launch_bounds__(NT)
+template <bool PHI, int EPW>
+__global__ void __launch_bounds__(NT * EPW)
 conv_fwd_kernel(ConvFwdArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[L_END];
+  static_assert(!PHI || EPW == 1, "the fused observation runs one env per workgroup");
+  using LY = Lay<EPW>;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LY::END];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, col = lane & 15;
-  const int e = a.e0 + blockIdx.x;
+  // EPW = 2: waves 0-7 (threads 0-511) env slot 0, waves 8-15 slot 1; w8 / t8 index within the slot
+  const int el = EPW == 1 ? 0 : wave >> 3;
+  const int w8 = wave & 7, t8 = tid & (NT - 1);
+  const int ev = a.e0 + EPW * blockIdx.x + el;
+  const bool valid = EPW == 1 || ev < a.e1;   // an idle slot (odd env count) computes env e1 - 1, stores nothing
+  const int e = valid ? ev : a.e1 - 1;
   const bool rgb = a.layout == FRAMES_RGB;
   constexpr int V = PLANE / 16;              // 441 uint4 per screen
   // the biases first: loads issued at the top land before the staging waits
@@ -176,19 +200,19 @@ conv_fwd_kernel(ConvFwdArgs a) {
 #define CF_STAMP() do {} while (0)
 #endif
   const float bias1 = a.b1[col];
-  const float bias2 = a.b2[16 * (wave & 1) + col];
+  const float bias2 = a.b2[16 * (w8 & 1) + col];
   const int64_t ks = a.ctl[CTL_STEP] + a.t;
   const int rs = (int)(ks % a.R);
   // conv1 tiles w, w + 8, w + 16 (and 24 on wave 0): 25 tiles over 8 waves in one
   // pass, 3-4 independent accumulator chains per wave (per-tile k order s = 0..7)
   constexpr int TJ = 4;
-  const bool has3 = wave + 24 < 25;   // wave-uniform
+  const bool has3 = w8 + 24 < 25;   // wave-uniform
   int baseX[TJ];
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
-    const int tl = (j < 3 || has3) ? wave + 8 * j : wave;
+    const int tl = (j < 3 || has3) ? w8 + 8 * j : w8;
     const int p = tl * 16 + col, oy = p / 20, ox = p - oy * 20;
-    baseX[j] = L_XB + (4 * oy) * XB_ROW + 8 * ox;
+    baseX[j] = LY::XB(el) + (4 * oy) * XB_ROW + 8 * ox;
   }
   f32x4 big[TJ], sml[TJ];
 #pragma unroll
@@ -207,7 +231,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
     }
   };
   auto w1_frag = [&](int s, bf16x8& wh, bf16x8& wm, bf16x8& wl) {
-    const int off = L_R1 + col * WROW + (4 * s + g) * 16;
+    const int off = LY::W1 + col * WROW + (4 * s + g) * 16;
     wh = lds_load<bf16x8>(lds, off);
     wm = lds_load<bf16x8>(lds, off + W1P);
     wl = lds_load<bf16x8>(lds, off + 2 * W1P);
@@ -351,35 +375,32 @@ conv_fwd_kernel(ConvFwdArgs a) {
     // into LDS; planes older than the last reset are zeroed here
     const int nv = a.nvalid[(int64_t)rs * a.n + e];
     float4 w1a, w1b, w2v[4];
-    w1_load(a.W1, rgb, tid, w1a, w1b);
-    w2_load(a.W2, tid, w2v);
-    int slot[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) slot[c] = (rs + a.R - 3 + c) % a.R;
+    w1_load(a.W1, rgb, t8, w1a, w1b);
+    w2_load(a.W2, t8, w2v);
     constexpr int NX = (4 * V + NT - 1) / NT;  // 4
     uint4 xv[NX];
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
-      const int i = tid + NT * j;
+      const int i = t8 + NT * j;
       // past the fourth plane: reload its last 16 bytes (every thread issues NX loads)
       const int c = i < 4 * V ? i / V : 3, oo = i < 4 * V ? i - c * V : V - 1;
       // RGB: conv plane 0 is the zero pad (c - 1 < 0 reads plane 0 and is zeroed below, nvalid = 3)
       xv[j] = reinterpret_cast<const uint4*>(
           a.frames + (a.layout == FRAMES_STACK ? ((int64_t)rs * a.n + e) * 4 + c
                       : a.layout == FRAMES_RGB ? ((int64_t)rs * a.n + e) * 3 + (c > 0 ? c - 1 : 0)
-                                               : (int64_t)slot[c] * a.n + e) * PLANE)[oo];
+                                               : (int64_t)((rs + a.R - 3 + c) % a.R) * a.n + e) * PLANE)[oo];
     }
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
-      const int i = tid + NT * j;
+      const int i = t8 + NT * j;
       if (i < 4 * V) {
         const int c = i / V, oo = i - c * V;
-        px16_store(lds + L_XB + c * XB_PLANE + oo * 32,
+        px16_store(lds + LY::XB(el) + c * XB_PLANE + oo * 32,
                    (!(ARL_ABLATE & 4) && c >= 4 - nv) ? xv[j] : make_uint4(0, 0, 0, 0));
       }
     }
-    w1_split_store(lds, tid, w1a, w1b, rgb);
-    w2_split_store(lds, tid, w2v);
+    if (el == 0) w1_split_store(lds, t8, w1a, w1b, rgb, LY::W1);
+    if (EPW == 1) w2_split_store(lds, t8, w2v, LY::W2);   // EPW = 2: after conv1 (its bytes hold screens / W1)
     CF_STAMP();   // 0: staged
     __syncthreads();
     CF_STAMP();   // 1: barrier
@@ -394,6 +415,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
     }
     CF_STAMP();   // 2: conv1 MFMAs issued
     __syncthreads();
+    if (EPW == 2 && el == 1) w2_split_store(lds, t8, w2v, LY::W2);   // read by conv2 after the next barrier
   }
   float* a1g = a.a1 + (int64_t)e * A1;
   {
@@ -401,18 +423,18 @@ conv_fwd_kernel(ConvFwdArgs a) {
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       if (j == 3 && !has3) break;
-      const int p0 = (wave + 8 * j) * 16 + g * 4;
+      const int p0 = (w8 + 8 * j) * 16 + g * 4;
       float ov[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         ov[r] = (ARL_ABLATE & 16) ? fmaxf(__fadd_rn(__fmul_rn(__fadd_rn(big[j][r], sml[j][r]), 1.f / 255.f), bias1), 0.f)
                                   : fmaxf(__fadd_rn(__fdiv_rn(__fadd_rn(big[j][r], sml[j][r]), 255.f), bias1), 0.f);
-      *reinterpret_cast<float4*>(a1g + col * C1_P + p0) = make_float4(ov[0], ov[1], ov[2], ov[3]);
+      if (valid) *reinterpret_cast<float4*>(a1g + col * C1_P + p0) = make_float4(ov[0], ov[1], ov[2], ov[3]);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         uint32_t h, m, l;
         split3(ov[r], h, m, l);
-        const int off = L_R1 + a1_slot(p0 + r, col >> 3) + (col & 7) * 2;
+        const int off = LY::A1(el) + a1_slot(p0 + r, col >> 3) + (col & 7) * 2;
         *reinterpret_cast<uint16_t*>(lds + off) = (uint16_t)h;
         *reinterpret_cast<uint16_t*>(lds + off + A1P) = (uint16_t)m;
         *reinterpret_cast<uint16_t*>(lds + off + 2 * A1P) = (uint16_t)l;
@@ -424,9 +446,9 @@ conv_fwd_kernel(ConvFwdArgs a) {
   CF_STAMP();   // 4: barrier
   // ---- conv2: wave -> n-tile nt = w & 1 (oc = 16 nt + col), m-tiles w >> 1, (w >> 1) + 4
   {
-    const int nt = wave & 1, oc = 16 * nt + col;
+    const int nt = w8 & 1, oc = 16 * nt + col;
     CF_STAMP();   // 5: (W2 fragments are read per k-step below)
-    const int mA = wave >> 1, mB = mA + 4;
+    const int mA = w8 >> 1, mB = mA + 4;
     const bool hasB = mB < 6;
     const int posA = 16 * mA + col, posB = 16 * (hasB ? mB : mA) + col;   // A row of this lane
     const int pcA = posA < C2_P ? posA : 0, pcB = posB < C2_P ? posB : 0;
@@ -437,18 +459,18 @@ conv_fwd_kernel(ConvFwdArgs a) {
     for (int s = 0; s < ((ARL_ABLATE & 2) ? 0 : 8); ++s) {
       bf16x8 w2h[1], w2m[1], w2l[1];   // this k-step's W2 fragments, read inside the loop
       {
-        const int off = L_W2 + oc * WROW + (2 * s + (g >> 1)) * 32 + (g & 1) * 16;
+        const int off = LY::W2 + oc * WROW + (2 * s + (g >> 1)) * 32 + (g & 1) * 16;
         w2h[0] = lds_load<bf16x8>(lds, off);
         w2m[0] = lds_load<bf16x8>(lds, off + W2P);
         w2l[0] = lds_load<bf16x8>(lds, off + 2 * W2P);
       }
       const int tap = 2 * s + (g >> 1), dP = (tap >> 2) * 20 + (tap & 3);
-      const int offA = L_R1 + a1_slot(PA0 + dP, g & 1);
+      const int offA = LY::A1(el) + a1_slot(PA0 + dP, g & 1);
       const bf16x8 ahA = lds_load<bf16x8>(lds, offA), amA = lds_load<bf16x8>(lds, offA + A1P),
                    alA = lds_load<bf16x8>(lds, offA + 2 * A1P);
       mfma_x6(ahA, amA, alA, w2h[0], w2m[0], w2l[0], bigA, smlA);
       if (hasB) {
-        const int offB = L_R1 + a1_slot(PB0 + dP, g & 1);
+        const int offB = LY::A1(el) + a1_slot(PB0 + dP, g & 1);
         const bf16x8 ahB = lds_load<bf16x8>(lds, offB), amB = lds_load<bf16x8>(lds, offB + A1P),
                      alB = lds_load<bf16x8>(lds, offB + 2 * A1P);
         mfma_x6(ahB, amB, alB, w2h[0], w2m[0], w2l[0], bigB, smlB);
@@ -460,19 +482,19 @@ conv_fwd_kernel(ConvFwdArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int p = 16 * mA + g * 4 + r;
-      if (p < C2_P) a2g[oc * C2_P + p] = fmaxf(__fadd_rn(__fadd_rn(bigA[r], smlA[r]), b), 0.f);
+      if (valid && p < C2_P) a2g[oc * C2_P + p] = fmaxf(__fadd_rn(__fadd_rn(bigA[r], smlA[r]), b), 0.f);
     }
     if (hasB) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int p = 16 * mB + g * 4 + r;
-        if (p < C2_P) a2g[oc * C2_P + p] = fmaxf(__fadd_rn(__fadd_rn(bigB[r], smlB[r]), b), 0.f);
+        if (valid && p < C2_P) a2g[oc * C2_P + p] = fmaxf(__fadd_rn(__fadd_rn(bigB[r], smlB[r]), b), 0.f);
       }
     }
 #if ARL_CF_STAMP
     CF_STAMP();   // 7: end
     if (lane == 0) {   // wave w's stamps -> a2[e][w * 8 ..]; wave 0 also the start time
-      uint32_t* o = reinterpret_cast<uint32_t*>(a2g) + wave * 10;
+      uint32_t* o = reinterpret_cast<uint32_t*>(a2g) + w8 * 10;
       for (int k = 0; k < 8; ++k) o[k] = stamp[k];
       o[8] = (uint32_t)t0;
       o[9] = (uint32_t)(t0 >> 32);
@@ -487,8 +509,14 @@ hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const i
   if (n <= 0) return hipSuccess;
   if (ne < 0) ne = n;
   if (ne <= 0) return hipSuccess;
-  ConvFwdArgs a{frames, nvalid, ctl, n, R, t, W1, b1, W2, b2, a1, a2, layout, e0, RingArgs{}};
-  hipLaunchKernelGGL(conv_fwd_kernel<false>, dim3(ne), dim3(NT), 0, s, a);
+  ConvFwdArgs a{frames, nvalid, ctl, n, R, t, W1, b1, W2, b2, a1, a2, layout, e0, RingArgs{}, e0 + ne};
+  // two envs a workgroup (16 waves sharing the weight planes) in nets of >= 512 envs, whether the
+  // launch covers all of them or one env group's range (C4 0.513 -> 0.503 ms, C3 1.227 -> 1.212 ms at
+  // two groups, profiles/r03/r3k); ARL_CONV_EPW=1 / 2 forces one form (A/B timing)
+  static const char* epw = getenv("ARL_CONV_EPW");
+  const int k = (epw && (epw[0] == '1' || epw[0] == '2')) ? epw[0] - '0' : (n >= 512 ? 2 : 1);
+  if (k == 2) hipLaunchKernelGGL((conv_fwd_kernel<false, 2>), dim3((ne + 1) / 2), dim3(2 * NT), 0, s, a);
+  else hipLaunchKernelGGL((conv_fwd_kernel<false, 1>), dim3(ne), dim3(NT), 0, s, a);
   return hipGetLastError();
 }
 
@@ -497,8 +525,8 @@ hipError_t launch_phi_conv_fwd(const RingArgs& ring, const float* W1, const floa
   const int ne = ring.ne < 0 ? ring.n : ring.ne;
   if (ne <= 0) return hipSuccess;
   ConvFwdArgs a{ring.frames, ring.nvalid, ring.ctl, ring.n, ring.R, ring.t, W1, b1, W2, b2, a1, a2, FRAMES_RING,
-                ring.e0, ring};
-  hipLaunchKernelGGL(conv_fwd_kernel<true>, dim3(ne), dim3(NT), 0, s, a);
+                ring.e0, ring, ring.e0 + ne};
+  hipLaunchKernelGGL((conv_fwd_kernel<true, 1>), dim3(ne), dim3(NT), 0, s, a);
   return hipGetLastError();
 }
 

@@ -22,6 +22,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "arl_internal.hpp"
 
 #ifndef ARL_ABLATE
@@ -191,11 +194,91 @@ fc_fwd_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, 
   if (tid == 0) __hip_atomic_store(&tickets[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---- partials-only launches over >= 512 envs: 64 x 64 output tiles on 16
+// waves (one 16 x 16 sub-tile each), so 512 envs are one workgroup per CU (256
+// workgroups) instead of two rounds of the 32 x 64 form, and each staged byte
+// feeds twice the MFMAs.  The same three K chunks in the same k order
+// (bit-identical partials), staged through two LDS buffers: chunks 0 and 1 are
+// issued together, chunk 2 into chunk 0's buffer once its MFMAs are done.
+namespace {
+constexpr int GBM = 64, GT = 1024, GW = GT / 64;
+constexpr int GROWS = GBM + FBN;                  // 128 staged rows (64 of a2, 64 of W)
+__host__ __device__ constexpr int g_pieces(int c) { return (GROWS * ch_ld(c) + 63) / 64; }   // 58, 58, 52
+constexpr int GBUF4 = g_pieces(0) * 64;           // float4 per buffer
+static_assert(g_pieces(1) == g_pieces(0) && g_pieces(2) <= g_pieces(0), "chunk buffers");
+__host__ __device__ constexpr int g_wave_pieces(int c, int w) { return (g_pieces(c) - w + GW - 1) / GW; }
+}  // namespace
+
+__global__ void __launch_bounds__(GT)
+fc_fwd_big_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) float S[2 * GBUF4 * 4];   // 118,784 B
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int split = blockIdx.x % FSPLIT, tile = blockIdx.x / FSPLIT;
+  constexpr int NTN = HID / FBN;
+  const int m0 = (tile / NTN) * GBM, n0 = (tile % NTN) * FBN, k0 = split * FKS;
+  auto issue = [&](int c) {   // slot i of chunk c -> row i / ld, float4 column min(i % ld, w - 1)
+    float* buf = S + 4 * (c & 1) * GBUF4;
+    for (int it = wave; it < g_pieces(c); it += GW) {
+      const int i = min(it * 64 + lane, GROWS * ch_ld(c) - 1);
+      const int r = i / ch_ld(c), cc = min(i - r * ch_ld(c), ch_w(c) - 1);
+      const float* src = r < GBM ? a2 + (int64_t)min(m0 + r, n - 1) * A2   // rows past n: never stored
+                                 : W + (int64_t)(n0 + r - GBM) * A2;
+      __builtin_amdgcn_global_load_lds(src + k0 + ch_k0(c) + 4 * cc,
+                                       (__attribute__((address_space(3))) void*)(buf + 4 * it * 64), 16, 0, 0);
+    }
+  };
+  issue(0);
+  issue(1);
+  const int q = lane >> 4, col = lane & 15;
+  const int ms = wave & 3, ns = wave >> 2;
+  f32x4 c0 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < FCH; ++c) {
+    // this wave's pieces of chunk c have landed (chunk c + 1's may still fly), then everyone's
+    fc_wait_vm(c + 1 < FCH ? g_wave_pieces(c + 1, wave) : 0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const float* buf = S + 4 * (c & 1) * GBUF4;
+    const float* Ar = buf + (ms * 16 + col) * 4 * ch_ld(c) + 4 * q;
+    const float* B0 = buf + (GBM + ns * 16 + col) * 4 * ch_ld(c) + 4 * q;
+    constexpr int G16[FCH] = {7, 7, 6};
+#pragma unroll
+    for (int s = 0; s < G16[c]; ++s) {
+      const f32x4 av = *reinterpret_cast<const f32x4*>(Ar + 16 * s);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(B0 + 16 * s);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], b0[r], c0, 0, 0, 0);
+    }
+    if (c == FCH - 1) c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ar[96 - 3 * q], B0[96 - 3 * q], c0, 0, 0, 0);
+    if (c == 0) {   // every wave is done reading buffer 0: chunk 2 goes there
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      issue(2);
+    }
+  }
+  float* part = slab + (int64_t)split * n * HID;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + ms * 16 + q * 4 + r;
+    if (m < n)
+      __hip_atomic_store(part + (int64_t)m * HID + n0 + ns * 16 + col, c0[r], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 int fc_fwd_tiles(int n) { return ((n + FBM - 1) / FBM) * (HID / FBN); }
 
 hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b, float* slab, int* tickets,
-                         float* hfc, hipStream_t s) {
+                         float* hfc, hipStream_t s, int n_total) {
   if (n <= 0) return hipSuccess;
+  // partials-only launches of a net of >= 512 envs (n_total; one launch or the env groups' ranges of it)
+  // on the 64-row tiles (ARL_FC_BIG=0 / 1 forces, A/B timing)
+  static const char* big = getenv("ARL_FC_BIG");
+  const bool use_big =
+      tickets == nullptr && (big && (big[0] == '0' || big[0] == '1') ? big[0] == '1' : std::max(n, n_total) >= 512);
+  if (use_big) {
+    hipLaunchKernelGGL(fc_fwd_big_kernel, dim3((unsigned)(((n + GBM - 1) / GBM) * (HID / FBN) * FSPLIT)), dim3(GT), 0,
+                       s, a2, n, W, slab);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(fc_fwd_kernel, dim3((unsigned)(fc_fwd_tiles(n) * FSPLIT)), dim3(FT), 0, s, a2, n, W, b, slab,
                      tickets, hfc);
   return hipGetLastError();

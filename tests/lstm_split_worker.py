@@ -31,7 +31,8 @@ def main(out, one=False):
     ag.run_window(dp, dr, dd, P, first=True, env_groups=2, split_update=one)
     if one:
         torch.cuda.synchronize()
-        per = {"g." + k.replace("/", "."): v.detach().cpu().numpy() for k, v in ag.net.state_dict(ag.net.grads).items()}
+        per = {"g." + k.replace("/", "."): np.asarray(v.detach().cpu().numpy() if torch.is_tensor(v) else v)
+               for k, v in ag.net.state_dict(ag.net.grads).items()}
         np.savez(out, grads=ag.net.grads.detach().cpu().numpy(),
                  hbuf=ag.net.buffer("hbuf", torch.float32).detach().cpu().numpy(),
                  dfc=ag.net.buffer("dfc", torch.float32).detach().cpu().numpy(), **per)
