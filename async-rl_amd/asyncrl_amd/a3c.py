@@ -394,9 +394,10 @@ class A3C:
         one kernel after chain g - 1, so one chain's latency-bound kernels
         (policy, FC ticket reduce) overlap another's conv / phi.  The streams
         join before arl_learn.  Results are identical to env_groups=1.
-        None picks DeviceNet.default_env_groups() (2 from 512 envs up: C3 LSTM
-        1024 envs 1.628 -> 1.542 ms, C4 FF 512 envs 0.683 -> 0.641 ms; at 256
-        envs one chain is faster, 0.414 vs 0.431-0.448 ms)."""
+        None picks DeviceNet.default_env_groups() (2 from 1,024 envs up: C3
+        LSTM 1,024 envs 1.215 -> 1.162 ms at two chains of 512; at 512 envs one
+        chain is faster since those launches run two envs a conv workgroup and
+        64-row FC tiles, C4 0.497 vs 0.509-0.518 ms; profiles/r03/r3l)."""
         net, T = self.net, self.t_max
         groups = net.env_groups(net.default_env_groups() if env_groups is None else env_groups)
         if len(groups) == 1:

@@ -225,9 +225,12 @@ class DeviceNet:
               "arl_observe_act_envs")
 
     def default_env_groups(self) -> int:
-        """Forward chains per window that measured fastest on one MI355X
-        (scripts/groups_ab.sh): 2 from 512 envs up, else 1."""
-        return 2 if self.n_envs >= 512 else 1
+        """Forward chains per window that measured fastest on one MI355X:
+        2 from 1,024 envs up, else 1.  Since the 512-env launches run two envs a
+        conv workgroup and 64-row FC tiles, one chain of 512 envs beats two of
+        256 (C4 0.497 vs 0.509-0.518 ms), while 1,024 LSTM envs still gain
+        from two chains of 512 (profiles/r03/r3l)."""
+        return 2 if self.n_envs >= 1024 else 1
 
     def env_groups(self, groups: int):
         """Split the envs into <= `groups` contiguous ranges (e0, ne) with e0 a

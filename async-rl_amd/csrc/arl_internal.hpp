@@ -236,7 +236,7 @@ inline PolicyArgs make_policy_args(const float* Wpi, const float* bpi, const flo
 constexpr int FC_SPLIT = 8;   // fc forward split-K (one slice per XCD)
 int fc_fwd_tiles(int n);      // tickets needed for n envs
 hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b, float* slab, int* tickets,
-                         float* hfc, hipStream_t s, int n_total = 0);
+                         float* hfc, hipStream_t s);
 // FC backward (fc_bwd.hip): dW / db straight into the gradient, da2 = (dfc W) * (a2 > 0)
 // weight gradients of the policy / value heads (a3c.py:126-130 through
 // policy.py / v_function.py Linear layers): rows a < A from dlogits, row A

@@ -22,7 +22,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <algorithm>
 #include <cstdlib>
 
 #include "arl_internal.hpp"
@@ -267,13 +266,13 @@ fc_fwd_big_kernel(const float* __restrict__ a2, int n, const float* __restrict__
 int fc_fwd_tiles(int n) { return ((n + FBM - 1) / FBM) * (HID / FBN); }
 
 hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b, float* slab, int* tickets,
-                         float* hfc, hipStream_t s, int n_total) {
+                         float* hfc, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  // partials-only launches of a net of >= 512 envs (n_total; one launch or the env groups' ranges of it)
-  // on the 64-row tiles (ARL_FC_BIG=0 / 1 forces, A/B timing)
+  // partials-only launches over >= 512 envs on the 64-row tiles (C4 0.503 -> 0.497 ms at one env group,
+  // C3 1.215 -> 1.162 ms; at 256-env launches, 128 workgroups of them lose: profiles/r03/r3l);
+  // ARL_FC_BIG=0 / 1 forces one form (A/B timing)
   static const char* big = getenv("ARL_FC_BIG");
-  const bool use_big =
-      tickets == nullptr && (big && (big[0] == '0' || big[0] == '1') ? big[0] == '1' : std::max(n, n_total) >= 512);
+  const bool use_big = tickets == nullptr && (big && (big[0] == '0' || big[0] == '1') ? big[0] == '1' : n >= 512);
   if (use_big) {
     hipLaunchKernelGGL(fc_fwd_big_kernel, dim3((unsigned)(((n + GBM - 1) / GBM) * (HID / FBN) * FSPLIT)), dim3(GT), 0,
                        s, a2, n, W, slab);

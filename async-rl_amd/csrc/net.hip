@@ -532,7 +532,7 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne, con
   const int64_t o = (int64_t)t * n + e0;
   float* fc_slab = net.at<float>(net.w_slab) + (int64_t)FC_SPLIT * e0 * HID;
   if (net.arch != ARCH_LSTM) {   // FF: split-K partials, reduce + relu + heads in one policy_fc launch
-    ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab, nullptr, nullptr, s, n));
+    ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab, nullptr, nullptr, s));
     return launch_policy_fc(fc_slab, ne, P + net.o_fcb, hfc,
                             make_policy_args(P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
                                              net.at<int64_t>(net.w_ctl), t, net.env_offset + e0, t < net.T ? mode : 0,
@@ -546,7 +546,7 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne, con
   // staging (lstm.hip XRED); ARL_LSTM_XRED=0 / the generic gate GEMM: the FC's ticket reduce
   const bool xred = !LSTM_GEMM_GENERIC && LSTM_XRED;
   ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab,
-                        xred ? nullptr : net.at<int>(net.w_tick) + fc_fwd_tiles(e0), xred ? nullptr : hfc, s, n));
+                        xred ? nullptr : net.at<int>(net.w_tick) + fc_fwd_tiles(e0), xred ? nullptr : hfc, s));
   const float* hpol = hfc;
   if (xred) {
     const int64_t r0 = (int64_t)t * n + e0;

@@ -107,7 +107,7 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--env-groups", type=int, default=0,
                     help="forward chains on separate streams per window (A3C.run_window env_groups); "
-                         "0: the library default (2 from 512 envs per GPU up, else 1)")
+                         "0: the library default (2 from 1,024 envs per GPU up, else 1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="0 disables the CPU baseline leg")
     ap.add_argument("--kernel-reps", type=int, default=50)
     return ap.parse_args()
