@@ -56,6 +56,15 @@
 #ifndef ARL_S3_UNROLL
 #define ARL_S3_UNROLL 3
 #endif
+// LDS operands of steps 2 / 3 read ahead of their MFMAs (one LDS wait per step-2 tile / per group of
+// three step-3 k-steps instead of one or two per k-step; A/B knobs, off: with ARL_S1_UNROLL=7 (21
+// spills) conv_bwd 67.8 -> 70.7 us at C2, step 3's 75-76 us, profiles/r03/r3q)
+#ifndef ARL_S2_PREFETCH
+#define ARL_S2_PREFETCH 0
+#endif
+#ifndef ARL_S3_PREFETCH
+#define ARL_S3_PREFETCH 0
+#endif
 #ifndef ARL_CB_STAMP
 #define ARL_CB_STAMP 0   // timing experiments only: s_memtime at every barrier into the slab (results wrong)
 #endif
@@ -402,13 +411,24 @@ conv_bwd_kernel(ConvBwdArgs a) {
         const int oy = keep ? 2 * (cy - 1) + py : 0, ox = keep ? 2 * (cx - 1) + px : 0;
         const uint32_t m = reinterpret_cast<const uint16_t*>(lds + L_MASK)[oy * 20 + ox];
         f32x4 big = {0.f, 0.f, 0.f, 0.f}, sml = big;
+        // the tile's B fragments of all four k-steps read first (12 b128 in flight, one LDS
+        // wait), then its 24 MFMAs -- read per k-step they left two exposed LDS waits a k-step
+        bf16x8 bh[4], bm[4], bl[4];
 #pragma unroll
-        for (int ks = 0; ks < ((ARL_ABLATE & 16) ? 0 : 4); ++ks) {
+        for (int ks = 0; ks < 4; ++ks) {
           const int dcell = (ks >> 1) * 11 + (ks & 1);
           const int o = L_D2 + d2_slot(cell < 121 ? cell - dcell : 0, g);
-          const bf16x8 bh = lds_load<bf16x8>(lds, o), bm = lds_load<bf16x8>(lds, o + D2P),
-                       bl = lds_load<bf16x8>(lds, o + 2 * D2P);
-          mfma_x6(w2h[ks], w2m[ks], w2l[ks], bh, bm, bl, big, sml);
+          bh[ks] = lds_load<bf16x8>(lds, o);
+          bm[ks] = lds_load<bf16x8>(lds, o + D2P);
+          bl[ks] = lds_load<bf16x8>(lds, o + 2 * D2P);
+          if (!ARL_S2_PREFETCH && !(ARL_ABLATE & 16))
+            mfma_x6(w2h[ks], w2m[ks], w2l[ks], bh[ks], bm[ks], bl[ks], big, sml);
+        }
+        if (ARL_S2_PREFETCH) {
+          __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs (the scheduler sinks them)
+#pragma unroll
+          for (int ks = 0; ks < ((ARL_ABLATE & 16) ? 0 : 4); ++ks)
+            mfma_x6(w2h[ks], w2m[ks], w2l[ks], bh[ks], bm[ks], bl[ks], big, sml);
         }
         if (keep) {
           uint8_t* d = lds + L_D1 + (4 * g) * D1_OC + oy * D1_ROW + ox * 2;
@@ -432,6 +452,45 @@ conv_bwd_kernel(ConvBwdArgs a) {
     // = (oy, X0 = 8 c): 8 positions (oy, X0..X0+7).  Tile a = rows (ky, kx =
     // 4 a + (col & 3)): the a = 0 and a = 1 fragments of a lane are pixels
     // X0..X0+7 and X0+1..X0+8 of one phase row, converted once and packed twice.
+#if ARL_S3_PREFETCH
+    // groups of three k-steps: every LDS operand of the group read first, one wait, then the
+    // pixel conversions and 18 MFMAs (same k order)
+    for (int k0 = 0; k0 < ((ARL_ABLATE & 32) ? 0 : 15); k0 += 3) {
+      bf16x8 bh[3], bm[3], bl[3];
+      uint2 lo[3];
+      uint32_t nx[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int Gk = 4 * (k0 + j) + g, oy = Gk / 3, c = Gk - 3 * oy;
+        const int ob = L_D1 + col * D1_OC + oy * D1_ROW + 16 * c;
+        bh[j] = lds_load<bf16x8>(lds, ob);
+        bm[j] = lds_load<bf16x8>(lds, ob + D1P);
+        bl[j] = lds_load<bf16x8>(lds, ob + 2 * D1P);
+        const int oa = xrow3 + oy * 16 * XR + 8 * c;
+        lo[j] = lds_load<uint2>(lds, oa);
+        nx[j] = lds_load<uint32_t>(lds, oa + 8);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        uint32_t f[9];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          f[k] = __float_as_uint((float)((lo[j].x >> (8 * k)) & 0xffu));
+          f[4 + k] = __float_as_uint((float)((lo[j].y >> (8 * k)) & 0xffu));
+        }
+        f[8] = __float_as_uint((float)(nx[j] & 0xffu));
+#pragma unroll
+        for (int a_ = 0; a_ < 2; ++a_) {
+          const bf16x8 xa = frag_from_pairs(__builtin_amdgcn_perm(f[a_ + 1], f[a_], 0x07060302u),
+                                            __builtin_amdgcn_perm(f[a_ + 3], f[a_ + 2], 0x07060302u),
+                                            __builtin_amdgcn_perm(f[a_ + 5], f[a_ + 4], 0x07060302u),
+                                            __builtin_amdgcn_perm(f[a_ + 7], f[a_ + 6], 0x07060302u));
+          mfma_x3(xa, bh[j], bm[j], bl[j], big3[a_], sml3[a_]);
+        }
+      }
+    }
+#else
 #pragma unroll ARL_S3_UNROLL
     for (int ks = 0; ks < ((ARL_ABLATE & 32) ? 0 : 15); ++ks) {
       const int Gk = 4 * ks + g, oy = Gk / 3, c = Gk - 3 * oy;
@@ -457,6 +516,7 @@ conv_bwd_kernel(ConvBwdArgs a) {
         mfma_x3(xa, bh, bm, bl, big3[a_], sml3[a_]);
       }
     }
+#endif
   }
   // ---- partial slab of this workgroup
   float* out = a.slab + (int64_t)blockIdx.x * SLAB;

@@ -47,6 +47,14 @@
                        // luminance, 128 resize)
 #endif
 
+// conv1 / conv2 k-steps software-pipelined: a k-step's LDS operands are read while the previous
+// k-step's MFMAs run (double-buffered registers) instead of read-then-wait inside each k-step.
+// A/B knob, off: 18.6 -> 19.6 us at 512 envs, 35 -> 38 us at 1,024 (95 -> 127 VGPRs; the other
+// waves of the CU already cover the LDS latency), C2 equal (profiles/r03/r3r)
+#ifndef ARL_CF_PREFETCH
+#define ARL_CF_PREFETCH 0
+#endif
+
 #ifndef ARL_CF_STAMP
 #define ARL_CF_STAMP 0   // timing experiments only: s_memtime at phase ends into a2 (results wrong)
 #endif
@@ -407,12 +415,37 @@ conv_fwd_kernel(ConvFwdArgs a) {
     // conv1 with each k-step's W1 fragments read from LDS inside the loop (their
     // reads overlap the MFMAs instead of forming a phase of their own), then a
     // barrier: every wave is done with the W1 planes before the a1 planes overwrite them
+#if ARL_CF_PREFETCH
+    {
+      // operands of k-step s in buffer s & 1; every lane loads a 4th tile fragment (the waves
+      // without tile 24 re-read tile w's) so the loads are unconditional
+      bf16x8 wh[2], wm[2], wl[2], xa[2][TJ];
+      auto load = [&](int s, int b) {
+        w1_frag(s, wh[b], wm[b], wl[b]);
+        const int u = 4 * s + g, off = (u >> 3) * XB_PLANE + (u & 7) * XB_ROW;
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) xa[b][j] = lds_load8_a8(lds, baseX[j] + off);
+      };
+      load(0, 0);
+#pragma unroll
+      for (int s = 0; s < ((ARL_ABLATE & 1) ? 0 : 8); ++s) {
+        const int b = s & 1;
+        if (s + 1 < 8) load(s + 1, b ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) mfma_x3(xa[b][j], wh[b], wm[b], wl[b], big[j], sml[j]);
+        if (has3) mfma_x3(xa[b][3], wh[b], wm[b], wl[b], big[3], sml[3]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#else
 #pragma unroll
     for (int s = 0; s < ((ARL_ABLATE & 1) ? 0 : 8); ++s) {
       bf16x8 wh, wm, wl;
       w1_frag(s, wh, wm, wl);
       conv1_step(s, wh, wm, wl);
     }
+#endif
     CF_STAMP();   // 2: conv1 MFMAs issued
     __syncthreads();
     if (EPW == 2 && el == 1) w2_split_store(lds, t8, w2v, LY::W2);   // read by conv2 after the next barrier
@@ -455,6 +488,33 @@ conv_fwd_kernel(ConvFwdArgs a) {
     const int oyA = pcA / 9, oxA = pcA - oyA * 9, oyB = pcB / 9, oxB = pcB - oyB * 9;
     const int PA0 = (2 * oyA) * 20 + 2 * oxA, PB0 = (2 * oyB) * 20 + 2 * oxB;
     f32x4 bigA = {0.f, 0.f, 0.f, 0.f}, smlA = bigA, bigB = bigA, smlB = bigA;
+#if ARL_CF_PREFETCH
+    {
+      // k-step s's W2 and a1 fragments in buffer s & 1 (tile B's re-read tile A's where absent)
+      bf16x8 w2[2][3], aA[2][3], aB[2][3];
+      auto load = [&](int s, int b) {
+        const int off = LY::W2 + oc * WROW + (2 * s + (g >> 1)) * 32 + (g & 1) * 16;
+        const int tap = 2 * s + (g >> 1), dP = (tap >> 2) * 20 + (tap & 3);
+        const int offA = LY::A1(el) + a1_slot(PA0 + dP, g & 1), offB = LY::A1(el) + a1_slot(PB0 + dP, g & 1);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          w2[b][k] = lds_load<bf16x8>(lds, off + k * W2P);
+          aA[b][k] = lds_load<bf16x8>(lds, offA + k * A1P);
+          aB[b][k] = lds_load<bf16x8>(lds, offB + k * A1P);
+        }
+      };
+      load(0, 0);
+#pragma unroll
+      for (int s = 0; s < ((ARL_ABLATE & 2) ? 0 : 8); ++s) {
+        const int b = s & 1;
+        if (s + 1 < 8) load(s + 1, b ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_x6(aA[b][0], aA[b][1], aA[b][2], w2[b][0], w2[b][1], w2[b][2], bigA, smlA);
+        if (hasB) mfma_x6(aB[b][0], aB[b][1], aB[b][2], w2[b][0], w2[b][1], w2[b][2], bigB, smlB);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#else
 #pragma unroll
     for (int s = 0; s < ((ARL_ABLATE & 2) ? 0 : 8); ++s) {
       bf16x8 w2h[1], w2m[1], w2l[1];   // this k-step's W2 fragments, read inside the loop
@@ -476,6 +536,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
         mfma_x6(ahB, amB, alB, w2h[0], w2m[0], w2l[0], bigB, smlB);
       }
     }
+#endif
     CF_STAMP();   // 6: conv2 MFMAs issued
     float* a2g = a.a2 + (int64_t)e * A2;
     const float b = bias2;   // b2[oc]

@@ -82,6 +82,32 @@ __device__ inline void fc_wait_vm(int n) {   // s_waitcnt vmcnt(n), n wave-unifo
   }
 }
 
+// The MFMAs of one staged chunk: every fragment read first (ARL_FC_PREFETCH: one LDS wait per chunk;
+// read per 16-k group, each group's reads were waited for right before its four MFMAs)
+#ifndef ARL_FC_PREFETCH
+#define ARL_FC_PREFETCH 1
+#endif
+template <int G>
+__device__ inline f32x4 fc_chunk_mfma(const float* Ar, const float* B0, f32x4 c0) {
+  f32x4 av[G], bv[G];
+#pragma unroll
+  for (int s = 0; s < G; ++s) {
+    av[s] = *reinterpret_cast<const f32x4*>(Ar + 16 * s);
+    bv[s] = *reinterpret_cast<const f32x4*>(B0 + 16 * s);
+    if (!ARL_FC_PREFETCH)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s][r], bv[s][r], c0, 0, 0, 0);
+  }
+  if (ARL_FC_PREFETCH) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < G; ++s)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s][r], bv[s][r], c0, 0, 0, 0);
+  }
+  return c0;
+}
+
 __global__ void __launch_bounds__(FT)
 fc_fwd_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, const float* __restrict__ bias,
               float* __restrict__ slab, int* __restrict__ tickets, float* __restrict__ hfc) {
@@ -123,13 +149,8 @@ fc_fwd_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, 
     const float* Ar = S + 4 * ch_base(c) + (ms * 16 + col) * 4 * ch_ld(c) + 4 * q;
     const float* B0 = S + 4 * ch_base(c) + (FBM + ns * 16 + col) * 4 * ch_ld(c) + 4 * q;
     constexpr int G16[FCH] = {7, 7, 6};   // whole 16-k groups per chunk
-#pragma unroll
-    for (int s = 0; s < ((ARL_ABLATE & 512) ? 0 : G16[c]); ++s) {   // lane quarter q holds k = 16 s + 4 q + r
-      const f32x4 av = *reinterpret_cast<const f32x4*>(Ar + 16 * s);
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(B0 + 16 * s);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], b0[r], c0, 0, 0, 0);
-    }
+    // lane quarter q holds k = 16 s + 4 q + r
+    if (!(ARL_ABLATE & 512)) c0 = G16[c] == 7 ? fc_chunk_mfma<7>(Ar, B0, c0) : fc_chunk_mfma<6>(Ar, B0, c0);
     if (c == FCH - 1 && !(ARL_ABLATE & 512)) {   // tail k = 320 + q (chunk column 96 + q)
       c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ar[96 - 3 * q], B0[96 - 3 * q], c0, 0, 0, 0);
     }
@@ -240,13 +261,7 @@ fc_fwd_big_kernel(const float* __restrict__ a2, int n, const float* __restrict__
     const float* Ar = buf + (ms * 16 + col) * 4 * ch_ld(c) + 4 * q;
     const float* B0 = buf + (GBM + ns * 16 + col) * 4 * ch_ld(c) + 4 * q;
     constexpr int G16[FCH] = {7, 7, 6};
-#pragma unroll
-    for (int s = 0; s < G16[c]; ++s) {
-      const f32x4 av = *reinterpret_cast<const f32x4*>(Ar + 16 * s);
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(B0 + 16 * s);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], b0[r], c0, 0, 0, 0);
-    }
+    c0 = G16[c] == 7 ? fc_chunk_mfma<7>(Ar, B0, c0) : fc_chunk_mfma<6>(Ar, B0, c0);
     if (c == FCH - 1) c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ar[96 - 3 * q], B0[96 - 3 * q], c0, 0, 0, 0);
     if (c == 0) {   // every wave is done reading buffer 0: chunk 2 goes there
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");

@@ -67,7 +67,7 @@ def _oracle_window(arch, params, states, acts, r, d, boot, st=None, dprev=None, 
     return {k: v.astype(np.float32) for k, v in g.items()}, out
 
 
-def _run_config(gpu, arch, N, A, windows=2, seed=0, kind="uniform"):
+def _run_config(gpu, arch, N, A, windows=2, seed=0, kind="uniform", env_groups=None):
     from asyncrl_amd import A3C, A3CFF, A3CLSTM, GradientClipping, RMSpropAsync
     rng = np.random.default_rng(seed)
     T, P = 5, 6          # pool of 6 steps, reused cyclically by the second window
@@ -78,7 +78,7 @@ def _run_config(gpu, arch, N, A, windows=2, seed=0, kind="uniform"):
     opt.add_hook(GradientClipping(40))
     agent = A3C(model, opt, T, 0.99)
     net = model.net
-    groups = net.env_groups(net.default_env_groups())
+    groups = net.env_groups(net.default_env_groups() if env_groups is None else env_groups)
     view = OracleEnvView(pairs, dones)
     dp, dr, dd = dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu)
     st = O.LSTMState(h=np.zeros((N, 256), np.float32), c=np.zeros((N, 256), np.float32), has=np.zeros(N, bool))
@@ -86,7 +86,7 @@ def _run_config(gpu, arch, N, A, windows=2, seed=0, kind="uniform"):
     for w in range(windows):
         k0 = w * T
         params = net.state_dict()
-        agent.run_window(dp, dr, dd, P, first=(w == 0), split_update=True)   # default env groups
+        agent.run_window(dp, dr, dd, P, first=(w == 0), split_update=True, env_groups=len(groups))
         torch.cuda.synchronize()
         states, boot = view.states_f32(k0, T)
         r, d = view.window_rd(rewards, k0, T)
@@ -129,9 +129,13 @@ def test_c3_lstm_1024_envs_shaped_frames(gpu):
     _run_config(gpu, O.ARCH_LSTM, 1024, 6, seed=13, kind="shaped")
 
 
-def test_c4_leg_ff_512_envs_two_groups(gpu):
-    groups = _run_config(gpu, O.ARCH_FF, 512, 4, seed=4)
-    assert len(groups) == 2
+@pytest.mark.parametrize("env_groups", [None, 2])
+def test_c4_leg_ff_512_envs(gpu, env_groups):
+    """The C4 per-GPU leg: the default one chain of 512 envs (two envs a conv
+    workgroup, 64-row FC tiles) and two chains of 256 (two envs a conv
+    workgroup, 32-row FC tiles)."""
+    groups = _run_config(gpu, O.ARCH_FF, 512, 4, seed=4, env_groups=env_groups)
+    assert len(groups) == (1 if env_groups is None else 2)
 
 
 def test_c2_ff_256_envs(gpu):
