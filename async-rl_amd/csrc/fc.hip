@@ -82,10 +82,11 @@ __device__ inline void fc_wait_vm(int n) {   // s_waitcnt vmcnt(n), n wave-unifo
   }
 }
 
-// The MFMAs of one staged chunk: every fragment read first (ARL_FC_PREFETCH: one LDS wait per chunk;
-// read per 16-k group, each group's reads were waited for right before its four MFMAs)
+// The MFMAs of one staged chunk.  ARL_FC_PREFETCH=1 (A/B knob, off): every fragment read first, one LDS
+// wait per chunk -- 9.7 -> 10.5 us at 512 envs, 19.6 -> 21-22.8 us at 1,024 (profiles/r03/r3s); the
+// default reads per 16-k group, each group's reads waited for right before its four MFMAs
 #ifndef ARL_FC_PREFETCH
-#define ARL_FC_PREFETCH 1
+#define ARL_FC_PREFETCH 0
 #endif
 template <int G>
 __device__ inline f32x4 fc_chunk_mfma(const float* Ar, const float* B0, f32x4 c0) {

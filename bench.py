@@ -180,6 +180,20 @@ def returns_bytes(N, T, A, mask=True, hid=256):
             + S * (4 * A + 4) + 8 * N + S * hid * 4)
 
 
+def conv_epw(n_envs):
+    """Envs per conv_fwd workgroup the library picks for a net of n_envs
+    (conv_fwd.hip launch_conv_fwd: two from 512 envs; ARL_CONV_EPW forces)."""
+    v = os.environ.get("ARL_CONV_EPW", "")[:1]
+    return int(v) if v in ("1", "2") else (2 if n_envs >= 512 else 1)
+
+
+def fc_big(n_launch):
+    """fc.hip launch_fc_fwd: 64-row tiles (fc_fwd_big_kernel) for partials-only
+    launches over >= 512 envs; ARL_FC_BIG forces."""
+    v = os.environ.get("ARL_FC_BIG", "")[:1]
+    return v == "1" if v in ("0", "1") else n_launch >= 512
+
+
 def source_version():
     """Digest of the HIP sources and the C-ABI header: PMC traffic files
     record the version they were measured on, and the bench uses one only
@@ -564,11 +578,13 @@ def main(a):
             ("phi", "rgb_ring_kernel" if doom else "phi_ring_kernel",
              lambda i: net.observe(1 + i % T, pairs, rewards, dones, P, stream=stream), 0 if fused else T + 1, "hbm",
              N * phi_bytes),
-            ("conv_fwd", "gemm_kernel x3 (implicit-GEMM convs)" if nat else "conv_fwd_kernel<false>",
+            ("conv_fwd", "gemm_kernel x3 (implicit-GEMM convs)" if nat else
+             f"conv_fwd_kernel<false, {conv_epw(N)}>",
              lambda i: net.run_stage("conv_fwd", i % T, stream=stream), 1 if fused else T + 1, "mfma",
              N * conv_fwd_flop),
             ("fc_fwd", "gemm_kernel + reduce_grad_kernel" if nat else
-             "fc_fwd_kernel (split-K partials)" if (not lstm or LSTM_XRED) else "fc_fwd_kernel",
+             (("fc_fwd_big_kernel" if fc_big(N) else "fc_fwd_kernel") + " (split-K partials)")
+             if (not lstm or LSTM_XRED) else "fc_fwd_kernel",
              lambda i: net.run_stage("fc_fwd", i % T, stream=stream), T + 1, "mfma", N * fc_fwd_flop),
             # FF NIPS / Doom FF: the FC split-K reduce + bias + relu runs in the policy launch
             # (policy_fc_kernel): it also reads the 8 partial slabs and writes h
@@ -627,7 +643,7 @@ def main(a):
                                              "frac": round(tf / F32_MFMA_PEAK_TFS, 4)}
         dom = max(kernels, key=lambda k: kernels[k]["window_share_us"])
         d = kernels[dom]
-        traffic = measured_traffic(N, T, arch, d["kernel"].split()[0])
+        traffic = measured_traffic(N, T, arch, d["kernel"].split(" (")[0])
         roof = {"bound": d["bound"], "kernel": d["kernel"], "achieved": d["achieved"], "peak": d["peak"],
                 "unit": d["unit"], "frac": d["frac"], "traffic": traffic, "avg_launch_us": d["avg_launch_us"],
                 "work_per_launch": d.get("flop_per_launch", d.get("bytes_per_launch")),
