@@ -39,6 +39,8 @@ constexpr int C1_OC = 16, C1_P = 400;  // conv1: 16 x 20 x 20
 constexpr int C2_OC = 32, C2_P = 81;   // conv2: 32 x 9 x 9
 constexpr int A1 = C1_OC * C1_P;       // 6400
 constexpr int A2 = C2_OC * C2_P;       // 2592
+constexpr int A2W = A2 / 32;             // 81 u32 words of a2 > 0 bits per env-step (fc_bwd job B mask)
+static_assert(A2 % 32 == 0, "mask words");
 constexpr int HID = 256;
 constexpr int GATES = 4 * HID;
 constexpr int ZERO_ROW_FLOATS = 64;     // LSTM: the zero row a reset sample's h_prev is DMA'd from (fc_bwd.hip)
@@ -117,7 +119,8 @@ struct Net {
   int64_t ws_bytes;
   int64_t w_ctl, w_frames, w_nvalid, w_reset, w_rewards, w_dones, w_a1, w_a2, w_hfc, w_gates, w_hbuf,
       w_cbuf, w_logits, w_probs, w_logp, w_v, w_ent, w_logpa, w_act, w_dlogits, w_dv, w_dh, w_dfc,
-      w_dG, w_dhn, w_dcn, w_da2, w_slab, w_norm, w_loss, w_tick, w_fcb_part = 0, w_fcb_tick = 0, w_zero = 0;
+      w_dG, w_dhn, w_dcn, w_da2, w_slab, w_norm, w_loss, w_tick, w_fcb_part = 0, w_fcb_tick = 0, w_zero = 0,
+      w_a2m = 0;   // (T+1, N, 81) a2 > 0 bits (ring-frame NIPS nets; 0: none)
   int64_t w_a3 = 0, w_da1 = 0, w_da3 = 0;   // Nature head only (w_da1 also ARCH_STATES)
   // LSTM recurrent state of pi_and_v on explicit states (A3CLSTM.pi_and_v, a3c_ale.py:55-63):
   // h, c (n, 256), the step's outputs hn, cn, and reset flags (1 = state is None)
@@ -190,10 +193,10 @@ hipError_t launch_heads_bwd(const float* dl, const float* dv, const float* Wpi, 
 // layout: FrameLayout of the ring (FRAMES_RGB: conv1 W (16, 3, 8, 8) on input planes 1..3)
 hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int t,
                            const float* W1, const float* b1, const float* W2, const float* b2, float* a1, float* a2,
-                           hipStream_t s, int layout = FRAMES_RING, int e0 = 0, int ne = -1);
+                           hipStream_t s, int layout = FRAMES_RING, int e0 = 0, int ne = -1, uint32_t* a2m = nullptr);
 // phi_ring_kernel + conv_fwd_kernel in one launch (one workgroup per env of ring.e0 + [0, ring.ne))
 hipError_t launch_phi_conv_fwd(const RingArgs& ring, const float* W1, const float* b1, const float* W2,
-                               const float* b2, float* a1, float* a2, hipStream_t s);
+                               const float* b2, float* a1, float* a2, hipStream_t s, uint32_t* a2m = nullptr);
 // the gradient's squared norm folded into the conv slab reduce (parts == null: not folded)
 struct NormFold {
   double* parts;            // conv_norm_parts(rest_blocks) f64 partials
@@ -249,7 +252,8 @@ struct HeadsDW {
   float *gWpi, *gbpi, *gWv, *gbv;
 };
 hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int S, float* gW, float* gb, float* da2,
-                         float* part, int* tick, hipStream_t s, const HeadsDW* heads = nullptr);
+                         float* part, int* tick, hipStream_t s, const HeadsDW* heads = nullptr,
+                         const uint32_t* a2m = nullptr);
 // LSTM gate weight gradients (upward W / b, lateral W) + dfc = (dG Wu) * (hfc > 0), the same kernel
 hipError_t launch_lstm_wgrad(const float* dG, const float* hfc, const float* hprev, const uint8_t* reset,
                              const float* zero, const float* Wu, int S, float* gWu, float* gWl, float* gbu, float* dfc,

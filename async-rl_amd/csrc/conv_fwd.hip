@@ -94,7 +94,11 @@ struct Lay {
   static constexpr int A1(int el) { return EPW == 1 ? W1 : el * 3 * A1P; }
   static constexpr int W2 = EPW == 1 ? L_W2 : 2 * 3 * A1P;           // 94,848 / 76,800
   static constexpr int END = EPW == 1 ? L_END : W1 + 3 * W1P;        // 145,536 / 138,240
+  // a2 > 0 mask words (81 u32 per env) in bytes dead during conv2: the screens (EPW 1), past the W2
+  // planes (EPW 2)
+  static constexpr int MSK(int el) { return EPW == 1 ? 0 : W2 + 3 * W2P + el * 336; }
 };
+static_assert(Lay<2>::MSK(1) + 336 <= Lay<2>::END && 336 <= Lay<1>::W1, "mask words");
 static_assert(Lay<2>::W2 + 3 * W2P <= Lay<2>::END && Lay<2>::END <= 160 * 1024, "EPW 2 layout");
 static_assert(Lay<1>::A1(0) == L_R1 && Lay<1>::END == L_END, "EPW 1 layout");
 }  // namespace
@@ -120,6 +124,7 @@ struct ConvFwdArgs {
   int e0;               // first env of this launch (env = e0 + EPW * blockIdx.x + env slot)
   RingArgs ring;        // PHI: the observation (pair pool, bookkeeping); frames / nvalid / ctl / n / R / t as above
   int e1;               // one past the last env of this launch (EPW = 2: an odd count leaves a slot idle)
+  uint32_t* a2m;        // (n, 81) bits of a2 > 0 for the FC backward's ReLU mask (fc_bwd.hip job B), or null
 };
 
 // W1 (16, 4, 8, 8) f32 -> the split planes [3][oc][k] in LDS: thread tid
@@ -451,6 +456,8 @@ conv_fwd_kernel(ConvFwdArgs a) {
     if (EPW == 2 && el == 1) w2_split_store(lds, t8, w2v, LY::W2);   // read by conv2 after the next barrier
   }
   float* a1g = a.a1 + (int64_t)e * A1;
+  uint32_t* msk = reinterpret_cast<uint32_t*>(lds + LY::MSK(el));
+  if (a.a2m != nullptr && t8 < A2W) msk[t8] = 0u;   // (its bytes are dead since conv1's barrier)
   {
     // C rows g*4 + r -> positions tile*16 + g*4 + r, col = oc
 #pragma unroll
@@ -540,17 +547,33 @@ conv_fwd_kernel(ConvFwdArgs a) {
     CF_STAMP();   // 6: conv2 MFMAs issued
     float* a2g = a.a2 + (int64_t)e * A2;
     const float b = bias2;   // b2[oc]
+    // a2 > 0 -> bit k = oc * 81 + p of the env's mask words (LDS ors, stored after a barrier)
+    const bool mk = a.a2m != nullptr;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int p = 16 * mA + g * 4 + r;
-      if (valid && p < C2_P) a2g[oc * C2_P + p] = fmaxf(__fadd_rn(__fadd_rn(bigA[r], smlA[r]), b), 0.f);
+      const float v = fmaxf(__fadd_rn(__fadd_rn(bigA[r], smlA[r]), b), 0.f);
+      if (valid && p < C2_P) a2g[oc * C2_P + p] = v;
+      if (mk && p < C2_P && v > 0.f) {
+        const int k = oc * C2_P + p;
+        __hip_atomic_fetch_or(msk + (k >> 5), 1u << (k & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
     }
     if (hasB) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int p = 16 * mB + g * 4 + r;
-        if (valid && p < C2_P) a2g[oc * C2_P + p] = fmaxf(__fadd_rn(__fadd_rn(bigB[r], smlB[r]), b), 0.f);
+        const float v = fmaxf(__fadd_rn(__fadd_rn(bigB[r], smlB[r]), b), 0.f);
+        if (valid && p < C2_P) a2g[oc * C2_P + p] = v;
+        if (mk && p < C2_P && v > 0.f) {
+          const int k = oc * C2_P + p;
+          __hip_atomic_fetch_or(msk + (k >> 5), 1u << (k & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
+    }
+    if (mk) {   // (block-uniform)
+      __syncthreads();
+      if (valid && t8 < A2W) a.a2m[(int64_t)e * (A2W) + t8] = msk[t8];
     }
 #if ARL_CF_STAMP
     CF_STAMP();   // 7: end
@@ -566,11 +589,11 @@ conv_fwd_kernel(ConvFwdArgs a) {
 
 hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int t,
                            const float* W1, const float* b1, const float* W2, const float* b2, float* a1, float* a2,
-                           hipStream_t s, int layout, int e0, int ne) {
+                           hipStream_t s, int layout, int e0, int ne, uint32_t* a2m) {
   if (n <= 0) return hipSuccess;
   if (ne < 0) ne = n;
   if (ne <= 0) return hipSuccess;
-  ConvFwdArgs a{frames, nvalid, ctl, n, R, t, W1, b1, W2, b2, a1, a2, layout, e0, RingArgs{}, e0 + ne};
+  ConvFwdArgs a{frames, nvalid, ctl, n, R, t, W1, b1, W2, b2, a1, a2, layout, e0, RingArgs{}, e0 + ne, a2m};
   // two envs a workgroup (16 waves sharing the weight planes) in nets of >= 512 envs, whether the
   // launch covers all of them or one env group's range (C4 0.513 -> 0.503 ms, C3 1.227 -> 1.212 ms at
   // two groups, profiles/r03/r3k); ARL_CONV_EPW=1 / 2 forces one form (A/B timing)
@@ -582,11 +605,11 @@ hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const i
 }
 
 hipError_t launch_phi_conv_fwd(const RingArgs& ring, const float* W1, const float* b1, const float* W2,
-                               const float* b2, float* a1, float* a2, hipStream_t s) {
+                               const float* b2, float* a1, float* a2, hipStream_t s, uint32_t* a2m) {
   const int ne = ring.ne < 0 ? ring.n : ring.ne;
   if (ne <= 0) return hipSuccess;
   ConvFwdArgs a{ring.frames, ring.nvalid, ring.ctl, ring.n, ring.R, ring.t, W1, b1, W2, b2, a1, a2, FRAMES_RING,
-                ring.e0, ring, ring.e0 + ne};
+                ring.e0, ring, ring.e0 + ne, a2m};
   hipLaunchKernelGGL((conv_fwd_kernel<true, 1>), dim3(ne), dim3(NT), 0, s, a);
   return hipGetLastError();
 }

@@ -181,6 +181,9 @@ struct FcBwdArgs {
   const uint8_t* reset;    // (S): the env reset at that step (its h_prev reads 0)
   const float* zero;       // >= 64 zero floats (the DMA source of a reset row)
   float* gW2;              // lateral W (1024, 256)
+  // FC: job B's ReLU mask as bits of a2 > 0 (S, 81 words; conv_fwd.hip writes them) instead of a2
+  // itself -- 324 instead of 10,368 bytes a sample; null: read a2
+  const uint32_t* a2m = nullptr;
 };
 
 // ---------------------------------------------------------------- job A: dW, db
@@ -527,22 +530,34 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
 #pragma unroll
   for (int i = 0; i < MT; ++i) mb[i] = 0u;
   f32x4 mraw[4];
+  uint32_t mw[4];
+  const bool bits = !SH::kLstm && a.a2m != nullptr;   // block-uniform
+  const __amdgpu_buffer_rsrc_t mskw = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint32_t*>(bits ? a.a2m : nullptr) + (int64_t)s0 * A2W, 0, bits ? rows * A2W * 4 : 0, BUF_DWORD3);
   issue(0);
 #pragma unroll 8
   for (int c = 0; c < NCH; ++c) {
     if (c + 1 < NCH) issue(c + 1);
     if (c >= 1 && c <= MT) {   // the band loaded one chunk ago (the compiler's own vmcnt wait)
+      if (bits) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+        for (int e = 0; e < 4; ++e) mb[c - 1] |= ((mw[e] >> (k & 31)) & 0xfu) << (4 * e);   // k % 4 == 0
+      } else {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) mb[c - 1] |= (mraw[e][u] > 0.f ? 1u : 0u) << (4 * e + u);
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) mb[c - 1] |= (mraw[e][u] > 0.f ? 1u : 0u) << (4 * e + u);
+      }
     }
     if (c < MT) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = wm * 16 * MT + 16 * c + 4 * q + e;
-        mraw[e] = __builtin_bit_cast(
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(msk, kin ? (row * NB + k) * 4 : OOB, 0, 0));
+        if (bits)
+          mw[e] = __builtin_amdgcn_raw_buffer_load_b32(mskw, kin ? (row * A2W + (k >> 5)) * 4 : OOB, 0, 0);
+        else
+          mraw[e] = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(msk, kin ? (row * NB + k) * 4 : OOB, 0, 0));
       }
     }
     // this chunk's DMA done: the next chunk's PIECES a wave and this chunk's mask band may still fly
@@ -728,7 +743,7 @@ int fc_bwd_tickets() { return 2 * NTA_MAX; }   // arrival tickets, then ready co
 // the bootstrap slot after the window's S rows) or the next parameters' (W),
 // and are never stored.
 hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int S, float* gW, float* gb, float* da2,
-                         float* part, int* tick, hipStream_t s, const HeadsDW* heads) {
+                         float* part, int* tick, hipStream_t s, const HeadsDW* heads, const uint32_t* a2m) {
   if (S <= 0) return hipSuccess;
   const int Z = fc_bwd_ranges(S);
   const int kpz = range_len(S, Z);
@@ -750,10 +765,12 @@ hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int 
   const int grid = (only && only[0] == 'a') ? na : (only && only[0] == 'b') ? nb : nc + na + nb;
   // ARL_FC_BWD_SPIN=1: ticket-first job A reduce (the last range's partial is never published)
   static const char* spin = getenv("ARL_FC_BWD_SPIN");
+  static const char* mask = getenv("ARL_FC_BWD_MASK");   // "f32": job B reads a2 for its mask (A/B timing)
+  if (mask && mask[0] == 'f') a2m = nullptr;
   static const char* xcd = getenv("ARL_FC_BWD_XCD");
   FcBwdArgs args{dfc, a2, W, S, Z, kpz, gW, gb, da2, part, tick, heads ? *heads : HeadsDW{}, nc, b0,
                  abl ? atoi(abl) : 0, (spin && atoi(spin) == 1) ? 1 : 0, (xcd && xcd[0] == '0') ? 0 : 1,
-                 nullptr, nullptr, nullptr, nullptr};
+                 nullptr, nullptr, nullptr, nullptr, a2m};
   if (split) hipLaunchKernelGGL((fc_bwd_kernel<2, true, ShapeFC>), dim3(grid), dim3(NT), 0, s, args);
   else if (MT == 2) hipLaunchKernelGGL((fc_bwd_kernel<2, false, ShapeFC>), dim3(grid), dim3(NT), 0, s, args);
   else hipLaunchKernelGGL((fc_bwd_kernel<4, false, ShapeFC>), dim3(grid), dim3(NT), 0, s, args);

@@ -434,6 +434,8 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   const int64_t H = net.hid, nA1 = NAT ? NA1 : A1, nA2 = NAT ? NA2 : A2;
   net.w_a1 = buf("a1", T1 * n * nA1 * 4);
   net.w_a2 = buf("a2", T1 * n * nA2 * 4);
+  // the FC backward's ReLU mask as bits, written by conv_fwd.hip (its f32-state / Nature paths write none)
+  net.w_a2m = buf("a2_mask", (NAT || sts) ? 0 : T1 * n * A2W * 4);
   net.w_a3 = buf("a3", NAT ? T1 * n * NA3 * 4 : 0);
   net.w_hfc = buf("hfc", T1 * n * H * 4);
   net.w_gates = buf("gates", L ? T1 * n * GATES * 4 : 0);
@@ -479,6 +481,13 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
 
 // ---------------------------------------------------------------- forward
 
+// a2 > 0 bits of window slot t (conv_fwd.hip writes them, fc_bwd.hip's job B reads them as its ReLU
+// mask); null for the nets whose conv forward is not conv_fwd.hip (Nature, f32 states)
+static uint32_t* a2_mask(const Net& net, int t) {
+  if (net.arch == ARCH_FF_NATURE || net.states) return nullptr;
+  return net.at<uint32_t>(net.w_a2m) + (int64_t)t * net.N * A2W;
+}
+
 // head after conv1 (conv2 -> fc) for n rows, activations at a1/a2/hfc
 static hipError_t fc_forward(const Net& net, int n, const float* a2, float* hfc, hipStream_t s) {
   return launch_fc_fwd(a2, n, net.p + net.o_fcW, net.p + net.o_fcb, net.at<float>(net.w_slab),
@@ -520,14 +529,15 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne, con
   if (obs != nullptr) {
     if (net.layout != FRAMES_RING || (part & ACT_AFTER_CONV) || obs->e0 != e0 || obs->ne != ne)
       return hipErrorInvalidValue;
-    ARL_TRY(launch_phi_conv_fwd(*obs, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W, P + net.o_c2b, a1, a2, s));
+    ARL_TRY(launch_phi_conv_fwd(*obs, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W, P + net.o_c2b, a1, a2, s,
+                                a2_mask(net, t)));
   } else if (!(part & ACT_AFTER_CONV) && net.states) {
     if (e0 != 0 || ne != n) return hipErrorInvalidValue;   // one launch over all envs
     ARL_TRY(states_conv_fwd(net, t, a1, a2, s));
   } else if (!(part & ACT_AFTER_CONV))
     ARL_TRY(launch_conv_fwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
                             net.at<int64_t>(net.w_ctl), n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W,
-                            P + net.o_c2b, a1, a2, s, net.layout, e0, ne));
+                            P + net.o_c2b, a1, a2, s, net.layout, e0, ne, a2_mask(net, t)));
   if (part & ACT_CONV_ONLY) return hipSuccess;
   const int64_t o = (int64_t)t * n + e0;
   float* fc_slab = net.at<float>(net.w_slab) + (int64_t)FC_SPLIT * e0 * HID;
@@ -817,7 +827,7 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
   //    one launch (fc_bwd.hip)
   if (!FC_BWD_GEMM)
     return launch_fc_bwd(dfc, a2, P + net.o_fcW, S, G + net.o_fcW, G + net.o_fcb, net.at<float>(net.w_da2),
-                         net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s, &heads);
+                         net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s, &heads, a2_mask(net, 0));
   ARL_TRY((launch_gemm2_nt<64, 64, 32, 2, 4, 512, GM, GM, GK, GM>(   // 8 waves, 2 sub-tiles each (ARL_FC_BWD=gemm)
       gemm_job<64, 32>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab_f, HID, A2 + 1}, HID, A2 + 1, S, pl.fc_w, 64),
       gemm_job<64, 32>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2}, EpiMask{da2, a2, A2}, S, A2, HID, 1, 64), s)));
@@ -844,7 +854,7 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
       return launch_conv_fwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
                              net.at<int64_t>(net.w_ctl), n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W,
                              P + net.o_c2b, net.at<float>(net.w_a1) + (int64_t)t * n * A1, a2 + (int64_t)t * n * A2,
-                             s, net.layout);
+                             s, net.layout, 0, -1, a2_mask(net, t));
     case STAGE_FC_FWD:   // as in net_act: FF (and the LSTM's XRED gate kernel) reduce the partials downstream
       if (net.arch != ARCH_LSTM || (!LSTM_GEMM_GENERIC && LSTM_XRED))
         return launch_fc_fwd(a2 + (int64_t)t * n * A2, n, P + net.o_fcW, P + net.o_fcb, slab, nullptr, nullptr, s);
@@ -867,7 +877,7 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
                             G + net.o_pib, G + net.o_vW, G + net.o_vb};
         return launch_fc_bwd(net.at<float>(net.w_dfc), a2, P + net.o_fcW, S, G + net.o_fcW, G + net.o_fcb,
                              net.at<float>(net.w_da2), net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s,
-                             &heads);
+                             &heads, a2_mask(net, 0));
       }
       const Plans pl = make_plans(net);
       const float* dfc = net.at<float>(net.w_dfc);

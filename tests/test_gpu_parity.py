@@ -838,3 +838,40 @@ def test_conv_fwd_two_envs_identical(gpu, tmp_path, n_envs):
     for o in outs[1:]:
         for k in outs[0].files:
             assert np.array_equal(outs[0][k], o[k]), k
+
+
+@pytest.mark.parametrize("arch,N", [("ff", 75), ("ff", 512), ("lstm", 80)])
+def test_a2_mask_bits_match_a2(gpu, arch, N):
+    """conv_fwd.hip's a2 > 0 bits (the FC backward's ReLU mask, 81 words per
+    env-step, EPW 1 and 2) equal a2 > 0 in every slot of a window, and the
+    window gradient is the same bits whether fc_bwd.hip's job B reads them or
+    a2 itself (ARL_FC_BWD_MASK=f32, a fresh process)."""
+    import subprocess
+    import sys
+    from asyncrl_amd import A3C, A3CFF, A3CLSTM, GradientClipping, RMSpropAsync
+    rng = np.random.default_rng(91)
+    T, P = 5, 7
+    pairs, rewards, dones = make_pools(rng, P, N, "uniform", p_done=0.1)
+    Model = A3CLSTM if arch == "lstm" else A3CFF
+    m = Model(4, n_envs=N, t_max=T, seed=5, init_seed=6, frames="pairs")
+    o = RMSpropAsync(lr=7e-4, eps=0.1, alpha=0.99).setup(m)
+    o.add_hook(GradientClipping(40))
+    ag = A3C(m, o, T, 0.99)
+    ag.run_window(dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu), P, first=True, env_groups=1)
+    torch.cuda.synchronize()
+    a2 = m.net.buffer("a2", torch.float32, (T + 1, N, 2592)).cpu().numpy()
+    words = m.net.buffer("a2_mask", torch.int32, (T + 1, N, 81)).cpu().numpy().view(np.uint32)
+    bits = (words[..., :, None] >> np.arange(32, dtype=np.uint32)) & 1
+    assert np.array_equal(bits.reshape(T + 1, N, 2592).astype(bool), a2 > 0)
+    if arch == "ff" and N == 75:
+        here = os.path.dirname(os.path.abspath(__file__))
+        outs = []
+        for mask in ("", "f32"):
+            f = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"a2mask_{os.getpid()}_{mask or 'bits'}.npz")
+            env = dict(os.environ, ARL_FC_BWD_MASK=mask)
+            subprocess.run([sys.executable, os.path.join(here, "conv_epw_worker.py"), f, str(N)], env=env,
+                           check=True, timeout=240)
+            outs.append(dict(np.load(f)))
+            os.remove(f)
+        for k in outs[0]:
+            assert np.array_equal(outs[0][k], outs[1][k]), k
