@@ -65,6 +65,15 @@
 #ifndef ARL_S3_PREFETCH
 #define ARL_S3_PREFETCH 0
 #endif
+// (1) on bf16 splits (A/B knob, off): C = da2 [oc][p'] x im2col(a1)^T with positions p' = 10 oy + ox
+// (ox 9 a zero column, 96 padded) over a1 split phase planes, so 8 consecutive positions of one
+// (ic, ky, kx) column are 8 consecutive bf16 (5 dword reads + v_alignbyte); 72 instead of 84 MFMA
+// issues a wave at half the cycles each, but the per-sample convert pass (a1 -> phase planes), its
+// barrier and the da1 pad re-zeroing cost more: conv_bwd 66.7-67.4 -> 68.6-69.0 us at C2,
+// 119.7-120.7 -> 121.3-122.0 at C4 (parity green, profiles/r03/r3w).  Default: exact-f32 16x16x4
+#ifndef ARL_S1_SPLIT
+#define ARL_S1_SPLIT 0
+#endif
 #ifndef ARL_CB_STAMP
 #define ARL_CB_STAMP 0   // timing experiments only: s_memtime at every barrier into the slab (results wrong)
 #endif
@@ -82,7 +91,6 @@ constexpr int PG = (GI + NT - 1) / NT;     // 1 per thread
 // 16-byte slots.
 constexpr int A1R = 24;                    // a1 f32 row stride (20 used)
 constexpr int A1C = 20 * A1R;              // a1 f32 channel stride
-constexpr int D2F_LD = 48;                 // da2 f32 [p][oc] row stride
 constexpr int XR = 24;                     // phase row: X = 0..20 (+ pad), uint8
 constexpr int D1_ROW = 48;                 // da1 plane row (oy): 24 bf16, X 20..23 zero
 constexpr int D1_OC = 992;                 // da1 plane oc row: 62 16-byte slots
@@ -94,12 +102,28 @@ constexpr int L_XPH = L_D1 + 3 * D1P;      // [ic][y][b][XR]                    
 constexpr int L_D2 = L_XPH + 4 * 84 * 4 * XR;   // da2 split grid, 3 x D2P          24,576
 constexpr int L_MASK = L_D2 + 3 * D2P;     // a1 > 0, u16 of 16 channel bits per pixel 800
 constexpr int L_A1 = L_MASK + 800;         // a1 f32 [16][20][A1R]                  30,720
+#if ARL_S1_SPLIT
+// (1)'s operands: da2 split planes [3][oc][p'] (row 208 B = 13 16-byte slots: the 16 rows a b128
+// lane group reads land on distinct slots), written by commit_a; a1 split phase planes
+// [3][ic][y & 1][x & 1][Y][X] (10 x 10, 224 B each: reads run up to 11 elements past the 100)
+// written from the DMA'd a1 by the convert pass into the da1 region, dead until (2) writes da1
+constexpr int DA_ROW = 208;
+constexpr int DAP = 32 * DA_ROW;           // 6,656 per plane
+constexpr int L_DA = L_A1 + C1_OC * A1C * 4;    // 3 x DAP                               19,968
+constexpr int L_END = L_DA + 3 * DAP;      // 155,936
+constexpr int PH_B = 224;                  // bytes per phase plane (112 bf16)
+constexpr int PHP = 64 * PH_B;             // 14,336 per split plane (16 ic x 4 phases)
+constexpr int L_PH = L_D1;
+static_assert(3 * PHP <= 3 * D1P && L_DA % 16 == 0, "phase planes in the da1 region");
+#else
+constexpr int D2F_LD = 48;                 // da2 f32 [p][oc] row stride
 constexpr int L_D2F = L_A1 + C1_OC * A1C * 4;   // da2 f32 [81][D2F_LD]             15,552
 constexpr int L_END = L_D2F + 81 * D2F_LD * 4;  // 151,520
+static_assert(L_D2F % 16 == 0, "alignment");
+#endif
 constexpr int L_RED = 0;                   // end: f32 [16][128] (after the last sample)
 static_assert(L_END <= 160 * 1024, "LDS");
-static_assert(L_XPH % 16 == 0 && L_D2 % 16 == 0 && L_A1 % 16 == 0 && L_D2F % 16 == 0 && L_MASK % 8 == 0,
-              "alignment");
+static_assert(L_XPH % 16 == 0 && L_D2 % 16 == 0 && L_A1 % 16 == 0 && L_MASK % 8 == 0, "alignment");
 }  // namespace
 
 // da2 plane byte offset of (cell, oc group g = oc >> 3): the 16 cells a
@@ -205,8 +229,9 @@ __device__ inline void dma_a1(const ConvBwdArgs& a, int s, uint8_t* lds) {
   }
 }
 
-// da2 f32 [p][oc] and the da2 split grid (border cells written as 0)
-__device__ inline void commit_a(const PrefetchA& r, uint8_t* lds) {
+// da2 f32 [p][oc] (split (1): the [oc][p'] split planes and the thread's bias sums b2a) and the
+// da2 split grid (border cells written as 0)
+__device__ inline void commit_a(const PrefetchA& r, uint8_t* lds, float (&b2a)[8]) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int j = 0; j < PG; ++j) {
@@ -226,9 +251,24 @@ __device__ inline void commit_a(const PrefetchA& r, uint8_t* lds) {
       *reinterpret_cast<uint4*>(dd + D2P) = make_uint4(m[0], m[1], m[2], m[3]);
       *reinterpret_cast<uint4*>(dd + 2 * D2P) = make_uint4(l[0], l[1], l[2], l[3]);
       if (v) {
+#if ARL_S1_SPLIT
+        const int cy = cell / 11, pp = (cy - 1) * 10 + (cell - cy * 11 - 1);   // p' = 10 oy + ox
+        uint8_t* da = lds + L_DA + (8 * grp) * DA_ROW + 2 * pp;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int sh = 16 * (k & 1);
+          *reinterpret_cast<uint16_t*>(da + k * DA_ROW) = (uint16_t)(h[k >> 1] >> sh);
+          *reinterpret_cast<uint16_t*>(da + k * DA_ROW + DAP) = (uint16_t)(m[k >> 1] >> sh);
+          *reinterpret_cast<uint16_t*>(da + k * DA_ROW + 2 * DAP) = (uint16_t)(l[k >> 1] >> sh);
+          b2a[k] = __fadd_rn(b2a[k], d[k]);
+        }
+        (void)p;
+#else
         float* f = reinterpret_cast<float*>(lds + L_D2F) + p * D2F_LD + 8 * grp;
         reinterpret_cast<float4*>(f)[0] = make_float4(d[0], d[1], d[2], d[3]);
         reinterpret_cast<float4*>(f)[1] = make_float4(d[4], d[5], d[6], d[7]);
+        (void)b2a;
+#endif
       }
     }
   }
@@ -286,13 +326,19 @@ conv_bwd_kernel(ConvBwdArgs a) {
 #define CB_STAMP() do {} while (0)
 #endif
   const float* a1s = reinterpret_cast<const float*>(lds + L_A1);
+#if ARL_S1_SPLIT
+  // the da1 / phase-plane region and the da2 [oc][p'] planes zeroed once: the phase-plane reads run
+  // past a plane into finite bytes, and commit_a never writes the [oc][p'] pad positions
+  for (int i = tid; i < 3 * D1P / 16; i += NT) reinterpret_cast<uint4*>(lds + L_D1)[i] = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < 3 * DAP / 16; i += NT) reinterpret_cast<uint4*>(lds + L_DA)[i] = make_uint4(0, 0, 0, 0);
+#else
   const float* d2f = reinterpret_cast<const float*>(lds + L_D2F);
-
   // zero the da1 pad columns X 20..23 once: (2) writes only X < 20
   for (int i = tid; i < 3 * 16 * 20; i += NT) {
     const int pl = i / 320, r = i - pl * 320;
     *reinterpret_cast<uint2*>(lds + L_D1 + pl * D1P + (r / 20) * D1_OC + (r % 20) * D1_ROW + 40) = make_uint2(0, 0);
   }
+#endif
 
   // (2) W2 fragments of this wave's parity class: lane (ic = col, g), k-step
   // ks = (dy, dx), k = oc = 8 g + j -> W2[oc][ic][py + 2 dy][px + 2 dx]
@@ -320,6 +366,12 @@ conv_bwd_kernel(ConvBwdArgs a) {
     acc1[0][i] = acc1[1][i] = big3[i] = sml3[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   float b2sum = 0.f, b1s[4] = {0.f, 0.f, 0.f, 0.f};   // b1s[rr]: channel 4 g + rr
+  float b2a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // split (1): bias sums of this thread's da2 item
+#if ARL_S1_SPLIT
+  f32x4 sml1[2][2];   // (1)'s small terms
+#pragma unroll
+  for (int i = 0; i < 2; ++i) sml1[0][i] = sml1[1][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#endif
 
   // (3): wave w -> screen ic = w >> 1, ky = 4 kyq + (col >> 2) with kyq = w & 1,
   // kx = 4 a + (col & 3) (tile a = 0, 1); A row base of lane (phase row b = col & 3)
@@ -335,7 +387,7 @@ conv_bwd_kernel(ConvBwdArgs a) {
   for (int s = blockIdx.x; s < a.S; s += G) {
     lds_barrier();                 // B0: the previous sample is done with every region
     CB_STAMP();
-    commit_a(pa, lds);
+    commit_a(pa, lds, b2a);
     commit_x(px_, lds);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this sample's a1 DMA has landed
     lds_barrier();                 // B1
@@ -345,6 +397,66 @@ conv_bwd_kernel(ConvBwdArgs a) {
       prefetch_a(a, sn, pa);                // in flight during (1)-(3)
       prefetch_x(a, step0, sn, px_);
     }
+#if ARL_S1_SPLIT
+    // ---- a1 -> split phase planes ([3][ic][y & 1][x & 1][Y][X]) and a1 > 0 per pixel as 16
+    // channel bits; thread t < 400: pixel (y, x) = divmod(t, 20), every channel
+    if (tid < C1_P) {
+      const int y = tid / 20, x = tid - 20 * (tid / 20);
+      const float* ap = a1s + y * A1R + x;
+      uint8_t* ph = lds + L_PH + (2 * (y & 1) + (x & 1)) * PH_B + 2 * (10 * (y >> 1) + (x >> 1));
+      uint32_t m = 0;
+#pragma unroll
+      for (int ic = 0; ic < C1_OC; ++ic) {
+        const float v = ap[ic * A1C];
+        m |= (v > 0.f ? 1u : 0u) << ic;
+        uint32_t h, mm, l;
+        split3(v, h, mm, l);
+        *reinterpret_cast<uint16_t*>(ph + ic * 4 * PH_B) = (uint16_t)h;
+        *reinterpret_cast<uint16_t*>(ph + ic * 4 * PH_B + PHP) = (uint16_t)mm;
+        *reinterpret_cast<uint16_t*>(ph + ic * 4 * PH_B + 2 * PHP) = (uint16_t)l;
+      }
+      reinterpret_cast<uint16_t*>(lds + L_MASK)[tid] = (uint16_t)m;
+    }
+    lds_barrier();                 // B1b: the phase planes are complete
+    CB_STAMP();
+    // ---- (1) conv2 weight gradient, bf16 splits: wave w owns n-tiles (ic) 2w, 2w+1 x both m-tiles
+    // (oc); k = p' = 10 oy + ox over 3 k-steps of 32.  Lane (col, g): A = the [oc][p'] planes, row
+    // oc = 16 mt + col, 8 positions from 32 ks + 8 g (one b128); B = phase plane (ic, ky & 1, kx & 1)
+    // of (ky, kx) = divmod(col, 4) from element 32 ks + 8 g + d, d = 10 (ky >> 1) + (kx >> 1):
+    // 5 dwords and 4 v_alignbyte (d odd: a 2-byte shift).  Same C layout as the f32 path.
+    if (!(ARL_ABLATE & 8)) {
+      const int ky = col >> 2, kx = col & 3;
+      const int pb = L_PH + (2 * (ky & 1) + (kx & 1)) * PH_B + 2 * (8 * g + 10 * (ky >> 1) + (kx >> 1));
+      const int ab = L_DA + col * DA_ROW + 16 * g;
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        bf16x8 av[2][3], bv[2][3];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int h = 0; h < 3; ++h) av[mt][h] = lds_load<bf16x8>(lds, ab + mt * 16 * DA_ROW + h * DAP + 64 * ks);
+#pragma unroll
+        for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+          for (int h = 0; h < 3; ++h) {
+            const int a = pb + (2 * wave + jn) * 4 * PH_B + h * PHP + 64 * ks;
+            const int a4 = a & ~3, sh = a & 3;
+            uint32_t w[5];
+#pragma unroll
+            for (int q = 0; q < 5; ++q) w[q] = lds_load<uint32_t>(lds, a4 + 4 * q);
+            bv[jn][h] = frag_from_pairs(__builtin_amdgcn_alignbyte(w[1], w[0], sh),
+                                        __builtin_amdgcn_alignbyte(w[2], w[1], sh),
+                                        __builtin_amdgcn_alignbyte(w[3], w[2], sh),
+                                        __builtin_amdgcn_alignbyte(w[4], w[3], sh));
+          }
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int jn = 0; jn < 2; ++jn)
+            mfma_x6(av[mt][0], av[mt][1], av[mt][2], bv[jn][0], bv[jn][1], bv[jn][2], acc1[mt][jn], sml1[mt][jn]);
+      }
+    }
+#else
     // ---- (1) conv2 weight gradient + bias; wave w: n-tiles (ic) 2w, 2w+1 x both m-tiles
     {
       // 16 chunks of <= 6 positions, summed in order: the six reads in flight together
@@ -391,9 +503,17 @@ conv_bwd_kernel(ConvBwdArgs a) {
       for (int ic = 0; ic < C1_OC; ++ic) m |= (ap[ic * A1C] > 0.f ? 1u : 0u) << ic;
       reinterpret_cast<uint16_t*>(lds + L_MASK)[tid] = (uint16_t)m;
     }
+#endif
     lds_barrier();                 // B2: a1 and the mask are consumed
     CB_STAMP();
     dma_a1(a, min(s + G, a.S - 1), lds);   // next sample's a1, in flight during (2)-(3)
+#if ARL_S1_SPLIT
+    // the da1 pad columns X 20..23 back to 0 ((2) writes only X < 20; (3) reads them)
+    for (int i = tid; i < 3 * 16 * 20; i += NT) {
+      const int pl = i / 320, r = i - pl * 320;
+      *reinterpret_cast<uint2*>(lds + L_D1 + pl * D1P + (r / 20) * D1_OC + (r % 20) * D1_ROW + 40) = make_uint2(0, 0);
+    }
+#endif
     // ---- (2) da1 = convT(da2, W2) * (a1 > 0) -> da1 split planes.
     {
       // C^T form: rows = ic (A = the W2 fragments), columns = 16 grid cells
@@ -527,7 +647,11 @@ conv_bwd_kernel(ConvBwdArgs a) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
+#if ARL_S1_SPLIT
+        out[(16 * mt + g * 4 + r) * 256 + 16 * (2 * wave + j) + col] = __fadd_rn(acc1[mt][j][r], sml1[mt][j][r]);
+#else
         out[(16 * mt + g * 4 + r) * 256 + 16 * (2 * wave + j) + col] = acc1[mt][j][r];
+#endif
   // dW1^T: tile a, C row g*4 + r -> ky = 4 (w & 1) + (row >> 2), kx = 4 a + (row & 3)
 #pragma unroll
   for (int a_ = 0; a_ < 2; ++a_) {
@@ -552,6 +676,20 @@ conv_bwd_kernel(ConvBwdArgs a) {
     for (int k = 0; k < nst && k < 30; ++k) o[8 + k] = stamp[k];
   }
 #endif
+#if ARL_S1_SPLIT
+  // conv2 bias: item thread i (oc group i / 121) holds 8 channel sums; channel oc adds its group's
+  // 121 cells in order
+  if (tid < GI)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[tid * 8 + k] = b2a[k];
+  __syncthreads();
+  if (tid < 32) {
+    float t = 0.f;
+    for (int c = 0; c < 121; ++c) t = __fadd_rn(t, red[((tid >> 3) * 121 + c) * 8 + (tid & 7)]);
+    out[SLAB_B2 + tid] = t;
+  }
+  (void)b2sum;
+#else
   red[tid] = b2sum;                  // lane's oc = tid & 31
   __syncthreads();
   if (tid < 32) {
@@ -559,6 +697,8 @@ conv_bwd_kernel(ConvBwdArgs a) {
     for (int c = 0; c < NT / 32; ++c) t = __fadd_rn(t, red[c * 32 + tid]);
     out[SLAB_B2 + tid] = t;
   }
+  (void)b2a;
+#endif
   __syncthreads();
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) red[(4 * g + rr) * 128 + wave * 16 + col] = b1s[rr];
