@@ -38,6 +38,12 @@ struct PhiShared {
 
 // Computes output rows [dy0, dy0+BAND) of one env's screen into `out`
 // (row stride 84).  cur/prev: the env's two RGB frames (HWC, uint8).
+// non-temporal loads of the frame pairs (A/B knob, off: phi_ring 10.1 -> 13.0 us at C2, 19.1 -> 23.7 us
+// at 512 envs, C5 0.678 -> 0.884 ms; profiles/r03/r3x)
+#ifndef ARL_PHI_NT
+#define ARL_PHI_NT 0
+#endif
+
 __device__ inline void phi_band(const uint8_t* __restrict__ cur, const uint8_t* __restrict__ prev,
                                 uint8_t* __restrict__ out, int dy0, int mode, PhiShared& sh) {
   const int tid = threadIdx.x;
@@ -54,10 +60,22 @@ __device__ inline void phi_band(const uint8_t* __restrict__ cur, const uint8_t* 
     else resize_coeff(dy0 + ly, SRC_H, DST, o, b0, b1);
     int sy = o + tap;
     if (sy > SRC_H - 1) sy = SRC_H - 1;
+#if ARL_PHI_NT
+    // the frame pairs are read once a window: non-temporal loads keep them out of the caches
+    typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
+    const u32x4_* pc = reinterpret_cast<const u32x4_*>(cur + (size_t)sy * SRC_W * 3 + c * 48);
+    const u32x4_* pp = reinterpret_cast<const u32x4_*>(prev + (size_t)sy * SRC_W * 3 + c * 48);
+    u32x4_ v[6] = {__builtin_nontemporal_load(pc), __builtin_nontemporal_load(pc + 1), __builtin_nontemporal_load(pc + 2),
+                   __builtin_nontemporal_load(pp), __builtin_nontemporal_load(pp + 1), __builtin_nontemporal_load(pp + 2)};
+    c0 = make_uint4(v[0][0], v[0][1], v[0][2], v[0][3]); c1 = make_uint4(v[1][0], v[1][1], v[1][2], v[1][3]);
+    c2 = make_uint4(v[2][0], v[2][1], v[2][2], v[2][3]); p0 = make_uint4(v[3][0], v[3][1], v[3][2], v[3][3]);
+    p1 = make_uint4(v[4][0], v[4][1], v[4][2], v[4][3]); p2 = make_uint4(v[5][0], v[5][1], v[5][2], v[5][3]);
+#else
     const uint4* pc = reinterpret_cast<const uint4*>(cur + (size_t)sy * SRC_W * 3 + c * 48);
     const uint4* pp = reinterpret_cast<const uint4*>(prev + (size_t)sy * SRC_W * 3 + c * 48);
     c0 = pc[0]; c1 = pc[1]; c2 = pc[2];
     p0 = pp[0]; p1 = pp[1]; p2 = pp[2];
+#endif
   }
   if (tid < DST) {
     int o, a0, a1;

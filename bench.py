@@ -86,7 +86,7 @@ WORKLOADS = {"c2": ("ff", 256, 4), "c3": ("lstm", 1024, 6), "c4": ("ff", 512, 4)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c4",
                     help="BASELINE.json configs: c4 FF 512 envs per GPU (default: 4096 over 8 GPUs, the north-star "
