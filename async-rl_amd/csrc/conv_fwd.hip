@@ -117,7 +117,7 @@ struct ConvFwdArgs {
   const float* b1;
   const float* W2;      // (32, 16, 4, 4)
   const float* b2;
-  float* a1;            // (n, 16, 400)
+  float* a1;            // (n, 16, 400), or null: not stored (the window's bootstrap slot T)
   float* a2;            // (n, 32, 81)
   int layout;           // FrameLayout: FRAMES_RGB = (R, n, 3, 84, 84), planes [0, R, G, B] of slot ks % R;
                         // FRAMES_STACK = (R, n, 4, 84, 84), the 4 planes of slot ks % R
@@ -469,7 +469,8 @@ conv_fwd_kernel(ConvFwdArgs a) {
       for (int r = 0; r < 4; ++r)
         ov[r] = (ARL_ABLATE & 16) ? fmaxf(__fadd_rn(__fmul_rn(__fadd_rn(big[j][r], sml[j][r]), 1.f / 255.f), bias1), 0.f)
                                   : fmaxf(__fadd_rn(__fdiv_rn(__fadd_rn(big[j][r], sml[j][r]), 255.f), bias1), 0.f);
-      if (valid) *reinterpret_cast<float4*>(a1g + col * C1_P + p0) = make_float4(ov[0], ov[1], ov[2], ov[3]);
+      if (valid && a.a1 != nullptr)   // (null: the bootstrap slot, which no backward reads)
+        *reinterpret_cast<float4*>(a1g + col * C1_P + p0) = make_float4(ov[0], ov[1], ov[2], ov[3]);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         uint32_t h, m, l;

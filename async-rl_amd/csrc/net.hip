@@ -522,22 +522,26 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne, con
   const int n = net.N, A = net.A;
   const int part = mode & (ACT_CONV_ONLY | ACT_AFTER_CONV);
   mode &= 3;
+  // the bootstrap slot T feeds only the FC / heads forward: no backward reads its a1 or a2 mask
+  // (the ring-frame conv kernels skip those stores: 25.6 KB an env)
   float* a1 = net.at<float>(net.w_a1) + (int64_t)t * n * A1;
+  float* a1_bwd = t < net.T ? a1 : nullptr;
+  uint32_t* mask_bwd = t < net.T ? a2_mask(net, t) : nullptr;
   float* a2 = net.at<float>(net.w_a2) + (int64_t)t * n * A2;
   float* hfc = net.at<float>(net.w_hfc) + ((int64_t)t * n + e0) * HID;
   const float* P = net.p;
   if (obs != nullptr) {
     if (net.layout != FRAMES_RING || (part & ACT_AFTER_CONV) || obs->e0 != e0 || obs->ne != ne)
       return hipErrorInvalidValue;
-    ARL_TRY(launch_phi_conv_fwd(*obs, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W, P + net.o_c2b, a1, a2, s,
-                                a2_mask(net, t)));
+    ARL_TRY(launch_phi_conv_fwd(*obs, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W, P + net.o_c2b, a1_bwd, a2, s,
+                                mask_bwd));
   } else if (!(part & ACT_AFTER_CONV) && net.states) {
     if (e0 != 0 || ne != n) return hipErrorInvalidValue;   // one launch over all envs
     ARL_TRY(states_conv_fwd(net, t, a1, a2, s));
   } else if (!(part & ACT_AFTER_CONV))
     ARL_TRY(launch_conv_fwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
                             net.at<int64_t>(net.w_ctl), n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W,
-                            P + net.o_c2b, a1, a2, s, net.layout, e0, ne, a2_mask(net, t)));
+                            P + net.o_c2b, a1_bwd, a2, s, net.layout, e0, ne, mask_bwd));
   if (part & ACT_CONV_ONLY) return hipSuccess;
   const int64_t o = (int64_t)t * n + e0;
   float* fc_slab = net.at<float>(net.w_slab) + (int64_t)FC_SPLIT * e0 * HID;
