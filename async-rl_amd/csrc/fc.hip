@@ -231,8 +231,10 @@ __host__ __device__ constexpr int g_wave_pieces(int c, int w) { return (g_pieces
 }  // namespace
 
 __global__ void __launch_bounds__(GT)
-fc_fwd_big_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, float* __restrict__ slab) {
+fc_fwd_big_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, float* __restrict__ slab,
+                  int* __restrict__ tickets, const float* __restrict__ bias, float* __restrict__ hfc) {
   __shared__ __attribute__((aligned(16))) float S[2 * GBUF4 * 4];   // 118,784 B
+  __shared__ int is_last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int split = blockIdx.x % FSPLIT, tile = blockIdx.x / FSPLIT;
   constexpr int NTN = HID / FBN;
@@ -277,6 +279,37 @@ fc_fwd_big_kernel(const float* __restrict__ a2, int n, const float* __restrict__
       __hip_atomic_store(part + (int64_t)m * HID + n0 + ns * 16 + col, c0[r], __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
   }
+  if (tickets == nullptr) return;
+  // the last of the tile's FSPLIT workgroups sums the partials in split order, adds the bias, applies
+  // relu and writes hfc (as fc_fwd_kernel's tail: sc1 stores drained before the relaxed agent-scope
+  // ticket, sc1 loads after it); one float4 of the 64 x 64 tile per thread
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int tid = threadIdx.x;
+  if (tid == 0) is_last = __hip_atomic_fetch_add(&tickets[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == FSPLIT - 1;
+  __syncthreads();
+  if (!is_last) return;
+  const int mrow = m0 + (tid >> 4), ccol = n0 + 4 * (tid & 15);
+  f32x4 p[FSPLIT];
+#pragma unroll
+  for (int z = 0; z < FSPLIT; ++z) {
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(slab + (int64_t)z * n * HID, 0, n * HID * 4, 0x00020000);
+    p[z] = __builtin_bit_cast(f32x4,
+                              __builtin_amdgcn_raw_buffer_load_b128(rsrc, (min(mrow, n - 1) * HID + ccol) * 4, 0, 16));
+  }
+  if (mrow < n) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int z = 0; z < FSPLIT; ++z)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] = __fadd_rn(acc[e], p[z][e]);
+    const float4 b = *reinterpret_cast<const float4*>(bias + ccol);
+    float4 o;
+    o.x = fmaxf(__fadd_rn(acc[0], b.x), 0.f); o.y = fmaxf(__fadd_rn(acc[1], b.y), 0.f);
+    o.z = fmaxf(__fadd_rn(acc[2], b.z), 0.f); o.w = fmaxf(__fadd_rn(acc[3], b.w), 0.f);
+    *reinterpret_cast<float4*>(hfc + (int64_t)mrow * HID + ccol) = o;
+  }
+  if (tid == 0) __hip_atomic_store(&tickets[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 int fc_fwd_tiles(int n) { return ((n + FBM - 1) / FBM) * (HID / FBN); }
@@ -288,10 +321,10 @@ hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b,
   // C3 1.215 -> 1.162 ms; at 256-env launches, 128 workgroups of them lose: profiles/r03/r3l);
   // ARL_FC_BIG=0 / 1 forces one form (A/B timing)
   static const char* big = getenv("ARL_FC_BIG");
-  const bool use_big = tickets == nullptr && (big && (big[0] == '0' || big[0] == '1') ? big[0] == '1' : n >= 512);
-  if (use_big) {
+  const bool use_big = (big && (big[0] == '0' || big[0] == '1')) ? big[0] == '1' : n >= 512;
+  if (use_big) {   // (its 64-row ticket tiles use the first half of the 32-row tiles' tickets)
     hipLaunchKernelGGL(fc_fwd_big_kernel, dim3((unsigned)(((n + GBM - 1) / GBM) * (HID / FBN) * FSPLIT)), dim3(GT), 0,
-                       s, a2, n, W, slab);
+                       s, a2, n, W, slab, tickets, b, hfc);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(fc_fwd_kernel, dim3((unsigned)(fc_fwd_tiles(n) * FSPLIT)), dim3(FT), 0, s, a2, n, W, b, slab,

@@ -191,12 +191,19 @@ static const bool LSTM_GEMM_GENERIC = [] {
   const char* e = getenv("ARL_LSTM_GEMM");
   return e != nullptr && e[0] == 'g';
 }();
-// ARL_LSTM_XRED=0: the FC forward's ticket reduce writes hfc and the gate kernel stages it
-// (the A arm for the reduce in the gate kernel's staging)
-static const bool LSTM_XRED = [] {
+// Where the LSTM step's FC split-K partials are reduced: in the gate kernel's staging (XRED) for
+// launches under 512 envs, by the FC's last-arriver ticket for 512 and more (fc_fwd_big_kernel's
+// tail; the gate kernel then stages hfc: every one of its 16 column-tile workgroups of a row block
+// otherwise re-reads the block's 8 partial slabs -- C3 1.185 -> 1.160 ms, profiles/r03/r3aa).
+// ARL_LSTM_XRED=1 / 0 forces one form (A/B timing).
+static const int LSTM_XRED_ENV = [] {
   const char* e = getenv("ARL_LSTM_XRED");
-  return e == nullptr || e[0] != '0';
+  return e == nullptr ? -1 : (e[0] != '0' ? 1 : 0);
 }();
+static bool lstm_xred(int launch_envs) {
+  if (LSTM_GEMM_GENERIC) return false;
+  return LSTM_XRED_ENV >= 0 ? LSTM_XRED_ENV == 1 : launch_envs < 512;
+}
 // ARL_LSTM_WGRAD=gemm: the gate weight gradients + dfc as the round-2 generic dual GEMM into the LSTM
 // slab (+ the LEARN_GATES_REDUCE reduce) instead of fc_bwd.hip's ShapeLSTM kernel -- A/B timing only
 static const bool LSTM_WGRAD_GEMM = [] {
@@ -557,8 +564,8 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne, con
                             s);
   }
   // LSTM: the FC's split-K partials only, their reduce + bias + relu in the gate kernel's
-  // staging (lstm.hip XRED); ARL_LSTM_XRED=0 / the generic gate GEMM: the FC's ticket reduce
-  const bool xred = !LSTM_GEMM_GENERIC && LSTM_XRED;
+  // staging (lstm.hip XRED) or the FC's ticket reduce (lstm_xred)
+  const bool xred = lstm_xred(ne);
   ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab,
                         xred ? nullptr : net.at<int>(net.w_tick) + fc_fwd_tiles(e0), xred ? nullptr : hfc, s));
   const float* hpol = hfc;
@@ -860,7 +867,7 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
                              P + net.o_c2b, net.at<float>(net.w_a1) + (int64_t)t * n * A1, a2 + (int64_t)t * n * A2,
                              s, net.layout, 0, -1, a2_mask(net, t));
     case STAGE_FC_FWD:   // as in net_act: FF (and the LSTM's XRED gate kernel) reduce the partials downstream
-      if (net.arch != ARCH_LSTM || (!LSTM_GEMM_GENERIC && LSTM_XRED))
+      if (net.arch != ARCH_LSTM || lstm_xred(n))
         return launch_fc_fwd(a2 + (int64_t)t * n * A2, n, P + net.o_fcW, P + net.o_fcb, slab, nullptr, nullptr, s);
       return fc_forward(net, n, a2 + (int64_t)t * n * A2, hfc + (int64_t)t * n * HID, s);
     case STAGE_POLICY: {
@@ -906,7 +913,7 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
     case STAGE_LSTM_GATES: {   // as net_act's LSTM step over all envs
       if (net.arch != ARCH_LSTM) return hipErrorInvalidValue;
       const int64_t r0 = (int64_t)t * n;
-      const bool xred = !LSTM_GEMM_GENERIC && LSTM_XRED;
+      const bool xred = lstm_xred(n);
       return launch_lstm_gates(xred ? nullptr : hfc + r0 * HID, net.at<float>(net.w_hbuf) + r0 * HID,
                                net.at<uint8_t>(net.w_reset) + r0, P + net.o_luW, P + net.o_llW, P + net.o_lub,
                                net.at<float>(net.w_gates) + r0 * GATES, net.at<float>(net.w_cbuf) + r0 * HID,

@@ -64,8 +64,11 @@ FC_SPLIT = 8                                # fc.hip split-K (partial slabs read
 LSTM_GATES_FLOP_PER_ENV = 2 * 512 * 1024
 LSTM_BPTT_FLOP_PER_ENV = 2 * 1024 * 256
 LSTM_WGRAD_FLOP_PER_SAMPLE = 2 * 513 * 1024 + 2 * 1024 * 256
-# the gate kernel forms x from the FC's split-K partials unless ARL_LSTM_XRED=0 (net.hip)
-LSTM_XRED = os.environ.get("ARL_LSTM_XRED", "1")[:1] != "0"
+# the LSTM gate kernel forms x from the FC's split-K partials (XRED) for launches under 512 envs, the
+# FC's ticket reduce does from 512 up (net.hip lstm_xred); ARL_LSTM_XRED=1 / 0 forces one
+def lstm_xred(n_launch):
+    v = os.environ.get("ARL_LSTM_XRED", "")[:1]
+    return v != "0" if v in ("0", "1") else n_launch < 512
 # the gate weight gradients run on fc_bwd.hip's ShapeLSTM kernel unless ARL_LSTM_WGRAD=gemm (net.hip)
 LSTM_WGRAD_GEMM = os.environ.get("ARL_LSTM_WGRAD", "")[:1] == "g"
 # ViZDoom models (train_a3c_doom.py:28,46): conv1 K = 3 * 64 (the kernels' zero input plane is not counted)
@@ -583,8 +586,8 @@ def main(a):
              lambda i: net.run_stage("conv_fwd", i % T, stream=stream), 1 if fused else T + 1, "mfma",
              N * conv_fwd_flop),
             ("fc_fwd", "gemm_kernel + reduce_grad_kernel" if nat else
-             (("fc_fwd_big_kernel" if fc_big(N) else "fc_fwd_kernel") + " (split-K partials)")
-             if (not lstm or LSTM_XRED) else "fc_fwd_kernel",
+             ("fc_fwd_big_kernel" if fc_big(N) else "fc_fwd_kernel") +
+             (" (split-K partials)" if (not lstm or lstm_xred(N)) else " (+ ticket reduce)"),
              lambda i: net.run_stage("fc_fwd", i % T, stream=stream), T + 1, "mfma", N * fc_fwd_flop),
             # FF NIPS / Doom FF: the FC split-K reduce + bias + relu runs in the policy launch
             # (policy_fc_kernel): it also reads the 8 partial slabs and writes h
@@ -597,7 +600,7 @@ def main(a):
              lambda i: net.run_stage("conv_bwd", 0, stream=stream), 1, "mfma", S * conv_bwd_flop),
             # LSTM: the gate kernel (LSTM_XRED: it also forms x from the FC's partials), the
             # truncated-BPTT steps, the gate weight gradients + dfc (a3c_ale.py:50-51,62)
-            ("lstm_gates", "lstm_gates_kernel" + ("<true> (FC reduce + gates + cell)" if LSTM_XRED else "<false>"),
+            ("lstm_gates", "lstm_gates_kernel" + ("<true> (FC reduce + gates + cell)" if lstm_xred(N) else "<false>"),
              lambda i: net.run_stage("lstm_gates", i % T, stream=stream), T + 1, "mfma",
              N * LSTM_GATES_FLOP_PER_ENV) if lstm and not doom else None,
             ("lstm_bptt", "lstm_bptt_kernel (dh GEMM + cell backward)",

@@ -20,7 +20,7 @@ from asyncrl_amd import A3C, A3CLSTM, GradientClipping, RMSpropAsync  # noqa: E4
 def main(out, one=False):
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(123)
-    N, T, P = 72, 5, 7
+    N, T, P = int(os.environ.get("LSTM_WORKER_N", "72")), 5, 7
     pairs, rewards, dones = make_pools(rng, P, N, "uniform", p_done=0.15)
     t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)  # noqa: E731
     dp, dr, dd = t(pairs), t(rewards), t(dones)

@@ -877,3 +877,24 @@ def test_a2_mask_bits_match_a2(gpu, arch, N):
             os.remove(f)
         for k in outs[0]:
             assert np.array_equal(outs[0][k], outs[1][k]), k
+
+
+def test_lstm_fc_ticket_big_tiles_identical(gpu, tmp_path):
+    """512 LSTM envs (fc.hip's 64-row tiles): the FC forward's last-arriver
+    ticket reduce (fc_fwd_big_kernel's tail, the default from 512-env
+    launches) and the reduce in the gate kernel's staging sum the same partials in the same
+    order, so hidden / cell states, gates, actions, gradients and parameters
+    match bit for bit."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    outs = []
+    for extra in ({"ARL_LSTM_XRED": "1"}, {"ARL_LSTM_XRED": "0"}):
+        f = str(tmp_path / f"lstm512_{len(outs)}.npz")
+        env = dict(os.environ, LSTM_WORKER_N="512", **extra)
+        subprocess.run([sys.executable, os.path.join(here, "lstm_split_worker.py"), f], env=env, check=True,
+                       timeout=240)
+        outs.append(np.load(f))
+    assert int((outs[0]["hbuf"] != 0).sum()) > 0
+    for k in outs[0].files:
+        assert np.array_equal(outs[0][k], outs[1][k]), k
