@@ -238,8 +238,12 @@ inline PolicyArgs make_policy_args(const float* Wpi, const float* bpi, const flo
 
 constexpr int FC_SPLIT = 8;   // fc forward split-K (one slice per XCD)
 int fc_fwd_tiles(int n);      // tickets needed for n envs
+bool fc_fwd_big(int n);       // launches over n envs run fc_fwd_big_kernel's 64-row tiles
+bool fc_fwd_heads(int n);     // ... and an FF step's heads run in its ticket tail
+// heads != null (FF, fc_fwd_heads(n)): the split-K reduce + relu -> hfc and the policy / value heads
+// with the draw in the same launch (policy_fc_kernel's work); tickets and hfc required
 hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b, float* slab, int* tickets,
-                         float* hfc, hipStream_t s);
+                         float* hfc, hipStream_t s, const PolicyArgs* heads = nullptr);
 // FC backward (fc_bwd.hip): dW / db straight into the gradient, da2 = (dfc W) * (a2 > 0)
 // weight gradients of the policy / value heads (a3c.py:126-130 through
 // policy.py / v_function.py Linear layers): rows a < A from dlogits, row A

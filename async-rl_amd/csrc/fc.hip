@@ -25,9 +25,13 @@
 #include <cstdlib>
 
 #include "arl_internal.hpp"
+#include "policy_rows.hpp"
 
 #ifndef ARL_ABLATE
 #define ARL_ABLATE 0   // timing experiments only (bits: 128 staging, 256 ticket/reduce, 512 MFMA)
+#endif
+#ifndef ARL_FC_HEADS_DEFAULT
+#define ARL_FC_HEADS_DEFAULT 0
 #endif
 
 namespace arl {
@@ -232,7 +236,8 @@ __host__ __device__ constexpr int g_wave_pieces(int c, int w) { return (g_pieces
 
 __global__ void __launch_bounds__(GT)
 fc_fwd_big_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, float* __restrict__ slab,
-                  int* __restrict__ tickets, const float* __restrict__ bias, float* __restrict__ hfc) {
+                  int* __restrict__ tickets, const float* __restrict__ bias, float* __restrict__ hfc,
+                  int* __restrict__ row_tickets, PolicyArgs pa) {
   __shared__ __attribute__((aligned(16))) float S[2 * GBUF4 * 4];   // 118,784 B
   __shared__ int is_last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -297,34 +302,106 @@ fc_fwd_big_kernel(const float* __restrict__ a2, int n, const float* __restrict__
     p[z] = __builtin_bit_cast(f32x4,
                               __builtin_amdgcn_raw_buffer_load_b128(rsrc, (min(mrow, n - 1) * HID + ccol) * 4, 0, 16));
   }
-  if (mrow < n) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int z = 0; z < FSPLIT; ++z)
+  for (int z = 0; z < FSPLIT; ++z)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc[e] = __fadd_rn(acc[e], p[z][e]);
-    const float4 b = *reinterpret_cast<const float4*>(bias + ccol);
-    float4 o;
-    o.x = fmaxf(__fadd_rn(acc[0], b.x), 0.f); o.y = fmaxf(__fadd_rn(acc[1], b.y), 0.f);
-    o.z = fmaxf(__fadd_rn(acc[2], b.z), 0.f); o.w = fmaxf(__fadd_rn(acc[3], b.w), 0.f);
-    *reinterpret_cast<float4*>(hfc + (int64_t)mrow * HID + ccol) = o;
-  }
+    for (int e = 0; e < 4; ++e) acc[e] = __fadd_rn(acc[e], p[z][e]);
+  const float4 b = *reinterpret_cast<const float4*>(bias + ccol);
+  f32x4 o;
+  o[0] = fmaxf(__fadd_rn(acc[0], b.x), 0.f); o[1] = fmaxf(__fadd_rn(acc[1], b.y), 0.f);
+  o[2] = fmaxf(__fadd_rn(acc[2], b.z), 0.f); o[3] = fmaxf(__fadd_rn(acc[3], b.w), 0.f);
+  if (mrow < n) *reinterpret_cast<f32x4*>(hfc + (int64_t)mrow * HID + ccol) = o;
   if (tid == 0) __hip_atomic_store(&tickets[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (row_tickets == nullptr) return;
+  // FF heads (row_tickets != null): this tile's 64 columns are the heads' K quarter kq = n0 / 64 --
+  // policy_rows16's wave kq -- so waves 0-3 form the quarter's partial logits / value of 16 rows each
+  // (heads_quarter: the same MFMA sequence) from the tile in LDS and store them over the tile's
+  // consumed split-0 partials; the last of the row block's 4 column tiles (second ticket) sums the
+  // quarters in wave order + bias and runs the softmax / draw of its 64 rows (heads_row_out).
+  static_assert(FBN * 4 == HID && GBM == 64, "one heads K quarter per column tile, 4 row groups of 16");
+  constexpr int HL = FBN + 4;   // LDS row stride (floats): the 16 rows a lane group reads start on distinct banks
+  constexpr int KW = HID / 4, NS = KW / 16, NTM = HeadsPrefetch<HID>::NTM;
+  const int kq = n0 / FBN, A = pa.A;
+  HeadsPrefetch<HID> pf;
+  if (wave < 4) pf = heads_prefetch<HID>(pa, kq);
+  float* hl = S;
+  *reinterpret_cast<f32x4*>(hl + (tid >> 4) * HL + 4 * (tid & 15)) = o;
+  __syncthreads();
+  if (wave < 4) {
+    f32x4 hv[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) hv[s] = *reinterpret_cast<const f32x4*>(hl + (16 * wave + col) * HL + 16 * s + 4 * q);
+#pragma unroll
+    for (int nt = 0; nt < NTM; ++nt) {
+      if (16 * nt > A) break;   // wave-uniform
+      const int j = 16 * nt + col;
+      const f32x4 c = heads_quarter(hv, pf.wv, nt, j <= A);
+      if (j <= A) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + 16 * wave + 4 * q + r;
+          if (m < n)
+            __hip_atomic_store(slab + (int64_t)m * HID + n0 + j, c[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int rb = m0 / GBM;
+  if (tid == 0)
+    is_last = __hip_atomic_fetch_add(&row_tickets[rb], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == HID / FBN - 1;
+  __syncthreads();
+  if (!is_last) return;
+  constexpr int ZL = MAXA + 2;
+  float* zs = S + GBM * HL;    // [64][ZL]
+  float* ez = zs + GBM * ZL;   // [64][ZL]
+  for (int i = tid; i < GBM * (A + 1); i += GT) {
+    const int r = i / (A + 1), j = i - r * (A + 1);
+    const float* src = slab + (int64_t)min(m0 + r, n - 1) * HID + j;
+    float pq[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) pq[w] = __hip_atomic_load(src + KW * w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float z = __fadd_rn(__fadd_rn(pq[0], pq[1]), __fadd_rn(pq[2], pq[3]));
+    zs[r * ZL + j] = __fadd_rn(z, j < A ? pa.bpi[j] : pa.bv[0]);
+  }
+  __syncthreads();
+  if (tid < GBM && m0 + tid < n) {
+    const int64_t step = pa.mode == 1 ? pa.ctl[CTL_STEP] + pa.step_off : 0;
+    heads_row_out(zs + tid * ZL, ez + tid * ZL, m0 + tid, pa, step);
+  }
+  if (tid == 0) __hip_atomic_store(&row_tickets[rb], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 int fc_fwd_tiles(int n) { return ((n + FBM - 1) / FBM) * (HID / FBN); }
 
-hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b, float* slab, int* tickets,
-                         float* hfc, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
+bool fc_fwd_big(int n) {
   // partials-only launches over >= 512 envs on the 64-row tiles (C4 0.503 -> 0.497 ms at one env group,
   // C3 1.215 -> 1.162 ms; at 256-env launches, 128 workgroups of them lose: profiles/r03/r3l);
   // ARL_FC_BIG=0 / 1 forces one form (A/B timing)
   static const char* big = getenv("ARL_FC_BIG");
-  const bool use_big = (big && (big[0] == '0' || big[0] == '1')) ? big[0] == '1' : n >= 512;
-  if (use_big) {   // (its 64-row ticket tiles use the first half of the 32-row tiles' tickets)
-    hipLaunchKernelGGL(fc_fwd_big_kernel, dim3((unsigned)(((n + GBM - 1) / GBM) * (HID / FBN) * FSPLIT)), dim3(GT), 0,
-                       s, a2, n, W, slab, tickets, b, hfc);
+  return (big && (big[0] == '0' || big[0] == '1')) ? big[0] == '1' : n >= 512;
+}
+
+bool fc_fwd_heads(int n) {
+  // FF heads in fc_fwd_big_kernel's ticket tail instead of policy_fc_kernel (ARL_FC_HEADS=0 / 1)
+  static const char* e = getenv("ARL_FC_HEADS");
+  const bool on = (e && (e[0] == '0' || e[0] == '1')) ? e[0] == '1' : ARL_FC_HEADS_DEFAULT;
+  return on && n >= 128 && fc_fwd_big(n);
+}
+
+hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b, float* slab, int* tickets,
+                         float* hfc, hipStream_t s, const PolicyArgs* heads) {
+  if (n <= 0) return hipSuccess;
+  if (heads != nullptr && (tickets == nullptr || hfc == nullptr || !fc_fwd_heads(n) || heads->A + 1 > FBN))
+    return hipErrorInvalidValue;
+  if (fc_fwd_big(n)) {
+    // its 64-row tiles use the first half of the 32-row tiles' tickets, the heads' row-block
+    // tickets the next ceil(n / 64) (within the ceil(n / 32) * 4 from n >= 128)
+    const int tiles = ((n + GBM - 1) / GBM) * (HID / FBN);
+    hipLaunchKernelGGL(fc_fwd_big_kernel, dim3((unsigned)(tiles * FSPLIT)), dim3(GT), 0, s, a2, n, W, slab, tickets, b,
+                       hfc, heads != nullptr ? tickets + tiles : nullptr, heads != nullptr ? *heads : PolicyArgs{});
     return hipGetLastError();
   }
   hipLaunchKernelGGL(fc_fwd_kernel, dim3((unsigned)(fc_fwd_tiles(n) * FSPLIT)), dim3(FT), 0, s, a2, n, W, b, slab,

@@ -553,15 +553,17 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne, con
   const int64_t o = (int64_t)t * n + e0;
   float* fc_slab = net.at<float>(net.w_slab) + (int64_t)FC_SPLIT * e0 * HID;
   if (net.arch != ARCH_LSTM) {   // FF: split-K partials, reduce + relu + heads in one policy_fc launch
+    const PolicyArgs pa = make_policy_args(P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
+                                           net.at<int64_t>(net.w_ctl), t, net.env_offset + e0, t < net.T ? mode : 0,
+                                           net.at<float>(net.w_logits) + o * A, net.at<float>(net.w_probs) + o * A,
+                                           net.at<float>(net.w_logp) + o * A, net.at<float>(net.w_v) + o,
+                                           net.at<float>(net.w_ent) + o, net.at<int32_t>(net.w_act) + o,
+                                           net.at<float>(net.w_logpa) + o);
+    if (fc_fwd_heads(ne))   // ... or all of it in the FC launch's ticket tails
+      return launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab,
+                           net.at<int>(net.w_tick) + fc_fwd_tiles(e0), hfc, s, &pa);
     ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab, nullptr, nullptr, s));
-    return launch_policy_fc(fc_slab, ne, P + net.o_fcb, hfc,
-                            make_policy_args(P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
-                                             net.at<int64_t>(net.w_ctl), t, net.env_offset + e0, t < net.T ? mode : 0,
-                                             net.at<float>(net.w_logits) + o * A, net.at<float>(net.w_probs) + o * A,
-                                             net.at<float>(net.w_logp) + o * A, net.at<float>(net.w_v) + o,
-                                             net.at<float>(net.w_ent) + o, net.at<int32_t>(net.w_act) + o,
-                                             net.at<float>(net.w_logpa) + o),
-                            s);
+    return launch_policy_fc(fc_slab, ne, P + net.o_fcb, hfc, pa, s);
   }
   // LSTM: the FC's split-K partials only, their reduce + bias + relu in the gate kernel's
   // staging (lstm.hip XRED) or the FC's ticket reduce (lstm_xred)

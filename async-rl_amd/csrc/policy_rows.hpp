@@ -44,11 +44,12 @@ struct HeadsPrefetch {
   float bias;
   int64_t step;
 };
+// kq: the K quarter whose fragments this wave loads (-1: the wave's own, wave & 3 of a 4-wave group)
 template <int HW>
-__device__ inline HeadsPrefetch<HW> heads_prefetch(const PolicyArgs& pa) {
+__device__ inline HeadsPrefetch<HW> heads_prefetch(const PolicyArgs& pa, int kq = -1) {
   using P = HeadsPrefetch<HW>;
   const int A = pa.A;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  const int tid = threadIdx.x, w = kq >= 0 ? kq : tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
   P pf;
 #pragma unroll
   for (int nt = 0; nt < P::NTM; ++nt) {
@@ -62,6 +63,72 @@ __device__ inline HeadsPrefetch<HW> heads_prefetch(const PolicyArgs& pa) {
   pf.bias = bj < A ? pa.bpi[bj] : pa.bv[0];
   pf.step = pa.mode == 1 ? pa.ctl[CTL_STEP] + pa.step_off : 0;
   return pf;
+}
+
+// One wave's K-quarter partial of head tile nt (columns 16 nt .. 16 nt + 15) for 16 rows: lane (g, col)
+// returns rows 4 g + r, column 16 nt + col.  hv / wv: the quarter's h and head-weight fragments (k
+// permuted identically on both sides); valid == false: a column past A (zero weights).
+template <int NS, int NTM>
+__device__ inline f32x4 heads_quarter(const f32x4 (&hv)[NS], const f32x4 (&wv)[NTM][NS], int nt, bool valid) {
+  f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const f32x4 wf = valid ? wv[nt][s] : f32x4{0.f, 0.f, 0.f, 0.f};
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][0], wf[0], c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][1], wf[1], c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][2], wf[2], c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][3], wf[3], c1, 0, 0, 0);
+  }
+  f32x4 c;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) c[r] = __fadd_rn(c0[r], c1[r]);
+  return c;
+}
+
+// One env row's softmax / log-softmax / entropy / draw from its A + 1 head
+// outputs z (z[A] = value); ez: A floats of scratch (exp(z - max) per action).
+__device__ inline void heads_row_out(const float* z, float* ez, int64_t row, const PolicyArgs& pa, int64_t step) {
+  const int A = pa.A;
+  // serial max / sum over k (policy_output.py:41-47; Chainer softmax, log_softmax)
+  float m = z[0];
+  for (int k = 1; k < A; ++k) m = fmaxf(m, z[k]);
+  float se = 0.f;
+  for (int k = 0; k < A; ++k) {
+    ez[k] = expf(__fsub_rn(z[k], m));
+    se = __fadd_rn(se, ez[k]);
+  }
+  const float lse = __fadd_rn(m, logf(se));
+  const int mode = pa.mode;
+  float u = 2.f;   // > any cdf: no draw
+  if (mode == 1) {
+    const uint4 r = philox4x32_10(make_uint4((uint32_t)(pa.env_offset + row), (uint32_t)step,
+                                             (uint32_t)((uint64_t)step >> 32), pa.stream), pa.seed_lo, pa.seed_hi);
+    u = (float)(r.x >> 8) * 5.9604644775390625e-08f;
+  }
+  float H = 0.f, cdf = 0.f, best = -1.f, la = 0.f;
+  int a = A - 1;
+  bool found = false;
+  for (int k = 0; k < A; ++k) {
+    const float p = __fdiv_rn(ez[k], se);                       // softmax: exp(z-m) / sum
+    const float lz = __fsub_rn(z[k], lse);                      // log_softmax: z - (m + log sum)
+    H = __fadd_rn(H, __fmul_rn(p, lz));                         // entropy: -sum p log p
+    pa.logits[row * A + k] = z[k];
+    pa.probs[row * A + k] = p;
+    pa.logp[row * A + k] = lz;
+    if (mode == 1) {
+      cdf = __fadd_rn(cdf, p);
+      if (!found && u < cdf) { a = k; la = lz; found = true; }
+    } else if (mode == 2 && p > best) {
+      best = p; a = k; la = lz;
+    }
+  }
+  if (mode == 1 && !found) la = __fsub_rn(z[A - 1], lse);
+  pa.v[row] = z[A];
+  pa.ent[row] = -H;
+  if (mode) {
+    pa.act[row] = a;
+    pa.logp_a[row] = la;
+  }
 }
 
 template <int HW, bool COH, bool LOCAL = false, int ROWS = 16>
@@ -92,18 +159,10 @@ __device__ inline void policy_rows16(const float* __restrict__ h, int64_t row0, 
   for (int nt = 0; nt < HeadsPrefetch<HW>::NTM; ++nt) {
     if (16 * nt > A) break;   // wave-uniform
     const int j = 16 * nt + col;
-    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const f32x4 wf = j <= A ? wv[nt][s] : f32x4{0.f, 0.f, 0.f, 0.f};
-      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][0], wf[0], c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][1], wf[1], c1, 0, 0, 0);
-      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][2], wf[2], c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][3], wf[3], c1, 0, 0, 0);
-    }
+    const f32x4 c = heads_quarter(hv, wv, nt, j <= A);
     if (j <= A) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) part[w][4 * g + r][j] = __fadd_rn(c0[r], c1[r]);   // C row 4g + r = env
+      for (int r = 0; r < 4; ++r) part[w][4 * g + r][j] = c[r];   // C row 4g + r = env
     }
   }
   __syncthreads();
@@ -114,50 +173,7 @@ __device__ inline void policy_rows16(const float* __restrict__ h, int64_t row0, 
   }
   __syncthreads();
   const int64_t row = row0 + tid;
-  if (tid < ROWS && row < n) {
-    float* z = zs[tid];
-    float* ez = part[0][tid];   // reused: exp(z - max) per action
-    // serial max / sum over k (policy_output.py:41-47; Chainer softmax, log_softmax)
-    float m = z[0];
-    for (int k = 1; k < A; ++k) m = fmaxf(m, z[k]);
-    float se = 0.f;
-    for (int k = 0; k < A; ++k) {
-      ez[k] = expf(__fsub_rn(z[k], m));
-      se = __fadd_rn(se, ez[k]);
-    }
-    const float lse = __fadd_rn(m, logf(se));
-    const int mode = pa.mode;
-    float u = 2.f;   // > any cdf: no draw
-    if (mode == 1) {
-      const uint4 r = philox4x32_10(make_uint4((uint32_t)(pa.env_offset + row), (uint32_t)step,
-                                               (uint32_t)((uint64_t)step >> 32), pa.stream), pa.seed_lo, pa.seed_hi);
-      u = (float)(r.x >> 8) * 5.9604644775390625e-08f;
-    }
-    float H = 0.f, cdf = 0.f, best = -1.f, la = 0.f;
-    int a = A - 1;
-    bool found = false;
-    for (int k = 0; k < A; ++k) {
-      const float p = __fdiv_rn(ez[k], se);                       // softmax: exp(z-m) / sum
-      const float lz = __fsub_rn(z[k], lse);                      // log_softmax: z - (m + log sum)
-      H = __fadd_rn(H, __fmul_rn(p, lz));                         // entropy: -sum p log p
-      pa.logits[row * A + k] = z[k];
-      pa.probs[row * A + k] = p;
-      pa.logp[row * A + k] = lz;
-      if (mode == 1) {
-        cdf = __fadd_rn(cdf, p);
-        if (!found && u < cdf) { a = k; la = lz; found = true; }
-      } else if (mode == 2 && p > best) {
-        best = p; a = k; la = lz;
-      }
-    }
-    if (mode == 1 && !found) la = __fsub_rn(z[A - 1], lse);
-    pa.v[row] = z[A];
-    pa.ent[row] = -H;
-    if (mode) {
-      pa.act[row] = a;
-      pa.logp_a[row] = la;
-    }
-  }
+  if (tid < ROWS && row < n) heads_row_out(zs[tid], part[0][tid], row, pa, step);
   __syncthreads();   // part / zs free for the caller's next group
 }
 

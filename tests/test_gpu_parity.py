@@ -815,20 +815,25 @@ def test_norm_fold_matches_grad_sqnorm(gpu):
     assert ok, err
 
 
-@pytest.mark.parametrize("n_envs", [75, 512])
+@pytest.mark.parametrize("n_envs", [75, 200, 512])
 def test_conv_fwd_two_envs_identical(gpu, tmp_path, n_envs):
     """The large-launch forms against the 256-env ones: conv_fwd.hip with two
-    envs a workgroup (EPW = 2: 16 waves sharing the weight planes) and fc.hip's
-    64-row tiles (fc_fwd_big_kernel), the defaults from 512 envs a launch.  The
-    per-tile k order is the same, so a1, a2, the actions, the window gradient
-    and the updated parameters match bit for bit -- at an odd env count (the
-    last conv workgroup's second slot idle, a partial FC tile) and at 512."""
+    envs a workgroup (EPW = 2: 16 waves sharing the weight planes), fc.hip's
+    64-row tiles (fc_fwd_big_kernel), the defaults from 512 envs a launch, and
+    the FF heads in fc_fwd_big_kernel's ticket tails (ARL_FC_HEADS: each
+    column tile forms its K quarter of the logits, the row block's last tile
+    sums them and draws; from 128 envs).  The per-tile k order is the same, so
+    a1, a2, hfc, the policy outputs and actions, the window gradient and the
+    updated parameters match bit for bit -- at an odd env count (the last conv
+    workgroup's second slot idle, a partial FC tile; too few envs for the fused
+    heads, which fall back), at 200 (a partial 64-row block) and at 512."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     outs = []
     for i, arm in enumerate(({"ARL_CONV_EPW": "1", "ARL_FC_BIG": "0"}, {"ARL_CONV_EPW": "2", "ARL_FC_BIG": "0"},
-                             {"ARL_CONV_EPW": "1", "ARL_FC_BIG": "1"})):
+                             {"ARL_CONV_EPW": "1", "ARL_FC_BIG": "1", "ARL_FC_HEADS": "0"},
+                             {"ARL_CONV_EPW": "1", "ARL_FC_BIG": "1", "ARL_FC_HEADS": "1"})):
         f = str(tmp_path / f"arm_{i}.npz")
         env = dict(os.environ, **arm)
         subprocess.run([sys.executable, os.path.join(here, "conv_epw_worker.py"), f, str(n_envs)], env=env,
