@@ -109,9 +109,9 @@ def parse():
     ap.add_argument("--pool", type=int, default=8)
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="window as one HIP graph replay or eager launches on one stream. auto: eager for a "
-                         "one-chain window without collectives (C4 0.503-0.504 vs 0.510-0.512 ms median, C2 "
-                         "0.313-0.316 vs 0.318-0.320, profiles/r03/r3ag), the graph for env-group chains "
-                         "(C3) and N > 1 (its conv backward graph overlaps the all-reduce)")
+                         "one-chain window (C4 0.503-0.504 vs 0.510-0.512 ms median, C2 0.313-0.316 vs "
+                         "0.318-0.320, the N > 1 window on a one-rank RCCL group 0.547-0.550 vs 0.561-0.565; "
+                         "profiles/r03/r3ag, r3am), the graph for env-group chains (C3)")
     ap.add_argument("--no-graph", action="store_true", help="= --graph off")
     ap.add_argument("--env-groups", type=int, default=0,
                     help="forward chains on separate streams per window (A3C.run_window env_groups); "
@@ -468,7 +468,7 @@ def main(a):
     P = a.pool
 
     n_groups = len(model.net.env_groups(a.env_groups or model.net.default_env_groups()))
-    use_graph = False if a.no_graph else a.graph == "on" or (a.graph == "auto" and (collectives or n_groups > 1))
+    use_graph = False if a.no_graph else a.graph == "on" or (a.graph == "auto" and n_groups > 1)
     graph = conv_graph = None
     stream = torch.cuda.Stream(device=dev)
     stream.wait_stream(torch.cuda.current_stream())
