@@ -58,6 +58,9 @@ STAGGER = os.environ.get("ARL_GROUP_STAGGER", "1") != "0"
 # hands every chain's first launches to the device early; ARL_GROUP_ORDER=chain
 # issues chain 0 whole, then chain 1, ... (the A arm)
 GROUP_ORDER = os.environ.get("ARL_GROUP_ORDER", "interleave")
+# env groups: ARL_GROUP_STREAMS=1 issues every chain on the window's one stream (step-interleaved,
+# no overlap between chains: the smaller launches alone, A/B knob)
+GROUPS_ONE_STREAM = os.environ.get("ARL_GROUP_STREAMS", "") == "1"
 # > 1 rank: split the gradient all-reduce around the conv backward (ARL_OVERLAP_ALLREDUCE=0: one call)
 OVERLAP_ALLREDUCE = os.environ.get("ARL_OVERLAP_ALLREDUCE", "1") != "0"
 # one rank: GradientClipping's norm from the learner's conv reduce (ARL_NORM_FOLD=0: grad_sqnorm launch)
@@ -404,9 +407,11 @@ class A3C:
             self._forward_chain(pair_pool, reward_pool, done_pool, pool_len, first, stream, None)
         else:
             main = stream if stream is not None else torch.cuda.current_stream(net.device)
-            side = self._side_streams(len(groups) - 1)
+            one = GROUPS_ONE_STREAM
+            side = [main] * (len(groups) - 1) if one else self._side_streams(len(groups) - 1)
             for s in side:
-                s.wait_stream(main)                  # fork before any chain is issued
+                if not one:
+                    s.wait_stream(main)              # fork before any chain is issued
             chains = [self._chain_steps(pair_pool, reward_pool, done_pool, pool_len, first,
                                         main if g == 0 else side[g - 1], envs) for g, envs in enumerate(groups)]
             started = [None] * len(chains)
@@ -422,7 +427,7 @@ class A3C:
                 step = 0
                 while live:
                     for g in list(live):
-                        if step == 0 and g > 0 and started[g - 1] is not None:
+                        if step == 0 and g > 0 and started[g - 1] is not None and not one:
                             side[g - 1].wait_event(started[g - 1])   # stagger: after chain g-1's first kernel
                         ev = next(chains[g], StopIteration)
                         if ev is StopIteration:
@@ -431,7 +436,8 @@ class A3C:
                             started[g] = ev
                     step += 1
             for s in side:
-                main.wait_stream(s)
+                if not one:
+                    main.wait_stream(s)
             stream = main
         self._learn(stream)
         if split_update:
