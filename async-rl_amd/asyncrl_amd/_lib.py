@@ -68,6 +68,10 @@ SIGNATURES = {
     "arl_observe_act_envs": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int,
                                      c_int, c_void_p]),
     "arl_run_stage": (c_int, [c_void_p, c_int, c_int, c_void_p]),
+    "arl_stamps_begin": (c_int, [c_void_p, c_int]),
+    "arl_stamp": (c_int, [c_void_p, c_int, c_void_p]),
+    "arl_stamps_end": (c_int, [c_void_p, ctypes.POINTER(c_int)]),
+    "arl_stamps_read": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "arl_learn": (c_int, [c_void_p, c_double, c_double, c_double, c_int, c_void_p]),
     "arl_learn_part": (c_int, [c_void_p, c_int, c_double, c_double, c_double, c_int, c_void_p]),
     "arl_optimize": (c_int, [c_void_p, c_double, c_i64, c_i64, c_double, c_double, c_double, c_void_p]),
@@ -105,6 +109,11 @@ ACT_CONV_ONLY = 4      # arl_act_envs mode bits (env-group staggering)
 ACT_AFTER_CONV = 8
 ENV_GROUP_ALIGN = 32   # arl_observe_envs / arl_act_envs: e0 % ENV_GROUP_ALIGN == 0
 LEARN_RETURNS, LEARN_HEADS_DW, LEARN_TRUNK, LEARN_GATES_REDUCE, LEARN_FC_REDUCE, LEARN_CONV = range(6)
+# window timeline stages (arl_stamps_*): arl_run_stage's 1..11, then the stamp-only ones
+STAGE_NAMES = {1: "conv_fwd", 2: "fc_fwd", 3: "policy", 4: "fc_bwd", 5: "conv_bwd", 6: "returns", 7: "conv_reduce",
+               8: "grad_sqnorm", 9: "lstm_gates", 10: "lstm_bptt", 11: "lstm_wgrad", 12: "phi", 13: "rmsprop",
+               14: "lstm_cell", 15: "host", 16: "other"}
+STAGE_HOST = 15
 RESIZE_SCALAR = 0
 RESIZE_SIMD = 1
 RESIZE_CROP = 2      # flag, combine with SCALAR / SIMD: ale.py crop_or_scale='crop'

@@ -66,6 +66,20 @@ OVERLAP_ALLREDUCE = os.environ.get("ARL_OVERLAP_ALLREDUCE", "1") != "0"
 # one rank: GradientClipping's norm from the learner's conv reduce (ARL_NORM_FOLD=0: grad_sqnorm launch)
 NORM_FOLD = os.environ.get("ARL_NORM_FOLD", "1") != "0"
 
+def _is_dqn_phi(phi) -> bool:
+    """phi is dqn_phi (dqn_phi.py:4-17): this package's, the reference's own
+    function of that name, or a functools.partial / wrapper of one (marked by
+    __wrapped__).  Its output is the uint8 screens / 255, which the conv
+    kernels apply bit-exactly, so the ring keeps the uint8 screens."""
+    seen = 0
+    while phi is not None and seen < 8:
+        if phi is _device_dqn_phi or getattr(phi, "__name__", None) == "dqn_phi":
+            return True
+        phi = getattr(phi, "func", None) or getattr(phi, "__wrapped__", None)
+        seen += 1
+    return False
+
+
 def _to_device_f32(state, device) -> torch.Tensor:
     t = state if torch.is_tensor(state) else torch.from_numpy(np.ascontiguousarray(np.asarray(state, np.float32)))
     t = t.to(device=device, dtype=torch.float32)
@@ -106,11 +120,18 @@ class A3CModel:
 
     def set_frames(self, frames: str):
         """Rebuild the device net for another observation layout ("stacks"
-        / "states"), keeping the parameters and the RMSProp statistics."""
+        / "states"), keeping the parameters and the RMSProp statistics.  Only
+        before an agent binds the model: an A3C holds the net it was built
+        with, so a later switch would leave it stepping parameters the
+        optimizer no longer updates."""
         if frames == self.frames:
             return
         if frames not in ("stacks", "states") or self.frames not in ("stacks", "states"):
             raise ValueError("set_frames switches between 'stacks' and 'states' only")
+        if getattr(self, "_bound", False):
+            raise ValueError(f"set_frames({frames!r}): an A3C agent already runs this model with frames="
+                             f"{self.frames!r}; pick the layout (the phi plugin) before the first agent binds it, "
+                             "or give the second agent its own model")
         old = self.net
         arch = self.arch | (ARCH_STACK if frames == "stacks" else ARCH_STATES)
         net = DeviceNet(arch, self.n_actions, old.n_envs, old.t_max, env_offset=old.env_offset, seed=old.seed,
@@ -214,9 +235,10 @@ class A3C:
         self.pg = process_group
         self.world, self.rank = world_info(process_group)
         if model.frames in ("stacks", "states") and model.net.n_envs == 1:
-            # a3c.py:73 feeds phi(state) to the model: uint8 screens for the device dqn_phi
-            # (bit-exact scaling in the conv kernels), phi's f32 output for any other phi
-            model.set_frames("stacks" if phi is _device_dqn_phi else "states")
+            # a3c.py:73 feeds phi(state) to the model: uint8 screens for dqn_phi (bit-exact
+            # scaling in the conv kernels), phi's f32 output for any other phi
+            model.set_frames("stacks" if _is_dqn_phi(phi) else "states")
+        model._bound = True
         self.net = model.net
         self.single = (self.net.stack or self.net.states) and self.net.n_envs == 1
         self.collectives = self.world > 1 if collectives is None else bool(collectives)
@@ -284,9 +306,12 @@ class A3C:
                                     stream=main)
                 if work is not None:
                     work.wait()
+                net.stamp(stream=main)          # (window timeline: the FC / heads section's wait)
                 allreduce_grads(net.grads[:o], self.pg, force=True)
+                net.stamp(stream=main)          # (the conv section)
             elif self.collectives:
                 allreduce_grads(net.grads, self.pg, force=True)
+                net.stamp(stream=main)
             self.optimizer.update(stream=main, advance_window=True)
 
     def _update(self, stream=None):

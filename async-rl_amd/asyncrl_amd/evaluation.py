@@ -23,7 +23,11 @@ and every env's game restarts at the start of the evaluation.  The envs are
 left partway through episodes when it returns.
 The run uses (and overwrites) the model's lockstep workspace -- frame ring,
 step counter, LSTM state -- so evaluate on a model of its own (copy the
-trained parameters in: `eval_model.net.params.copy_(model.net.params)`).
+trained parameters in: `eval_model.net.params.copy_(model.net.params)`), and
+on a VecALE of its own: every env's game is restarted and left mid-episode,
+so a training learner stepping the same envs would carry its frame ring,
+LSTM state and n-step bootstrap across an unrelated game without a terminal
+(the reference builds a fresh ALE per evaluation run, a3c_ale.py:75-76).
 Host-side driver code; the per-step work is the device forward.
 """
 from __future__ import annotations
@@ -38,7 +42,8 @@ MODE_SAMPLE, MODE_GREEDY = 1, 2
 def run_episodes(model, vec_env, n_runs: int, deterministic: bool = False, max_steps: int | None = None,
                  stream=None):
     """Run `n_runs` evaluation episodes over `vec_env` (a VecALE with exactly
-    model.net.n_envs envs) with the model's lockstep workspace.  Returns
+    model.net.n_envs envs, not the training learner's: its games restart)
+    with the model's lockstep workspace.  Returns
     (scores, trace): scores[k] is the raw reward sum of run k (run k = env
     k % N's (k // N)-th episode); trace holds per-step host copies of the
     actions and done flags, (steps, N) each, for checking."""

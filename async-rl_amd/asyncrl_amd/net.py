@@ -17,7 +17,7 @@ import torch
 
 from ._lib import (ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, ARCH_STACK, ARCH_STATES, ENV_GROUP_ALIGN, FWD_KEEP_STATE,
                    LEARN_CONV, LEARN_FC_REDUCE, LEARN_GATES_REDUCE, LEARN_HEADS_DW, LEARN_RETURNS, LEARN_TRUNK,
-                   RESIZE_SCALAR, check, lib, ptr, stream_handle)
+                   RESIZE_SCALAR, STAGE_HOST, STAGE_NAMES, check, lib, ptr, stream_handle)
 
 
 def param_shapes(arch: int, n_actions: int):
@@ -247,7 +247,7 @@ class DeviceNet:
         return out
 
     STAGES = {"conv_fwd": 1, "fc_fwd": 2, "policy": 3, "fc_bwd": 4, "conv_bwd": 5, "returns": 6, "conv_reduce": 7,
-              "grad_sqnorm": 8, "lstm_gates": 9, "lstm_bptt": 10, "lstm_wgrad": 11}
+              "grad_sqnorm": 8, "lstm_gates": 9, "lstm_bptt": 10, "lstm_wgrad": 11, "rmsprop": 13}
 
     def run_stage(self, stage: str, t: int = 0, stream=None):
         """One window stage alone on the current workspace (timing / profiling)."""
@@ -312,6 +312,34 @@ class DeviceNet:
             raise ValueError(f"forward_states: need (n, {c}, 84, 84) float32 states")
         m = mode | (FWD_KEEP_STATE if keep_same_state else 0)
         check(lib.arl_forward_states(self._h, ptr(states), n, m, stream_handle(stream)), "arl_forward_states")
+
+    # ------------------------------------------------------------ window timeline (measurement)
+    stamping = False
+
+    def stamps_begin(self, cap: int):
+        """From now on every stage launch records a timing event after its
+        kernel(s) (arl_stamps_begin); read them with stamps_end()."""
+        check(lib.arl_stamps_begin(self._h, int(cap)), "arl_stamps_begin")
+        self.stamping = True
+
+    def stamp(self, stage: int = STAGE_HOST, stream=None):
+        """A caller's stamp (e.g. after a collective); no-op unless stamping."""
+        if self.stamping:
+            check(lib.arl_stamp(self._h, int(stage), stream_handle(stream)), "arl_stamp")
+
+    def stamps_end(self):
+        """Stop the timeline; returns (ms, stages): ms[i] = time from stamp
+        i - 1 to stamp i (ms[0] = 0), stages[i] = the stage name stamp i
+        closes (arl_stamps_read; waits for the last stamp)."""
+        self.stamping = False
+        cnt = ctypes.c_int()
+        check(lib.arl_stamps_end(self._h, ctypes.byref(cnt)), "arl_stamps_end")
+        n = cnt.value
+        ms = (ctypes.c_float * max(n, 1))()
+        st = (ctypes.c_int * max(n, 1))()
+        check(lib.arl_stamps_read(self._h, 0, n, ctypes.cast(ms, ctypes.c_void_p), ctypes.cast(st, ctypes.c_void_p)),
+              "arl_stamps_read")
+        return np.array(ms[:n], np.float64), [STAGE_NAMES.get(int(x), str(int(x))) for x in st[:n]]
 
     # ------------------------------------------------------------ outputs
     def step_outputs(self, t: int) -> dict:

@@ -94,7 +94,13 @@ int arl_net_create(arl_net** out, int arch, int n_actions, int n_envs, int t_max
   return ARL_OK;
 }
 
-void arl_net_destroy(arl_net* h) { delete h; }
+void arl_net_destroy(arl_net* h) {
+  if (h && h->net.stamps) {
+    for (hipEvent_t e : h->net.stamps->ev) (void)hipEventDestroy(e);
+    delete h->net.stamps;
+  }
+  delete h;
+}
 
 int64_t arl_net_param_floats(const arl_net* h) { return h ? h->net.param_floats : -1; }
 int arl_net_param_count(const arl_net* h) { return h ? (int)h->net.params.size() : -1; }
@@ -149,6 +155,7 @@ int arl_net_reset(arl_net* h, void* s) {
   if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_nvalid, 0, (size_t)n.R * n.N, S(s));
   if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_reset, 1, (size_t)(n.T + 1) * n.N, S(s));
   if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_tick, 0, (size_t)arl::fc_fwd_tiles(n.N) * 4, S(s));
+  if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_norm, 0, (size_t)arl::NORM_SCRATCH * 8, S(s));
   if (e == hipSuccess && n.w_fcb_tick)
     e = hipMemsetAsync(n.ws + n.w_fcb_tick, 0, (size_t)arl::fc_bwd_tickets() * 4, S(s));
   if (e == hipSuccess && n.arch == arl::ARCH_LSTM) {
@@ -198,10 +205,11 @@ static int observe_common(arl_net* h, int t, const uint8_t* pool, const float* r
   arl::RingArgs a;
   if (int rc = ring_args(h, t, pool, reward_pool, done_pool, pool_len, force_reset, mode, H, W, e0, ne, a)) return rc;
   const arl::Net& n = h->net;
-  return hip_status(n.layout == arl::FRAMES_RGB     ? arl::launch_rgb_ring(a, S(s))
-                    : (n.layout == arl::FRAMES_STACK || n.layout == arl::FRAMES_STATES) ? arl::launch_stack_ring(a, S(s))
-                                                    : arl::launch_phi_ring(a, S(s)),
-                    "observe");
+  hipError_t e = n.layout == arl::FRAMES_RGB ? arl::launch_rgb_ring(a, S(s))
+                 : (n.layout == arl::FRAMES_STACK || n.layout == arl::FRAMES_STATES) ? arl::launch_stack_ring(a, S(s))
+                                                                                    : arl::launch_phi_ring(a, S(s));
+  if (e == hipSuccess) e = arl::stamp(n, arl::STAGE_PHI, S(s));
+  return hip_status(e, "observe");
 }
 
 int arl_observe(arl_net* h, int t, const uint8_t* pair_pool, const float* reward_pool, const uint8_t* done_pool,
@@ -337,13 +345,61 @@ int arl_observe_act_envs(arl_net* h, int t, int e0, int ne, const uint8_t* pair_
 
 int arl_run_stage(arl_net* h, int stage, int t, void* s) {
   NEED_BOUND(h);
-  if (stage < ARL_STAGE_CONV_FWD || stage > ARL_STAGE_LSTM_WGRAD) return fail(ARL_EINVAL, "run_stage: unknown stage");
+  if (stage < ARL_STAGE_CONV_FWD || (stage > ARL_STAGE_LSTM_WGRAD && stage != ARL_STAGE_RMSPROP))
+    return fail(ARL_EINVAL, "run_stage: unknown stage");
   if (stage >= ARL_STAGE_RETURNS && h->net.arch == arl::ARCH_FF_NATURE)
     return fail(ARL_EINVAL, "run_stage: returns / conv reduce / grad sqnorm stages are NIPS-head only");
   if (stage >= ARL_STAGE_LSTM_GATES && h->net.arch != arl::ARCH_LSTM)
     return fail(ARL_EINVAL, "run_stage: the LSTM stages need an LSTM net");
   if (t < 0 || t > h->net.T) return fail(ARL_EINVAL, "run_stage: t out of [0, t_max]");
   return hip_status(arl::net_stage(h->net, stage, t, S(s)), "run_stage");
+}
+
+int arl_stamps_begin(arl_net* h, int cap) {
+  NEED_BOUND(h);
+  if (cap < 1 || cap > (1 << 20)) return fail(ARL_EINVAL, "stamps_begin: cap out of [1, 2^20]");
+  arl::Net& n = h->net;
+  if (!n.stamps) n.stamps = new arl::Stamps();
+  arl::Stamps& st = *n.stamps;
+  while ((int)st.ev.size() < cap) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return fail(ARL_EHIP, "stamps_begin: hipEventCreate");
+    st.ev.push_back(e);
+  }
+  st.stage.assign(st.ev.size(), 0);
+  st.count = 0;
+  st.on = true;
+  return ARL_OK;
+}
+
+int arl_stamp(arl_net* h, int stage, void* s) {
+  NEED_BOUND(h);
+  if (stage < 0 || stage > arl::STAGE_OTHER) return fail(ARL_EINVAL, "stamp: unknown stage");
+  return hip_status(arl::stamp(h->net, stage, S(s)), "stamp");
+}
+
+int arl_stamps_end(arl_net* h, int* count) {
+  NEED_BOUND(h);
+  arl::Stamps* st = h->net.stamps;
+  if (st) st->on = false;
+  if (count) *count = st ? st->count : 0;
+  return ARL_OK;
+}
+
+int arl_stamps_read(arl_net* h, int i0, int n, float* ms, int* stage) {
+  NEED_BOUND(h);
+  arl::Stamps* st = h->net.stamps;
+  if (!st || i0 < 0 || n < 0 || i0 + n > st->count) return fail(ARL_EINVAL, "stamps_read: range outside the stamps");
+  if (n == 0) return ARL_OK;
+  if (!ms || !stage) return fail(ARL_EINVAL, "stamps_read: null output");
+  hipError_t e = hipEventSynchronize(st->ev[i0 + n - 1]);
+  for (int i = i0; i < i0 + n && e == hipSuccess; ++i) {
+    float t = 0.f;
+    if (i > 0) e = hipEventElapsedTime(&t, st->ev[i - 1], st->ev[i]);
+    ms[i - i0] = t;
+    stage[i - i0] = st->stage[i];
+  }
+  return hip_status(e, "stamps_read");
 }
 
 int arl_learn(arl_net* h, double gamma, double beta, double vcoef, int clip_reward, void* s) {
@@ -401,10 +457,13 @@ int arl_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, doubl
   if (clip > 0 && !parts) return fail(ARL_EINVAL, "rmsprop: clip needs norm_partials scratch");
   hipError_t e = hipSuccess;
   const int blocks = 256;
-  if (clip > 0) e = arl::launch_grad_sqnorm(g, n, parts, blocks, S(s));
+  if (clip > 0) {   // the scratch's arrival ticket, armed per call (arl_internal.hpp NORM_TICKET)
+    e = hipMemsetAsync(parts + arl::NORM_TICKET, 0, sizeof(int), S(s));
+    if (e == hipSuccess) e = arl::launch_grad_sqnorm(g, n, parts, blocks, S(s));
+  }
   if (e == hipSuccess)
-    e = arl::launch_rmsprop(p, ms, g, n, lr, alpha, eps, clip > 0 ? parts : nullptr, blocks, (float)clip, nullptr, 0,
-                            0, 0, S(s));
+    e = arl::launch_rmsprop(p, ms, g, n, lr, alpha, eps, clip > 0 ? parts + arl::NORM_RESULT : nullptr, (float)clip,
+                            nullptr, 0, 0, 0, S(s));
   return hip_status(e, "rmsprop");
 }
 
@@ -440,8 +499,8 @@ int arl_returns_lossgrad(const float* rewards, const uint8_t* dones, const float
 int arl_stream_copy(const void* src, void* dst, int64_t bytes, int blocks, int mode, void* s) {
   if (bytes < 0 || (bytes > 0 && (!src || !dst))) return fail(ARL_EINVAL, "stream_copy: null pointer / bytes < 0");
   if (bytes % 16 || !aligned(src, 16) || !aligned(dst, 16)) return fail(ARL_EINVAL, "stream_copy: 16-byte units");
-  if (blocks < 1 || blocks > 65535) return fail(ARL_EINVAL, "stream_copy: blocks out of [1, 65535]");
-  if (mode < 0 || mode > 1) return fail(ARL_EINVAL, "stream_copy: mode must be 0 or 1");
+  if (mode < 0 || mode > 3) return fail(ARL_EINVAL, "stream_copy: mode must be 0, 1, 2 or 3");
+  if (mode < 2 && (blocks < 1 || blocks > 65535)) return fail(ARL_EINVAL, "stream_copy: blocks out of [1, 65535]");
   if (bytes == 0) return ARL_OK;
   return hip_status(arl::launch_stream_copy(src, dst, bytes, blocks, mode, S(s)), "stream_copy");
 }

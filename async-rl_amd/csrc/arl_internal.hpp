@@ -90,8 +90,19 @@ struct ParamInfo {
   int64_t numel;
 };
 
+// window timeline (measurement, arl_stamps_*): while `on`, every stage launch of a window records a
+// timing event on its stream right after the kernel(s) and remembers the stage (Stage) it closes, so
+// the intervals between consecutive stamps split one eager window into its stages as it ran
+struct Stamps {
+  std::vector<hipEvent_t> ev;
+  std::vector<int> stage;
+  int count = 0;
+  bool on = false;
+};
+
 struct Net {
   int arch, A, N, T, R;
+  Stamps* stamps = nullptr;   // null / off: stamp() is a no-op
   bool rgb = false;        // ARCH_RGB: 3 planes per obs step in the ring, conv1 W (16, 3, 8, 8)
   bool stack = false;      // ARCH_STACK: 4 planes (a whole stack) per obs step in the ring
   bool states = false;     // ARCH_STATES: 4 f32 planes (phi's output) per obs step in the ring
@@ -157,7 +168,17 @@ hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_tot
 hipError_t net_advance(Net& net, hipStream_t s);
 enum Stage { STAGE_CONV_FWD = 1, STAGE_FC_FWD = 2, STAGE_POLICY = 3, STAGE_FC_BWD = 4, STAGE_CONV_BWD = 5,
              STAGE_RETURNS = 6, STAGE_CONV_REDUCE = 7, STAGE_GRAD_SQNORM = 8,
-             STAGE_LSTM_GATES = 9, STAGE_LSTM_BPTT = 10, STAGE_LSTM_WGRAD = 11 };
+             STAGE_LSTM_GATES = 9, STAGE_LSTM_BPTT = 10, STAGE_LSTM_WGRAD = 11,
+             // stamp-only stages (timeline, not arl_run_stage): the observation, the update kernel,
+             // the separate LSTM cell launches, a caller's stamp (e.g. after a collective), others
+             STAGE_PHI = 12, STAGE_RMSPROP = 13, STAGE_LSTM_CELL = 14, STAGE_HOST = 15, STAGE_OTHER = 16 };
+// record the stamp closing `stage` on stream s (no-op unless the net's timeline is on)
+inline hipError_t stamp(const Net& net, int stage, hipStream_t s) {
+  Stamps* st = net.stamps;
+  if (st == nullptr || !st->on || st->count >= (int)st->ev.size()) return hipSuccess;
+  st->stage[st->count] = stage;
+  return hipEventRecord(st->ev[st->count++], s);
+}
 hipError_t net_stage(Net& net, int stage, int t, hipStream_t s);
 // keep: LSTM keep_same_state (the pi_and_v recurrent state is not advanced)
 hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_t s, bool keep = false);
@@ -199,7 +220,7 @@ hipError_t launch_phi_conv_fwd(const RingArgs& ring, const float* W1, const floa
                                const float* b2, float* a1, float* a2, hipStream_t s, uint32_t* a2m = nullptr);
 // the gradient's squared norm folded into the conv slab reduce (parts == null: not folded)
 struct NormFold {
-  double* parts;            // conv_norm_parts(rest_blocks) f64 partials
+  double* parts;            // NORM_SCRATCH f64: conv_norm_parts(rest_blocks) partials, result, ticket
   const float* g;           // the flat gradient
   int64_t rest_begin, rest_end;   // floats of g outside the conv tensors (final before the reduce)
   int rest_blocks;
@@ -284,8 +305,44 @@ struct AdvanceArgs {
   float* cbuf;
   int T, n;
 };
+// GradientClipping's squared norm: f64 partials [0, nparts) of the launch that sums
+// them (grad_sqnorm_kernel, or reduce_conv_bwd_kernel with a NormFold), whose last block
+// leaves the total in [NORM_RESULT]; [NORM_TICKET] is its arrival counter (an int, zero
+// before the first launch, re-armed by each)
+constexpr int NORM_MAX_PARTS = 1000, NORM_RESULT = 1000, NORM_TICKET = 1001, NORM_SCRATCH = 1024;
+// Cross-workgroup hand-off of the norm partials (MI355X_MICROARCH.md, "Valid forms", table
+// row 1): lane 0 of each block stores its partial sc1 (agent-scope relaxed atomic store =
+// write-through), drains it (s_waitcnt vmcnt(0)) and then adds to ONE unsharded ticket; the
+// block whose add returned nparts - 1 is the last, its wave 0 loads every partial sc1 and sums
+// them in index order (lane l: l, l + 64, ...; then the lanes in xor-tree order, a fixed
+// order), writes the squared norm to parts[NORM_RESULT] and re-arms the ticket.  The next
+// launch on the stream (rmsprop_kernel) reads the result after the kernel boundary.
+__device__ inline void norm_finish(double mine, int b, int nparts, double* parts) {
+  __shared__ int last;
+  int* ticket = reinterpret_cast<int*>(parts + NORM_TICKET);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(parts + b), __double_as_longlong(mine),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nparts - 1;
+  }
+  __syncthreads();
+  if (!last || threadIdx.x >= 64) return;
+  double t = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 64)
+    t += __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<unsigned long long*>(parts + i),
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o);
+  if (threadIdx.x == 0) {
+    parts[NORM_RESULT] = t;
+    __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// norm_sq: &partials[NORM_RESULT] (null: no clip)
 hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, double alpha, double eps,
-                          const double* norm_partials, int norm_blocks, float clip, const int64_t* ctl,
+                          const double* norm_sq, float clip, const int64_t* ctl,
                           int64_t total_steps, int64_t n_total, int t_max, hipStream_t s,
                           const AdvanceArgs* adv = nullptr);
 hipError_t launch_grad_sqnorm(const float* g, int64_t n, double* partials, int blocks, hipStream_t s);

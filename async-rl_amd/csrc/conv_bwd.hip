@@ -718,7 +718,8 @@ conv_bwd_kernel(ConvBwdArgs a) {
 // gradient values it wrote in parts[block], and rest_blocks extra blocks sum
 // the squares of g[rest_begin, rest_end) -- the gradient the FC / heads / LSTM
 // backward has already finished -- into parts[nconv + b]; the optimizer then
-// reduces these partials instead of a separate grad_sqnorm launch.
+// reads their sum, which the last block to finish leaves in parts[NORM_RESULT]
+// (norm_finish, arl_internal.hpp), instead of a separate grad_sqnorm launch.
 constexpr int RED_O = 64, RED_Z = 16;
 constexpr int RED_BLOCKS = (SLAB + RED_O - 1) / RED_O;   // 193
 __device__ inline double block_sum_f64_1024(double x, double* sh) {   // 1,024 threads, fixed order
@@ -751,7 +752,7 @@ reduce_conv_bwd_kernel(const float* __restrict__ slab, int G, float* __restrict_
       t += (double)v * v;
     }
     t = block_sum_f64_1024(t, shn);
-    if (threadIdx.x == 0) nf.parts[RED_BLOCKS + b] = t;
+    norm_finish(t, RED_BLOCKS + b, RED_BLOCKS + nf.rest_blocks, nf.parts);
     return;
   }
   const int ol = threadIdx.x & (RED_O - 1), zg = threadIdx.x / RED_O;
@@ -779,7 +780,7 @@ reduce_conv_bwd_kernel(const float* __restrict__ slab, int G, float* __restrict_
   }
   if (nf.parts != nullptr) {   // (block-uniform)
     sq = block_sum_f64_1024(sq, shn);
-    if (threadIdx.x == 0) nf.parts[blockIdx.x] = sq;
+    norm_finish(sq, blockIdx.x, RED_BLOCKS + nf.rest_blocks, nf.parts);
   }
 }
 

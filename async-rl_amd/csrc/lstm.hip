@@ -2,7 +2,8 @@
 // L.LSTM(256, 256) = upward Linear(256, 1024) + lateral Linear(256, 1024, no
 // bias) -> Chainer 1.8.1 F.lstm; one launch per lockstep step):
 //
-//   gates[m][j] = x[m] . Wu[j] + (reset[m] ? 0 : h[m] . Wl[j]) + b[j]
+//   gates[m][j] = (x[m] . Wu[j] + b[j]) + (reset[m] ? 0 : h[m] . Wl[j])   (Chainer's order:
+//                 upward(x) with its bias, then + lateral(h))
 //   (a, i, f, o) = gates[m][4u .. 4u + 3]          (interleaved, reshape(n, 256, 4))
 //   c' = tanh(a) sig(i) + sig(f) c,   h' = sig(o) tanh(c')
 //
@@ -18,8 +19,8 @@
 //     an episode end, a3c.py:166 / a3c_ale.py:65-66) drops the h half at the
 //     epilogue instead of zero-filling staged rows;
 //   * epilogue: the tile through LDS (row stride 68 floats: the four lane
-//     quarters' rows on distinct banks), one (row, unit) per thread: bias, the
-//     gates written for the backward, and the cell -- the arithmetic of
+//     quarters' rows on distinct banks; the bias added before it), one (row,
+//     unit) per thread: the gates written for the backward, and the cell -- the arithmetic of
 //     lstm_cell_fwd_kernel (net.hip), op for op.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -216,10 +217,15 @@ lstm_gates_kernel(LstmGatesArgs a) {
 
   // ---- epilogue tile into stage 1 (free since the barrier before chunk 2):
   // C row q*4 + r, column col of sub-tile (ms, ns)
+  // Chainer's order (a3c_ale.py:50-51, L.LSTM): upward(x) = x Wu^T + b first, then + lateral(h) = h Wl^T
+  // (a reset row's state is None: no lateral term)
   float* T = S + 4 * LSTAGE4;
+  const float bcol = a.b[n0 + ns * 16 + col];
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
-    T[(ms * 16 + q * 4 + r) * TLD + ns * 16 + col] = rs[r] ? accx[r] : __fadd_rn(accx[r], acch[r]);
+  for (int r = 0; r < 4; ++r) {
+    const float up = __fadd_rn(accx[r], bcol);
+    T[(ms * 16 + q * 4 + r) * TLD + ns * 16 + col] = rs[r] ? up : __fadd_rn(up, acch[r]);
+  }
   if constexpr (XRED) {
     if (n0 == 0) {   // hfc for the backward, from the column-tile-0 workgroups
 #pragma unroll
@@ -232,9 +238,7 @@ lstm_gates_kernel(LstmGatesArgs a) {
   lstm_lds_barrier();
   const int row = tid >> 4, u = tid & 15, m = m0 + row, n = n0 + 4 * u;
   if (m >= a.n) return;
-  const float4 bb = *reinterpret_cast<const float4*>(a.b + n);
-  const float4 v = *reinterpret_cast<const float4*>(T + row * TLD + 4 * u);
-  const float4 g = make_float4(__fadd_rn(v.x, bb.x), __fadd_rn(v.y, bb.y), __fadd_rn(v.z, bb.z), __fadd_rn(v.w, bb.w));
+  const float4 g = *reinterpret_cast<const float4*>(T + row * TLD + 4 * u);   // bias added above
   *reinterpret_cast<float4*>(a.gates + (int64_t)m * GATES + n) = g;
   if (!a.cell) return;
   const int64_t i = (int64_t)m * HID + (n >> 2);

@@ -471,7 +471,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
     net.w_slab_fc = buf("slab_fc", (int64_t)pl.fc_w * HID * (A2 + 1) * 4);
     net.w_slab_lstm = buf("slab_lstm", L ? (int64_t)pl.lstm_w * GATES * (2 * HID + 1) * 4 : 0);
   }
-  net.w_norm = buf("norm_partials", (int64_t)std::max(net.norm_blocks, conv_norm_parts(net.norm_rest_blocks)) * 8);
+  net.w_norm = buf("norm_partials", (int64_t)NORM_SCRATCH * 8);   // partials, result, ticket (arl_internal.hpp)
   net.w_tick = buf("tickets", (int64_t)fc_fwd_tiles((int)n) * 4);
   net.w_fcb_part = buf("fc_bwd_partials", NAT ? 0 : fc_bwd_part_floats((int)S) * 4);
   net.w_fcb_tick = buf("fc_bwd_tickets", NAT ? 0 : (int64_t)fc_bwd_tickets() * 4);
@@ -542,13 +542,17 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne, con
       return hipErrorInvalidValue;
     ARL_TRY(launch_phi_conv_fwd(*obs, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W, P + net.o_c2b, a1_bwd, a2, s,
                                 mask_bwd));
+    ARL_TRY(stamp(net, STAGE_CONV_FWD, s));
   } else if (!(part & ACT_AFTER_CONV) && net.states) {
     if (e0 != 0 || ne != n) return hipErrorInvalidValue;   // one launch over all envs
     ARL_TRY(states_conv_fwd(net, t, a1, a2, s));
-  } else if (!(part & ACT_AFTER_CONV))
+    ARL_TRY(stamp(net, STAGE_CONV_FWD, s));
+  } else if (!(part & ACT_AFTER_CONV)) {
     ARL_TRY(launch_conv_fwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
                             net.at<int64_t>(net.w_ctl), n, net.R, t, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W,
                             P + net.o_c2b, a1_bwd, a2, s, net.layout, e0, ne, mask_bwd));
+    ARL_TRY(stamp(net, STAGE_CONV_FWD, s));
+  }
   if (part & ACT_CONV_ONLY) return hipSuccess;
   const int64_t o = (int64_t)t * n + e0;
   float* fc_slab = net.at<float>(net.w_slab) + (int64_t)FC_SPLIT * e0 * HID;
@@ -559,17 +563,22 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne, con
                                            net.at<float>(net.w_logp) + o * A, net.at<float>(net.w_v) + o,
                                            net.at<float>(net.w_ent) + o, net.at<int32_t>(net.w_act) + o,
                                            net.at<float>(net.w_logpa) + o);
-    if (fc_fwd_heads(ne))   // ... or all of it in the FC launch's ticket tails
-      return launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab,
-                           net.at<int>(net.w_tick) + fc_fwd_tiles(e0), hfc, s, &pa);
+    if (fc_fwd_heads(ne)) {   // ... or all of it in the FC launch's ticket tails
+      ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab,
+                            net.at<int>(net.w_tick) + fc_fwd_tiles(e0), hfc, s, &pa));
+      return stamp(net, STAGE_FC_FWD, s);
+    }
     ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab, nullptr, nullptr, s));
-    return launch_policy_fc(fc_slab, ne, P + net.o_fcb, hfc, pa, s);
+    ARL_TRY(stamp(net, STAGE_FC_FWD, s));
+    ARL_TRY(launch_policy_fc(fc_slab, ne, P + net.o_fcb, hfc, pa, s));
+    return stamp(net, STAGE_POLICY, s);
   }
   // LSTM: the FC's split-K partials only, their reduce + bias + relu in the gate kernel's
   // staging (lstm.hip XRED) or the FC's ticket reduce (lstm_xred)
   const bool xred = lstm_xred(ne);
   ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab,
                         xred ? nullptr : net.at<int>(net.w_tick) + fc_fwd_tiles(e0), xred ? nullptr : hfc, s));
+  ARL_TRY(stamp(net, STAGE_FC_FWD, s));
   const float* hpol = hfc;
   if (xred) {
     const int64_t r0 = (int64_t)t * n + e0;
@@ -581,11 +590,13 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne, con
     const float* cprev = net.at<float>(net.w_cbuf) + r0 * HID;
     ARL_TRY(launch_lstm_gates(nullptr, hprev, rs, P + net.o_luW, P + net.o_llW, P + net.o_lub, gates, cprev, cout,
                               hout, ne, !LSTM_SPLIT, s, fc_slab, P + net.o_fcb, hfc));
+    ARL_TRY(stamp(net, STAGE_LSTM_GATES, s));
     if (LSTM_SPLIT) {
       const int64_t cnt = (int64_t)ne * HID;
       hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, gates, cprev,
                          rs, cout, hout, cnt);
       ARL_TRY(hipGetLastError());
+      ARL_TRY(stamp(net, STAGE_LSTM_CELL, s));
     }
     hpol = hout;
   } else if (net.arch == ARCH_LSTM) {
@@ -600,13 +611,15 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne, con
     // the cell runs in the GEMM's epilogue (EpiLstmCell; ARL_LSTM_SPLIT=1: a separate launch)
     ARL_TRY(lstm_gates_cell(LstmGateA{hfc, hprev, rs}, LstmGateB{P + net.o_luW, P + net.o_llW}, P + net.o_lub, gates,
                             cprev, rs, cout, hout, ne, s));
+    ARL_TRY(stamp(net, STAGE_LSTM_GATES, s));
     hpol = hout;
   }
-  return launch_policy(hpol, ne, P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
-                       net.at<int64_t>(net.w_ctl), t, net.env_offset + e0, t < net.T ? mode : 0,
-                       net.at<float>(net.w_logits) + o * A, net.at<float>(net.w_probs) + o * A,
-                       net.at<float>(net.w_logp) + o * A, net.at<float>(net.w_v) + o, net.at<float>(net.w_ent) + o,
-                       net.at<int32_t>(net.w_act) + o, net.at<float>(net.w_logpa) + o, s);
+  ARL_TRY(launch_policy(hpol, ne, P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
+                        net.at<int64_t>(net.w_ctl), t, net.env_offset + e0, t < net.T ? mode : 0,
+                        net.at<float>(net.w_logits) + o * A, net.at<float>(net.w_probs) + o * A,
+                        net.at<float>(net.w_logp) + o * A, net.at<float>(net.w_v) + o, net.at<float>(net.w_ent) + o,
+                        net.at<int32_t>(net.w_act) + o, net.at<float>(net.w_logpa) + o, s));
+  return stamp(net, STAGE_POLICY, s);
 }
 
 // Policy arguments of a forward on explicit states (slot T): a sampled action
@@ -681,6 +694,21 @@ static NormFold norm_fold_args(const Net& net) {
   return NormFold{net.at<double>(net.w_norm), net.g, net.o_fcW, net.param_floats, net.norm_rest_blocks};
 }
 
+// the fused conv backward (per-sample slabs) and its slab reduce (with the folded clip norm's
+// partials when nf.parts is set): the learner's last part
+static hipError_t conv_backward(Net& net, hipStream_t s, const NormFold& nf) {
+  const int S = net.T * net.N;
+  float* slab = net.at<float>(net.w_slab);
+  ARL_TRY(launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl),
+                          net.N, net.R, S, net.at<float>(net.w_a1), net.at<float>(net.w_da2), net.p + net.o_c2W, slab,
+                          net.g + net.o_c2W, net.g + net.o_c2b, net.g + net.o_c1W, net.g + net.o_c1b, s,
+                          /*reduce=*/false, net.layout));
+  ARL_TRY(stamp(net, STAGE_CONV_BWD, s));
+  ARL_TRY(launch_conv_reduce(slab, S, net.g + net.o_c2W, net.g + net.o_c2b, net.g + net.o_c1W, net.g + net.o_c1b, s,
+                             net.layout, nf));
+  return stamp(net, STAGE_CONV_REDUCE, s);
+}
+
 hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s) {
   if (net.arch == ARCH_FF_NATURE) return nature_learn(net, gamma, beta, vcoef, clip_reward, s);
   for (int part = 0; part < LEARN_CONV; ++part) ARL_TRY(net_learn_part(net, part, gamma, beta, vcoef, clip_reward, s));
@@ -691,11 +719,7 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
     net.norm_ready = false;
     return hipSuccess;
   }
-  const NormFold nf = norm_fold_args(net);
-  ARL_TRY(launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid), net.at<int64_t>(net.w_ctl),
-                          net.N, net.R, net.T * net.N, net.at<float>(net.w_a1), net.at<float>(net.w_da2),
-                          net.p + net.o_c2W, net.at<float>(net.w_slab), net.g + net.o_c2W, net.g + net.o_c2b,
-                          net.g + net.o_c1W, net.g + net.o_c1b, s, /*reduce=*/true, net.layout, nf));
+  ARL_TRY(conv_backward(net, s, norm_fold_args(net)));
   net.norm_ready = net.norm_fold;
   return hipSuccess;
 }
@@ -750,15 +774,18 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
                            net.at<float>(net.w_probs), net.at<float>(net.w_logp), net.at<int32_t>(net.w_act), T, n, A,
                            gamma, beta, vcoef, clip_reward, dl, dv, net.at<float>(net.w_loss), s,
                            net.at<int64_t>(net.w_ctl), net.pi_coef, net.keep_scale));
-    return launch_heads_bwd(dl, dv, P + net.o_piW, P + net.o_vW, A, HID, L ? nullptr : hfc,
-                            L ? net.at<float>(net.w_dh) : dfc, S, s);
+    ARL_TRY(launch_heads_bwd(dl, dv, P + net.o_piW, P + net.o_vW, A, HID, L ? nullptr : hfc,
+                             L ? net.at<float>(net.w_dh) : dfc, S, s));
+    return stamp(net, STAGE_RETURNS, s);
   }
-  if (part == LEARN_RETURNS)
-    return launch_returns_heads(net.at<float>(net.w_rewards), net.at<uint8_t>(net.w_dones), net.at<float>(net.w_v),
-                                net.at<float>(net.w_probs), net.at<float>(net.w_logp), net.at<int32_t>(net.w_act), T,
-                                n, A, gamma, beta, vcoef, clip_reward, dl, dv, net.at<float>(net.w_loss), s,
-                                net.at<int64_t>(net.w_ctl), net.pi_coef, net.keep_scale, P + net.o_piW, P + net.o_vW,
-                                L ? nullptr : hfc, L ? net.at<float>(net.w_dh) : dfc);
+  if (part == LEARN_RETURNS) {
+    ARL_TRY(launch_returns_heads(net.at<float>(net.w_rewards), net.at<uint8_t>(net.w_dones), net.at<float>(net.w_v),
+                                 net.at<float>(net.w_probs), net.at<float>(net.w_logp), net.at<int32_t>(net.w_act), T,
+                                 n, A, gamma, beta, vcoef, clip_reward, dl, dv, net.at<float>(net.w_loss), s,
+                                 net.at<int64_t>(net.w_ctl), net.pi_coef, net.keep_scale, P + net.o_piW, P + net.o_vW,
+                                 L ? nullptr : hfc, L ? net.at<float>(net.w_dh) : dfc));
+    return stamp(net, STAGE_RETURNS, s);
+  }
   // heads: weight grads (ones column = bias) and dh.  With the fused FC
   // backward the weight grads are its job C (LEARN_TRUNK): nothing here.
   const HeadsDW heads{dl, dv, hheads, A, G + net.o_piW, G + net.o_pib, G + net.o_vW, G + net.o_vb};
@@ -779,16 +806,16 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
     return FC_BWD_GEMM ? launch_reduce_grad(slab_f, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s)
                        : hipSuccess;
   const float* a2 = net.at<float>(net.w_a2);
-  const float* a1 = net.at<float>(net.w_a1);
   float* da2 = net.at<float>(net.w_da2);
-  if (part == LEARN_CONV && net.states) return states_conv_bwd(net, s);
+  if (part == LEARN_CONV && net.states) {
+    ARL_TRY(states_conv_bwd(net, s));
+    return stamp(net, STAGE_CONV_BWD, s);
+  }
   if (part == LEARN_CONV)
     // fused conv backward per sample (conv_bwd.hip): conv2 dW/db,
     // da1 = conv_transpose(da2, W2) * (a1 > 0) kept in LDS, conv1 dW/db
-    // straight from the frame ring
-    return launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
-                           net.at<int64_t>(net.w_ctl), n, net.R, S, a1, da2, P + net.o_c2W, slab, G + net.o_c2W,
-                           G + net.o_c2b, G + net.o_c1W, G + net.o_c1b, s, /*reduce=*/true, net.layout);
+    // straight from the frame ring; then its slab reduce
+    return conv_backward(net, s, NormFold{});
   if (part != LEARN_TRUNK) return hipErrorInvalidValue;
   // (the heads' dh was written by LEARN_RETURNS)
   // 2. LSTM: truncated BPTT over the window, gate weight gradients, dfc
@@ -813,12 +840,14 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
                            cbuf + (o + n) * HID, cbuf + o * HID, rs + o, dH + o * HID, dhn, dcn, dG + o * GATES,
                            t == T - 1 ? 1 : 0, cnt);
         ARL_TRY(hipGetLastError());
+        ARL_TRY(stamp(net, STAGE_LSTM_CELL, s));
       }
       if (t > 0 && !LSTM_BPTT_GENERIC) {   // lstm.hip: dh GEMM + mask + step t-1's cell in one launch
         const int64_t op = o - n;
         ARL_TRY(launch_lstm_bptt(dG + o * GATES, P + net.o_llW, rs + o, gates + op * GATES, cbuf + (op + n) * HID,
                                  cbuf + op * HID, rs + op, dH + op * HID, dcn, dG + op * GATES, dhn, n, !LSTM_SPLIT,
                                  s));
+        ARL_TRY(stamp(net, STAGE_LSTM_BPTT, s));
       } else if (t > 0) {
         ARL_TRY((launch_gemm<32, 64, 32, 2, 2, GK, GM>(RowMajor{dG + o * GATES, GATES}, RowMajor{P + net.o_llW, HID},
                                                        EpiSlab{slab, n, HID}, n, HID, GATES, BPTT_SPLIT, s)));
@@ -831,20 +860,24 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
                              dG + op * GATES, cnt);
           ARL_TRY(hipGetLastError());
         }
+        ARL_TRY(stamp(net, STAGE_LSTM_BPTT, s));
       }
     }
     // gate weight gradients and dfc = (dG Wu) * (hfc > 0): independent, one launch
     ARL_TRY(lstm_wgrad(net, s));
+    ARL_TRY(stamp(net, STAGE_LSTM_WGRAD, s));
   }
   // 3. FC: dW + db straight into the gradient and da2 = (dfc W) * (a2 > 0),
   //    one launch (fc_bwd.hip)
-  if (!FC_BWD_GEMM)
-    return launch_fc_bwd(dfc, a2, P + net.o_fcW, S, G + net.o_fcW, G + net.o_fcb, net.at<float>(net.w_da2),
-                         net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s, &heads, a2_mask(net, 0));
+  if (!FC_BWD_GEMM) {
+    ARL_TRY(launch_fc_bwd(dfc, a2, P + net.o_fcW, S, G + net.o_fcW, G + net.o_fcb, net.at<float>(net.w_da2),
+                          net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s, &heads, a2_mask(net, 0)));
+    return stamp(net, STAGE_FC_BWD, s);
+  }
   ARL_TRY((launch_gemm2_nt<64, 64, 32, 2, 4, 512, GM, GM, GK, GM>(   // 8 waves, 2 sub-tiles each (ARL_FC_BWD=gemm)
       gemm_job<64, 32>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab_f, HID, A2 + 1}, HID, A2 + 1, S, pl.fc_w, 64),
       gemm_job<64, 32>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2}, EpiMask{da2, a2, A2}, S, A2, HID, 1, 64), s)));
-  return hipSuccess;
+  return stamp(net, STAGE_FC_BWD, s);
 }
 
 // One stage of a window on the current workspace contents (arl_run_stage):
@@ -937,6 +970,9 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
     case STAGE_LSTM_WGRAD:
       if (net.arch != ARCH_LSTM) return hipErrorInvalidValue;
       return lstm_wgrad(net, s);
+    case STAGE_RMSPROP:   // the update kernel as a window runs it (clip 40 from the last norm the window left), lr 0
+      return launch_rmsprop(net.p, net.ms, net.g, net.param_floats, 0.0, 0.99, 0.1,
+                            net.at<double>(net.w_norm) + NORM_RESULT, 40.f, nullptr, 0, 0, net.T, s);
     default:
       return hipErrorInvalidValue;
   }
@@ -951,15 +987,18 @@ hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_tot
   const bool fused = advance;
   const bool folded = do_clip && net.norm_ready;   // partials left by arl_learn's conv reduce
   net.norm_ready = false;
-  if (do_clip && !folded) ARL_TRY(launch_grad_sqnorm(net.g, net.param_floats, parts, net.norm_blocks, s));
-  const int nparts = folded ? conv_norm_parts(net.norm_rest_blocks) : net.norm_blocks;
+  if (do_clip && !folded) {
+    ARL_TRY(launch_grad_sqnorm(net.g, net.param_floats, parts, net.norm_blocks, s));
+    ARL_TRY(stamp(net, STAGE_GRAD_SQNORM, s));
+  }
   const bool L = net.arch == ARCH_LSTM;
   const AdvanceArgs adv{net.at<int64_t>(net.w_ctl), net.at<uint8_t>(net.w_reset),
                         L ? net.at<float>(net.w_hbuf) : nullptr, L ? net.at<float>(net.w_cbuf) : nullptr, net.T,
                         net.N};
-  ARL_TRY(launch_rmsprop(net.p, net.ms, net.g, net.param_floats, lr0, alpha, eps, do_clip ? parts : nullptr,
-                         nparts, clip, total_steps > 0 ? net.at<int64_t>(net.w_ctl) : nullptr, total_steps,
+  ARL_TRY(launch_rmsprop(net.p, net.ms, net.g, net.param_floats, lr0, alpha, eps,
+                         do_clip ? parts + NORM_RESULT : nullptr, clip, total_steps > 0 ? net.at<int64_t>(net.w_ctl) : nullptr, total_steps,
                          n_total, net.T, s, fused ? &adv : nullptr));
+  ARL_TRY(stamp(net, STAGE_RMSPROP, s));
   return advance && !fused ? net_advance(net, s) : hipSuccess;
 }
 

@@ -7,10 +7,12 @@
 //
 // Two launches per update, both HBM-streaming over the padded flat buffer:
 //   grad_sqnorm_kernel: per-block partial sum of g^2 (f32 per thread over a
-//     grid-stride, f64 across the block) -> partials[block];
-//   rmsprop_kernel: every block first re-reduces the (<= 1024) f64 partials
-//     (4-8 KB, L2-resident) to the global norm, so the clip rate needs no host
-//     round trip and no extra launch; then 4 parameters per thread per
+//     grid-stride, f64 across the block) -> partials[block]; the block that
+//     finishes last (arrival ticket) sums the partials in block order and
+//     leaves the squared norm in partials[NORM_RESULT] (norm_finish), so the
+//     clip rate needs no host round trip and no extra launch (the folded form:
+//     reduce_conv_bwd_kernel leaves it the same way, conv_bwd.hip);
+//   rmsprop_kernel: reads that one f64, then 4 parameters per thread per
 //     iteration: g' = clip ? g*f32(rate) : g; ms = ms*alpha; ms += (c*g')*g';
 //     p -= (lr*g') / sqrt(ms + eps) -- every op an explicit round-to-nearest
 //     f32 op in the reference's order (NumPy f32 semantics, no FMA), so the
@@ -52,7 +54,7 @@ grad_sqnorm_kernel(const float* __restrict__ g, int64_t n, double* __restrict__ 
     acc = __fadd_rn(acc, __fmul_rn(v, v));
   }
   const double t = block_sum_f64((double)acc, sh);
-  if (threadIdx.x == 0) partials[blockIdx.x] = t;
+  norm_finish(t, blockIdx.x, gridDim.x, partials);
 }
 
 struct RmsConst {   // (AdvanceArgs is declared in arl_internal.hpp)
@@ -76,8 +78,7 @@ __device__ inline void rms1(float& p, float& ms, float g, const RmsConst& c) {
 
 __global__ void __launch_bounds__(256)
 rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __restrict__ g, int64_t n, RmsConst c,
-               const double* __restrict__ partials, int nparts, float clip, AdvanceArgs adv) {
-  __shared__ double sh[8];
+               const double* __restrict__ norm_sq, float clip, AdvanceArgs adv) {
   if (c.ctl != nullptr && c.total > 0) {
     const int64_t gt = (c.ctl[c.ctl_idx] + c.t_max) * c.n_total;
     // clamped at 0: the reference stops training once global_t passes the
@@ -89,8 +90,8 @@ rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __res
   float4* m4 = reinterpret_cast<float4*>(ms);
   const float4* g4 = reinterpret_cast<const float4*>(g);
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  // the first float4 of p / ms / g is in flight while the block reduces the
-  // norm partials (the grid normally covers the buffer in one pass)
+  // the first float4 of p / ms / g is in flight with the squared norm's load
+  // (the grid normally covers the buffer in one pass)
   float4 pv, mv, gv;
   if (i0 < n4) {
     pv = p4[i0];
@@ -99,11 +100,8 @@ rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __res
   }
   float scale = 1.f;
   bool do_clip = false;
-  if (partials != nullptr) {
-    double t = 0.0;
-    for (int i = threadIdx.x; i < nparts; i += blockDim.x) t += partials[i];
-    t = block_sum_f64(t, sh);
-    const double norm = sqrt(t);
+  if (norm_sq != nullptr) {
+    const double norm = sqrt(*norm_sq);
     const double rate = (double)clip / norm;
     if (norm > 0.0 && rate < 1.0) {
       do_clip = true;
@@ -158,12 +156,13 @@ static int stream_blocks(int64_t n) {
 }
 
 hipError_t launch_grad_sqnorm(const float* g, int64_t n, double* partials, int blocks, hipStream_t s) {
+  if (blocks < 1 || blocks > NORM_MAX_PARTS) return hipErrorInvalidValue;
   hipLaunchKernelGGL(grad_sqnorm_kernel, dim3(blocks), dim3(256), 0, s, g, n, partials);
   return hipGetLastError();
 }
 
 hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, double alpha, double eps,
-                          const double* norm_partials, int norm_blocks, float clip, const int64_t* ctl,
+                          const double* norm_sq, float clip, const int64_t* ctl,
                           int64_t total_steps, int64_t n_total, int t_max, hipStream_t s, const AdvanceArgs* adv) {
   if (n <= 0) return hipSuccess;
   // each Python-float hyperparameter meets the f32 arrays as f32(value)
@@ -180,8 +179,7 @@ hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double
   c.ctl_idx = adv != nullptr ? CTL_STEP_SNAP : CTL_STEP;
   AdvanceArgs a{};
   if (adv != nullptr) a = *adv;
-  hipLaunchKernelGGL(rmsprop_kernel, dim3(stream_blocks(n)), dim3(256), 0, s, p, ms, g, n, c, norm_partials,
-                     norm_blocks, clip, a);
+  hipLaunchKernelGGL(rmsprop_kernel, dim3(stream_blocks(n)), dim3(256), 0, s, p, ms, g, n, c, norm_sq, clip, a);
   return hipGetLastError();
 }
 
@@ -225,9 +223,40 @@ stream_copy_blocks_kernel(const cp_f32x4* __restrict__ src, cp_f32x4* __restrict
     dst[i] = src[i];
 }
 
+//   mode 2 / 3: a one-shot grid of bytes / 32 KB workgroups (the `blocks` argument is
+//           ignored), each copying its own contiguous 32 KB: 8 lane-linear 16-byte loads per
+//           lane in flight, then 8 stores; mode 3 with non-temporal loads / stores.
+template <bool NT>
+__global__ void __launch_bounds__(256)
+stream_copy_chunk_kernel(const cp_f32x4* __restrict__ src, cp_f32x4* __restrict__ dst, int64_t n4) {
+  constexpr int U = 8;
+  const int64_t base = (int64_t)blockIdx.x * (256 * U) + threadIdx.x;
+  cp_f32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (base + 256 * u < n4) v[u] = NT ? __builtin_nontemporal_load(src + base + 256 * u) : src[base + 256 * u];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (base + 256 * u < n4) {
+      if (NT) __builtin_nontemporal_store(v[u], dst + base + 256 * u);
+      else dst[base + 256 * u] = v[u];
+    }
+}
+
 hipError_t launch_stream_copy(const void* src, void* dst, int64_t bytes, int blocks, int mode, hipStream_t s) {
   const float4* a = reinterpret_cast<const float4*>(src);
   float4* b = reinterpret_cast<float4*>(dst);
+  if (mode >= 2) {
+    const int64_t grid = (bytes / 16 + 256 * 8 - 1) / (256 * 8);
+    if (grid > 0x7fffffff) return hipErrorInvalidValue;
+    if (mode == 3)
+      hipLaunchKernelGGL(stream_copy_chunk_kernel<true>, dim3((unsigned)grid), dim3(256), 0, s,
+                         reinterpret_cast<const cp_f32x4*>(src), reinterpret_cast<cp_f32x4*>(dst), bytes / 16);
+    else
+      hipLaunchKernelGGL(stream_copy_chunk_kernel<false>, dim3((unsigned)grid), dim3(256), 0, s,
+                         reinterpret_cast<const cp_f32x4*>(src), reinterpret_cast<cp_f32x4*>(dst), bytes / 16);
+    return hipGetLastError();
+  }
   if (mode == 1)
     hipLaunchKernelGGL(stream_copy_blocks_kernel, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const cp_f32x4*>(src),
                        reinterpret_cast<cp_f32x4*>(dst), bytes / 16);

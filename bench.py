@@ -116,6 +116,13 @@ def parse():
     ap.add_argument("--env-groups", type=int, default=0,
                     help="forward chains on separate streams per window (A3C.run_window env_groups); "
                          "0: the library default (2 from 1,024 envs per GPU up, else 1)")
+    ap.add_argument("--stamp-windows", type=int, default=100,
+                    help="after the median windows: this many eager windows with a HIP event after every stage "
+                         "launch (arl_stamps_*), whose intervals give each stage's in-window time and share; 0 "
+                         "disables (the per-stage table then falls back to standalone relaunches)")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="> 1 rank: torch.distributed timeout (s); a rank stuck in a collective raises and the "
+                         "launcher exits non-zero")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="0 disables the CPU baseline leg")
     ap.add_argument("--kernel-reps", type=int, default=50)
     return ap.parse_args()
@@ -137,6 +144,10 @@ def launch_ranks(n: int) -> int:
     and exits with the first failing child's status after stopping the rest
     (a rank left alone would wait in a collective forever)."""
     port = os.environ.get("MASTER_PORT") or str(_free_port())
+    # a whole-run deadline on top of the ranks' collective timeout: a rank that hangs outside a
+    # collective (e.g. in a kernel) would otherwise hold the run (and its peers) forever
+    deadline_s = float(os.environ.get("ARL_BENCH_DEADLINE_S", "1800"))
+    t_start = time.time()
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
@@ -148,6 +159,11 @@ def launch_ranks(n: int) -> int:
             bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
             if bad:
                 rc = bad[0]
+                break
+            if time.time() - t_start > deadline_s:
+                print(f"bench.py: ranks still running after {deadline_s:.0f} s (ARL_BENCH_DEADLINE_S); stopping them",
+                      file=sys.stderr)
+                rc = 124
                 break
             time.sleep(0.1)
     finally:
@@ -235,7 +251,8 @@ def measured_traffic(N, T, arch, kernel):
     return None
 
 
-def init_dist():
+def init_dist(timeout_s: float = 300.0):
+    from datetime import timedelta
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -255,27 +272,31 @@ def init_dist():
             os.environ.setdefault("MASTER_PORT", str(_free_port()))
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
+        # a timeout so a rank stuck in a collective raises (RCCL's watchdog aborts it) and exits non-zero
+        to = timedelta(seconds=timeout_s)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=to)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=to)
     return world, rank, local, (world > 1 or force)
 
 
 def measure_copy_peak(dev, mib: int = 1024, reps: int = 10):
-    """HBM stream-copy rate on this GPU (arl_stream_copy, both forms: grid-
-    stride with four 16-byte loads in flight per lane, and 64 KB blocks per
-    workgroup with non-temporal accesses): a 1 GiB buffer (4x the 256 MiB
-    Infinity Cache) copied `reps` times per form and grid size; the best
-    one's read + write bytes / time."""
+    """HBM stream-copy rate on this GPU (arl_stream_copy, every form: grid-
+    stride with four 16-byte loads in flight per lane, 64 KB blocks per
+    workgroup with non-temporal accesses, and a one-shot grid of 32 KB
+    workgroups with default-policy / non-temporal accesses): a 1 GiB buffer
+    (4x the 256 MiB Infinity Cache) copied `reps` times per form and grid
+    size; the best one's read + write bytes / time."""
     from asyncrl_amd._lib import check, lib, ptr
     n = mib << 20
     src = torch.ones(n // 4, dtype=torch.float32, device=dev)
     dst = torch.empty_like(src)
     s = torch.cuda.current_stream(dev)
     best, best_cfg, tried = 0.0, None, {}
-    for mode in (0, 1):
-        for blocks in (1024, 2048, 4096, 8192):
+    forms = {0: "gridstride", 1: "blocks64k_nt", 2: "chunk32k", 3: "chunk32k_nt"}
+    for mode in (0, 1, 2, 3):
+        for blocks in ((1024, 2048, 4096, 8192) if mode < 2 else (0,)):
             for _ in range(2):
                 check(lib.arl_stream_copy(ptr(src), ptr(dst), n, blocks, mode, s.cuda_stream), "arl_stream_copy")
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -285,14 +306,15 @@ def measure_copy_peak(dev, mib: int = 1024, reps: int = 10):
             ev1.record(s)
             ev1.synchronize()
             gbs = 2 * n * reps / (ev0.elapsed_time(ev1) * 1e-3) / 1e9
-            tried["%s/%d" % ("gridstride" if mode == 0 else "blocks64k_nt", blocks)] = round(gbs, 1)
+            tried["%s/%d" % (forms[mode], blocks)] = round(gbs, 1)
             if gbs > best:
                 best, best_cfg = gbs, (mode, blocks)
     ok = bool(torch.equal(src, dst))
     del src, dst
     torch.cuda.empty_cache()
     return {"GB/s": round(best, 1), "frac_of_spec": round(best / HBM_PEAK_GBS, 4), "bytes_per_copy": 2 * n,
-            "kernel": "stream_copy_kernel" if best_cfg[0] == 0 else "stream_copy_blocks_kernel (optim.hip)",
+            "kernel": {0: "stream_copy_kernel", 1: "stream_copy_blocks_kernel", 2: "stream_copy_chunk_kernel<false>",
+                       3: "stream_copy_chunk_kernel<true>"}[best_cfg[0]] + " (optim.hip)",
             "blocks": best_cfg[1], "tried_GBs": tried, "copy_verified": ok}
 
 
@@ -423,7 +445,7 @@ def main(a):
         mp_ctx = mp.get_context("forkserver")
         mp_ctx.set_forkserver_preload(["cpu_baseline"])
         forkserver.ensure_running()
-    world, rank, local, collectives = init_dist()
+    world, rank, local, collectives = init_dist(a.dist_timeout)
     if world != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE {world}")
     dev = torch.device("cuda", local)
@@ -554,16 +576,55 @@ def main(a):
                    "note": "HIP events per window on the bench stream; median = max over ranks of each rank's "
                            "median, p10 / p90 rank 0's"}
     finite = bool(torch.isfinite(model.net.params).all())
+    replicas = None
+    if collectives:   # every rank applied the same update to the same reduced gradient (distributed.py)
+        from asyncrl_amd.distributed import replicas_identical
+        replicas = bool(replicas_identical(model.net.params) and replicas_identical(model.net.ms))
+
+    # ---------------------------------------------------------------- window timeline
+    # More eager windows with a HIP event recorded after every stage launch
+    # (arl_stamps_*; A3C adds one after each collective): consecutive
+    # intervals split a window into its stages as it ran, launch boundaries
+    # included, so the per-stage shares add up to the window.  Every rank runs
+    # them (the collectives need all ranks); rank 0 reports its own.
+    timeline = None
+    net = model.net
+    if a.stamp_windows > 0 and not use_graph and n_groups == 1 and not nat:
+        from asyncrl_amd._lib import STAGE_NAMES
+        M = a.stamp_windows
+        net.stamps_begin(M * 64 + 8)
+        with torch.cuda.stream(stream):
+            net.stamp(16, stream=stream)           # the mark the first interval starts from (ARL_STAGE_OTHER)
+            for _ in range(M):
+                window()
+        stream.synchronize()
+        ms_st, st_names = net.stamps_end()
+        per = {}
+        for x, name in zip(ms_st[1:], st_names[1:]):
+            name = "allreduce_wait" if name == STAGE_NAMES[15] else name
+            d = per.setdefault(name, [0.0, 0])
+            d[0] += float(x)
+            d[1] += 1
+        total_ms = float(ms_st[1:].sum())
+        timeline = {"windows": M, "stamps_per_window": (len(ms_st) - 1) / M, "mean_window_ms": round(total_ms / M, 4),
+                    "stages": {k: {"window_share_us": round(1e3 * v[0] / M, 2),
+                                   "launches_per_window": round(v[1] / M, 3),
+                                   "us_per_launch": round(1e3 * v[0] / v[1], 3)} for k, v in per.items()},
+                    "note": "stamped eager windows: interval from the previous stage's event to this stage's, "
+                            "so each launch's share includes its dependent-launch boundary; allreduce_wait = the "
+                            "compute stream's wait for the collectives (A3C._reduce_and_step)"}
+        if windows is not None:
+            timeline["unstamped_median_ms"] = windows["median_ms"]
+            timeline["sum_vs_unstamped_median"] = round(total_ms / M / windows["median_ms"], 4)
 
     # ---------------------------------------------------------------- per-kernel roofline
-    # Every stage of the window is re-launched alone on the same stream and
-    # workspace, kernel-reps times back to back between two HIP events (on
-    # that stream) -> average launch duration.  Algorithmic work per launch
-    # (SURVEY 8(d)); the dominant stage (us x launches per window)
-    # is the "roofline" kernel, the rest are listed under "kernels".
+    # Each stage's algorithmic work per launch over its
+    # in-window time per launch (the timeline above); every stage is also
+    # re-launched alone kernel-reps times back to back between two HIP events
+    # on the bench stream ("standalone_us", beside it).  The stage with the
+    # largest in-window share is the "roofline" kernel.
     roof, kernels = None, None
     if rank == 0:
-        net = model.net
         S = N * T
 
         def timed(fn):
@@ -578,14 +639,15 @@ def main(a):
             return 1e3 * ev0.elapsed_time(ev1) / a.kernel_reps
 
         fused = net.fused_observe   # steps 1..T: phi inside the conv launch; step 0 (window start) conv only
-        specs = [  # name, kernel, launch fn, launches per window, bound, algorithmic work per launch
+        specs = [  # name, kernel, launch fn, nominal launches per window, bound, algorithmic work per launch
             # phi + conv fused (conv_fwd_kernel<true>): reads the frame pair and the 3 older ring planes,
             # writes the new plane, a1 and a2
             ("phi_conv", "conv_fwd_kernel<true> (phi + conv1 + conv2)",
              lambda i: net.observe_act(1 + i % T, pairs, rewards, dones, P, mode=ACT_CONV_ONLY, stream=stream),
              T, "hbm", N * (phi_bytes + 3 * PLANE_BYTES + 4 * (A1_FLOATS + A2_FLOATS))) if fused else None,
+            # a window observes steps 1..T (step 0 of a window is the previous window's bootstrap observation)
             ("phi", "rgb_ring_kernel" if doom else "phi_ring_kernel",
-             lambda i: net.observe(1 + i % T, pairs, rewards, dones, P, stream=stream), 0 if fused else T + 1, "hbm",
+             lambda i: net.observe(1 + i % T, pairs, rewards, dones, P, stream=stream), 0 if fused else T, "hbm",
              N * phi_bytes),
             ("conv_fwd", "gemm_kernel x3 (implicit-GEMM convs)" if nat else
              f"conv_fwd_kernel<false, {conv_epw(N)}>",
@@ -616,7 +678,10 @@ def main(a):
              "fc_bwd_kernel<ShapeLSTM> (gate dW / db + dfc, straight into the gradient)",
              lambda i: net.run_stage("lstm_wgrad", stream=stream), 1, "mfma",
              S * LSTM_WGRAD_FLOP_PER_SAMPLE) if lstm and not doom else None,
-            ("rmsprop", "rmsprop_kernel", lambda i: net.optimize(lr0=1e-12, clip=0.0, stream=stream), 1, "hbm",
+            # the update kernel as the window runs it: clip 40 from the norm the learner left (lr 0 alone)
+            ("rmsprop", "rmsprop_kernel (clip + RMSProp + window advance)",
+             (lambda i: net.run_stage("rmsprop", stream=stream)) if not nat else
+             (lambda i: net.optimize(lr0=0.0, clip=0.0, stream=stream)), 1, "hbm",
              net.n_params * RMSPROP_BYTES_PER_PARAM),
             # the learner's small HBM-bound launches (NIPS heads): returns + loss gradient + heads dh,
             # the conv backward's slab reduce, the gradient's squared norm (GradientClipping)
@@ -633,32 +698,52 @@ def main(a):
             ("grad_sqnorm", "grad_sqnorm_kernel", lambda i: net.run_stage("grad_sqnorm", stream=stream),
              0 if (not collectives and NORM_FOLD) else 1, "hbm", net.n_params * 4),
         ]
+        tl = timeline["stages"] if timeline is not None else {}
         kernels = {}
         with torch.cuda.stream(stream):
             for name, kname, fn, calls, bound, work in filter(None, specs):
-                us = timed(fn)
-                if bound == "hbm":
-                    ach, peak, unit = work / (us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s"
-                else:
-                    ach, peak, unit = work / (us * 1e-6) / 1e12, F32_MFMA_PEAK_TFS, "TFLOP/s"
+                us_alone = timed(fn)
+                tname = "conv_fwd" if name == "phi_conv" else name
+                win = tl.get(tname)
+                us = win["us_per_launch"] if win is not None else us_alone
+
+                def rate(t_us):
+                    if bound == "hbm":
+                        return work / (t_us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s"
+                    return work / (t_us * 1e-6) / 1e12, F32_MFMA_PEAK_TFS, "TFLOP/s"
+                ach, peak, unit = rate(us)
+                ach1 = rate(us_alone)[0]
                 kernels[name] = {"kernel": kname, "bound": bound, "avg_launch_us": round(us, 2),
-                                 "launches_per_window": calls, "window_share_us": round(us * calls, 1),
+                                 "time_source": "window" if win is not None else "standalone",
+                                 "launches_per_window": win["launches_per_window"] if win is not None else calls,
+                                 "window_share_us": win["window_share_us"] if win is not None else round(us * calls, 1),
                                  "achieved": round(ach, 2), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
-                                 ("bytes" if bound == "hbm" else "flop") + "_per_launch": int(work)}
+                                 ("bytes" if bound == "hbm" else "flop") + "_per_launch": int(work),
+                                 "standalone_us": round(us_alone, 2), "standalone_frac": round(ach1 / peak, 4)}
                 if name == "phi_conv":   # its MFMA side: the conv layers' FLOPs at the same launch time
                     tf = N * conv_fwd_flop / (us * 1e-6) / 1e12
                     kernels[name]["mfma"] = {"flop_per_launch": int(N * conv_fwd_flop), "achieved": round(tf, 2),
                                              "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                                              "frac": round(tf / F32_MFMA_PEAK_TFS, 4)}
-        dom = max(kernels, key=lambda k: kernels[k]["window_share_us"])
+        for tname, win in tl.items():   # timeline stages without a standalone form (LSTM cells, collectives)
+            if tname not in kernels and not (tname == "conv_fwd" and "phi_conv" in kernels):
+                kernels[tname] = {"kernel": tname, "bound": None, "time_source": "window",
+                                  "avg_launch_us": win["us_per_launch"],
+                                  "launches_per_window": win["launches_per_window"],
+                                  "window_share_us": win["window_share_us"]}
+        dom = max((k for k in kernels if kernels[k]["bound"] is not None), key=lambda k: kernels[k]["window_share_us"])
         d = kernels[dom]
         traffic = measured_traffic(N, T, arch, d["kernel"].split(" (")[0])
         roof = {"bound": d["bound"], "kernel": d["kernel"], "achieved": d["achieved"], "peak": d["peak"],
                 "unit": d["unit"], "frac": d["frac"], "traffic": traffic, "avg_launch_us": d["avg_launch_us"],
+                "time_source": d["time_source"], "standalone_us": d["standalone_us"],
+                "standalone_frac": d["standalone_frac"],
                 "work_per_launch": d.get("flop_per_launch", d.get("bytes_per_launch")),
                 "peak_note": (("exact f32 MFMA (v_mfma_f32_16x16x4_f32) vs the dense fp32 matrix peak" if nat else
                                "f32-equivalent FLOP/s vs the dense fp32 matrix peak (bf16-split f32 emulation, "
-                               "DESIGN.md)") if d["bound"] == "mfma" else "HBM3E spec peak")}
+                               "DESIGN.md)") if d["bound"] == "mfma" else "HBM3E spec peak") +
+                             ("; time = the in-window interval per launch (window timeline), launch boundary "
+                              "included" if d["time_source"] == "window" else "")}
         if copy_peak is not None:
             # HBM-bound stages also against the copy rate measured on this GPU
             for k in kernels.values():
@@ -711,7 +796,8 @@ def main(a):
             "ranks_seen": seen, "collectives": (("rccl" if dist.get_backend() == "nccl" else dist.get_backend())
                                                 if collectives else None),
             "allreduce_bytes_per_window": (4 * model.net.grads.numel()) if collectives else 0,
-            "windows": windows, "hbm_copy_peak": copy_peak,
+            "replicas_identical": replicas,
+            "windows": windows, "timeline": timeline, "hbm_copy_peak": copy_peak,
             "roofline": roof, "kernels": kernels, "cpu_baseline": cpu, "params_finite": finite,
         }
         print(json.dumps(out), flush=True)

@@ -237,7 +237,8 @@ int arl_optimize(arl_net* net, double lr0, int64_t total_steps, int64_t n_total,
 
 /* One stage of a window, run alone on the current workspace contents (the
  * same launches arl_act / arl_learn make), for per-kernel timing and
- * profiling.  t selects the window step for the forward stages. */
+ * profiling.  t selects the window step for the forward stages.  Stages 1-11
+ * and ARL_STAGE_RMSPROP. */
 enum {
   ARL_STAGE_CONV_FWD = 1,   /* fused conv1 + conv2 forward from the frame ring */
   ARL_STAGE_FC_FWD = 2,     /* Linear(2592, 256): FF nets write the 8 split-K partials only; LSTM
@@ -252,9 +253,30 @@ enum {
   ARL_STAGE_GRAD_SQNORM = 8,  /* squared-norm partials of the whole gradient (GradientClipping) */
   ARL_STAGE_LSTM_GATES = 9,   /* LSTM: the gate kernel of slot t (cell in its epilogue) */
   ARL_STAGE_LSTM_BPTT = 10,   /* LSTM: one truncated-BPTT step (dh GEMM + the previous step's cell backward) */
-  ARL_STAGE_LSTM_WGRAD = 11   /* LSTM: the gate weight gradients + dfc (one dual-GEMM launch) */
+  ARL_STAGE_LSTM_WGRAD = 11,  /* LSTM: the gate weight gradients + dfc (one dual-GEMM launch) */
+  /* timeline-only stages (arl_stamps_*, not arl_run_stage) */
+  ARL_STAGE_PHI = 12,         /* the observation (phi into the frame ring) */
+  ARL_STAGE_RMSPROP = 13,     /* clip + RMSProp (+ the window advance); arl_run_stage: the update
+                                 kernel alone, lr 0, clip 40 at the norm the last window left */
+  ARL_STAGE_LSTM_CELL = 14,   /* a separate LSTM cell launch */
+  ARL_STAGE_HOST = 15,        /* a caller's stamp (arl_stamp), e.g. after a collective */
+  ARL_STAGE_OTHER = 16
 };
 int arl_run_stage(arl_net* net, int stage, int t, void* stream);
+
+/* Window timeline (measurement; no reference counterpart).  After
+ * arl_stamps_begin(net, cap) every stage launch of the window (arl_observe*,
+ * arl_act*, arl_learn*, arl_optimize*) records a timing event on its stream
+ * right after its kernel(s), with the stage it closes (ARL_STAGE_*), up to cap
+ * events; arl_stamp records one for the caller.  arl_stamps_end stops and
+ * returns the count.  arl_stamps_read waits for stamp i0 + n - 1 and returns,
+ * for i in [i0, i0 + n), ms[i - i0] = the time from stamp i - 1 to stamp i (0
+ * for i = 0) and stage[i - i0]: consecutive intervals split an eager window
+ * into its stages as it ran, launch boundaries included. */
+int arl_stamps_begin(arl_net* net, int cap);
+int arl_stamp(arl_net* net, int stage, void* stream);
+int arl_stamps_end(arl_net* net, int* count);
+int arl_stamps_read(arl_net* net, int i0, int n, float* ms, int* stage);
 
 /* End of window: advance step counters, carry reset flags / LSTM state. */
 int arl_advance(arl_net* net, void* stream);
@@ -284,7 +306,8 @@ int arl_reset_state(arl_net* net, int64_t e0, int64_t n, void* stream);
 
 /* RMSpropAsync.update_one (rmsprop_async.py:23-38) on flat f32 arrays, with
  * optional Chainer GradientClipping (norm over g, scale if clip/norm < 1).
- * norm_partials: device f64[1024] scratch (needed when clip > 0). */
+ * norm_partials: device f64[1024] scratch (needed when clip > 0): the norm
+ * pass's partials, its result ([1000]) and its arrival ticket ([1001]). */
 int arl_rmsprop(float* param, float* ms, const float* grad, int64_t n, double lr, double alpha, double eps,
                 double clip, double* norm_partials, void* stream);
 
@@ -315,7 +338,9 @@ int arl_returns_lossgrad(const float* rewards, const uint8_t* dones, const float
  * buffers) by a grid of `blocks` 256-thread workgroups, 16-byte loads: the HBM
  * stream-copy peak the bench reports beside the 8 TB/s spec (SURVEY 8(d);
  * no reference counterpart).  mode 0: grid-stride, 4 loads in flight per lane;
- * mode 1: 64 KB blocks per workgroup, 16 non-temporal loads in flight per lane. */
+ * mode 1: 64 KB blocks per workgroup, 16 non-temporal loads in flight per lane;
+ * mode 2 / 3: a one-shot grid of bytes / 32 KB workgroups (`blocks` ignored), 8
+ * lane-linear loads in flight per lane (3: non-temporal). */
 int arl_stream_copy(const void* src, void* dst, int64_t bytes, int blocks, int mode, void* stream);
 
 #ifdef __cplusplus

@@ -2,6 +2,7 @@
 RCCL needs one GPU per rank), env-sharded A3C over 2 windows.  Rank 0 also
 runs the single-process learner over the union of envs for comparison."""
 import json
+from datetime import timedelta
 import os
 import sys
 
@@ -27,7 +28,7 @@ def agent(n, off, group):
 
 def main():
     out = sys.argv[1]
-    dist.init_process_group("gloo")
+    dist.init_process_group("gloo", timeout=timedelta(seconds=240))
     rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
     dev = torch.device("cuda:0")

@@ -48,6 +48,7 @@ def test_bench_starts_its_ranks(gpu):
     assert d["config"]["global_envs"] == 2 * d["config"]["envs_per_gpu"]
     assert d["allreduce_bytes_per_window"] >= 4 * 677429
     assert d["params_finite"] and d["windows"]["n"] == 20
+    assert d["replicas_identical"] is True                                          # after the timed windows
     assert len([ln for ln in r.stdout.splitlines() if ln.startswith("{")]) == 1     # rank 0 only
 
 
@@ -58,6 +59,28 @@ def test_bench_rccl_one_rank(gpu):
     d = _last_json(r.stdout)
     assert d["n_gpus"] == 1 and d["ranks_seen"] == 1 and d["collectives"] == "rccl", d
     assert d["params_finite"]
+
+
+def test_bench_window_timeline(gpu):
+    """The per-stage table is the window's own: stamped eager windows give
+    each stage's launches per window (phi T = 5, the forward stages T + 1, the
+    learner's launches once) and the stage shares add up to the window."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "1"] + SMALL + ["--stamp-windows", "30"], capture_output=True,
+                       text=True, timeout=300, env=_env())
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    tl = d["timeline"]
+    want = {"phi": 5, "conv_fwd": 6, "fc_fwd": 6, "policy": 6, "returns": 1, "fc_bwd": 1, "conv_bwd": 1,
+            "conv_reduce": 1, "rmsprop": 1}
+    assert {k: v["launches_per_window"] for k, v in tl["stages"].items()} == want, tl
+    share = sum(v["window_share_us"] for v in tl["stages"].values())
+    assert abs(share / 1e3 - tl["mean_window_ms"]) <= 0.01 * tl["mean_window_ms"], tl
+    assert 0.9 <= tl["sum_vs_unstamped_median"] <= 1.15, tl
+    for k, v in d["kernels"].items():
+        assert v["time_source"] == "window", (k, v)
+        if v.get("bound") == "hbm":
+            assert v["frac"] <= 1.0 and v.get("frac_measured_peak", 0) <= 1.0, (k, v)
+    assert d["roofline"]["time_source"] == "window"
 
 
 def test_bench_gpus_mismatch_fails(gpu):

@@ -21,50 +21,15 @@ import torch
 
 import oracle as O
 from conftest import close_normscaled, grads_match
-from sim import OracleEnvView, make_pools
+from sim import OracleEnvView, make_pools, oracle_window_chunks as _oracle_window
 
 pytestmark = pytest.mark.gpu
 
 RTOL = 1e-5
-CHUNK = 128
 
 
 def dev(x, gpu):
     return torch.from_numpy(np.ascontiguousarray(x)).to(gpu)
-
-
-def _sum_into(acc, g):
-    for k, v in g.items():
-        acc[k] = acc.get(k, 0.0) + v.astype(np.float64)
-
-
-def _oracle_window(arch, params, states, acts, r, d, boot, st=None, dprev=None, acts_dev=None):
-    """O.ff_window_grads / O.lstm_window over env chunks; gradients summed
-    in f64, per-env outputs concatenated."""
-    T, N = acts.shape
-    g, aux, mag = {}, {}, {}
-    for e0 in range(0, N, CHUNK):
-        sl = slice(e0, min(N, e0 + CHUNK))
-        da = tuple(a[:, sl].reshape((-1,) + a.shape[2:]) for a in acts_dev)
-        if arch == O.ARCH_LSTM:
-            s0 = O.LSTMState(h=st.h[sl], c=st.c[sl], has=st.has[sl])
-            gc, ac = O.lstm_window(params, states[:, sl], acts[:, sl], r[:, sl], dprev[:, sl], d[:, sl], boot[sl], s0,
-                                   dev_acts=da)
-        else:
-            gc, ac = O.ff_window_grads(params, states[:, sl], acts[:, sl], r[:, sl], d[:, sl], boot[sl],
-                                       dev_acts=da)
-        _sum_into(g, gc)
-        for k, m in ac["grad_mag"].items():
-            mag[k] = mag.get(k, 0.0) + m.astype(np.float64) ** 2
-        for k in ("logits", "v", "dlogits", "dv"):
-            aux.setdefault(k, []).append(ac[k])
-        aux.setdefault("vboot", []).append(ac["vboot"])
-        if arch == O.ARCH_LSTM:
-            for k in ("h_last", "c_last"):
-                aux.setdefault(k, []).append(ac[k])
-    out = {k: np.concatenate(v, axis=0 if k in ("vboot", "h_last", "c_last") else 1) for k, v in aux.items()}
-    out["grad_mag"] = {k: np.sqrt(v) for k, v in mag.items()}
-    return {k: v.astype(np.float32) for k, v in g.items()}, out
 
 
 def _run_config(gpu, arch, N, A, windows=2, seed=0, kind="uniform", env_groups=None):
