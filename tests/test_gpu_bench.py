@@ -77,8 +77,8 @@ def test_bench_window_timeline(gpu):
     assert abs(share / 1e3 - tl["mean_window_ms"]) <= 0.01 * tl["mean_window_ms"], tl
     assert 0.9 <= tl["sum_vs_unstamped_median"] <= 1.15, tl
     for k, v in d["kernels"].items():
-        assert v["time_source"] == "window", (k, v)
-        if v.get("bound") == "hbm":
+        assert v["time_source"] == "window" or k not in want, (k, v)
+        if v.get("bound") == "hbm" and k in want:
             assert v["frac"] <= 1.0 and v.get("frac_measured_peak", 0) <= 1.0, (k, v)
     assert d["roofline"]["time_source"] == "window"
 
