@@ -2,7 +2,8 @@
 env group and saves a1, a2, the actions, the window-1 gradient and the
 parameters to an .npz (argv[1]).  test_gpu_parity.test_conv_fwd_two_envs_identical
 runs it under ARL_CONV_EPW=1 / 2 (conv_fwd.hip: one or two envs a workgroup,
-read once per process), ARL_FC_BIG and ARL_FC_HEADS and compares the files bitwise."""
+read once per process), ARL_FC_BIG, ARL_FC_HEADS and ARL_PHI_DMA (phi_ring_kernel's
+LDS-DMA staging) and compares the files bitwise."""
 import os
 import sys
 
@@ -39,6 +40,7 @@ def main(out, N):
     net = ag.net
     np.savez(out, grads1=g1, params=net.params.detach().cpu().numpy(),
              a1=net.buffer("a1", torch.float32).cpu().numpy(), a2=net.buffer("a2", torch.float32).cpu().numpy(),
+             frames=net.buffer("frames").cpu().numpy(),
              actions=net.buffer("actions", torch.int32, (T + 1, N)).cpu().numpy(),
              **{k: net.buffer(k, torch.float32).cpu().numpy() for k in ("hfc", "logits", "probs", "logp", "v",
                                                                        "entropy", "logp_a")})

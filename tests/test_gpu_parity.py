@@ -828,14 +828,16 @@ def test_conv_fwd_two_envs_identical(gpu, tmp_path, n_envs):
     a1, a2, hfc, the policy outputs and actions, the window gradient and the
     updated parameters match bit for bit -- at an odd env count (the last conv
     workgroup's second slot idle, a partial FC tile; too few envs for the fused
-    heads, which fall back), at 200 (a partial 64-row block) and at 512."""
+    heads, which fall back), at 200 (a partial 64-row block) and at 512.  The
+    frame ring too, against phi_ring_kernel's LDS-DMA staging (ARL_PHI_DMA)."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     outs = []
     for i, arm in enumerate(({"ARL_CONV_EPW": "1", "ARL_FC_BIG": "0"}, {"ARL_CONV_EPW": "2", "ARL_FC_BIG": "0"},
                              {"ARL_CONV_EPW": "1", "ARL_FC_BIG": "1", "ARL_FC_HEADS": "0"},
-                             {"ARL_CONV_EPW": "1", "ARL_FC_BIG": "1", "ARL_FC_HEADS": "1"})):
+                             {"ARL_CONV_EPW": "1", "ARL_FC_BIG": "1", "ARL_FC_HEADS": "1"},
+                             {"ARL_PHI_DMA": "1"})):
         f = str(tmp_path / f"arm_{i}.npz")
         env = dict(os.environ, **arm)
         subprocess.run([sys.executable, os.path.join(here, "conv_epw_worker.py"), f, str(n_envs)], env=env,
