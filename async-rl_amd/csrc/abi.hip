@@ -349,7 +349,7 @@ int arl_run_stage(arl_net* h, int stage, int t, void* s) {
     return fail(ARL_EINVAL, "run_stage: unknown stage");
   if (stage >= ARL_STAGE_RETURNS && h->net.arch == arl::ARCH_FF_NATURE)
     return fail(ARL_EINVAL, "run_stage: returns / conv reduce / grad sqnorm stages are NIPS-head only");
-  if (stage >= ARL_STAGE_LSTM_GATES && h->net.arch != arl::ARCH_LSTM)
+  if (stage >= ARL_STAGE_LSTM_GATES && stage <= ARL_STAGE_LSTM_WGRAD && h->net.arch != arl::ARCH_LSTM)
     return fail(ARL_EINVAL, "run_stage: the LSTM stages need an LSTM net");
   if (t < 0 || t > h->net.T) return fail(ARL_EINVAL, "run_stage: t out of [0, t_max]");
   return hip_status(arl::net_stage(h->net, stage, t, S(s)), "run_stage");

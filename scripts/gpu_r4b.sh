@@ -1,0 +1,25 @@
+#!/bin/bash
+# round 4: bench tests, the default bench line + conv_fwd stamps + rocprof stats, then A/Bs
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${TAG:-r4b}; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:--k bench} > $O/pytest.log 2>&1; rc=$?
+echo "pytest rc=$rc" > $O/status
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 400 python bench.py > $O/bench.log 2>&1 || exit $?
+echo "bench ok" >> $O/status
+if [ -f async-rl_amd/csrc/build_var_cfstamp/libasyncrl_hip.so ]; then
+  for n in 512 256; do
+    ASYNCRL_HIP_LIB=$PWD/async-rl_amd/csrc/build_var_cfstamp/libasyncrl_hip.so timeout -k 10 200 python scripts/cf_stamps.py $n > $O/cfstamps$n.txt 2>&1 || exit $?
+  done
+fi
+(cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/prof" -o c4 -- python3 "$GRAFT_REPO_ROOT/bench.py" --cpu-seconds 0 --copy-peak 0 > "$GRAFT_REPO_ROOT/$O/bench_prof.log" 2>&1) || exit $?
+echo "prof ok" >> $O/status
+for ab in $AB; do
+  case $ab in
+    phidma) bash scripts/env_ab.sh ARL_PHI_DMA=0 ARL_PHI_DMA=1 "" 2 phidma || exit $? ;;
+    c3streams) bash scripts/env_ab.sh ARL_GROUP_STREAMS=0 ARL_GROUP_STREAMS=1 "--workload c3" 2 c3streams || exit $? ;;
+  esac
+  echo "ab $ab ok" >> $O/status
+done
