@@ -11,7 +11,7 @@ for r in $(seq 1 ${2:-1}); do
     name=$(basename $(dirname $lib))
     ASYNCRL_HIP_LIB=$PWD/$lib timeout -k 10 200 python -u bench.py $ARGS --cpu-seconds 0 > gpurun_out/var/$name.log 2>&1
     rc=$?; [ $rc -ne 0 ] && { tail -n 5 gpurun_out/var/$name.log; exit $rc; }
-    python -c "import json; d=json.loads(open('gpurun_out/var/$name.log').read().strip().splitlines()[-1]); print('$name', d['ms_per_step'], {k: v['avg_launch_us'] for k, v in d['kernels'].items()})"
+    python -c "import json; d=json.loads(open('gpurun_out/var/$name.log').read().strip().splitlines()[-1]); print('$name', d['ms_per_step'], d['windows']['median_ms'], {k: (v['avg_launch_us'], v.get('standalone_us')) for k, v in d['kernels'].items()})"
   done
 done
 exit 0
