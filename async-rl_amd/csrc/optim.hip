@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "arl_internal.hpp"
 
 namespace arl {
@@ -76,6 +78,10 @@ __device__ inline void rms1(float& p, float& ms, float g, const RmsConst& c) {
   p = __fsub_rn(p, __fdiv_rn(__fmul_rn(c.lr, g), sqrtf(__fadd_rn(ms, c.eps))));  // p -= lr*g/sqrt(ms+eps)
 }
 
+// U float4 of p / ms / g per thread and pass, every load of a pass issued before the arithmetic
+// (U = 1: the grid covers the buffer in one pass; ARL_RMS_U=2: half the workgroups, two float4 a
+// thread in flight together -- A/B knob)
+template <int U>
 __global__ void __launch_bounds__(256)
 rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __restrict__ g, int64_t n, RmsConst c,
                const double* __restrict__ norm_sq, float clip, AdvanceArgs adv) {
@@ -89,14 +95,16 @@ rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __res
   float4* p4 = reinterpret_cast<float4*>(p);
   float4* m4 = reinterpret_cast<float4*>(ms);
   const float4* g4 = reinterpret_cast<const float4*>(g);
+  const int64_t gsz = (int64_t)gridDim.x * blockDim.x;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  // the first float4 of p / ms / g is in flight with the squared norm's load
-  // (the grid normally covers the buffer in one pass)
-  float4 pv, mv, gv;
-  if (i0 < n4) {
-    pv = p4[i0];
-    mv = m4[i0];
-    gv = g4[i0];
+  // the first pass's float4 of p / ms / g are in flight with the squared norm's load
+  float4 pv[U], mv[U], gv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = min(i0 + u * gsz, n4 - 1);   // (clamped: a duplicate, not stored)
+    pv[u] = p4[i];
+    mv[u] = m4[i];
+    gv[u] = g4[i];
   }
   float scale = 1.f;
   bool do_clip = false;
@@ -108,41 +116,49 @@ rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __res
       scale = (float)rate;
     }
   }
-  for (int64_t i = i0; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    if (i != i0) {
-      pv = p4[i];
-      mv = m4[i];
-      gv = g4[i];
+  for (int64_t ib = i0; ib < n4; ib += U * gsz) {
+    if (ib != i0) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = min(ib + u * gsz, n4 - 1);
+        pv[u] = p4[i];
+        mv[u] = m4[i];
+        gv[u] = g4[i];
+      }
     }
-    if (do_clip) {
-      gv.x = __fmul_rn(gv.x, scale); gv.y = __fmul_rn(gv.y, scale);
-      gv.z = __fmul_rn(gv.z, scale); gv.w = __fmul_rn(gv.w, scale);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (do_clip) {
+        gv[u].x = __fmul_rn(gv[u].x, scale); gv[u].y = __fmul_rn(gv[u].y, scale);
+        gv[u].z = __fmul_rn(gv[u].z, scale); gv[u].w = __fmul_rn(gv[u].w, scale);
+      }
+      rms1(pv[u].x, mv[u].x, gv[u].x, c);
+      rms1(pv[u].y, mv[u].y, gv[u].y, c);
+      rms1(pv[u].z, mv[u].z, gv[u].z, c);
+      rms1(pv[u].w, mv[u].w, gv[u].w, c);
+      if (ib + u * gsz < n4) {
+        p4[ib + u * gsz] = pv[u];
+        m4[ib + u * gsz] = mv[u];
+      }
     }
-    rms1(pv.x, mv.x, gv.x, c);
-    rms1(pv.y, mv.y, gv.y, c);
-    rms1(pv.z, mv.z, gv.z, c);
-    rms1(pv.w, mv.w, gv.w, c);
-    p4[i] = pv;
-    m4[i] = mv;
   }
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
     const int64_t j = (n4 << 2) + threadIdx.x;
-    float gv = g[j];
-    if (do_clip) gv = __fmul_rn(gv, scale);
-    float pv = p[j], mv = ms[j];
-    rms1(pv, mv, gv, c);
-    p[j] = pv;
-    ms[j] = mv;
+    float gt = g[j];
+    if (do_clip) gt = __fmul_rn(gt, scale);
+    float pt = p[j], mt = ms[j];
+    rms1(pt, mt, gt, c);
+    p[j] = pt;
+    ms[j] = mt;
   }
   if (adv.ctl == nullptr) return;
-  const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, gsz = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = gtid; i < adv.n; i += gsz) adv.reset[i] = adv.reset[(int64_t)adv.T * adv.n + i];
+  for (int64_t i = i0; i < adv.n; i += gsz) adv.reset[i] = adv.reset[(int64_t)adv.T * adv.n + i];
   if (adv.hbuf != nullptr)
-    for (int64_t i = gtid; i < (int64_t)adv.n * HID; i += gsz) {
+    for (int64_t i = i0; i < (int64_t)adv.n * HID; i += gsz) {
       adv.hbuf[i] = adv.hbuf[(int64_t)adv.T * adv.n * HID + i];
       adv.cbuf[i] = adv.cbuf[(int64_t)adv.T * adv.n * HID + i];
     }
-  if (gtid == 0) {
+  if (i0 == 0) {
     adv.ctl[CTL_STEP] += adv.T;
     adv.ctl[CTL_WINDOW] += 1;
   }
@@ -179,7 +195,15 @@ hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double
   c.ctl_idx = adv != nullptr ? CTL_STEP_SNAP : CTL_STEP;
   AdvanceArgs a{};
   if (adv != nullptr) a = *adv;
-  hipLaunchKernelGGL(rmsprop_kernel, dim3(stream_blocks(n)), dim3(256), 0, s, p, ms, g, n, c, norm_sq, clip, a);
+  static const bool u2 = [] {
+    const char* e = getenv("ARL_RMS_U");
+    return e != nullptr && e[0] == '2';
+  }();
+  if (u2)
+    hipLaunchKernelGGL(rmsprop_kernel<2>, dim3((stream_blocks(n) + 1) / 2), dim3(256), 0, s, p, ms, g, n, c, norm_sq,
+                       clip, a);
+  else
+    hipLaunchKernelGGL(rmsprop_kernel<1>, dim3(stream_blocks(n)), dim3(256), 0, s, p, ms, g, n, c, norm_sq, clip, a);
   return hipGetLastError();
 }
 
