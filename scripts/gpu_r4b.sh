@@ -21,6 +21,7 @@ for ab in $AB; do
     phidma) bash scripts/env_ab.sh ARL_PHI_DMA=0 ARL_PHI_DMA=1 "" 2 phidma || exit $? ;;
     c3streams) bash scripts/env_ab.sh ARL_GROUP_STREAMS=0 ARL_GROUP_STREAMS=1 "--workload c3" 2 c3streams || exit $? ;;
     variants) bash scripts/gpu_variants.sh "--steps 30 --warmup 5 --kernel-reps 3 --copy-peak 0" 1 > $O/variants.txt 2>&1 || exit $? ;;
+    rmsu) bash scripts/env_ab.sh ARL_RMS_U=1 ARL_RMS_U=2 "" 2 rmsu || exit $? ;;
     fcbz) for z in 2 4 5; do bash scripts/env_ab.sh ARL_FC_BWD_Z=3 ARL_FC_BWD_Z=$z "" 1 fcbz$z || exit $?; done ;;
   esac
   echo "ab $ab ok" >> $O/status
