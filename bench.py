@@ -123,6 +123,10 @@ def parse():
     ap.add_argument("--dist-timeout", type=float, default=300.0,
                     help="> 1 rank: torch.distributed timeout (s); a rank stuck in a collective raises and the "
                          "launcher exits non-zero")
+    ap.add_argument("--secondary", default="auto",
+                    help="comma-separated BASELINE workloads (c2, c3) also measured on one GPU after the headline, "
+                         "with the same protocol (W warmup, K timed windows, median over 100), reported under "
+                         "'secondary'; auto: c3 beside the default c4 line at N = 1; none disables")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="0 disables the CPU baseline leg")
     ap.add_argument("--kernel-reps", type=int, default=50)
     return ap.parse_args()
@@ -431,6 +435,73 @@ def bench_phi(a, world, rank, dev, n_default, copy_peak=None):
         print(json.dumps(out))
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def secondary_line(a, pkg, dev, workload):
+    """One more BASELINE workload on this GPU (N = 1), measured as the headline
+    is: W warmup windows, K timed windows between two synchronizes (wall
+    clock), then 100 windows between HIP events for the median.  The window is
+    the library default's: env-group chains as one graph replay from 1,024
+    envs (C3), eager launches for one chain."""
+    w_arch, N, A = WORKLOADS[workload]
+    T, P = a.t_max, a.pool
+    Model = pkg.A3CLSTM if w_arch == "lstm" else pkg.A3CFF
+    model = Model(A, n_envs=N, t_max=T, seed=1234, init_seed=0, device=dev, frames="pairs")
+    opt = pkg.RMSpropAsync(lr=7e-4, eps=1e-1, alpha=0.99).setup(model)
+    opt.add_hook(pkg.GradientClipping(40))
+    opt.anneal_total_steps, opt.n_total_envs = 8 * 10 ** 7, N
+    agent = pkg.A3C(model, opt, T, 0.99, beta=1e-2, collectives=False)
+    pairs, rewards, dones = synth_pools(N, P, 0, dev)
+    groups = len(model.net.env_groups(model.net.default_env_groups()))
+    stream = torch.cuda.Stream(device=dev)
+    stream.wait_stream(torch.cuda.current_stream())
+    graph = None
+    with torch.cuda.stream(stream):
+        agent.run_window(pairs, rewards, dones, P, first=True, stream=stream)
+        for _ in range(max(0, a.warmup - 1)):
+            agent.run_window(pairs, rewards, dones, P, stream=stream)
+        if groups > 1:
+            stream.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=stream):
+                agent.run_window(pairs, rewards, dones, P, stream=stream)
+            graph.replay()
+    stream.synchronize()
+
+    def window():
+        if graph is not None:
+            graph.replay()
+        else:
+            agent.run_window(pairs, rewards, dones, P, stream=stream)
+
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        for _ in range(a.steps):
+            window()
+    stream.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    M = 100
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(M + 1)]
+    with torch.cuda.stream(stream):
+        evs[0].record(stream)
+        for i in range(M):
+            window()
+            evs[i + 1].record(stream)
+    stream.synchronize()
+    med = float(np.median([evs[i].elapsed_time(evs[i + 1]) for i in range(M)]))
+    out = {"workload": "%s: A3C %s NIPS-DQN head, %d envs x t_max=%d on one GPU, A = %d" % (workload, w_arch.upper(),
+                                                                                           N, T, A),
+           "value": round(N * T * a.steps / elapsed, 1), "unit": "env-steps/s", "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 4), "env_groups": groups,
+           "graph": graph is not None, "median_window_ms": round(med, 4),
+           "median_env_steps_per_s": round(N * T / (med * 1e-3), 1),
+           "params_finite": bool(torch.isfinite(model.net.params).all())}
+    del graph, agent, opt, model, pairs, rewards, dones
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
 
 
 def main(a):
@@ -779,6 +850,12 @@ def main(a):
         cpu["parallel"] = par
         cpu["gpu_vs_parallel"] = round(value / par["value"], 1)
 
+    secondary = None
+    sec = a.secondary if a.secondary != "auto" else ("c3" if (a.workload == "c4" and world == 1 and arch == "ff")
+                                                    else "none")
+    if world == 1 and sec not in ("", "none"):   # (the headline's buffers stay: 288 GB of HBM)
+        secondary = [secondary_line(a, pkg, dev, w.strip()) for w in sec.split(",") if w.strip()]
+
     if rank == 0:
         out = {
             "metric": "env-steps/sec (phi+forward+sample+update) at 1/2/4/8 MI355X; % roofline",
@@ -799,6 +876,7 @@ def main(a):
             "replicas_identical": replicas,
             "windows": windows, "timeline": timeline, "hbm_copy_peak": copy_peak,
             "roofline": roof, "kernels": kernels, "cpu_baseline": cpu, "params_finite": finite,
+            "secondary": secondary,
         }
         print(json.dumps(out), flush=True)
     if collectives:

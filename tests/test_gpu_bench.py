@@ -21,7 +21,7 @@ from conftest import ROOT
 pytestmark = pytest.mark.gpu
 
 BENCH = os.path.join(ROOT, "bench.py")
-SMALL = ["--workload", "c2", "--steps", "10", "--warmup", "3", "--cpu-seconds", "0", "--kernel-reps", "3",
+SMALL = ["--workload", "c2", "--steps", "10", "--warmup", "3", "--cpu-seconds", "0", "--kernel-reps", "3", "--secondary", "none",
          "--median-windows", "20", "--copy-peak", "0"]
 
 
@@ -81,6 +81,18 @@ def test_bench_window_timeline(gpu):
         if v.get("bound") == "hbm" and k in want:
             assert v["frac"] <= 1.0 and v.get("frac_measured_peak", 0) <= 1.0, (k, v)
     assert d["roofline"]["time_source"] == "window"
+
+
+def test_bench_secondary_workload(gpu):
+    """--secondary: another BASELINE workload measured after the headline with
+    the same protocol, reported beside it (the default line carries C3)."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "1"] + SMALL + ["--secondary", "c2", "--stamp-windows", "0"],
+                       capture_output=True, text=True, timeout=300, env=_env())
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    (sec,) = d["secondary"]
+    assert sec["workload"].startswith("c2") and sec["steps"] == 10 and sec["params_finite"], sec
+    assert sec["value"] > 0 and sec["median_window_ms"] > 0
 
 
 def test_bench_gpus_mismatch_fails(gpu):
