@@ -609,6 +609,7 @@ def main(a):
     with torch.cuda.stream(stream):
         for _ in range(a.steps):
             window()
+    t_enq = time.perf_counter() - t0      # host time to issue the K windows (eager launches / replays)
     stream.synchronize()
     if collectives:
         dist.barrier()
@@ -870,6 +871,7 @@ def main(a):
                        "graph": use_graph, "env_groups": len(model.net.env_groups(a.env_groups or model.net.default_env_groups())),
                        "parallelism": "dp%d" % world,
                        "units_per_step": N * T * world},
+            "host_issue_ms_per_step": round(1e3 * t_enq / a.steps, 4),
             "ranks_seen": seen, "collectives": (("rccl" if dist.get_backend() == "nccl" else dist.get_backend())
                                                 if collectives else None),
             "allreduce_bytes_per_window": (4 * model.net.grads.numel()) if collectives else 0,
