@@ -73,6 +73,8 @@ SIGNATURES = {
     "arl_stamps_end": (c_int, [c_void_p, ctypes.POINTER(c_int)]),
     "arl_stamps_read": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "arl_learn": (c_int, [c_void_p, c_double, c_double, c_double, c_int, c_void_p]),
+    "arl_run_window": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int, c_double, c_double,
+                               c_double, c_int, c_double, c_i64, c_i64, c_double, c_double, c_double, c_void_p]),
     "arl_learn_part": (c_int, [c_void_p, c_int, c_double, c_double, c_double, c_int, c_void_p]),
     "arl_optimize": (c_int, [c_void_p, c_double, c_i64, c_i64, c_double, c_double, c_double, c_void_p]),
     "arl_advance": (c_int, [c_void_p, c_void_p]),

@@ -65,6 +65,9 @@ GROUPS_ONE_STREAM = os.environ.get("ARL_GROUP_STREAMS", "") == "1"
 OVERLAP_ALLREDUCE = os.environ.get("ARL_OVERLAP_ALLREDUCE", "1") != "0"
 # one rank: GradientClipping's norm from the learner's conv reduce (ARL_NORM_FOLD=0: grad_sqnorm launch)
 NORM_FOLD = os.environ.get("ARL_NORM_FOLD", "1") != "0"
+# a single-chain window without collectives as one C call (arl_run_window: the same launches without a
+# host round trip per step); ARL_WINDOW_C=0 issues them step by step from Python (the A arm)
+WINDOW_C = os.environ.get("ARL_WINDOW_C", "1") != "0"
 
 def _is_dqn_phi(phi) -> bool:
     """phi is dqn_phi (dqn_phi.py:4-17): this package's, the reference's own
@@ -428,6 +431,13 @@ class A3C:
         64-row FC tiles, C4 0.497 vs 0.509-0.518 ms; profiles/r03/r3l)."""
         net, T = self.net, self.t_max
         groups = net.env_groups(net.default_env_groups() if env_groups is None else env_groups)
+        if (WINDOW_C and len(groups) == 1 and not split_update and not self.collectives and not net.fused_observe
+                and net.arch == net.base_arch and net.base_arch in (ARCH_FF, ARCH_LSTM)):
+            # one C call: T x (observe, act), bootstrap, learn, clip + RMSProp, advance (arl_run_window)
+            net.run_window(pair_pool, reward_pool, done_pool, pool_len, first, self.resize_mode, self.gamma, self.beta,
+                           self._vcoef, self.clip_reward, stream=stream, **self.optimizer.update_args())
+            self.t += T
+            return
         if len(groups) == 1:
             self._forward_chain(pair_pool, reward_pool, done_pool, pool_len, first, stream, None)
         else:

@@ -300,6 +300,16 @@ class DeviceNet:
             check(lib.arl_optimize(self._h, lr0, int(total_steps), int(n_total), alpha, eps, clip,
                                    stream_handle(stream)), "arl_optimize")
 
+    def run_window(self, pair_pool, reward_pool, done_pool, pool_len: int, first: bool, resize_mode: int,
+                   gamma: float, beta: float, v_loss_coef: float, clip_reward: bool, lr0: float, total_steps: int,
+                   n_total: int, alpha: float, eps: float, clip: float, stream=None):
+        """A whole lockstep window in one call (arl_run_window): T x (observe,
+        act), the bootstrap, learn, clip + RMSProp and the advance -- the
+        launches of observe / act / learn / optimize(advance=True) in order."""
+        check(lib.arl_run_window(self._h, ptr(pair_pool), ptr(reward_pool), ptr(done_pool), pool_len, int(first),
+                                 resize_mode, gamma, beta, v_loss_coef, int(clip_reward), lr0, int(total_steps),
+                                 int(n_total), alpha, eps, clip, stream_handle(stream)), "arl_run_window")
+
     def advance(self, stream=None):
         check(lib.arl_advance(self._h, stream_handle(stream)), "arl_advance")
 

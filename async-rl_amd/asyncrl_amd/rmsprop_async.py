@@ -56,19 +56,22 @@ class RMSpropAsync:
                 return h.threshold
         return 0.0
 
-    def update(self, stream=None, advance_window=False):
-        """GradientClipping hook(s) then update_one for every parameter,
-        on the bound model's device buffers (a3c.py:139).  advance_window:
-        also end the lockstep window (arl_optimize_advance)."""
-        net = self.target.net
+    def update_args(self) -> dict:
+        """The arguments of one update (net.optimize's, without the stream),
+        counting it (Chainer's Optimizer.t)."""
         if self.anneal_total_steps > 0 and self.n_total_envs <= 0:
             # global_t per window = (window start + t_max) * n_total_envs: with 0
             # envs it never moves and the anneal would silently keep lr fixed
             raise ValueError("anneal_total_steps > 0 needs n_total_envs > 0 (envs over all ranks)")
         self.t += 1
-        net.optimize(lr0=self.lr, total_steps=self.anneal_total_steps, n_total=self.n_total_envs,
-                     alpha=self.alpha, eps=self.eps, clip=self.clip_threshold, stream=stream,
-                     advance=advance_window)
+        return dict(lr0=self.lr, total_steps=self.anneal_total_steps, n_total=self.n_total_envs, alpha=self.alpha,
+                    eps=self.eps, clip=self.clip_threshold)
+
+    def update(self, stream=None, advance_window=False):
+        """GradientClipping hook(s) then update_one for every parameter,
+        on the bound model's device buffers (a3c.py:139).  advance_window:
+        also end the lockstep window (arl_optimize_advance)."""
+        self.target.net.optimize(stream=stream, advance=advance_window, **self.update_args())
 
     def update_arrays(self, param: torch.Tensor, ms: torch.Tensor, grad: torch.Tensor, stream=None):
         """update_one on explicit flat f32 device tensors (the drop-in for

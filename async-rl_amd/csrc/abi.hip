@@ -421,6 +421,29 @@ int arl_optimize(arl_net* h, double lr0, int64_t total_steps, int64_t n_total, d
   return hip_status(arl::net_optimize(h->net, lr0, total_steps, n_total, alpha, eps, (float)clip, S(s)), "optimize");
 }
 
+int arl_run_window(arl_net* h, const uint8_t* pair_pool, const float* reward_pool, const uint8_t* done_pool,
+                   int64_t pool_len, int first, int resize_mode, double gamma, double beta, double vcoef,
+                   int clip_reward, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
+                   double clip, void* s) {
+  NEED_BOUND(h);
+  arl::Net& n = h->net;
+  if (n.rgb || n.stack || n.states || n.arch == arl::ARCH_FF_NATURE)
+    return fail(ARL_ESTATE, "run_window: frame-pair nets with the NIPS head only (FF / LSTM)");
+  if (resize_mode < 0 || resize_mode > (ARL_RESIZE_SIMD | ARL_RESIZE_CROP)) return fail(ARL_EINVAL, "bad resize_mode");
+  for (int t = 0; t <= n.T; ++t) {
+    if (t > 0 || first) {   // slot 0 of a continuing window: the previous window's bootstrap observation
+      const int rc = observe_common(h, t, pair_pool, reward_pool, done_pool, pool_len, t == 0 ? 1 : 0, resize_mode, 0,
+                                    0, s);
+      if (rc != ARL_OK) return rc;
+    }
+    const hipError_t e = arl::net_act(n, t, 1, S(s));   // (slot T: the bootstrap forward, no draw)
+    if (e != hipSuccess) return hip_status(e, "run_window: act");
+  }
+  hipError_t e = arl::net_learn(n, gamma, (float)beta, (float)vcoef, clip_reward, S(s));
+  if (e == hipSuccess) e = arl::net_optimize(n, lr0, total_steps, n_total, alpha, eps, (float)clip, S(s), true);
+  return hip_status(e, "run_window");
+}
+
 int arl_optimize_advance(arl_net* h, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
                          double clip, void* s) {
   NEED_BOUND(h);

@@ -278,6 +278,18 @@ int arl_stamp(arl_net* net, int stage, void* stream);
 int arl_stamps_end(arl_net* net, int* count);
 int arl_stamps_read(arl_net* net, int i0, int n, float* ms, int* stage);
 
+/* One whole lockstep window in one call, for frame-pair nets with the NIPS
+ * head (FF / LSTM): t = 0..t_max: arl_observe(t) (slot 0 only when first != 0,
+ * with force_reset) + arl_act(t) (sampled; slot t_max the bootstrap forward,
+ * a3c.py:85), then arl_learn and arl_optimize_advance (a3c.py:88-144) -- the
+ * same launches in the same order as those calls one by one, issued without a
+ * host round trip per step (A3C.run_window's single-chain window without
+ * collectives). */
+int arl_run_window(arl_net* net, const uint8_t* pair_pool, const float* reward_pool, const uint8_t* done_pool,
+                   int64_t pool_len, int first, int resize_mode, double gamma, double beta, double v_loss_coef,
+                   int clip_reward, double lr0, int64_t total_steps, int64_t n_total, double alpha, double eps,
+                   double clip, void* stream);
+
 /* End of window: advance step counters, carry reset flags / LSTM state. */
 int arl_advance(arl_net* net, void* stream);
 

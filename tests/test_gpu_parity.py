@@ -829,7 +829,9 @@ def test_conv_fwd_two_envs_identical(gpu, tmp_path, n_envs):
     updated parameters match bit for bit -- at an odd env count (the last conv
     workgroup's second slot idle, a partial FC tile; too few envs for the fused
     heads, which fall back), at 200 (a partial 64-row block) and at 512.  The
-    frame ring too, against phi_ring_kernel's LDS-DMA staging (ARL_PHI_DMA)."""
+    frame ring too, against phi_ring_kernel's LDS-DMA staging (ARL_PHI_DMA); and the
+    window as one C call (arl_run_window) against its launches issued step by
+    step from Python (ARL_WINDOW_C=0)."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -837,7 +839,7 @@ def test_conv_fwd_two_envs_identical(gpu, tmp_path, n_envs):
     for i, arm in enumerate(({"ARL_CONV_EPW": "1", "ARL_FC_BIG": "0"}, {"ARL_CONV_EPW": "2", "ARL_FC_BIG": "0"},
                              {"ARL_CONV_EPW": "1", "ARL_FC_BIG": "1", "ARL_FC_HEADS": "0"},
                              {"ARL_CONV_EPW": "1", "ARL_FC_BIG": "1", "ARL_FC_HEADS": "1"},
-                             {"ARL_PHI_DMA": "1"})):
+                             {"ARL_PHI_DMA": "1"}, {"ARL_WINDOW_C": "0"})):
         f = str(tmp_path / f"arm_{i}.npz")
         env = dict(os.environ, **arm)
         subprocess.run([sys.executable, os.path.join(here, "conv_epw_worker.py"), f, str(n_envs)], env=env,
