@@ -363,7 +363,10 @@ int arl_stamps_begin(arl_net* h, int cap) {
   arl::Stamps& st = *n.stamps;
   while ((int)st.ev.size() < cap) {
     hipEvent_t e;
-    if (hipEventCreate(&e) != hipSuccess) return fail(ARL_EHIP, "stamps_begin: hipEventCreate");
+    // timing events without the system-scope fence (cache writeback / invalidate) a default event
+    // record performs: the stamps perturb the window they measure less
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess)
+      return fail(ARL_EHIP, "stamps_begin: hipEventCreateWithFlags");
     st.ev.push_back(e);
   }
   st.stage.assign(st.ev.size(), 0);
@@ -485,8 +488,9 @@ int arl_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, doubl
     if (e == hipSuccess) e = arl::launch_grad_sqnorm(g, n, parts, blocks, S(s));
   }
   if (e == hipSuccess)
-    e = arl::launch_rmsprop(p, ms, g, n, lr, alpha, eps, clip > 0 ? parts + arl::NORM_RESULT : nullptr, (float)clip,
-                            nullptr, 0, 0, 0, S(s));
+    e = arl::launch_rmsprop(p, ms, g, n, lr, alpha, eps,
+                            clip > 0 ? parts + (arl::norm_ticket() ? arl::NORM_RESULT : 0) : nullptr,
+                            (clip > 0 && !arl::norm_ticket()) ? blocks : 0, (float)clip, nullptr, 0, 0, 0, S(s));
   return hip_status(e, "rmsprop");
 }
 

@@ -224,6 +224,7 @@ struct NormFold {
   const float* g;           // the flat gradient
   int64_t rest_begin, rest_end;   // floats of g outside the conv tensors (final before the reduce)
   int rest_blocks;
+  int finish = 1;           // norm_finish's ticket (norm_ticket())
 };
 int conv_norm_parts(int rest_blocks);
 hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int S,
@@ -317,7 +318,11 @@ constexpr int NORM_MAX_PARTS = 1000, NORM_RESULT = 1000, NORM_TICKET = 1001, NOR
 // them in index order (lane l: l, l + 64, ...; then the lanes in xor-tree order, a fixed
 // order), writes the squared norm to parts[NORM_RESULT] and re-arms the ticket.  The next
 // launch on the stream (rmsprop_kernel) reads the result after the kernel boundary.
-__device__ inline void norm_finish(double mine, int b, int nparts, double* parts) {
+__device__ inline void norm_finish(double mine, int b, int nparts, double* parts, bool finish = true) {
+  if (!finish) {   // (ARL_NORM_TICKET=0: the partials only; rmsprop_kernel re-reduces them in every block)
+    if (threadIdx.x == 0) parts[b] = mine;
+    return;
+  }
   __shared__ int last;
   int* ticket = reinterpret_cast<int*>(parts + NORM_TICKET);
   if (threadIdx.x == 0) {
@@ -329,9 +334,16 @@ __device__ inline void norm_finish(double mine, int b, int nparts, double* parts
   __syncthreads();
   if (!last || threadIdx.x >= 64) return;
   double t = 0.0;
-  for (int i = threadIdx.x; i < nparts; i += 64)
-    t += __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<unsigned long long*>(parts + i),
-                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  for (int base = 0; base < nparts; base += 8 * 64) {   // 8 loads a lane in flight before the sums
+    unsigned long long v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      v[k] = __hip_atomic_load(reinterpret_cast<unsigned long long*>(parts + min(base + (int)threadIdx.x + 64 * k, nparts - 1)),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (base + (int)threadIdx.x + 64 * k < nparts) t += __longlong_as_double((long long)v[k]);
+  }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o);
   if (threadIdx.x == 0) {
@@ -340,9 +352,13 @@ __device__ inline void norm_finish(double mine, int b, int nparts, double* parts
   }
 }
 
-// norm_sq: &partials[NORM_RESULT] (null: no clip)
+// the norm's hand-off (ARL_NORM_TICKET, default on): the norm launch's last block leaves the total;
+// off: partials only, every rmsprop_kernel block re-reduces them (round 3's form, the A arm)
+bool norm_ticket();
+// norm_sq: &partials[NORM_RESULT] (nparts = 0), or the partials themselves (nparts > 0, re-reduced);
+// null: no clip
 hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, double alpha, double eps,
-                          const double* norm_sq, float clip, const int64_t* ctl,
+                          const double* norm_sq, int nparts, float clip, const int64_t* ctl,
                           int64_t total_steps, int64_t n_total, int t_max, hipStream_t s,
                           const AdvanceArgs* adv = nullptr);
 hipError_t launch_grad_sqnorm(const float* g, int64_t n, double* partials, int blocks, hipStream_t s);

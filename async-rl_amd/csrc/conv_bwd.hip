@@ -752,7 +752,7 @@ reduce_conv_bwd_kernel(const float* __restrict__ slab, int G, float* __restrict_
       t += (double)v * v;
     }
     t = block_sum_f64_1024(t, shn);
-    norm_finish(t, RED_BLOCKS + b, RED_BLOCKS + nf.rest_blocks, nf.parts);
+    norm_finish(t, RED_BLOCKS + b, RED_BLOCKS + nf.rest_blocks, nf.parts, nf.finish != 0);
     return;
   }
   const int ol = threadIdx.x & (RED_O - 1), zg = threadIdx.x / RED_O;
@@ -780,7 +780,7 @@ reduce_conv_bwd_kernel(const float* __restrict__ slab, int G, float* __restrict_
   }
   if (nf.parts != nullptr) {   // (block-uniform)
     sq = block_sum_f64_1024(sq, shn);
-    norm_finish(sq, blockIdx.x, RED_BLOCKS + nf.rest_blocks, nf.parts);
+    norm_finish(sq, blockIdx.x, RED_BLOCKS + nf.rest_blocks, nf.parts, nf.finish != 0);
   }
 }
 

@@ -691,7 +691,8 @@ hipError_t net_reset_state(Net& net, int e0, int n, hipStream_t s) {
 // before the conv slab reduce
 static NormFold norm_fold_args(const Net& net) {
   if (!net.norm_fold) return NormFold{};
-  return NormFold{net.at<double>(net.w_norm), net.g, net.o_fcW, net.param_floats, net.norm_rest_blocks};
+  return NormFold{net.at<double>(net.w_norm), net.g, net.o_fcW, net.param_floats, net.norm_rest_blocks,
+                  norm_ticket() ? 1 : 0};
 }
 
 // the fused conv backward (per-sample slabs) and its slab reduce (with the folded clip norm's
@@ -972,7 +973,8 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
       return lstm_wgrad(net, s);
     case STAGE_RMSPROP:   // the update kernel as a window runs it (clip 40 from the last norm the window left), lr 0
       return launch_rmsprop(net.p, net.ms, net.g, net.param_floats, 0.0, 0.99, 0.1,
-                            net.at<double>(net.w_norm) + NORM_RESULT, 40.f, nullptr, 0, 0, net.T, s);
+                            net.at<double>(net.w_norm) + (norm_ticket() ? NORM_RESULT : 0),
+                            norm_ticket() ? 0 : (net.norm_ready ? conv_norm_parts(net.norm_rest_blocks) : net.norm_blocks), 40.f, nullptr, 0, 0, net.T, s);
     default:
       return hipErrorInvalidValue;
   }
@@ -996,7 +998,9 @@ hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_tot
                         L ? net.at<float>(net.w_hbuf) : nullptr, L ? net.at<float>(net.w_cbuf) : nullptr, net.T,
                         net.N};
   ARL_TRY(launch_rmsprop(net.p, net.ms, net.g, net.param_floats, lr0, alpha, eps,
-                         do_clip ? parts + NORM_RESULT : nullptr, clip, total_steps > 0 ? net.at<int64_t>(net.w_ctl) : nullptr, total_steps,
+                         do_clip ? parts + (norm_ticket() ? NORM_RESULT : 0) : nullptr,
+                         (do_clip && !norm_ticket()) ? (folded ? conv_norm_parts(net.norm_rest_blocks) : net.norm_blocks) : 0,
+                         clip, total_steps > 0 ? net.at<int64_t>(net.w_ctl) : nullptr, total_steps,
                          n_total, net.T, s, fused ? &adv : nullptr));
   ARL_TRY(stamp(net, STAGE_RMSPROP, s));
   return advance && !fused ? net_advance(net, s) : hipSuccess;

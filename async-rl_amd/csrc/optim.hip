@@ -41,7 +41,7 @@ __device__ inline double block_sum_f64(double x, double* sh) {
 }
 
 __global__ void __launch_bounds__(256)
-grad_sqnorm_kernel(const float* __restrict__ g, int64_t n, double* __restrict__ partials) {
+grad_sqnorm_kernel(const float* __restrict__ g, int64_t n, double* __restrict__ partials, int finish) {
   __shared__ double sh[8];
   const int64_t n4 = n >> 2;
   float acc = 0.f;
@@ -56,7 +56,7 @@ grad_sqnorm_kernel(const float* __restrict__ g, int64_t n, double* __restrict__ 
     acc = __fadd_rn(acc, __fmul_rn(v, v));
   }
   const double t = block_sum_f64((double)acc, sh);
-  norm_finish(t, blockIdx.x, gridDim.x, partials);
+  norm_finish(t, blockIdx.x, gridDim.x, partials, finish != 0);
 }
 
 struct RmsConst {   // (AdvanceArgs is declared in arl_internal.hpp)
@@ -84,7 +84,8 @@ __device__ inline void rms1(float& p, float& ms, float g, const RmsConst& c) {
 template <int U>
 __global__ void __launch_bounds__(256)
 rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __restrict__ g, int64_t n, RmsConst c,
-               const double* __restrict__ norm_sq, float clip, AdvanceArgs adv) {
+               const double* __restrict__ norm_sq, int nparts, float clip, AdvanceArgs adv) {
+  __shared__ double sh[8];
   if (c.ctl != nullptr && c.total > 0) {
     const int64_t gt = (c.ctl[c.ctl_idx] + c.t_max) * c.n_total;
     // clamped at 0: the reference stops training once global_t passes the
@@ -109,7 +110,20 @@ rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __res
   float scale = 1.f;
   bool do_clip = false;
   if (norm_sq != nullptr) {
-    const double norm = sqrt(*norm_sq);
+    double t;
+    if (nparts > 0) {   // re-reduce the partials (loads in flight with the first pass's)
+      t = 0.0;
+      double v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = norm_sq[min((int)threadIdx.x + 256 * k, nparts - 1)];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if ((int)threadIdx.x + 256 * k < nparts) t += v[k];
+      t = block_sum_f64(t, sh);
+    } else {
+      t = *norm_sq;
+    }
+    const double norm = sqrt(t);
     const double rate = (double)clip / norm;
     if (norm > 0.0 && rate < 1.0) {
       do_clip = true;
@@ -171,15 +185,24 @@ static int stream_blocks(int64_t n) {
   return (int)b;
 }
 
+bool norm_ticket() {
+  static const bool on = [] {
+    const char* e = getenv("ARL_NORM_TICKET");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  return on;
+}
+
 hipError_t launch_grad_sqnorm(const float* g, int64_t n, double* partials, int blocks, hipStream_t s) {
-  if (blocks < 1 || blocks > NORM_MAX_PARTS) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(grad_sqnorm_kernel, dim3(blocks), dim3(256), 0, s, g, n, partials);
+  if (blocks < 1 || blocks > 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(grad_sqnorm_kernel, dim3(blocks), dim3(256), 0, s, g, n, partials, norm_ticket() ? 1 : 0);
   return hipGetLastError();
 }
 
 hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, double alpha, double eps,
-                          const double* norm_sq, float clip, const int64_t* ctl,
+                          const double* norm_sq, int nparts, float clip, const int64_t* ctl,
                           int64_t total_steps, int64_t n_total, int t_max, hipStream_t s, const AdvanceArgs* adv) {
+  if (nparts > 1024) return hipErrorInvalidValue;
   if (n <= 0) return hipSuccess;
   // each Python-float hyperparameter meets the f32 arrays as f32(value)
   RmsConst c;
@@ -201,9 +224,10 @@ hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double
   }();
   if (u2)
     hipLaunchKernelGGL(rmsprop_kernel<2>, dim3((stream_blocks(n) + 1) / 2), dim3(256), 0, s, p, ms, g, n, c, norm_sq,
-                       clip, a);
+                       nparts, clip, a);
   else
-    hipLaunchKernelGGL(rmsprop_kernel<1>, dim3(stream_blocks(n)), dim3(256), 0, s, p, ms, g, n, c, norm_sq, clip, a);
+    hipLaunchKernelGGL(rmsprop_kernel<1>, dim3(stream_blocks(n)), dim3(256), 0, s, p, ms, g, n, c, norm_sq, nparts,
+                       clip, a);
   return hipGetLastError();
 }
 

@@ -9,7 +9,7 @@ echo "pytest rc=$rc" > $O/status
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 400 python bench.py > $O/bench.log 2>&1 || exit $?
 echo "bench ok" >> $O/status
-if [ -f async-rl_amd/csrc/build_var_cfstamp/libasyncrl_hip.so ]; then
+if [ "${CFSTAMP:-0}" = 1 ] && [ -f async-rl_amd/csrc/build_var_cfstamp/libasyncrl_hip.so ]; then
   for n in 512 256; do
     ASYNCRL_HIP_LIB=$PWD/async-rl_amd/csrc/build_var_cfstamp/libasyncrl_hip.so timeout -k 10 200 python scripts/cf_stamps.py $n > $O/cfstamps$n.txt 2>&1 || exit $?
   done
@@ -21,6 +21,8 @@ for ab in $AB; do
     phidma) bash scripts/env_ab.sh ARL_PHI_DMA=0 ARL_PHI_DMA=1 "" 2 phidma || exit $? ;;
     c3streams) bash scripts/env_ab.sh ARL_GROUP_STREAMS=0 ARL_GROUP_STREAMS=1 "--workload c3" 2 c3streams || exit $? ;;
     variants) bash scripts/gpu_variants.sh "--steps 30 --warmup 5 --kernel-reps 3 --copy-peak 0" 1 > $O/variants.txt 2>&1 || exit $? ;;
+    norm) bash scripts/env_ab.sh ARL_NORM_TICKET=0 ARL_NORM_TICKET=1 "" 2 norm || exit $?
+          bash scripts/env_ab.sh ARL_NORM_TICKET=0 ARL_NORM_TICKET=1 "--workload c2" 2 normc2 || exit $? ;;
     rmsu) bash scripts/env_ab.sh ARL_RMS_U=1 ARL_RMS_U=2 "" 2 rmsu || exit $? ;;
     fcbz) for z in 2 4 5; do bash scripts/env_ab.sh ARL_FC_BWD_Z=3 ARL_FC_BWD_Z=$z "" 1 fcbz$z || exit $?; done ;;
   esac
