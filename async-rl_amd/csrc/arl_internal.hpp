@@ -295,6 +295,17 @@ PolicyArgs states_policy_args(Net& net, int mode);
 hipError_t launch_policy_fc(const float* slab, int n, const float* fc_bias, float* hfc, const PolicyArgs& pa,
                             hipStream_t s);
 
+// x / 255 correctly rounded, i.e. __fdiv_rn(x, 255.f), in three ops instead of the ~10 of the
+// general division: q = x * RN(1/255), the exact residual r = x - 255 q (fma), q + r * RN(1/255)
+// (fma).  scripts/div255_check.c compares it with IEEE division over every finite f32: equal
+// except x = -0 (+0 instead of -0), which no caller passes (byte values; MFMA sums from +0
+// accumulators).  Needs f32 denormals on (the kernels' default float_denorm_mode 3).
+__device__ inline float div255(float x) {
+  constexpr float inv = 1.f / 255.f;
+  const float q = __fmul_rn(x, inv);
+  return __fmaf_rn(__fmaf_rn(-q, 255.f, x), inv, q);
+}
+
 // end-of-window advance folded into the update (NIPS learner): the lr reads
 // the learner's snapshot CTL_STEP_SNAP, so no workgroup reads CTL_STEP and one
 // thread can move it without a ticket; reset flags (and the LSTM h / c carry)

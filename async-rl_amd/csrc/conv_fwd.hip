@@ -468,7 +468,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         ov[r] = (ARL_ABLATE & 16) ? fmaxf(__fadd_rn(__fmul_rn(__fadd_rn(big[j][r], sml[j][r]), 1.f / 255.f), bias1), 0.f)
-                                  : fmaxf(__fadd_rn(__fdiv_rn(__fadd_rn(big[j][r], sml[j][r]), 255.f), bias1), 0.f);
+                                  : fmaxf(__fadd_rn(div255(__fadd_rn(big[j][r], sml[j][r])), bias1), 0.f);
       if (valid && a.a1 != nullptr)   // (null: the bootstrap slot, which no backward reads)
         *reinterpret_cast<float4*>(a1g + col * C1_P + p0) = make_float4(ov[0], ov[1], ov[2], ov[3]);
 #pragma unroll

@@ -35,7 +35,7 @@ namespace {
 constexpr int NFC_SPLIT = 8;   // FC forward split-K (K = 3136 -> 8 slices of 416)
 
 // dqn_phi.py:14-16: f32(byte) / 255 as an IEEE f32 division
-__device__ inline float phi_scale(uint32_t b) { return __fdiv_rn((float)b, 255.f); }
+__device__ inline float phi_scale(uint32_t b) { return div255((float)b); }
 
 // conv1 im2col from the frame ring (ale.py:135,155-158 stack, oldest plane
 // first, planes older than the env's last reset read as 0).  Sample s =

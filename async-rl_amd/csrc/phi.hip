@@ -305,10 +305,10 @@ __device__ inline void rgb_band(const uint8_t* __restrict__ img, int H, int W, v
     const int dy = dy0 + ly;
     if (OUT_F32) {
       float4 o;
-      o.x = __fdiv_rn((float)v4[0], 255.f);
-      o.y = __fdiv_rn((float)v4[1], 255.f);
-      o.z = __fdiv_rn((float)v4[2], 255.f);
-      o.w = __fdiv_rn((float)v4[3], 255.f);
+      o.x = div255((float)v4[0]);
+      o.y = div255((float)v4[1]);
+      o.z = div255((float)v4[2]);
+      o.w = div255((float)v4[3]);
       *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + ch * PLANE + dy * DST + q * 4) = o;
     } else {
       const uint32_t packed = (uint32_t)v4[0] | ((uint32_t)v4[1] << 8) | ((uint32_t)v4[2] << 16) |
@@ -394,13 +394,13 @@ __global__ void dqn_phi_kernel(const uint8_t* __restrict__ in, float* __restrict
   if (i + 3 < count) {
     const uint32_t w = *reinterpret_cast<const uint32_t*>(in + i);
     float4 o;
-    o.x = __fdiv_rn((float)(w & 0xff), 255.f);
-    o.y = __fdiv_rn((float)((w >> 8) & 0xff), 255.f);
-    o.z = __fdiv_rn((float)((w >> 16) & 0xff), 255.f);
-    o.w = __fdiv_rn((float)(w >> 24), 255.f);
+    o.x = div255((float)(w & 0xff));
+    o.y = div255((float)((w >> 8) & 0xff));
+    o.z = div255((float)((w >> 16) & 0xff));
+    o.w = div255((float)(w >> 24));
     *reinterpret_cast<float4*>(out + i) = o;
   } else {
-    for (int64_t j = i; j < count; ++j) out[j] = __fdiv_rn((float)in[j], 255.f);
+    for (int64_t j = i; j < count; ++j) out[j] = div255((float)in[j]);
   }
 }
 
