@@ -91,6 +91,14 @@ __device__ inline void mfma_x3(bf16x8 a, bf16x8 bh, bf16x8 bm, bf16x8 bl, f32x4&
   big = mfma_bf16(a, bh, big);
 }
 
+// mfma_x3 with the operands' roles swapped: the same exact products and k order, the transposed
+// tile (C^T: rows from the split operand, columns from a), so a lane holds 4 consecutive rows of B
+__device__ inline void mfma_x3_t(bf16x8 a, bf16x8 bh, bf16x8 bm, bf16x8 bl, f32x4& big, f32x4& small) {
+  small = mfma_bf16(bl, a, small);
+  small = mfma_bf16(bm, a, small);
+  big = mfma_bf16(bh, a, big);
+}
+
 // both split: big += Ah.Bh; small += Al.Bh + Am.Bm + Ah.Bl + Am.Bh + Ah.Bm
 __device__ inline void mfma_x6(bf16x8 ah, bf16x8 am, bf16x8 al, bf16x8 bh, bf16x8 bm, bf16x8 bl, f32x4& big,
                                f32x4& small) {

@@ -212,7 +212,8 @@ conv_fwd_kernel(ConvFwdArgs a) {
 #else
 #define CF_STAMP() do {} while (0)
 #endif
-  const float bias1 = a.b1[col];
+  // conv1 runs transposed (mfma_x3_t): lane (g, col) holds oc 4g..4g+3 of position tile * 16 + col
+  const float bias1[4] = {a.b1[4 * g], a.b1[4 * g + 1], a.b1[4 * g + 2], a.b1[4 * g + 3]};
   const float bias2 = a.b2[16 * (w8 & 1) + col];
   const int64_t ks = a.ctl[CTL_STEP] + a.t;
   const int rs = (int)(ks % a.R);
@@ -236,11 +237,11 @@ conv_fwd_kernel(ConvFwdArgs a) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const bf16x8 xa = lds_load8_a8(lds, baseX[j] + off);
-      mfma_x3(xa, wh, wm, wl, big[j], sml[j]);
+      mfma_x3_t(xa, wh, wm, wl, big[j], sml[j]);
     }
     if (has3) {
       const bf16x8 xa = lds_load8_a8(lds, baseX[3] + off);
-      mfma_x3(xa, wh, wm, wl, big[3], sml[3]);
+      mfma_x3_t(xa, wh, wm, wl, big[3], sml[3]);
     }
   };
   auto w1_frag = [&](int s, bf16x8& wh, bf16x8& wm, bf16x8& wl) {
@@ -438,8 +439,8 @@ conv_fwd_kernel(ConvFwdArgs a) {
         if (s + 1 < 8) load(s + 1, b ^ 1);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < 3; ++j) mfma_x3(xa[b][j], wh[b], wm[b], wl[b], big[j], sml[j]);
-        if (has3) mfma_x3(xa[b][3], wh[b], wm[b], wl[b], big[3], sml[3]);
+        for (int j = 0; j < 3; ++j) mfma_x3_t(xa[b][j], wh[b], wm[b], wl[b], big[j], sml[j]);
+        if (has3) mfma_x3_t(xa[b][3], wh[b], wm[b], wl[b], big[3], sml[3]);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -459,27 +460,29 @@ conv_fwd_kernel(ConvFwdArgs a) {
   uint32_t* msk = reinterpret_cast<uint32_t*>(lds + LY::MSK(el));
   if (a.a2m != nullptr && t8 < A2W) msk[t8] = 0u;   // (its bytes are dead since conv1's barrier)
   {
-    // C rows g*4 + r -> positions tile*16 + g*4 + r, col = oc
+    // C^T rows 4g + r = oc, column col -> position tile * 16 + col: the lane's 4 oc are 4 consecutive
+    // ic of the a1 planes, one 8-byte LDS store per plane
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       if (j == 3 && !has3) break;
-      const int p0 = (w8 + 8 * j) * 16 + g * 4;
+      const int p = (w8 + 8 * j) * 16 + col;
       float ov[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        ov[r] = (ARL_ABLATE & 16) ? fmaxf(__fadd_rn(__fmul_rn(__fadd_rn(big[j][r], sml[j][r]), 1.f / 255.f), bias1), 0.f)
-                                  : fmaxf(__fadd_rn(div255(__fadd_rn(big[j][r], sml[j][r])), bias1), 0.f);
-      if (valid && a.a1 != nullptr)   // (null: the bootstrap slot, which no backward reads)
-        *reinterpret_cast<float4*>(a1g + col * C1_P + p0) = make_float4(ov[0], ov[1], ov[2], ov[3]);
+        ov[r] = (ARL_ABLATE & 16)
+                    ? fmaxf(__fadd_rn(__fmul_rn(__fadd_rn(big[j][r], sml[j][r]), 1.f / 255.f), bias1[r]), 0.f)
+                    : fmaxf(__fadd_rn(div255(__fadd_rn(big[j][r], sml[j][r])), bias1[r]), 0.f);
+      if (valid && a.a1 != nullptr) {   // (null: the bootstrap slot, which no backward reads)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        uint32_t h, m, l;
-        split3(ov[r], h, m, l);
-        const int off = LY::A1(el) + a1_slot(p0 + r, col >> 3) + (col & 7) * 2;
-        *reinterpret_cast<uint16_t*>(lds + off) = (uint16_t)h;
-        *reinterpret_cast<uint16_t*>(lds + off + A1P) = (uint16_t)m;
-        *reinterpret_cast<uint16_t*>(lds + off + 2 * A1P) = (uint16_t)l;
+        for (int r = 0; r < 4; ++r) a1g[(4 * g + r) * C1_P + p] = ov[r];
       }
+      uint2 ph, pm, pl;
+      split3_pack(ov[0], ov[1], ph.x, pm.x, pl.x);
+      split3_pack(ov[2], ov[3], ph.y, pm.y, pl.y);
+      const int off = LY::A1(el) + a1_slot(p, g >> 1) + (g & 1) * 8;
+      *reinterpret_cast<uint2*>(lds + off) = ph;
+      *reinterpret_cast<uint2*>(lds + off + A1P) = pm;
+      *reinterpret_cast<uint2*>(lds + off + 2 * A1P) = pl;
     }
   }
   CF_STAMP();   // 3: a1 epilogue
