@@ -551,29 +551,40 @@ conv_fwd_kernel(ConvFwdArgs a) {
     CF_STAMP();   // 6: conv2 MFMAs issued
     float* a2g = a.a2 + (int64_t)e * A2;
     const float b = bias2;   // b2[oc]
-    // a2 > 0 -> bit k = oc * 81 + p of the env's mask words (LDS ors, stored after a barrier)
+    // a2 > 0 -> bit k = oc * 81 + p of the env's mask words: a lane's 4 positions 16 m + 4 g + r are 4
+    // consecutive bits, lanes g = 0..3 of one oc a 16-bit run, or'd into the LDS words by lane g = 0
+    // (one or two ors per oc and tile, no two lanes on one word; stored after a barrier)
     const bool mk = a.a2m != nullptr;
+    auto mask_or = [&](unsigned nib, int m) {
+      nib <<= 4 * g;
+      nib |= __shfl_xor(nib, 16);
+      nib |= __shfl_xor(nib, 32);
+      if (g == 0 && nib != 0u) {
+        const int k = oc * C2_P + 16 * m, sh = k & 31;
+        __hip_atomic_fetch_or(msk + (k >> 5), nib << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (sh > 16)
+          __hip_atomic_fetch_or(msk + (k >> 5) + 1, nib >> (32 - sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    };
+    unsigned nibA = 0u;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int p = 16 * mA + g * 4 + r;
       const float v = fmaxf(__fadd_rn(__fadd_rn(bigA[r], smlA[r]), b), 0.f);
       if (valid && p < C2_P) a2g[oc * C2_P + p] = v;
-      if (mk && p < C2_P && v > 0.f) {
-        const int k = oc * C2_P + p;
-        __hip_atomic_fetch_or(msk + (k >> 5), 1u << (k & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
+      if (p < C2_P && v > 0.f) nibA |= 1u << r;
     }
+    if (mk) mask_or(nibA, mA);
     if (hasB) {
+      unsigned nibB = 0u;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int p = 16 * mB + g * 4 + r;
         const float v = fmaxf(__fadd_rn(__fadd_rn(bigB[r], smlB[r]), b), 0.f);
         if (valid && p < C2_P) a2g[oc * C2_P + p] = v;
-        if (mk && p < C2_P && v > 0.f) {
-          const int k = oc * C2_P + p;
-          __hip_atomic_fetch_or(msk + (k >> 5), 1u << (k & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+        if (p < C2_P && v > 0.f) nibB |= 1u << r;
       }
+      if (mk) mask_or(nibB, mB);
     }
     if (mk) {   // (block-uniform)
       __syncthreads();
