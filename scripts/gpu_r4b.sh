@@ -23,6 +23,10 @@ for ab in $AB; do
     variants) bash scripts/gpu_variants.sh "--steps 30 --warmup 5 --kernel-reps 3 --copy-peak 0" 1 > $O/variants.txt 2>&1 || exit $? ;;
     norm) bash scripts/env_ab.sh ARL_NORM_TICKET=0 ARL_NORM_TICKET=1 "" 2 norm || exit $?
           bash scripts/env_ab.sh ARL_NORM_TICKET=0 ARL_NORM_TICKET=1 "--workload c2" 2 normc2 || exit $? ;;
+    c3g) for r in 1 2; do for g in 1 2; do
+           timeout -k 10 200 python -u bench.py --workload c3 --env-groups $g --steps 100 --warmup 10 --cpu-seconds 0 --kernel-reps 5 --copy-peak 0 --secondary none > $O/c3g$g.$r.log 2>&1 || exit $?
+           python -c "import json; d=json.loads(open('$O/c3g$g.$r.log').read().strip().splitlines()[-1]); print('c3 env_groups $g', d['ms_per_step'], d['windows']['median_ms'], d['config'].get('graph'))"
+         done; done ;;
     rmsu) bash scripts/env_ab.sh ARL_RMS_U=1 ARL_RMS_U=2 "" 2 rmsu || exit $? ;;
     fcbz) for z in 2 4 5; do bash scripts/env_ab.sh ARL_FC_BWD_Z=3 ARL_FC_BWD_Z=$z "" 1 fcbz$z || exit $?; done ;;
   esac
