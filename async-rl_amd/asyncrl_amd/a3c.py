@@ -58,9 +58,6 @@ STAGGER = os.environ.get("ARL_GROUP_STAGGER", "1") != "0"
 # hands every chain's first launches to the device early; ARL_GROUP_ORDER=chain
 # issues chain 0 whole, then chain 1, ... (the A arm)
 GROUP_ORDER = os.environ.get("ARL_GROUP_ORDER", "interleave")
-# env groups: ARL_GROUP_STREAMS=1 issues every chain on the window's one stream (step-interleaved,
-# no overlap between chains: the smaller launches alone, A/B knob)
-GROUPS_ONE_STREAM = os.environ.get("ARL_GROUP_STREAMS", "") == "1"
 # > 1 rank: split the gradient all-reduce around the conv backward (ARL_OVERLAP_ALLREDUCE=0: one call)
 OVERLAP_ALLREDUCE = os.environ.get("ARL_OVERLAP_ALLREDUCE", "1") != "0"
 # one rank: GradientClipping's norm from the learner's conv reduce (ARL_NORM_FOLD=0: grad_sqnorm launch)
@@ -442,11 +439,9 @@ class A3C:
             self._forward_chain(pair_pool, reward_pool, done_pool, pool_len, first, stream, None)
         else:
             main = stream if stream is not None else torch.cuda.current_stream(net.device)
-            one = GROUPS_ONE_STREAM
-            side = [main] * (len(groups) - 1) if one else self._side_streams(len(groups) - 1)
+            side = self._side_streams(len(groups) - 1)
             for s in side:
-                if not one:
-                    s.wait_stream(main)              # fork before any chain is issued
+                s.wait_stream(main)                  # fork before any chain is issued
             chains = [self._chain_steps(pair_pool, reward_pool, done_pool, pool_len, first,
                                         main if g == 0 else side[g - 1], envs) for g, envs in enumerate(groups)]
             started = [None] * len(chains)

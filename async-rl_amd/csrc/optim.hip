@@ -7,12 +7,13 @@
 //
 // Two launches per update, both HBM-streaming over the padded flat buffer:
 //   grad_sqnorm_kernel: per-block partial sum of g^2 (f32 per thread over a
-//     grid-stride, f64 across the block) -> partials[block]; the block that
-//     finishes last (arrival ticket) sums the partials in block order and
-//     leaves the squared norm in partials[NORM_RESULT] (norm_finish), so the
-//     clip rate needs no host round trip and no extra launch (the folded form:
-//     reduce_conv_bwd_kernel leaves it the same way, conv_bwd.hip);
-//   rmsprop_kernel: reads that one f64, then 4 parameters per thread per
+//     grid-stride, f64 across the block) -> partials[block] (the folded form:
+//     reduce_conv_bwd_kernel leaves the same partials, conv_bwd.hip), so the
+//     clip rate needs no host round trip and no extra launch;
+//   rmsprop_kernel: every block sums the partials in block order (their loads
+//     in flight with its first p / ms / g loads; ARL_NORM_TICKET=1: the norm
+//     launch's last-arriving block leaves the sum in partials[NORM_RESULT]
+//     instead, norm_finish -- measured slower), then 4 parameters per thread per
 //     iteration: g' = clip ? g*f32(rate) : g; ms = ms*alpha; ms += (c*g')*g';
 //     p -= (lr*g') / sqrt(ms + eps) -- every op an explicit round-to-nearest
 //     f32 op in the reference's order (NumPy f32 semantics, no FMA), so the
@@ -186,9 +187,9 @@ static int stream_blocks(int64_t n) {
 }
 
 bool norm_ticket() {
-  static const bool on = [] {
-    const char* e = getenv("ARL_NORM_TICKET");
-    return !(e != nullptr && e[0] == '0');
+  static const bool on = [] {   // off by default: C4 0.4983-0.5000 vs 0.5014-0.5022 ms, C2 0.3108-0.3118 vs
+    const char* e = getenv("ARL_NORM_TICKET");   // 0.3140-0.3155 (r4c): the ticket adds 3.3 us to the conv
+    return e != nullptr && e[0] == '1';          // reduce, the re-reduce costs the update 0.5 us
   }();
   return on;
 }

@@ -19,10 +19,9 @@ echo "prof ok" >> $O/status
 for ab in $AB; do
   case $ab in
     phidma) bash scripts/env_ab.sh ARL_PHI_DMA=0 ARL_PHI_DMA=1 "" 2 phidma || exit $? ;;
-    c3streams) bash scripts/env_ab.sh ARL_GROUP_STREAMS=0 ARL_GROUP_STREAMS=1 "--workload c3" 2 c3streams || exit $? ;;
     variants) bash scripts/gpu_variants.sh "--steps 30 --warmup 5 --kernel-reps 3 --copy-peak 0" 1 > $O/variants.txt 2>&1 || exit $? ;;
-    norm) bash scripts/env_ab.sh ARL_NORM_TICKET=0 ARL_NORM_TICKET=1 "" 2 norm || exit $?
-          bash scripts/env_ab.sh ARL_NORM_TICKET=0 ARL_NORM_TICKET=1 "--workload c2" 2 normc2 || exit $? ;;
+    norm) bash scripts/env_ab.sh ARL_NORM_TICKET=1 ARL_NORM_TICKET=0 "" 2 norm || exit $?
+          bash scripts/env_ab.sh ARL_NORM_TICKET=1 ARL_NORM_TICKET=0 "--workload c2" 2 normc2 || exit $? ;;
     c3g) for r in 1 2; do for g in 1 2; do
            timeout -k 10 200 python -u bench.py --workload c3 --env-groups $g --steps 100 --warmup 10 --cpu-seconds 0 --kernel-reps 5 --copy-peak 0 --secondary none > $O/c3g$g.$r.log 2>&1 || exit $?
            python -c "import json; d=json.loads(open('$O/c3g$g.$r.log').read().strip().splitlines()[-1]); print('c3 env_groups $g', d['ms_per_step'], d['windows']['median_ms'], d['config'].get('graph'))"

@@ -690,27 +690,23 @@ def test_lstm_fused_cell_identical(gpu, tmp_path):
     pi_and_v) and into the BPTT step (backward) gives the same bits as the
     cell as separate launches (ARL_LSTM_SPLIT=1); so do the FC forward's
     ticket reduce instead of the reduce in the gate kernel's staging
-    (ARL_LSTM_XRED=0), the env-group chains issued chain by chain
-    (ARL_GROUP_ORDER=chain) and every chain issued on the window's one stream
-    (ARL_GROUP_STREAMS=1): hidden / cell states, gates, actions, values,
+    (ARL_LSTM_XRED=0) and the env-group chains issued chain by chain
+    (ARL_GROUP_ORDER=chain): hidden / cell states, gates, actions, values,
     gradients, parameters."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     outs = []
-    for extra in ({}, {"ARL_LSTM_SPLIT": "1"}, {"ARL_LSTM_XRED": "0"}, {"ARL_GROUP_ORDER": "chain"},
-                  {"ARL_GROUP_STREAMS": "1"}):
+    for extra in ({}, {"ARL_LSTM_SPLIT": "1"}, {"ARL_LSTM_XRED": "0"}, {"ARL_GROUP_ORDER": "chain"}):
         f = str(tmp_path / f"lstm_{len(outs)}.npz")
         env = dict(os.environ, **extra)
         subprocess.run([sys.executable, os.path.join(here, "lstm_split_worker.py"), f], env=env, check=True,
                        timeout=240)
         outs.append(np.load(f))
     assert int((outs[0]["hbuf"] != 0).sum()) > 0
-    for o in outs[1:-1]:
+    for o in outs[1:]:
         for k in outs[0].files:
             assert np.array_equal(outs[0][k], o[k]), k
-    for k in outs[0].files:
-        np.testing.assert_allclose(outs[-1][k], outs[0][k], rtol=1e-6, atol=1e-7, err_msg=k)
 
 
 def test_lstm_bptt_kernel_matches_generic(gpu, tmp_path):
@@ -833,9 +829,9 @@ def test_conv_fwd_two_envs_identical(gpu, tmp_path, n_envs):
     heads, which fall back), at 200 (a partial 64-row block) and at 512.  The
     frame ring too, against phi_ring_kernel's LDS-DMA staging (ARL_PHI_DMA); and the
     window as one C call (arl_run_window) against its launches issued step by
-    step from Python (ARL_WINDOW_C=0).  And the clip norm's ticket hand-off
-    against every update block re-reducing the partials (ARL_NORM_TICKET=0): the
-    f64 sums run in another order, so that arm is held to 1e-6 relative."""
+    step from Python (ARL_WINDOW_C=0).  And every update block re-reducing the
+    clip norm's partials against the ticket hand-off (ARL_NORM_TICKET=1): the f64
+    sums run in another order, so that arm is held to 1e-6 relative."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -843,7 +839,7 @@ def test_conv_fwd_two_envs_identical(gpu, tmp_path, n_envs):
     for i, arm in enumerate(({"ARL_CONV_EPW": "1", "ARL_FC_BIG": "0"}, {"ARL_CONV_EPW": "2", "ARL_FC_BIG": "0"},
                              {"ARL_CONV_EPW": "1", "ARL_FC_BIG": "1", "ARL_FC_HEADS": "0"},
                              {"ARL_CONV_EPW": "1", "ARL_FC_BIG": "1", "ARL_FC_HEADS": "1"},
-                             {"ARL_PHI_DMA": "1"}, {"ARL_WINDOW_C": "0"}, {"ARL_NORM_TICKET": "0"})):
+                             {"ARL_PHI_DMA": "1"}, {"ARL_WINDOW_C": "0"}, {"ARL_NORM_TICKET": "1"})):
         f = str(tmp_path / f"arm_{i}.npz")
         env = dict(os.environ, **arm)
         subprocess.run([sys.executable, os.path.join(here, "conv_epw_worker.py"), f, str(n_envs)], env=env,
