@@ -14,6 +14,11 @@ if [ "${CFSTAMP:-0}" = 1 ] && [ -f async-rl_amd/csrc/build_var_cfstamp/libasyncr
     ASYNCRL_HIP_LIB=$PWD/async-rl_amd/csrc/build_var_cfstamp/libasyncrl_hip.so timeout -k 10 200 python scripts/cf_stamps.py $n > $O/cfstamps$n.txt 2>&1 || exit $?
   done
 fi
+if [ "${CBSTAMP:-0}" = 1 ] && [ -f async-rl_amd/csrc/build_var_cbstamp/libasyncrl_hip.so ]; then
+  for n in 512 256; do
+    ASYNCRL_HIP_LIB=$PWD/async-rl_amd/csrc/build_var_cbstamp/libasyncrl_hip.so timeout -k 10 200 python scripts/cb_stamps.py $n > $O/cbstamps$n.txt 2>&1 || exit $?
+  done
+fi
 (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/prof" -o c4 -- python3 "$GRAFT_REPO_ROOT/bench.py" --cpu-seconds 0 --copy-peak 0 > "$GRAFT_REPO_ROOT/$O/bench_prof.log" 2>&1) || exit $?
 echo "prof ok" >> $O/status
 for ab in $AB; do
