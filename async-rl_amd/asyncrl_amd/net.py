@@ -332,12 +332,6 @@ class DeviceNet:
         check(lib.arl_stamps_begin(self._h, int(cap)), "arl_stamps_begin")
         self.stamping = True
 
-    def stamps_sparse(self, period: int):
-        """Right after stamps_begin, for windows of `period` stamp calls: window w
-        records only its calls t - 1 and t (t = w mod period; arl_stamps_sparse);
-        stamps_end then gives ms = -1 for the intervals between unrelated calls."""
-        check(lib.arl_stamps_sparse(self._h, int(period)), "arl_stamps_sparse")
-
     def stamp(self, stage: int = STAGE_HOST, stream=None):
         """A caller's stamp (e.g. after a collective); no-op unless stamping."""
         if self.stamping:
