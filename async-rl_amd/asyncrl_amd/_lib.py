@@ -69,6 +69,7 @@ SIGNATURES = {
                                      c_int, c_void_p]),
     "arl_run_stage": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "arl_stamps_begin": (c_int, [c_void_p, c_int]),
+    "arl_stamps_sparse": (c_int, [c_void_p, c_int]),
     "arl_stamp": (c_int, [c_void_p, c_int, c_void_p]),
     "arl_stamps_end": (c_int, [c_void_p, ctypes.POINTER(c_int)]),
     "arl_stamps_read": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),

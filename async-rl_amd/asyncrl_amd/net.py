@@ -63,6 +63,16 @@ LEARN_FORK = os.environ.get("ARL_LEARN_FORK", "0") == "1"
 FUSE_OBS = os.environ.get("ARL_FUSE_OBS", "0") == "1"
 
 
+
+def check_pools(pool_len: int, *pools):
+    """pool_len against each pool's leading dimension: the C ABI sees only
+    pointers, so a pool_len past a pool's end would read past its buffer."""
+    if pool_len < 1:
+        raise ValueError(f"pool_len must be >= 1, got {pool_len}")
+    for p in pools:
+        if p is not None and isinstance(p, torch.Tensor) and (p.dim() == 0 or p.shape[0] < pool_len):
+            raise ValueError(f"pool_len {pool_len} exceeds a pool of shape {tuple(p.shape)}")
+
 class DeviceNet:
     """One arl_net handle + the device memory it borrows."""
 
@@ -145,6 +155,7 @@ class DeviceNet:
         """pair_pool: (pool_len, n, 2, 210, 160, 3) uint8 frame pairs; for an
         RGB net (arch | ARCH_RGB) the screens (pool_len, n, H, W, 3) instead.
         envs=(e0, ne): only envs [e0, e0 + ne) (arl_observe_envs)."""
+        check_pools(pool_len, pair_pool, reward_pool, done_pool)
         if (self.stack or self.states) and envs is None:
             self.observe_stack(t, pair_pool, reward_pool, done_pool, pool_len, force_reset, stream)
             return
@@ -169,6 +180,7 @@ class DeviceNet:
         frame stacks (arl_observe_stack); ARCH_STATES nets: (pool_len, n, 4,
         84, 84) f32 states, phi's output (arl_observe_states).  None ingests
         only the reward / done of step t (a terminal observation)."""
+        check_pools(pool_len, stack_pool, reward_pool, done_pool)
         if self.states:
             if stack_pool is not None and stack_pool.dtype != torch.float32:
                 raise ValueError("observe_stack: an ARCH_STATES net takes float32 states")
@@ -219,6 +231,7 @@ class DeviceNet:
             self.observe(t, pair_pool, reward_pool, done_pool, pool_len, force_reset, resize_mode, stream, envs)
             self.act(t, mode, stream, envs)
             return
+        check_pools(pool_len, pair_pool, reward_pool, done_pool)
         e0, ne = envs if envs is not None else (0, -1)
         check(lib.arl_observe_act_envs(self._h, t, e0, ne, ptr(pair_pool), ptr(reward_pool), ptr(done_pool), pool_len,
                                        int(force_reset), resize_mode, mode, stream_handle(stream)),
@@ -306,6 +319,7 @@ class DeviceNet:
         """A whole lockstep window in one call (arl_run_window): T x (observe,
         act), the bootstrap, learn, clip + RMSProp and the advance -- the
         launches of observe / act / learn / optimize(advance=True) in order."""
+        check_pools(pool_len, pair_pool, reward_pool, done_pool)
         check(lib.arl_run_window(self._h, ptr(pair_pool), ptr(reward_pool), ptr(done_pool), pool_len, int(first),
                                  resize_mode, gamma, beta, v_loss_coef, int(clip_reward), lr0, int(total_steps),
                                  int(n_total), alpha, eps, clip, stream_handle(stream)), "arl_run_window")
@@ -331,6 +345,12 @@ class DeviceNet:
         kernel(s) (arl_stamps_begin); read them with stamps_end()."""
         check(lib.arl_stamps_begin(self._h, int(cap)), "arl_stamps_begin")
         self.stamping = True
+
+    def stamps_sparse(self, period: int):
+        """Right after stamps_begin, for windows of `period` stamp calls: window w
+        records only its calls t - 1 and t (t = w mod period; arl_stamps_sparse);
+        stamps_end then gives ms = -1 for the intervals between unrelated calls."""
+        check(lib.arl_stamps_sparse(self._h, int(period)), "arl_stamps_sparse")
 
     def stamp(self, stage: int = STAGE_HOST, stream=None):
         """A caller's stamp (e.g. after a collective); no-op unless stamping."""

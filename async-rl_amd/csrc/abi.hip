@@ -370,8 +370,20 @@ int arl_stamps_begin(arl_net* h, int cap) {
     st.ev.push_back(e);
   }
   st.stage.assign(st.ev.size(), 0);
+  st.seq.assign(st.ev.size(), 0);
   st.count = 0;
+  st.calls = 0;
+  st.period = 0;
   st.on = true;
+  return ARL_OK;
+}
+
+int arl_stamps_sparse(arl_net* h, int period) {
+  NEED_BOUND(h);
+  arl::Stamps* st = h->net.stamps;
+  if (!st || !st->on || st->calls != 0) return fail(ARL_EINVAL, "stamps_sparse: call right after arl_stamps_begin");
+  if (period < 0 || period > 4096) return fail(ARL_EINVAL, "stamps_sparse: period out of [0, 4096]");
+  st->period = period;
   return ARL_OK;
 }
 
@@ -398,7 +410,8 @@ int arl_stamps_read(arl_net* h, int i0, int n, float* ms, int* stage) {
   hipError_t e = hipEventSynchronize(st->ev[i0 + n - 1]);
   for (int i = i0; i < i0 + n && e == hipSuccess; ++i) {
     float t = 0.f;
-    if (i > 0) e = hipEventElapsedTime(&t, st->ev[i - 1], st->ev[i]);
+    if (i > 0 && st->seq[i] != st->seq[i - 1] + 1) t = -1.f;   // (sparse: not one stage's interval)
+    else if (i > 0) e = hipEventElapsedTime(&t, st->ev[i - 1], st->ev[i]);
     ms[i - i0] = t;
     stage[i - i0] = st->stage[i];
   }

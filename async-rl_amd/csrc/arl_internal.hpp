@@ -96,8 +96,11 @@ struct ParamInfo {
 struct Stamps {
   std::vector<hipEvent_t> ev;
   std::vector<int> stage;
+  std::vector<int64_t> seq;   // the stamp call each recorded event answers
   int count = 0;
   bool on = false;
+  int period = 0;             // > 0: sparse (arl_stamps_sparse): window w records only calls t - 1, t of its
+  int64_t calls = 0;          //   period, t = w mod period
 };
 
 struct Net {
@@ -176,7 +179,13 @@ enum Stage { STAGE_CONV_FWD = 1, STAGE_FC_FWD = 2, STAGE_POLICY = 3, STAGE_FC_BW
 inline hipError_t stamp(const Net& net, int stage, hipStream_t s) {
   Stamps* st = net.stamps;
   if (st == nullptr || !st->on || st->count >= (int)st->ev.size()) return hipSuccess;
+  const int64_t q = st->calls++;
+  if (st->period > 0) {
+    const int64_t P = st->period, i = q % P, t = (q / P) % P;
+    if (i != t && i != t - 1) return hipSuccess;
+  }
   st->stage[st->count] = stage;
+  st->seq[st->count] = q;
   return hipEventRecord(st->ev[st->count++], s);
 }
 hipError_t net_stage(Net& net, int stage, int t, hipStream_t s);

@@ -663,41 +663,51 @@ def main(a):
     net = model.net
     if a.stamp_windows > 0 and not use_graph and n_groups == 1 and not nat:
         from asyncrl_amd._lib import STAGE_NAMES
-        M = a.stamp_windows
-        net.stamps_begin(M * 64 + 8)
-        with torch.cuda.stream(stream):
-            net.stamp(16, stream=stream)           # the mark the first interval starts from (ARL_STAGE_OTHER)
-            for _ in range(M):
-                window()
-        stream.synchronize()
-        ms_st, st_names = net.stamps_end()
+
+        def stamped(n_win, period=0):
+            net.stamps_begin(n_win * 64 + 8)
+            if period:
+                net.stamps_sparse(period)
+            with torch.cuda.stream(stream):
+                if not period:
+                    net.stamp(16, stream=stream)   # the mark the first interval starts from (ARL_STAGE_OTHER)
+                for _ in range(n_win):
+                    window()
+            stream.synchronize()
+            ms_st, names = net.stamps_end()
+            return ms_st[1:], ["allreduce_wait" if x == STAGE_NAMES[15] else x for x in names[1:]]
+
+        # dense: every stage launch stamped (each event lengthens the interval it closes by ~1 us);
+        # sparse: n_st stamp calls a window, window w records only calls t - 1 and t (t = w mod n_st),
+        # so each launch's in-window interval is timed with no other event in its window
+        m_dense = min(a.stamp_windows, 20)
+        ms_d, names_d = stamped(m_dense)
+        n_st = len(ms_d) // m_dense
+        dense_ms = float(ms_d.sum()) / m_dense
+        reps = max(4, -(-a.stamp_windows // n_st))
+        ms_s, names_s = stamped(n_st * reps, n_st)
         per = {}
-        for x, name in zip(ms_st[1:], st_names[1:]):
-            name = "allreduce_wait" if name == STAGE_NAMES[15] else name
-            d = per.setdefault(name, [0.0, 0])
-            d[0] += float(x)
-            d[1] += 1
-        total_ms = float(ms_st[1:].sum())
-        P = (len(ms_st) - 1) / M
-        timeline = {"windows": M, "stamps_per_window": P, "mean_window_ms": round(total_ms / M, 4),
-                    "stages": {k: {"window_share_us": round(1e3 * v[0] / M, 2),
-                                   "launches_per_window": round(v[1] / M, 3),
-                                   "us_per_launch": round(1e3 * v[0] / v[1], 3)} for k, v in per.items()},
-                    "note": "stamped eager windows: interval from the previous stage's event to this stage's, "
-                            "so each launch's share includes its dependent-launch boundary; allreduce_wait = the "
-                            "compute stream's wait for the collectives (A3C._reduce_and_step)"}
+        for x, name in zip(ms_s, names_s):
+            if x >= 0:
+                per.setdefault(name, []).append(float(x))
+        count = {}
+        for name in names_d[:n_st]:
+            count[name] = count.get(name, 0) + 1
+        stages = {k: {"window_share_us": round(1e3 * float(np.mean(per[k])) * count[k], 2),
+                      "launches_per_window": count[k], "us_per_launch": round(1e3 * float(np.mean(per[k])), 3),
+                      "samples": len(per[k])} for k in count if k in per}
+        total_ms = sum(v["window_share_us"] for v in stages.values()) / 1e3
+        timeline = {"windows": n_st * reps, "stamps_per_window": n_st, "sum_of_shares_ms": round(total_ms, 4),
+                    "stages": stages, "dense_windows": m_dense, "dense_mean_window_ms": round(dense_ms, 4),
+                    "note": "sparse stamps (arl_stamps_sparse): each stage launch's interval from the previous "
+                            "launch's event to its own, timed in windows that record only those two events, so "
+                            "a launch's share includes its dependent-launch boundary; dense_mean_window_ms = "
+                            "windows with every launch stamped; allreduce_wait = the compute stream's wait for "
+                            "the collectives (A3C._reduce_and_step)"}
         if windows is not None:
-            # every event adds a little to the interval it closes: the stamped windows run longer than
-            # the unstamped median by o per event; the *_corrected figures take o off every launch
-            o_ms = max(0.0, (total_ms / M - windows["median_ms"]) / P)
             timeline["unstamped_median_ms"] = windows["median_ms"]
-            timeline["sum_vs_unstamped_median"] = round(total_ms / M / windows["median_ms"], 4)
-            timeline["stamp_overhead_us"] = round(1e3 * o_ms, 3)
-            for k, v in timeline["stages"].items():
-                v["us_per_launch_corrected"] = round(v["us_per_launch"] - 1e3 * o_ms, 3)
-                v["window_share_us_corrected"] = round(v["window_share_us"] - 1e3 * o_ms * v["launches_per_window"], 2)
-            timeline["corrected_sum_vs_unstamped_median"] = round(
-                sum(v["window_share_us_corrected"] for v in timeline["stages"].values()) / 1e3 / windows["median_ms"], 4)
+            timeline["sum_vs_unstamped_median"] = round(total_ms / windows["median_ms"], 4)
+            timeline["dense_vs_unstamped_median"] = round(dense_ms / windows["median_ms"], 4)
 
     # ---------------------------------------------------------------- per-kernel roofline
     # Each stage's algorithmic work per launch over its
@@ -787,7 +797,7 @@ def main(a):
                 us_alone = timed(fn)
                 tname = "conv_fwd" if name == "phi_conv" else name
                 win = tl.get(tname)
-                us = win.get("us_per_launch_corrected", win["us_per_launch"]) if win is not None else us_alone
+                us = win["us_per_launch"] if win is not None else us_alone
 
                 def rate(t_us):
                     if bound == "hbm":
@@ -798,8 +808,7 @@ def main(a):
                 kernels[name] = {"kernel": kname, "bound": bound, "avg_launch_us": round(us, 2),
                                  "time_source": "window" if win is not None else "standalone",
                                  "launches_per_window": win["launches_per_window"] if win is not None else calls,
-                                 "window_share_us": win.get("window_share_us_corrected", win["window_share_us"])
-                                 if win is not None else round(us * calls, 1),
+                                 "window_share_us": win["window_share_us"] if win is not None else round(us * calls, 1),
                                  "achieved": round(ach, 2), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
                                  ("bytes" if bound == "hbm" else "flop") + "_per_launch": int(work),
                                  "standalone_us": round(us_alone, 2), "standalone_frac": round(ach1 / peak, 4)}
@@ -825,8 +834,8 @@ def main(a):
                 "peak_note": (("exact f32 MFMA (v_mfma_f32_16x16x4_f32) vs the dense fp32 matrix peak" if nat else
                                "f32-equivalent FLOP/s vs the dense fp32 matrix peak (bf16-split f32 emulation, "
                                "DESIGN.md)") if d["bound"] == "mfma" else "HBM3E spec peak") +
-                             ("; time = the in-window interval per launch (window timeline, the per-event "
-                              "overhead taken off), launch boundary included" if d["time_source"] == "window" else "")}
+                             ("; time = the in-window interval per launch (sparse window timeline), launch "
+                              "boundary included" if d["time_source"] == "window" else "")}
         if copy_peak is not None:
             # HBM-bound stages also against the copy rate measured on this GPU
             for k in kernels.values():

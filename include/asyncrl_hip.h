@@ -272,8 +272,14 @@ int arl_run_stage(arl_net* net, int stage, int t, void* stream);
  * returns the count.  arl_stamps_read waits for stamp i0 + n - 1 and returns,
  * for i in [i0, i0 + n), ms[i - i0] = the time from stamp i - 1 to stamp i (0
  * for i = 0) and stage[i - i0]: consecutive intervals split an eager window
- * into its stages as it ran, launch boundaries included. */
+ * into its stages as it ran, launch boundaries included.
+ * arl_stamps_sparse(net, P), right after arl_stamps_begin, for windows of P
+ * stamp calls: window w records only its calls t - 1 and t, t = w mod P, so
+ * each window carries at most two events and P windows time every stage once
+ * nearly unperturbed; arl_stamps_read then returns ms = -1 for an interval
+ * that is not between consecutive calls. */
 int arl_stamps_begin(arl_net* net, int cap);
+int arl_stamps_sparse(arl_net* net, int period);
 int arl_stamp(arl_net* net, int stage, void* stream);
 int arl_stamps_end(arl_net* net, int* count);
 int arl_stamps_read(arl_net* net, int i0, int n, float* ms, int* stage);

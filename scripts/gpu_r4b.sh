@@ -4,7 +4,10 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${TAG:-r4b}; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:--k bench} > $O/pytest.log 2>&1; rc=$?
+# PYTEST_K: the -k expression (default "bench"; ALL: the whole -m gpu suite)
+K=${PYTEST_K:-bench}
+if [ "$K" = ALL ]; then KA=(); else KA=(-k "$K"); fi
+timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread "${KA[@]}" > $O/pytest.log 2>&1; rc=$?
 echo "pytest rc=$rc" > $O/status
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 400 python bench.py > $O/bench.log 2>&1 || exit $?

@@ -138,3 +138,18 @@ def test_bench_launcher_propagates_rank_failure():
     assert r.returncode != 0
     assert "a rank failed" in r.stderr, r.stderr[-2000:]
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_pool_len_checked_against_the_pools():
+    """The C ABI sees only the pools' pointers: the Python mirror refuses a
+    pool_len past any pool's leading dimension before a kernel could read past
+    its buffer (a bench pass once handed pool_len 28 to an 8-entry pool)."""
+    import torch
+    from asyncrl_amd.net import check_pools
+    pairs, rewards = torch.zeros(8, 2, 3, dtype=torch.uint8), torch.zeros(8, 2)
+    check_pools(8, pairs, rewards, None)
+    for bad in (0, 9, 28):
+        with pytest.raises(ValueError):
+            check_pools(bad, pairs, rewards, None)
+    with pytest.raises(ValueError):
+        check_pools(8, pairs, torch.zeros(4, 2))

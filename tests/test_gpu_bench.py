@@ -62,10 +62,10 @@ def test_bench_rccl_one_rank(gpu):
 
 
 def test_bench_window_timeline(gpu):
-    """The per-stage table is the window's own: stamped eager windows give
-    each stage's launches per window (phi T = 5, the forward stages T + 1, the
-    learner's launches once) and the stage shares add up to the window; the
-    per-event overhead taken off every launch, to the unstamped window."""
+    """The per-stage table is the window's own: sparsely stamped eager windows
+    give each stage's launches per window (phi T = 5, the forward stages T + 1,
+    the learner's launches once) and the stage shares add up to the unstamped
+    window within 5 %."""
     r = subprocess.run([sys.executable, BENCH, "--gpus", "1"] + SMALL + ["--stamp-windows", "30"], capture_output=True,
                        text=True, timeout=300, env=_env())
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -75,10 +75,9 @@ def test_bench_window_timeline(gpu):
             "conv_reduce": 1, "rmsprop": 1}
     assert {k: v["launches_per_window"] for k, v in tl["stages"].items()} == want, tl
     share = sum(v["window_share_us"] for v in tl["stages"].values())
-    assert abs(share / 1e3 - tl["mean_window_ms"]) <= 0.01 * tl["mean_window_ms"], tl
-    assert 0.95 <= tl["sum_vs_unstamped_median"] <= 1.12, tl
-    assert 0.99 <= tl["corrected_sum_vs_unstamped_median"] <= 1.01, tl
-    assert 0.0 <= tl["stamp_overhead_us"] < 3.0, tl
+    assert abs(share / 1e3 - tl["sum_of_shares_ms"]) <= 0.01 * tl["sum_of_shares_ms"], tl
+    assert min(v["samples"] for v in tl["stages"].values()) >= 4, tl
+    assert 0.95 <= tl["sum_vs_unstamped_median"] <= 1.05, tl
     for k, v in d["kernels"].items():
         assert v["time_source"] == "window" or k not in want, (k, v)
         if v.get("bound") == "hbm" and k in want:
