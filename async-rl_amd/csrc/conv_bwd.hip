@@ -398,23 +398,31 @@ conv_bwd_kernel(ConvBwdArgs a) {
       prefetch_x(a, step0, sn, px_);
     }
 #if ARL_S1_SPLIT
-    // ---- a1 -> split phase planes ([3][ic][y & 1][x & 1][Y][X]) and a1 > 0 per pixel as 16
-    // channel bits; thread t < 400: pixel (y, x) = divmod(t, 20), every channel
+    // ---- a1 -> split phase planes ([3][ic][y & 1][x & 1][Y][X]): item (ic, phase, quad) = 4
+    // consecutive L = 10 Y + X of one phase plane, one 8-byte store per split plane; then a1 > 0 per
+    // pixel as 16 channel bits (threads < 400)
+    for (int it = tid; it < C1_OC * 4 * 25; it += NT) {
+      const int ic = it / 100, r = it - 100 * ic, ph = r / 25, q = r - 25 * ph;
+      const int py = ph >> 1, pxx = ph & 1;
+      float v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int L = 4 * q + k, Y = L / 10, X = L - 10 * Y;
+        v[k] = a1s[ic * A1C + (2 * Y + py) * A1R + 2 * X + pxx];
+      }
+      uint2 h, m, l;
+      split3_pack(v[0], v[1], h.x, m.x, l.x);
+      split3_pack(v[2], v[3], h.y, m.y, l.y);
+      uint8_t* d = lds + L_PH + (ic * 4 + ph) * PH_B + 8 * q;
+      *reinterpret_cast<uint2*>(d) = h;
+      *reinterpret_cast<uint2*>(d + PHP) = m;
+      *reinterpret_cast<uint2*>(d + 2 * PHP) = l;
+    }
     if (tid < C1_P) {
-      const int y = tid / 20, x = tid - 20 * (tid / 20);
-      const float* ap = a1s + y * A1R + x;
-      uint8_t* ph = lds + L_PH + (2 * (y & 1) + (x & 1)) * PH_B + 2 * (10 * (y >> 1) + (x >> 1));
+      const float* ap = a1s + (tid / 20) * A1R + tid % 20;
       uint32_t m = 0;
 #pragma unroll
-      for (int ic = 0; ic < C1_OC; ++ic) {
-        const float v = ap[ic * A1C];
-        m |= (v > 0.f ? 1u : 0u) << ic;
-        uint32_t h, mm, l;
-        split3(v, h, mm, l);
-        *reinterpret_cast<uint16_t*>(ph + ic * 4 * PH_B) = (uint16_t)h;
-        *reinterpret_cast<uint16_t*>(ph + ic * 4 * PH_B + PHP) = (uint16_t)mm;
-        *reinterpret_cast<uint16_t*>(ph + ic * 4 * PH_B + 2 * PHP) = (uint16_t)l;
-      }
+      for (int ic = 0; ic < C1_OC; ++ic) m |= (ap[ic * A1C] > 0.f ? 1u : 0u) << ic;
       reinterpret_cast<uint16_t*>(lds + L_MASK)[tid] = (uint16_t)m;
     }
     lds_barrier();                 // B1b: the phase planes are complete
