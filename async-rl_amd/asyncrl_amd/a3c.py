@@ -457,7 +457,7 @@ class A3C:
                 step = 0
                 while live:
                     for g in list(live):
-                        if step == 0 and g > 0 and started[g - 1] is not None and not one:
+                        if step == 0 and g > 0 and started[g - 1] is not None:
                             side[g - 1].wait_event(started[g - 1])   # stagger: after chain g-1's first kernel
                         ev = next(chains[g], StopIteration)
                         if ev is StopIteration:
@@ -466,8 +466,7 @@ class A3C:
                             started[g] = ev
                     step += 1
             for s in side:
-                if not one:
-                    main.wait_stream(s)
+                main.wait_stream(s)
             stream = main
         self._learn(stream)
         if split_update:
