@@ -388,9 +388,10 @@ conv_fwd_kernel(ConvFwdArgs a) {
     // four ring planes whatever nvalid says), then bf16 conversion / splitting
     // into LDS; planes older than the last reset are zeroed here
     const int nv = a.nvalid[(int64_t)rs * a.n + e];
+    // EPW = 2: slot 0 loads (and splits) W1 only, slot 1 W2 only (wave-uniform)
     float4 w1a, w1b, w2v[4];
-    w1_load(a.W1, rgb, t8, w1a, w1b);
-    w2_load(a.W2, t8, w2v);
+    if (EPW == 1 || el == 0) w1_load(a.W1, rgb, t8, w1a, w1b);
+    if (EPW == 1 || el == 1) w2_load(a.W2, t8, w2v);
     constexpr int NX = (4 * V + NT - 1) / NT;  // 4
     uint4 xv[NX];
 #pragma unroll
