@@ -38,6 +38,8 @@ for ab in $AB; do
            timeout -k 10 200 python -u bench.py --workload c3 --env-groups $g --steps 100 --warmup 10 --cpu-seconds 0 --kernel-reps 5 --copy-peak 0 --secondary none > $O/c3g$g.$r.log 2>&1 || exit $?
            python -c "import json; d=json.loads(open('$O/c3g$g.$r.log').read().strip().splitlines()[-1]); print('c3 env_groups $g', d['ms_per_step'], d['windows']['median_ms'], d['config'].get('graph'))"
          done; done ;;
+    fcbabl) FCB_N=512 ABLS="0 1 2 3 4" bash scripts/gpu_fcb_abl.sh > $O/fcbabl512.txt 2>&1 || exit $?
+            timeout -k 10 60 python -u scripts/fc_bwd_bench.py 512 200 >> $O/fcbabl512.txt 2>&1 || exit $? ;;
     rmsu) bash scripts/env_ab.sh ARL_RMS_U=1 ARL_RMS_U=2 "" 2 rmsu || exit $? ;;
     fcbz) for z in 2 4 5; do bash scripts/env_ab.sh ARL_FC_BWD_Z=3 ARL_FC_BWD_Z=$z "" 1 fcbz$z || exit $?; done ;;
   esac
