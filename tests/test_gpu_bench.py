@@ -77,9 +77,12 @@ def test_bench_window_timeline(gpu):
     share = sum(v["window_share_us"] for v in tl["stages"].values())
     assert abs(share / 1e3 - tl["sum_of_shares_ms"]) <= 0.01 * tl["sum_of_shares_ms"], tl
     assert min(v["samples"] for v in tl["stages"].values()) >= 4, tl
-    # (an event between two launches exposes the dispatch of the second, which an unstamped stream
-    # overlaps with the first's tail: +0.5 us a launch at C2's short kernels, 1.054 measured (r4f))
-    assert 0.95 <= tl["sum_vs_unstamped_median"] <= 1.08, tl
+    # an event between two launches exposes the dispatch of the second, which an unstamped stream
+    # overlaps with the first's tail: ~1 us a measured launch (C2 1.054 / 1.108, C4 1.065: r4f, r4g);
+    # the bench estimates it from the sum and takes it off every launch
+    assert 0.95 <= tl["sum_vs_unstamped_median"] <= 1.15, tl
+    assert 0.0 <= tl["exposure_us_per_launch"] < 2.5, tl
+    assert 0.99 <= tl["corrected_sum_vs_unstamped_median"] <= 1.01, tl
     for k, v in d["kernels"].items():
         assert v["time_source"] == "window" or k not in want, (k, v)
         if v.get("bound") == "hbm" and k in want:
