@@ -40,7 +40,7 @@ for ab in $AB; do
          done; done ;;
     fcbabl) FCB_N=512 ABLS="0 1 2 3 4" bash scripts/gpu_fcb_abl.sh > $O/fcbabl512.txt 2>&1 || exit $?
             timeout -k 10 60 python -u scripts/fc_bwd_bench.py 512 200 >> $O/fcbabl512.txt 2>&1 || exit $? ;;
-    fcbpmc) for j in a b ab; do for c in FETCH_SIZE WRITE_SIZE; do
+    fcbpmc) for j in a b x; do for c in FETCH_SIZE WRITE_SIZE; do
               (cd /tmp && ARL_FC_BWD_JOBS=$j timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$O/fcbpmc_${j}_$c" -o run -- python3 "$GRAFT_REPO_ROOT/scripts/fc_bwd_bench.py" 512 20 > "$GRAFT_REPO_ROOT/$O/fcbpmc_${j}_$c.log" 2>&1) || exit $?
               python scripts/pmc_one.py $O/fcbpmc_${j}_$c fc_bwd_kernel >> $O/fcbpmc.txt 2>&1
             done; done ;;
