@@ -63,8 +63,17 @@ constexpr int OOB = 0x7ffffff0;         // a buffer offset past every range: the
 constexpr int NT = 256;                 // 4 waves
 constexpr int NW = NT / 64;
 constexpr int BK = 32;                  // K chunk (rows of a stage)
-constexpr int STAGE = 8192;             // floats per LDS stage
-constexpr int AJ = 128, AK = 64;        // job A tile: 128 j x 64 k
+// job A tile: AJ j x AK k (AJ AK = 8192).  ARL_FCB_AJ=256 (A/B knob): tiles spanning every j of the FC,
+// 256 x 32, so each a2 column block is streamed once instead of once per j tile (the dfc rows, L2-resident,
+// twice as wide); the waves then split j only (64 j x 32 k each)
+#ifndef ARL_FCB_AJ
+#define ARL_FCB_AJ 128
+#endif
+constexpr int AJ = ARL_FCB_AJ, AK = 8192 / ARL_FCB_AJ;
+constexpr int AWN = AK / 32;            // job A waves along k (64: 2, 32: 1)
+constexpr int STAGE = BK * (AJ + AK) > 8192 ? BK * (AJ + AK) : 8192;   // floats per LDS stage
+constexpr int AKEY = AK == 64 ? 1 : 0;  // job A's X image: 64-float rows need the 8 * (row & 1) key, 32-float
+                                        // rows are conflict-free (a b64 lane group spans two 128-B rows)
 constexpr int BN = 128;                 // job B tile: 32 MT samples x 128 k
 constexpr int PART = AJ * AK + AJ;      // floats per published partial (dW tile + db)
 constexpr int FLUSH = 4;                // job A: f32 MFMA sums over 4 chunks (128 samples), then f64
@@ -99,7 +108,7 @@ struct Dims {
   static_assert(SH::J % AJ == 0 && SH::J % BK == 0 && SH::KW % 4 == 0 && SH::NB % 4 == 0, "tiles");
   static_assert(SH::KW1 % AK == 0 || SH::KW1 == SH::KW, "a k tile never straddles the two dW blocks");
 };
-static_assert(A2 % AK == 32, "FC: the last job A k tile is half full");
+static_assert(A2 % AK == 32 || A2 % AK == 0, "FC: the last job A k tile is half or wholly full");
 constexpr int NTA_MAX = Dims<ShapeFC>::NTA;
 static_assert(Dims<ShapeLSTM>::NTA <= NTA_MAX, "ticket / partial workspace");
 constexpr int RST_MAX = 1024;           // LSTM job A: reset flags of a sample range, staged in LDS
@@ -211,7 +220,7 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds, uint8_t* rst) {
   constexpr int NTA = D::NTA;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, col = lane & 15;
-  const int wm = wave >> 1, wn = wave & 1;   // wave: 64 j x 32 k
+  const int wm = wave / AWN, wn = wave % AWN;   // wave: 64 j x 32 k
   int tile = job % NTA, z = job / NTA;
   if (a.xcd) {   // linear order (z, kt, jt), jt fastest
     const int lin = xcd_order(job, NTA * a.Z);
@@ -249,9 +258,9 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds, uint8_t* rst) {
     float* st = lds + (c & 1) * STAGE;
     stage_tile<BK, AJ, 0>(st, a.dfc, SH::J, r0 + c * BK, r1 - 1, j0);       // dY[s][j0 .. j0+127]
     if (SH::kLstm && hpart)
-      stage_tile<BK, AK, 1, true>(st + BK * AJ, xsrc, XLD, r0 + c * BK, r1 - 1, xc0, rst, r0, a.zero);
+      stage_tile<BK, AK, AKEY, true>(st + BK * AJ, xsrc, XLD, r0 + c * BK, r1 - 1, xc0, rst, r0, a.zero);
     else
-      stage_tile<BK, AK, 1>(st + BK * AJ, xsrc, XLD, r0 + c * BK, r1 - 1, xc0);   // X[s][k0 .. k0+63]
+      stage_tile<BK, AK, AKEY>(st + BK * AJ, xsrc, XLD, r0 + c * BK, r1 - 1, xc0);   // X[s][k0 .. k0+AK-1]
   };
   const int nb = wn * 32 + 2 * col;
   f32x4 acc[4][2], bs;
@@ -282,7 +291,7 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds, uint8_t* rst) {
       for (int ks = 0; ks < BK / 4; ++ks) {
         const int r = 4 * ks + q;
         av[ks] = *reinterpret_cast<const f32x4*>(As + r * AJ + wm * 64 + 4 * col);
-        bv[ks] = *reinterpret_cast<const f32x2*>(Bs + r * AK + (((nb >> 2) ^ (8 * (r & 1))) << 2) + (nb & 3));
+        bv[ks] = *reinterpret_cast<const f32x2*>(Bs + r * AK + (((nb >> 2) ^ (AKEY * 8 * (r & 1))) << 2) + (nb & 3));
       }
       if (kvalid < BK) {   // the range's last chunk only
 #pragma unroll
@@ -712,7 +721,7 @@ __device__ void job_heads(const FcBwdArgs& a, int jt, float* lds) {
 template <int MT, bool SPLIT, class SH>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2)))
 fc_bwd_kernel(FcBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];   // 64 KB
+  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];   // 64 KB (72 KB with ARL_FCB_AJ=256)
   __shared__ uint8_t rst[SH::kLstm ? RST_MAX : 4];                 // LSTM: a range's reset flags
   const int b = a.b0 + blockIdx.x;
   const int na = Dims<SH>::NTA * a.Z;

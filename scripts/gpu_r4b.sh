@@ -40,10 +40,14 @@ for ab in $AB; do
          done; done ;;
     fcbabl) FCB_N=512 ABLS="0 1 2 3 4" bash scripts/gpu_fcb_abl.sh > $O/fcbabl512.txt 2>&1 || exit $?
             timeout -k 10 60 python -u scripts/fc_bwd_bench.py 512 200 >> $O/fcbabl512.txt 2>&1 || exit $? ;;
-    fcbpmc) for j in a b x; do for c in FETCH_SIZE WRITE_SIZE; do
-              (cd /tmp && ARL_FC_BWD_JOBS=$j timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$O/fcbpmc_${j}_$c" -o run -- python3 "$GRAFT_REPO_ROOT/scripts/fc_bwd_bench.py" 512 20 > "$GRAFT_REPO_ROOT/$O/fcbpmc_${j}_$c.log" 2>&1) || exit $?
-              python scripts/pmc_one.py $O/fcbpmc_${j}_$c fc_bwd_kernel >> $O/fcbpmc.txt 2>&1
-            done; done ;;
+    fcbpmc) for v in default $VARIANTS; do
+              L=$PWD/async-rl_amd/asyncrl_amd/libasyncrl_hip.so; [ $v = default ] || L=$PWD/async-rl_amd/csrc/build_var_$v/libasyncrl_hip.so
+              for j in a b x; do for c in FETCH_SIZE WRITE_SIZE; do
+                (cd /tmp && ASYNCRL_HIP_LIB=$L ARL_FC_BWD_JOBS=$j timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$O/fcbpmc_${v}_${j}_$c" -o run -- python3 "$GRAFT_REPO_ROOT/scripts/fc_bwd_bench.py" 512 20 > "$GRAFT_REPO_ROOT/$O/fcbpmc_${v}_${j}_$c.log" 2>&1) || exit $?
+                echo "$v jobs=$j $(python scripts/pmc_one.py $O/fcbpmc_${v}_${j}_$c fc_bwd_kernel 2>&1)" >> $O/fcbpmc.txt
+              done; done
+              for j in a b x; do echo "$v jobs=$j $(ASYNCRL_HIP_LIB=$L ARL_FC_BWD_JOBS=$j timeout -k 10 60 python -u scripts/fc_bwd_bench.py 512 200 2>&1 | tail -1)" >> $O/fcbpmc.txt; done
+            done ;;
     rmsu) bash scripts/env_ab.sh ARL_RMS_U=1 ARL_RMS_U=2 "" 2 rmsu || exit $? ;;
     fcbz) for z in 2 4 5; do bash scripts/env_ab.sh ARL_FC_BWD_Z=3 ARL_FC_BWD_Z=$z "" 1 fcbz$z || exit $?; done ;;
   esac
