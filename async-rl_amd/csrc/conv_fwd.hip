@@ -220,11 +220,15 @@ conv_fwd_kernel(ConvFwdArgs a) {
   // conv1 tiles w, w + 8, w + 16 (and 24 on wave 0): 25 tiles over 8 waves in one
   // pass, 3-4 independent accumulator chains per wave (per-tile k order s = 0..7)
   constexpr int TJ = 4;
-  const bool has3 = w8 + 24 < 25;   // wave-uniform
+  // wt: the wave's conv1 tile set.  Slot 1 rotates it by one wave so its 4-tile wave (wt = 0) sits on another
+  // SIMD than slot 0's (a workgroup's waves go to SIMDs in a fixed cyclic order): 13 + 13 + 12 + 12 tiles
+  // over the 4 SIMDs instead of 14 + 12 + 12 + 12 (the same tiles and k order: bit-identical)
+  const int wt = EPW == 2 ? (w8 + 8 - el) & 7 : w8;
+  const bool has3 = wt + 24 < 25;   // wave-uniform
   int baseX[TJ];
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
-    const int tl = (j < 3 || has3) ? w8 + 8 * j : w8;
+    const int tl = (j < 3 || has3) ? wt + 8 * j : wt;
     const int p = tl * 16 + col, oy = p / 20, ox = p - oy * 20;
     baseX[j] = LY::XB(el) + (4 * oy) * XB_ROW + 8 * ox;
   }
@@ -466,7 +470,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       if (j == 3 && !has3) break;
-      const int p = (w8 + 8 * j) * 16 + col;
+      const int p = (wt + 8 * j) * 16 + col;
       float ov[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
