@@ -294,7 +294,7 @@ hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int 
 // LSTM gate weight gradients (upward W / b, lateral W) + dfc = (dG Wu) * (hfc > 0), the same kernel
 hipError_t launch_lstm_wgrad(const float* dG, const float* hfc, const float* hprev, const uint8_t* reset,
                              const float* zero, const float* Wu, int S, float* gWu, float* gWl, float* gbu, float* dfc,
-                             float* part, int* tick, hipStream_t s, uint16_t* dfcp = nullptr);
+                             float* part, int* tick, hipStream_t s);
 int64_t fc_bwd_part_floats(int S);   // workspace of its in-launch split reduction (both launches)
 int fc_bwd_tickets();                 // int counters, zero before the first launch (re-armed by it)
 hipError_t launch_policy_args(const float* h, int64_t n, const PolicyArgs& pa, hipStream_t s, int hid);

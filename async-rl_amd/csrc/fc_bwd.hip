@@ -200,8 +200,6 @@ struct FcBwdArgs {
   // elements; the DPL kernels read their dfc fragments from these instead of splitting f32 dfc
   const uint16_t* dfcp = nullptr;
   int64_t pst = 0;
-  // LSTM: job B also writes its dX (dfc) as those split planes (plane stride pst), or null
-  uint16_t* dxp = nullptr;
 };
 
 __device__ inline bf16x8 frag_u32(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3) {
@@ -770,12 +768,6 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
   // per-store branch, so no store waits for the one before it.
   const __amdgpu_buffer_rsrc_t out =
       __builtin_amdgcn_make_buffer_rsrc(a.da2 + (int64_t)s0 * NB, 0, rows * NB * 4, BUF_DWORD3);
-  const bool planes = SH::kLstm && a.dxp != nullptr;   // block-uniform
-  __amdgpu_buffer_rsrc_t outp[3];
-#pragma unroll
-  for (int p = 0; p < 3; ++p)
-    outp[p] = __builtin_amdgcn_make_buffer_rsrc(planes ? a.dxp + p * a.pst + (int64_t)s0 * NB : nullptr, 0,
-                                                planes ? rows * NB * 2 : 0, BUF_DWORD3);
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -789,16 +781,6 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
         o[u] = (mb[i] >> (4 * e + u)) & 1u ? v : 0.f;
       }
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), out, kin ? (row * NB + k) * 4 : OOB, 0, 0);
-      if (planes) {   // the same 4 values as exact bf16 split planes (the FC backward's DPL operand)
-        uint32_t h0, m0, l0, h1, m1, l1;
-        split3_pack(o[0], o[1], h0, m0, l0);
-        split3_pack(o[2], o[3], h1, m1, l1);
-        const int off = kin ? (row * NB + k) * 2 : OOB;
-        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2{h0, h1}, outp[0], off, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2{m0, m1}, outp[1], off, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2{l0, l1}, outp[2], off, 0, 0);
-      }
     }
 }
 
@@ -940,7 +922,7 @@ hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int 
 // gradient, job B dfc = (dG Wu) * (hfc > 0).  zero: >= 64 zero floats.
 hipError_t launch_lstm_wgrad(const float* dG, const float* hfc, const float* hprev, const uint8_t* reset,
                              const float* zero, const float* Wu, int S, float* gWu, float* gWl, float* gbu, float* dfc,
-                             float* part, int* tick, hipStream_t s, uint16_t* dfcp) {
+                             float* part, int* tick, hipStream_t s) {
   if (S <= 0) return hipSuccess;
   const int Z = lstm_wgrad_ranges(S);
   const int kpz = range_len(S, Z);
@@ -950,7 +932,7 @@ hipError_t launch_lstm_wgrad(const float* dG, const float* hfc, const float* hpr
   const int na = D::NTA * Z, nb = ((S + BMT - 1) / BMT) * D::NKB;
   static const char* xcd = getenv("ARL_FC_BWD_XCD");
   FcBwdArgs args{dG, hfc, Wu, S, Z, kpz, gWu, gbu, dfc, part, tick, HeadsDW{}, 0, 0, 0, 0,
-                 (xcd && xcd[0] == '0') ? 0 : 1, hprev, reset, zero, gWl, nullptr, nullptr, (int64_t)S * HID, dfcp};
+                 (xcd && xcd[0] == '0') ? 0 : 1, hprev, reset, zero, gWl};
   hipLaunchKernelGGL((fc_bwd_kernel<2, true, ShapeLSTM>), dim3(na + nb), dim3(NT), 0, s, args);
   return hipGetLastError();
 }

@@ -460,7 +460,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   net.w_dh = buf("dh", L ? S * HID * 4 : 0);
   net.w_dfc = buf("dfc", S * H * 4);
   // FF: dfc also as exact bf16 split planes [3][S][256], written by the returns kernel for fc_bwd (dfc_planes)
-  net.w_dfcp = buf("dfc_planes", NAT ? 0 : 3 * S * H * 2);
+  net.w_dfcp = buf("dfc_planes", (L || NAT) ? 0 : 3 * S * H * 2);
   net.w_dG = buf("dG", L ? S * GATES * 4 : 0);
   net.w_dhn = buf("dhn", L ? n * HID * 4 : 0);
   net.w_dcn = buf("dcn", L ? n * HID * 4 : 0);
@@ -688,14 +688,13 @@ hipError_t net_reset_state(Net& net, int e0, int n, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- backward
-// dfc's split planes (written by the returns kernel, FF, or the LSTM weight-gradient launch's job B;
-// ARL_FC_DPL=0: none, fc_bwd splits the f32 dfc itself -- the A arm)
+// dfc's split planes (FF nets; ARL_FC_DPL=0: none, fc_bwd splits the f32 dfc itself -- the A arm)
 static uint16_t* dfc_planes(Net& net) {
   static const bool on = [] {
     const char* e = getenv("ARL_FC_DPL");
     return !(e != nullptr && e[0] == '0');
   }();
-  if (!on || net.arch == ARCH_FF_NATURE) return nullptr;
+  if (!on || net.arch == ARCH_LSTM || net.arch == ARCH_FF_NATURE) return nullptr;
   return net.at<uint16_t>(net.w_dfcp);
 }
 
@@ -754,7 +753,7 @@ static hipError_t lstm_wgrad(Net& net, hipStream_t s) {
     return launch_lstm_wgrad(dG, hfc, net.at<float>(net.w_hbuf), net.at<uint8_t>(net.w_reset),
                              net.at<float>(net.w_zero), net.p + net.o_luW, S, net.g + net.o_luW, net.g + net.o_llW,
                              net.g + net.o_lub, net.at<float>(net.w_dfc), net.at<float>(net.w_fcb_part),
-                             net.at<int>(net.w_fcb_tick), s, dfc_planes(net));
+                             net.at<int>(net.w_fcb_tick), s);
   return launch_gemm2<64, 64, 32, 2, 2, GM, GM, GK, GM>(
       gemm_job<64, 32>(ColMajor{dG, GATES}, LstmWB{hfc, net.at<float>(net.w_hbuf), net.at<uint8_t>(net.w_reset)},
                        EpiSlab{net.at<float>(net.w_slab_lstm), GATES, 2 * HID + 1}, GATES, 2 * HID + 1, S, pl.lstm_w,
@@ -886,7 +885,7 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
   if (!FC_BWD_GEMM) {
     ARL_TRY(launch_fc_bwd(dfc, a2, P + net.o_fcW, S, G + net.o_fcW, G + net.o_fcb, net.at<float>(net.w_da2),
                           net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s, &heads, a2_mask(net, 0),
-                          ((L && LSTM_WGRAD_GEMM) || (!L && RETURNS_SPLIT)) ? nullptr : dfc_planes(net)));
+                          (L || RETURNS_SPLIT) ? nullptr : dfc_planes(net)));
     return stamp(net, STAGE_FC_BWD, s);
   }
   ARL_TRY((launch_gemm2_nt<64, 64, 32, 2, 4, 512, GM, GM, GK, GM>(   // 8 waves, 2 sub-tiles each (ARL_FC_BWD=gemm)
@@ -938,9 +937,7 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
                             G + net.o_pib, G + net.o_vW, G + net.o_vb};
         return launch_fc_bwd(net.at<float>(net.w_dfc), a2, P + net.o_fcW, S, G + net.o_fcW, G + net.o_fcb,
                              net.at<float>(net.w_da2), net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s,
-                             &heads, a2_mask(net, 0),
-                             ((net.arch == ARCH_LSTM && LSTM_WGRAD_GEMM) || (net.arch != ARCH_LSTM && RETURNS_SPLIT))
-                                 ? nullptr : dfc_planes(net));
+                             &heads, a2_mask(net, 0), RETURNS_SPLIT ? nullptr : dfc_planes(net));
       }
       const Plans pl = make_plans(net);
       const float* dfc = net.at<float>(net.w_dfc);

@@ -690,17 +690,14 @@ def test_lstm_fused_cell_identical(gpu, tmp_path):
     pi_and_v) and into the BPTT step (backward) gives the same bits as the
     cell as separate launches (ARL_LSTM_SPLIT=1); so do the FC forward's
     ticket reduce instead of the reduce in the gate kernel's staging
-    (ARL_LSTM_XRED=0), the env-group chains issued chain by chain
-    (ARL_GROUP_ORDER=chain) and the FC backward splitting f32 dfc itself
-    instead of reading the split planes the gate weight-gradient launch writes
-    (ARL_FC_DPL=0): hidden / cell states, gates, actions, values, gradients,
-    parameters."""
+    (ARL_LSTM_XRED=0) and the env-group chains issued chain by chain
+    (ARL_GROUP_ORDER=chain): hidden / cell states, gates, actions, values,
+    gradients, parameters."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     outs = []
-    for extra in ({}, {"ARL_LSTM_SPLIT": "1"}, {"ARL_LSTM_XRED": "0"}, {"ARL_GROUP_ORDER": "chain"},
-                  {"ARL_FC_DPL": "0"}):
+    for extra in ({}, {"ARL_LSTM_SPLIT": "1"}, {"ARL_LSTM_XRED": "0"}, {"ARL_GROUP_ORDER": "chain"}):
         f = str(tmp_path / f"lstm_{len(outs)}.npz")
         env = dict(os.environ, **extra)
         subprocess.run([sys.executable, os.path.join(here, "lstm_split_worker.py"), f], env=env, check=True,
