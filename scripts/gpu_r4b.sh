@@ -48,8 +48,6 @@ for ab in $AB; do
               done; done
               for j in a b x; do echo "$v jobs=$j $(ASYNCRL_HIP_LIB=$L ARL_FC_BWD_JOBS=$j timeout -k 10 60 python -u scripts/fc_bwd_bench.py 512 200 2>&1 | tail -1)" >> $O/fcbpmc.txt; done
             done ;;
-    dpl) bash scripts/env_ab.sh ARL_FC_DPL=0 ARL_FC_DPL=1 "" 2 dpl || exit $?
-         bash scripts/env_ab.sh ARL_FC_DPL=0 ARL_FC_DPL=1 "--workload c2" 2 dplc2 || exit $? ;;
     rmsu) bash scripts/env_ab.sh ARL_RMS_U=1 ARL_RMS_U=2 "" 2 rmsu || exit $? ;;
     fcbz) for z in 2 4 5; do bash scripts/env_ab.sh ARL_FC_BWD_Z=3 ARL_FC_BWD_Z=$z "" 1 fcbz$z || exit $?; done ;;
   esac
