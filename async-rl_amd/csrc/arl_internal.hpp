@@ -133,7 +133,7 @@ struct Net {
   int64_t ws_bytes;
   int64_t w_ctl, w_frames, w_nvalid, w_reset, w_rewards, w_dones, w_a1, w_a2, w_hfc, w_gates, w_hbuf,
       w_cbuf, w_logits, w_probs, w_logp, w_v, w_ent, w_logpa, w_act, w_dlogits, w_dv, w_dh, w_dfc,
-      w_dG, w_dhn, w_dcn, w_dfcp = 0, w_da2, w_slab, w_norm, w_loss, w_tick, w_fcb_part = 0, w_fcb_tick = 0, w_zero = 0,
+      w_dG, w_dhn, w_dcn, w_da2, w_slab, w_norm, w_loss, w_tick, w_fcb_part = 0, w_fcb_tick = 0, w_zero = 0,
       w_a2m = 0;   // (T+1, N, 81) a2 > 0 bits (ring-frame NIPS nets; 0: none)
   int64_t w_a3 = 0, w_da1 = 0, w_da3 = 0;   // Nature head only (w_da1 also ARCH_STATES)
   // LSTM recurrent state of pi_and_v on explicit states (A3CLSTM.pi_and_v, a3c_ale.py:55-63):
@@ -286,11 +286,9 @@ struct HeadsDW {
   int A;
   float *gWpi, *gbpi, *gWv, *gbv;
 };
-// dfcp: dfc as three exact bf16 split planes [3][S][256] (launch_returns_heads' dhp), or null: fc_bwd splits the
-// f32 dfc itself (ARL_FC_DPL=0 ignores the planes)
 hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int S, float* gW, float* gb, float* da2,
                          float* part, int* tick, hipStream_t s, const HeadsDW* heads = nullptr,
-                         const uint32_t* a2m = nullptr, const uint16_t* dfcp = nullptr);
+                         const uint32_t* a2m = nullptr);
 // LSTM gate weight gradients (upward W / b, lateral W) + dfc = (dG Wu) * (hfc > 0), the same kernel
 hipError_t launch_lstm_wgrad(const float* dG, const float* hfc, const float* hprev, const uint8_t* reset,
                              const float* zero, const float* Wu, int S, float* gWu, float* gWl, float* gbu, float* dfc,
@@ -402,6 +400,6 @@ hipError_t launch_returns_heads(const float* rewards, const uint8_t* dones, cons
                                 const float* logp, const int32_t* act, int T, int n, int A, double gamma, float beta,
                                 float vcoef, int clip_reward, float* dlogits, float* dv, float* loss, hipStream_t s,
                                 int64_t* ctl_snap, float pcoef, int keep_scale, const float* Wpi, const float* Wv,
-                                const float* mask, float* dh, uint16_t* dhp = nullptr);
+                                const float* mask, float* dh);
 
 }  // namespace arl

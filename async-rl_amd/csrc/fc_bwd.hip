@@ -71,9 +71,7 @@ constexpr int BK = 32;                  // K chunk (rows of a stage)
 #endif
 constexpr int AJ = ARL_FCB_AJ, AK = 8192 / ARL_FCB_AJ;
 constexpr int AWN = AK / 32;            // job A waves along k (64: 2, 32: 1)
-constexpr int cmax(int x, int y) { return x > y ? x : y; }
-// floats per LDS stage: job A f32 (dfc + X) or split-plane (3 bf16 dfc planes + X) images, job B's
-constexpr int STAGE = cmax(8192, cmax(BK * (AJ + AK), BK * (3 * AJ / 2 + AK)));
+constexpr int STAGE = BK * (AJ + AK) > 8192 ? BK * (AJ + AK) : 8192;   // floats per LDS stage
 constexpr int AKEY = AK == 64 ? 1 : 0;  // job A's X image: 64-float rows need the 8 * (row & 1) key, 32-float
                                         // rows are conflict-free (a b64 lane group spans two 128-B rows)
 constexpr int BN = 128;                 // job B tile: 32 MT samples x 128 k
@@ -160,7 +158,6 @@ __device__ inline void stage_tile(float* dst, const float* __restrict__ g, int64
     int key = 0;
     if constexpr (KEY == 1) key = 8 * (r & 1);
     else if constexpr (KEY == 2) key = (r >> 1) & 7;
-    else if constexpr (KEY == 3) key = (r >> 2) & 3;
     const int row = min(row0 + r, rmax);
     const float* src = g + (int64_t)row * ld + col0 + 4 * (pc ^ key);
     if constexpr (ZR) {
@@ -196,16 +193,7 @@ struct FcBwdArgs {
   // FC: job B's ReLU mask as bits of a2 > 0 (S, 81 words; conv_fwd.hip writes them) instead of a2
   // itself -- 324 instead of 10,368 bytes a sample; null: read a2
   const uint32_t* a2m = nullptr;
-  // FC: dfc as exact bf16 split planes [3][S][256] (the returns kernel writes them), plane stride pst
-  // elements; the DPL kernels read their dfc fragments from these instead of splitting f32 dfc
-  const uint16_t* dfcp = nullptr;
-  int64_t pst = 0;
 };
-
-__device__ inline bf16x8 frag_u32(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3) {
-  return __builtin_bit_cast(bf16x8, (u32x4{p0, p1, p2, p3}));
-}
-__device__ inline float bf16_f32(uint32_t b) { return __uint_as_float(b << 16); }
 
 // ---------------------------------------------------------------- job A: dW, db
 // range z's partial of `tile` into its slot: write-through sc1 stores; the
@@ -226,10 +214,8 @@ __device__ inline void publish_dw(const FcBwdArgs& a, int tile, int z, const dou
       __hip_atomic_store(dst + AJ * AK + wm * 64 + 4 * col + t, (float)sb[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool SPLIT, class SH, bool DPL = false>
+template <bool SPLIT, class SH>
 __device__ void job_dw(const FcBwdArgs& a, int job, float* lds, uint8_t* rst) {
-  static_assert(!DPL || (SPLIT && !SH::kLstm), "split planes: the FC's split path only");
-  constexpr int AIMG = DPL ? 3 * BK * AJ / 2 : BK * AJ;   // floats of the dfc image (3 bf16 planes or f32)
   using D = Dims<SH>;
   constexpr int NTA = D::NTA;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -270,18 +256,11 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds, uint8_t* rst) {
   auto issue = [&](int c) {
     if (a.abl & 2) return;
     float* st = lds + (c & 1) * STAGE;
-    if constexpr (DPL) {   // the three planes' rows s, j0 .. j0+AJ-1 (bf16 pairs as floats), key 8 (row & 1)
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-        stage_tile<BK, AJ / 2, 1>(st + p * (BK * AJ / 2), reinterpret_cast<const float*>(a.dfcp + p * a.pst), SH::J / 2,
-                                  r0 + c * BK, r1 - 1, j0 / 2);
-    } else {
-      stage_tile<BK, AJ, 0>(st, a.dfc, SH::J, r0 + c * BK, r1 - 1, j0);       // dY[s][j0 .. j0+AJ-1]
-    }
+    stage_tile<BK, AJ, 0>(st, a.dfc, SH::J, r0 + c * BK, r1 - 1, j0);       // dY[s][j0 .. j0+127]
     if (SH::kLstm && hpart)
-      stage_tile<BK, AK, AKEY, true>(st + AIMG, xsrc, XLD, r0 + c * BK, r1 - 1, xc0, rst, r0, a.zero);
+      stage_tile<BK, AK, AKEY, true>(st + BK * AJ, xsrc, XLD, r0 + c * BK, r1 - 1, xc0, rst, r0, a.zero);
     else
-      stage_tile<BK, AK, AKEY>(st + AIMG, xsrc, XLD, r0 + c * BK, r1 - 1, xc0);   // X[s][k0 .. k0+AK-1]
+      stage_tile<BK, AK, AKEY>(st + BK * AJ, xsrc, XLD, r0 + c * BK, r1 - 1, xc0);   // X[s][k0 .. k0+AK-1]
   };
   const int nb = wn * 32 + 2 * col;
   f32x4 acc[4][2], bs;
@@ -295,7 +274,7 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds, uint8_t* rst) {
     barrier_lds();
     if (c + 1 < nchunks) issue(c + 1);
     const float* As = lds + (c & 1) * STAGE;
-    const float* Bs = As + AIMG;
+    const float* Bs = As + BK * AJ;
     const int kvalid = r1 - (r0 + c * BK);   // rows >= kvalid: clamped copies, masked to 0
     if (c % FLUSH == 0) {
 #pragma unroll
@@ -304,69 +283,7 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds, uint8_t* rst) {
         for (int u = 0; u < 2; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
       bs = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    if (DPL && !(a.abl & 1)) {
-      // dfc fragments straight from the planes: per k-step 4 bf16 (j = wm*64 + 4col + 0..3) of sample
-      // 4 ks + q and plane p; m-tile t's fragment takes element t of the 8 k-steps (v_perm pairs) --
-      // the same bf16 values the split below forms from f32 dfc, so the same MFMAs and bits
-      uint2 dv[BK / 4][3];
-      f32x2 bv[BK / 4];
-      const int c16 = (wm * 64 + 4 * col) >> 3, half = 8 * (col & 1);
-      const uint8_t* Ab = reinterpret_cast<const uint8_t*>(As);
-#pragma unroll
-      for (int ks = 0; ks < BK / 4; ++ks) {
-        const int r = 4 * ks + q;
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          dv[ks][p] = *reinterpret_cast<const uint2*>(Ab + p * (BK * AJ * 2) + r * (AJ * 2) +
-                                                      ((c16 ^ (8 * (r & 1))) << 4) + half);
-        bv[ks] = *reinterpret_cast<const f32x2*>(Bs + r * AK + (((nb >> 2) ^ (AKEY * 8 * (r & 1))) << 2) + (nb & 3));
-      }
-      if (kvalid < BK) {   // the range's last chunk only
-#pragma unroll
-        for (int ks = 0; ks < BK / 4; ++ks)
-          if (4 * ks + q >= kvalid)
-#pragma unroll
-            for (int p = 0; p < 3; ++p) dv[ks][p] = make_uint2(0u, 0u);
-      }
-      bf16x8 bh[2], bm[2], bl[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        float x[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) x[i] = bv[i][u];
-        split3_x8(x, bh[u], bm[u], bl[u]);
-      }
-      auto frag = [&](int t, int p) {
-        uint32_t w[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t lo = t < 2 ? dv[2 * k][p].x : dv[2 * k][p].y;
-          const uint32_t hi = t < 2 ? dv[2 * k + 1][p].x : dv[2 * k + 1][p].y;
-          w[k] = __builtin_amdgcn_perm(hi, lo, (t & 1) ? 0x07060302u : 0x05040100u);
-        }
-        return frag_u32(w[0], w[1], w[2], w[3]);
-      };
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const bf16x8 ah = frag(t, 0), am = frag(t, 1), al = frag(t, 2);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) acc[t][u] = mfma_x6_acc(ah, am, al, bh[u], bm[u], bl[u], acc[t][u]);
-      }
-      if (bias)   // db from the planes' exact sum h + (m + l) = dfc, added in the f32 path's order
-#pragma unroll
-        for (int ks = 0; ks < BK / 4; ++ks) {
-          f32x4 v;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int sh = 16 * (t & 1);
-            const uint32_t h = ((t < 2 ? dv[ks][0].x : dv[ks][0].y) >> sh) & 0xffffu;
-            const uint32_t m = ((t < 2 ? dv[ks][1].x : dv[ks][1].y) >> sh) & 0xffffu;
-            const uint32_t l = ((t < 2 ? dv[ks][2].x : dv[ks][2].y) >> sh) & 0xffffu;
-            v[t] = __fadd_rn(bf16_f32(h), __fadd_rn(bf16_f32(m), bf16_f32(l)));
-          }
-          bs += v;
-        }
-    } else if (!(a.abl & 1)) {
+    if (!(a.abl & 1)) {
       // every fragment of the chunk first (counted LDS waits), then the MFMAs
       f32x4 av[BK / 4];
       f32x2 bv[BK / 4];
@@ -575,14 +492,12 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds, uint8_t* rst) {
 
 // ---------------------------------------------------------------- job B: da2
 // MT m-tiles per wave: workgroup tiles of BMT = 32 MT samples x 128 k
-template <int MT, bool SPLIT, class SH, bool DPL = false>
+template <int MT, bool SPLIT, class SH>
 __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
-  static_assert(!DPL || (SPLIT && !SH::kLstm), "split planes: the FC's split path only");
   using D = Dims<SH>;
   constexpr int NKB = D::NKB, NB = SH::NB;
   constexpr int BMT = 32 * MT;
-  constexpr int AIMG = DPL ? 3 * BMT * BK / 2 : BMT * BK;   // floats of the dfc image (3 bf16 planes or f32)
-  constexpr int PIECES = (AIMG + BK * BN) / 256 / NW;       // LDS-DMA pieces per wave per chunk
+  constexpr int PIECES = (BMT * BK + BK * BN) / 256 / NW;   // LDS-DMA pieces per wave per chunk
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, col = lane & 15;
   const int wm = wave >> 1, wn = wave & 1;   // wave: 16 MT s x 64 k
@@ -598,16 +513,8 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
   auto issue = [&](int c) {
     if (a.abl & 2) return;
     float* sg = lds + (c & 1) * STAGE;
-    if constexpr (DPL) {   // the three planes' rows s, j = 32 c .. 32 c + 31 (bf16 pairs as floats), key (row >> 2) & 3
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-        stage_tile<BMT, BK / 2, 3>(sg + p * (BMT * BK / 2),
-                                   reinterpret_cast<const float*>(a.dfcp + p * a.pst) + c * (BK / 2), SH::J / 2, s0,
-                                   a.S - 1, 0);
-    } else {
-      stage_tile<BMT, BK, 2>(sg, a.dfc + c * BK, SH::J, s0, a.S - 1, 0);                  // dY[s][j]
-    }
-    stage_tile<BK, BN, 0>(sg + AIMG, a.W + (int64_t)c * BK * NB, NB, 0, BK - 1, k0);      // W[j][k0..k0+127]
+    stage_tile<BMT, BK, 2>(sg, a.dfc + c * BK, SH::J, s0, a.S - 1, 0);                  // dY[s][j]
+    stage_tile<BK, BN, 0>(sg + BMT * BK, a.W + (int64_t)c * BK * NB, NB, 0, BK - 1, k0);  // W[j][k0..k0+127]
   };
   f32x4 acc[MT][4];                          // m-tile i: rows 16 i + col; n-tile u: cols 4 col + u
   f32x4 sml[SPLIT ? MT : 1][4];              // split path: the 5 small terms (acc: the h.h term)
@@ -671,44 +578,8 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
     }
     barrier_lds();
     const float* As = lds + (c & 1) * STAGE;
-    const float* Bs = As + AIMG;
-    if (DPL && !(a.abl & 1)) {
-      // dfc fragments straight from the planes: lane (col, q) of m-tile i is sample m, elements 4 g + r =
-      // j 16 g + 4 q + r (two 8-byte reads a plane) -- the bf16 values the split below forms from f32 dfc
-      bf16x8 af[MT][3];
-      f32x4 bv[BK / 16][4];
-      const uint8_t* Ab = reinterpret_cast<const uint8_t*>(As);
-#pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        const int m = wm * 16 * MT + i * 16 + col, key = (m >> 2) & 3;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          const uint8_t* row = Ab + p * (BMT * BK * 2) + m * (BK * 2) + 8 * (q & 1);
-          const uint2 d0 = *reinterpret_cast<const uint2*>(row + ((((q >> 1)) ^ key) << 4));
-          const uint2 d1 = *reinterpret_cast<const uint2*>(row + (((2 + (q >> 1)) ^ key) << 4));
-          af[i][p] = frag_u32(d0.x, d0.y, d1.x, d1.y);
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < BK / 16; ++g)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)   // k = 16 g + 4 q + r
-          bv[g][r] = *reinterpret_cast<const f32x4*>(Bs + (16 * g + 4 * q + r) * BN + wn * 64 + 4 * col);
-      bf16x8 bh[4], bm[4], bl[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float x[8];
-#pragma unroll
-        for (int g = 0; g < 2; ++g)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) x[4 * g + r] = bv[g][r][u];
-        split3_x8(x, bh[u], bm[u], bl[u]);
-      }
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) mfma_x6(af[i][0], af[i][1], af[i][2], bh[u], bm[u], bl[u], acc[i][u], sml[i][u]);
-    } else if (!(a.abl & 1)) {
+    const float* Bs = As + BMT * BK;
+    if (!(a.abl & 1)) {
       // every fragment of the chunk first (counted LDS waits), then the MFMAs
       f32x4 av[BK / 16][MT], bv[BK / 16][4];
 #pragma unroll
@@ -847,7 +718,7 @@ __device__ void job_heads(const FcBwdArgs& a, int jt, float* lds) {
   }
 }
 
-template <int MT, bool SPLIT, class SH, bool DPL = false>
+template <int MT, bool SPLIT, class SH>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2)))
 fc_bwd_kernel(FcBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];   // 64 KB (72 KB with ARL_FCB_AJ=256)
@@ -855,8 +726,8 @@ fc_bwd_kernel(FcBwdArgs a) {
   const int b = a.b0 + blockIdx.x;
   const int na = Dims<SH>::NTA * a.Z;
   if (b < a.nc) job_heads(a, b, lds);   // first: the smallest, longest-latency jobs
-  else if (b < a.nc + na) job_dw<SPLIT, SH, DPL>(a, b - a.nc, lds, rst);
-  else job_da2<MT, SPLIT, SH, DPL>(a, b - a.nc - na, lds);
+  else if (b < a.nc + na) job_dw<SPLIT, SH>(a, b - a.nc, lds, rst);
+  else job_da2<MT, SPLIT, SH>(a, b - a.nc - na, lds);
 }
 
 // ~800 samples per job A range, at most 16 ranges (bf16-split steps, sweep in
@@ -881,8 +752,7 @@ int fc_bwd_tickets() { return 2 * NTA_MAX; }   // arrival tickets, then ready co
 // the bootstrap slot after the window's S rows) or the next parameters' (W),
 // and are never stored.
 hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int S, float* gW, float* gb, float* da2,
-                         float* part, int* tick, hipStream_t s, const HeadsDW* heads, const uint32_t* a2m,
-                         const uint16_t* dfcp) {
+                         float* part, int* tick, hipStream_t s, const HeadsDW* heads, const uint32_t* a2m) {
   if (S <= 0) return hipSuccess;
   const int Z = fc_bwd_ranges(S);
   const int kpz = range_len(S, Z);
@@ -909,9 +779,8 @@ hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int 
   static const char* xcd = getenv("ARL_FC_BWD_XCD");
   FcBwdArgs args{dfc, a2, W, S, Z, kpz, gW, gb, da2, part, tick, heads ? *heads : HeadsDW{}, nc, b0,
                  abl ? atoi(abl) : 0, (spin && atoi(spin) == 1) ? 1 : 0, (xcd && xcd[0] == '0') ? 0 : 1,
-                 nullptr, nullptr, nullptr, nullptr, a2m, dfcp, (int64_t)S * HID};
-  if (split && dfcp != nullptr) hipLaunchKernelGGL((fc_bwd_kernel<2, true, ShapeFC, true>), dim3(grid), dim3(NT), 0, s, args);
-  else if (split) hipLaunchKernelGGL((fc_bwd_kernel<2, true, ShapeFC>), dim3(grid), dim3(NT), 0, s, args);
+                 nullptr, nullptr, nullptr, nullptr, a2m};
+  if (split) hipLaunchKernelGGL((fc_bwd_kernel<2, true, ShapeFC>), dim3(grid), dim3(NT), 0, s, args);
   else if (MT == 2) hipLaunchKernelGGL((fc_bwd_kernel<2, false, ShapeFC>), dim3(grid), dim3(NT), 0, s, args);
   else hipLaunchKernelGGL((fc_bwd_kernel<4, false, ShapeFC>), dim3(grid), dim3(NT), 0, s, args);
   return hipGetLastError();

@@ -459,8 +459,6 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   net.w_dv = buf("dv", S * 4);
   net.w_dh = buf("dh", L ? S * HID * 4 : 0);
   net.w_dfc = buf("dfc", S * H * 4);
-  // FF: dfc also as exact bf16 split planes [3][S][256], written by the returns kernel for fc_bwd (dfc_planes)
-  net.w_dfcp = buf("dfc_planes", (L || NAT) ? 0 : 3 * S * H * 2);
   net.w_dG = buf("dG", L ? S * GATES * 4 : 0);
   net.w_dhn = buf("dhn", L ? n * HID * 4 : 0);
   net.w_dcn = buf("dcn", L ? n * HID * 4 : 0);
@@ -688,16 +686,6 @@ hipError_t net_reset_state(Net& net, int e0, int n, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- backward
-// dfc's split planes (FF nets; ARL_FC_DPL=0: none, fc_bwd splits the f32 dfc itself -- the A arm)
-static uint16_t* dfc_planes(Net& net) {
-  static const bool on = [] {
-    const char* e = getenv("ARL_FC_DPL");
-    return !(e != nullptr && e[0] == '0');
-  }();
-  if (!on || net.arch == ARCH_LSTM || net.arch == ARCH_FF_NATURE) return nullptr;
-  return net.at<uint16_t>(net.w_dfcp);
-}
-
 // the folded clip norm's arguments (none unless arl_net_set_norm_fold): the
 // conv tensors are [0, o_fcW) of the flat gradient, everything after is final
 // before the conv slab reduce
@@ -796,7 +784,7 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
                                  net.at<float>(net.w_probs), net.at<float>(net.w_logp), net.at<int32_t>(net.w_act), T,
                                  n, A, gamma, beta, vcoef, clip_reward, dl, dv, net.at<float>(net.w_loss), s,
                                  net.at<int64_t>(net.w_ctl), net.pi_coef, net.keep_scale, P + net.o_piW, P + net.o_vW,
-                                 L ? nullptr : hfc, L ? net.at<float>(net.w_dh) : dfc, L ? nullptr : dfc_planes(net)));
+                                 L ? nullptr : hfc, L ? net.at<float>(net.w_dh) : dfc));
     return stamp(net, STAGE_RETURNS, s);
   }
   // heads: weight grads (ones column = bias) and dh.  With the fused FC
@@ -884,8 +872,7 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
   //    one launch (fc_bwd.hip)
   if (!FC_BWD_GEMM) {
     ARL_TRY(launch_fc_bwd(dfc, a2, P + net.o_fcW, S, G + net.o_fcW, G + net.o_fcb, net.at<float>(net.w_da2),
-                          net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s, &heads, a2_mask(net, 0),
-                          (L || RETURNS_SPLIT) ? nullptr : dfc_planes(net)));
+                          net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s, &heads, a2_mask(net, 0)));
     return stamp(net, STAGE_FC_BWD, s);
   }
   ARL_TRY((launch_gemm2_nt<64, 64, 32, 2, 4, 512, GM, GM, GK, GM>(   // 8 waves, 2 sub-tiles each (ARL_FC_BWD=gemm)
@@ -937,7 +924,7 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
                             G + net.o_pib, G + net.o_vW, G + net.o_vb};
         return launch_fc_bwd(net.at<float>(net.w_dfc), a2, P + net.o_fcW, S, G + net.o_fcW, G + net.o_fcb,
                              net.at<float>(net.w_da2), net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s,
-                             &heads, a2_mask(net, 0), RETURNS_SPLIT ? nullptr : dfc_planes(net));
+                             &heads, a2_mask(net, 0));
       }
       const Plans pl = make_plans(net);
       const float* dfc = net.at<float>(net.w_dfc);

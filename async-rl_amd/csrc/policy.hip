@@ -26,7 +26,6 @@
 #include <cstdlib>
 
 #include "arl_internal.hpp"
-#include "bf16split.hpp"
 #include "policy_rows.hpp"
 
 namespace arl {
@@ -325,8 +324,7 @@ __device__ inline int rh_envs(int T) { return 1; }
 template <int AM, int RB>
 __global__ void __launch_bounds__(256)
 returns_heads_kernel(ReturnsArgs a, const float* __restrict__ Wpi, const float* __restrict__ Wv,
-                     const float* __restrict__ mask, float* __restrict__ dh, int abl, uint16_t* __restrict__ dhp,
-                     int64_t pst) {
+                     const float* __restrict__ mask, float* __restrict__ dh, int abl) {
   __shared__ float lpi[64], lv[64];
   __shared__ float sdl[64 * (AM + 1)];
   if (a.ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) a.ctl[CTL_STEP_SNAP] = a.ctl[CTL_STEP];
@@ -379,15 +377,7 @@ returns_heads_kernel(ReturnsArgs a, const float* __restrict__ Wpi, const float* 
       float acc = 0.f;
       for (int k = 0; k < A; ++k) acc = __fadd_rn(acc, __fmul_rn(d[k], w[k * HID + j]));
       acc = __fadd_rn(acc, __fmul_rn(d[A], w[A * HID + j]));
-      const float o = mv[u] > 0.f ? acc : 0.f;
-      dh[so[u]] = o;
-      if (dhp != nullptr) {   // also as exact bf16 split planes (fc_bwd.hip's dfc operand): same index per plane
-        uint32_t h, m, l;
-        split3(o, h, m, l);
-        dhp[so[u]] = (uint16_t)h;
-        dhp[pst + so[u]] = (uint16_t)m;
-        dhp[2 * pst + so[u]] = (uint16_t)l;
-      }
+      dh[so[u]] = mv[u] > 0.f ? acc : 0.f;
     }
   }
 }
@@ -409,9 +399,8 @@ hipError_t launch_returns_heads(const float* rewards, const uint8_t* dones, cons
                                 const float* logp, const int32_t* act, int T, int n, int A, double gamma, float beta,
                                 float vcoef, int clip_reward, float* dlogits, float* dv, float* loss, hipStream_t s,
                                 int64_t* ctl_snap, float pcoef, int keep_scale, const float* Wpi, const float* Wv,
-                                const float* mask, float* dh, uint16_t* dhp) {
+                                const float* mask, float* dh) {
   if (n <= 0) return hipSuccess;
-  const int64_t pst = (int64_t)T * n * HID;   // plane stride of dhp (elements)
   if (T < 1 || T > 64 || A < 1 || A > MAXA) return hipErrorInvalidValue;
   const int EB = 1;   // rh_envs
   const ReturnsArgs ra{rewards, dones, v, probs, logp, act, T, n, A, gamma, beta, vcoef, pcoef, clip_reward,
@@ -420,11 +409,11 @@ hipError_t launch_returns_heads(const float* rewards, const uint8_t* dones, cons
   const dim3 grid((n + EB - 1) / EB), blk(256);
   const int ablv = ab ? atoi(ab) : 0;
   if (T <= 8) {
-    if (A <= 4) hipLaunchKernelGGL((returns_heads_kernel<4, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh, ablv, dhp, pst);
-    else if (A <= 8) hipLaunchKernelGGL((returns_heads_kernel<8, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh, ablv, dhp, pst);
-    else hipLaunchKernelGGL((returns_heads_kernel<MAXA, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh, ablv, dhp, pst);
+    if (A <= 4) hipLaunchKernelGGL((returns_heads_kernel<4, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh, ablv);
+    else if (A <= 8) hipLaunchKernelGGL((returns_heads_kernel<8, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh, ablv);
+    else hipLaunchKernelGGL((returns_heads_kernel<MAXA, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh, ablv);
   } else {
-    hipLaunchKernelGGL((returns_heads_kernel<MAXA, 32>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh, ablv, dhp, pst);
+    hipLaunchKernelGGL((returns_heads_kernel<MAXA, 32>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh, ablv);
   }
   return hipGetLastError();
 }

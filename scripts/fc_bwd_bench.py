@@ -23,15 +23,6 @@ net.params.copy_(torch.rand(net.params.shape, device="cuda", generator=g) - 0.5)
 for name, shape in (("a2", ((T + 1) * N, 2592)), ("dfc", (T * N, 256))):
     b = net.buffer(name, torch.float32, shape)
     b.copy_(torch.relu(torch.randn(shape, device="cuda", generator=g)))
-if arch == 0:   # FF: dfc's exact bf16 split planes, as the returns kernel writes them (fc_bwd reads those)
-    x = net.buffer("dfc", torch.float32, (T * N, 256))
-    mask = torch.tensor(-65536, dtype=torch.int32, device="cuda")   # 0xffff0000
-    hb = x.view(torch.int32) & mask
-    r1 = x - hb.view(torch.float32)
-    mb = r1.view(torch.int32) & mask
-    r2 = r1 - mb.view(torch.float32)
-    planes = torch.stack([hb >> 16, mb >> 16, r2.view(torch.int32) >> 16]).to(torch.int16)
-    net.buffer("dfc_planes", torch.int16, (3, T * N, 256)).copy_(planes)
 s = torch.cuda.current_stream()
 for _ in range(10):
     net.run_stage("fc_bwd")

@@ -762,18 +762,15 @@ def test_lstm_wgrad_kernel_matches_gemm(gpu, tmp_path):
 
 def test_fc_bwd_variants(gpu, tmp_path):
     """FC backward knobs at S = 1,280 (two dW ranges): the ticket-first reduce
-    (ARL_FC_BWD_SPIN=1) sums the same partials in the same order, and the dfc
-    fragments split from f32 in the kernel (ARL_FC_DPL=0) are the bf16 values
-    the returns kernel's split planes hold, so every bit matches the default;
-    the exact-f32 16x16x4 steps (ARL_FC_BWD_F32=1)
+    (ARL_FC_BWD_SPIN=1) sums the same partials in the same order, so every
+    bit matches the default; the exact-f32 16x16x4 steps (ARL_FC_BWD_F32=1)
     and the default bf16-split steps are both f32-accurate, so the window
     gradients agree to 1e-5 of each tensor's scale (close_normscaled)."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     outs = {}
-    for name, extra in (("default", {}), ("spin", {"ARL_FC_BWD_SPIN": "1"}), ("dpl0", {"ARL_FC_DPL": "0"}),
-                        ("f32", {"ARL_FC_BWD_F32": "1"})):
+    for name, extra in (("default", {}), ("spin", {"ARL_FC_BWD_SPIN": "1"}), ("f32", {"ARL_FC_BWD_F32": "1"})):
         f = str(tmp_path / f"fcb_{name}.npz")
         env = dict(os.environ, **extra)
         env.pop("ARL_FC_BWD_Z", None)
@@ -783,7 +780,6 @@ def test_fc_bwd_variants(gpu, tmp_path):
     assert float(np.abs(d["grads1"]).max()) > 0
     for k in d.files:
         assert np.array_equal(d[k], sp[k]), k
-        assert np.array_equal(d[k], outs["dpl0"][k]), k
     ok, err = close_normscaled(f32["grads1"], d["grads1"], 1e-5)
     assert ok, err
     assert not np.array_equal(f32["grads1"], d["grads1"])   # the knob did switch the k-steps
@@ -833,9 +829,7 @@ def test_conv_fwd_two_envs_identical(gpu, tmp_path, n_envs):
     heads, which fall back), at 200 (a partial 64-row block) and at 512.  The
     frame ring too, against phi_ring_kernel's LDS-DMA staging (ARL_PHI_DMA); and the
     window as one C call (arl_run_window) against its launches issued step by
-    step from Python (ARL_WINDOW_C=0); the FC backward splitting f32 dfc
-    itself instead of reading the returns kernel's planes (ARL_FC_DPL=0).  And
-    every update block re-reducing the
+    step from Python (ARL_WINDOW_C=0).  And every update block re-reducing the
     clip norm's partials against the ticket hand-off (ARL_NORM_TICKET=1): the f64
     sums run in another order, so that arm is held to 1e-6 relative."""
     import subprocess
@@ -845,8 +839,7 @@ def test_conv_fwd_two_envs_identical(gpu, tmp_path, n_envs):
     for i, arm in enumerate(({"ARL_CONV_EPW": "1", "ARL_FC_BIG": "0"}, {"ARL_CONV_EPW": "2", "ARL_FC_BIG": "0"},
                              {"ARL_CONV_EPW": "1", "ARL_FC_BIG": "1", "ARL_FC_HEADS": "0"},
                              {"ARL_CONV_EPW": "1", "ARL_FC_BIG": "1", "ARL_FC_HEADS": "1"},
-                             {"ARL_PHI_DMA": "1"}, {"ARL_WINDOW_C": "0"}, {"ARL_FC_DPL": "0"},
-                             {"ARL_NORM_TICKET": "1"})):
+                             {"ARL_PHI_DMA": "1"}, {"ARL_WINDOW_C": "0"}, {"ARL_NORM_TICKET": "1"})):
         f = str(tmp_path / f"arm_{i}.npz")
         env = dict(os.environ, **arm)
         subprocess.run([sys.executable, os.path.join(here, "conv_epw_worker.py"), f, str(n_envs)], env=env,
