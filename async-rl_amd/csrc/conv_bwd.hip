@@ -74,9 +74,6 @@
 #ifndef ARL_S1_SPLIT
 #define ARL_S1_SPLIT 0
 #endif
-#ifndef ARL_CB_EARLY_A
-#define ARL_CB_EARLY_A 1
-#endif
 #ifndef ARL_CB_STAMP
 #define ARL_CB_STAMP 0   // timing experiments only: s_memtime at every barrier into the slab (results wrong)
 #endif
@@ -384,26 +381,20 @@ conv_bwd_kernel(ConvBwdArgs a) {
   PrefetchA pa;
   PrefetchX px_;
   const int64_t step0 = a.ctl[CTL_STEP];
-  // da2 of sample s + G is committed during step 3 of sample s (its regions are free after B3), so a
-  // sample's B0 phase holds only the screens' commit (ARL_CB_EARLY_A=0: both at B0, the A arm)
   prefetch_a(a, blockIdx.x, pa);
   prefetch_x(a, step0, blockIdx.x, px_);
   dma_a1(a, blockIdx.x, lds);
-  if (ARL_CB_EARLY_A) {
-    commit_a(pa, lds, b2a);
-    prefetch_a(a, min(blockIdx.x + G, a.S - 1), pa);
-  }
   for (int s = blockIdx.x; s < a.S; s += G) {
     lds_barrier();                 // B0: the previous sample is done with every region
     CB_STAMP();
-    if (!ARL_CB_EARLY_A) commit_a(pa, lds, b2a);
+    commit_a(pa, lds, b2a);
     commit_x(px_, lds);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this sample's a1 DMA has landed
     lds_barrier();                 // B1
     CB_STAMP();
     {
       const int sn = min(s + G, a.S - 1);   // unconditional: the registers are redefined here
-      if (!ARL_CB_EARLY_A) prefetch_a(a, sn, pa);   // in flight during (1)-(3)
+      prefetch_a(a, sn, pa);                // in flight during (1)-(3)
       prefetch_x(a, step0, sn, px_);
     }
 #if ARL_S1_SPLIT
@@ -585,10 +576,6 @@ conv_bwd_kernel(ConvBwdArgs a) {
     }
     lds_barrier();                 // B3
     CB_STAMP();
-    if (ARL_CB_EARLY_A && s + G < a.S) {   // (block-uniform) the next sample's da2: steps 1 and 2 are done with it
-      commit_a(pa, lds, b2a);
-      prefetch_a(a, min(s + 2 * G, a.S - 1), pa);
-    }
     // ---- (3) conv1 weight gradient: k-step ks, quarter g -> group Gk = 4 ks + g
     // = (oy, X0 = 8 c): 8 positions (oy, X0..X0+7).  Tile a = rows (ky, kx =
     // 4 a + (col & 3)): the a = 0 and a = 1 fragments of a lane are pixels
