@@ -65,14 +65,19 @@ namespace {
 constexpr int NT = 512;                  // threads per workgroup (8 waves)
 constexpr int XB_ROW = 84 * 2;           // bytes per bf16 screen row
 constexpr int XB_PLANE = PLANE * 2;      // 14,112 bytes per bf16 screen
-constexpr int WROW = 528;                // bytes per oc row of a weight plane (512 + 16: conflict-free b128)
-constexpr int W1P = 16 * WROW;           // 8,448 per W1 plane
-constexpr int W2P = 32 * WROW;           // 16,896 per W2 plane
-constexpr int A1P = C1_P * 32;           // 12,800 per a1 plane: 400 pixels x 16 ic bf16
+// bytes per oc row of a weight plane: 512 + 32, so the 16 rows a ds_read_b128 lane group reads (8 of one
+// 16-byte k half, 8 of the other) land on 16 distinct bank quads (528 = 512 + 16 left a 2-way conflict)
+constexpr int WROW = 544;
+constexpr int W1P = 16 * WROW;           // 8,704 per W1 plane
+constexpr int W2P = 32 * WROW;           // 17,408 per W2 plane
+// a1 planes: 16-byte slots (8 ic bf16) of pixel (y, x), ic half h, in phase-split order -- slot
+// h * A1_HALF + ((y & 1) * 2 + (x & 1)) * A1_PS + a1_pos(y >> 1, x >> 1), see a1_off
+constexpr int A1_PS = 108, A1_HALF = 4 * A1_PS;
+constexpr int A1P = 2 * A1_HALF * 16;    // 13,824 per a1 plane (400 pixels x 16 ic bf16 + pad)
 constexpr int L_XB = 0;
 constexpr int L_R1 = L_XB + 4 * XB_PLANE;   // 56,448
-constexpr int L_W2 = L_R1 + 3 * A1P;        // 94,848
-constexpr int L_END = L_W2 + 3 * W2P;       // 145,536
+constexpr int L_W2 = L_R1 + 3 * A1P;        // 97,920
+constexpr int L_END = L_W2 + 3 * W2P;       // 150,144
 static_assert(3 * W1P <= 3 * A1P, "W1 planes fit the a1 region");
 // PHI: gray tap rows + coefficient tables in the W2 region (W2 is split into it after the resize)
 constexpr int G_ROWS = 2 * DST;                       // 168 (output row, tap) source rows
@@ -84,16 +89,16 @@ constexpr int PHI_J = (PHI_TASKS + NT - 1) / NT;      // 4
 
 // LDS layout by envs per workgroup (EPW).  EPW = 1 is the layout above.  EPW = 2
 // (1,024 threads; waves 0-7 take env 0, waves 8-15 env 1, both share the weight
-// planes): conv1 phase  [screens e0 | screens e1 | W1 planes]       138,240 B;
-//          conv2 phase  [a1 planes e0 | a1 planes e1 | W2 planes]  127,488 B
+// planes): conv1 phase  [screens e0 | screens e1 | W1 planes]       139,008 B;
+//          conv2 phase  [a1 planes e0 | a1 planes e1 | W2 planes]  135,168 B
 // (W2 is split into the dead screen / W1 bytes after conv1's barrier).
 template <int EPW>
 struct Lay {
   static constexpr int XB(int el) { return el * 4 * XB_PLANE; }
   static constexpr int W1 = EPW * 4 * XB_PLANE;                      // 56,448 / 112,896
   static constexpr int A1(int el) { return EPW == 1 ? W1 : el * 3 * A1P; }
-  static constexpr int W2 = EPW == 1 ? L_W2 : 2 * 3 * A1P;           // 94,848 / 76,800
-  static constexpr int END = EPW == 1 ? L_END : W1 + 3 * W1P;        // 145,536 / 138,240
+  static constexpr int W2 = EPW == 1 ? L_W2 : 2 * 3 * A1P;           // 97,920 / 82,944
+  static constexpr int END = EPW == 1 ? L_END : W1 + 3 * W1P;        // 150,144 / 139,008
   // a2 > 0 mask words (81 u32 per env) in bytes dead during conv2: the screens (EPW 1), past the W2
   // planes (EPW 2)
   static constexpr int MSK(int el) { return EPW == 1 ? 0 : W2 + 3 * W2P + el * 336; }
@@ -103,10 +108,16 @@ static_assert(Lay<2>::W2 + 3 * W2P <= Lay<2>::END && Lay<2>::END <= 160 * 1024, 
 static_assert(Lay<1>::A1(0) == L_R1 && Lay<1>::END == L_END, "EPW 1 layout");
 }  // namespace
 
-// a1 plane byte offset of (pixel P, ic half h): 16-byte slot 2P + h with its
-// low 4 bits XORed by P >> 3, so conv2's 16 lanes (positions 2 pixels apart)
-// spread over the LDS banks
-__device__ inline int a1_slot(int P, int h) { return (((2 * P + h) ^ ((P >> 3) & 15)) << 4); }
+// a1 plane byte offset of pixel (y, x), ic half h.  conv2's lanes read, for one tap (ky, kx), the pixels
+// (2 oy + ky, 2 ox + kx) of 16 consecutive output positions r = 9 oy + ox; in the tap's phase plane
+// (y & 1, x & 1) that is (Y, X) = (oy + ky / 2, ox + kx / 2), so a slot index congruent to 9 Y + X mod 16
+// puts those 16 reads on 16 distinct bank quads (16 consecutive r, shifted by 9 (ky / 2) + kx / 2), and
+// A1_HALF = 0 mod 16 keeps that across the lane group's two ic halves.  a1_pos: 9 Y + X for X < 9
+// (0..89); the 10 pixels of column X = 9 in the free slots >= 90 of the same residue.
+__device__ inline int a1_pos(int Y, int X) { return X < 9 ? 9 * Y + X : 90 + ((9 * Y + 15) & 15); }
+__device__ inline int a1_off(int y, int x, int h) {
+  return (h * A1_HALF + ((y & 1) * 2 + (x & 1)) * A1_PS + a1_pos(y >> 1, x >> 1)) << 4;
+}
 
 struct ConvFwdArgs {
   const uint8_t* frames;
@@ -484,7 +495,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
       uint2 ph, pm, pl;
       split3_pack(ov[0], ov[1], ph.x, pm.x, pl.x);
       split3_pack(ov[2], ov[3], ph.y, pm.y, pl.y);
-      const int off = LY::A1(el) + a1_slot(p, g >> 1) + (g & 1) * 8;
+      const int off = LY::A1(el) + a1_off(p / 20, p % 20, g >> 1) + (g & 1) * 8;
       *reinterpret_cast<uint2*>(lds + off) = ph;
       *reinterpret_cast<uint2*>(lds + off + A1P) = pm;
       *reinterpret_cast<uint2*>(lds + off + 2 * A1P) = pl;
@@ -500,9 +511,13 @@ conv_fwd_kernel(ConvFwdArgs a) {
     const int mA = w8 >> 1, mB = mA + 4;
     const bool hasB = mB < 6;
     const int posA = 16 * mA + col, posB = 16 * (hasB ? mB : mA) + col;   // A row of this lane
-    const int pcA = posA < C2_P ? posA : 0, pcB = posB < C2_P ? posB : 0;
+    // rows past the 81 positions compute (and drop) the position 16 before: 16 consecutive positions
+    // whatever the tile, so the a1 reads stay on distinct banks
+    const int pcA = posA < C2_P ? posA : posA - 16, pcB = posB < C2_P ? posB : posB - 16;
     const int oyA = pcA / 9, oxA = pcA - oyA * 9, oyB = pcB / 9, oxB = pcB - oyB * 9;
-    const int PA0 = (2 * oyA) * 20 + 2 * oxA, PB0 = (2 * oyB) * 20 + 2 * oxB;
+    // a1 offset of tap (ky, kx) = divmod(2 s + (g >> 1), 4) for this lane's position of tile A / B
+    auto a1A = [&](int tap) { return LY::A1(el) + a1_off(2 * oyA + (tap >> 2), 2 * oxA + (tap & 3), g & 1); };
+    auto a1B = [&](int tap) { return LY::A1(el) + a1_off(2 * oyB + (tap >> 2), 2 * oxB + (tap & 3), g & 1); };
     f32x4 bigA = {0.f, 0.f, 0.f, 0.f}, smlA = bigA, bigB = bigA, smlB = bigA;
 #if ARL_CF_PREFETCH
     {
@@ -510,8 +525,8 @@ conv_fwd_kernel(ConvFwdArgs a) {
       bf16x8 w2[2][3], aA[2][3], aB[2][3];
       auto load = [&](int s, int b) {
         const int off = LY::W2 + oc * WROW + (2 * s + (g >> 1)) * 32 + (g & 1) * 16;
-        const int tap = 2 * s + (g >> 1), dP = (tap >> 2) * 20 + (tap & 3);
-        const int offA = LY::A1(el) + a1_slot(PA0 + dP, g & 1), offB = LY::A1(el) + a1_slot(PB0 + dP, g & 1);
+        const int tap = 2 * s + (g >> 1);
+        const int offA = a1A(tap), offB = a1B(tap);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
           w2[b][k] = lds_load<bf16x8>(lds, off + k * W2P);
@@ -540,13 +555,13 @@ conv_fwd_kernel(ConvFwdArgs a) {
         w2m[0] = lds_load<bf16x8>(lds, off + W2P);
         w2l[0] = lds_load<bf16x8>(lds, off + 2 * W2P);
       }
-      const int tap = 2 * s + (g >> 1), dP = (tap >> 2) * 20 + (tap & 3);
-      const int offA = LY::A1(el) + a1_slot(PA0 + dP, g & 1);
+      const int tap = 2 * s + (g >> 1);
+      const int offA = a1A(tap);
       const bf16x8 ahA = lds_load<bf16x8>(lds, offA), amA = lds_load<bf16x8>(lds, offA + A1P),
                    alA = lds_load<bf16x8>(lds, offA + 2 * A1P);
       mfma_x6(ahA, amA, alA, w2h[0], w2m[0], w2l[0], bigA, smlA);
       if (hasB) {
-        const int offB = LY::A1(el) + a1_slot(PB0 + dP, g & 1);
+        const int offB = a1B(tap);
         const bf16x8 ahB = lds_load<bf16x8>(lds, offB), amB = lds_load<bf16x8>(lds, offB + A1P),
                      alB = lds_load<bf16x8>(lds, offB + 2 * A1P);
         mfma_x6(ahB, amB, alB, w2h[0], w2m[0], w2l[0], bigB, smlB);
