@@ -246,12 +246,13 @@ conv_fwd_kernel(ConvFwdArgs a) {
   // over the 4 SIMDs instead of 14 + 12 + 12 + 12 (the same tiles and k order: bit-identical)
   const int wt = EPW == 2 ? (w8 + 8 - el) & 7 : w8;
   const bool has3 = wt + 24 < 25;   // wave-uniform
-  int baseX[TJ];
+  int baseX[TJ], a1o[TJ];   // screen row base of the tile's position; its a1 slot (the epilogue's store)
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int tl = (j < 3 || has3) ? wt + 8 * j : wt;
     const int p = tl * 16 + col, oy = p / 20, ox = p - oy * 20;
     baseX[j] = LY::XB(el) + (4 * oy) * XB_ROW + 8 * ox;
+    a1o[j] = LY::A1(el) + a1_off(oy, ox, g >> 1) + (g & 1) * 8;
   }
   f32x4 big[TJ], sml[TJ];
 #pragma unroll
@@ -505,7 +506,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
       uint2 ph, pm, pl;
       split3_pack(ov[0], ov[1], ph.x, pm.x, pl.x);
       split3_pack(ov[2], ov[3], ph.y, pm.y, pl.y);
-      const int off = LY::A1(el) + a1_off(p / 20, p % 20, g >> 1) + (g & 1) * 8;
+      const int off = a1o[j];
       *reinterpret_cast<uint2*>(lds + off) = ph;
       *reinterpret_cast<uint2*>(lds + off + A1P) = pm;
       *reinterpret_cast<uint2*>(lds + off + 2 * A1P) = pl;
