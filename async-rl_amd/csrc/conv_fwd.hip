@@ -64,10 +64,7 @@ namespace arl {
 namespace {
 constexpr int NT = 512;                  // threads per workgroup (8 waves)
 constexpr int XB_ROW = 84 * 2;           // bytes per bf16 screen row
-// bytes per bf16 screen: 14,112 + 96, so the plane stride is 128 mod 256 bytes -- conv1's lane groups 0 / 1
-// (and 2 / 3) of a k-step read planes c and c ^ 1 of one kernel row (k_plane, k_row), whose 16 positions
-// then fill the other half of the 64 banks (a 32-lane ds_read_b64 without conflicts)
-constexpr int XB_PLANE = PLANE * 2 + 96;
+constexpr int XB_PLANE = PLANE * 2;      // 14,112 bytes per bf16 screen
 // bytes per oc row of a weight plane: 512 + 32, so the 16 rows a ds_read_b128 lane group reads (8 of one
 // 16-byte k half, 8 of the other) land on 16 distinct bank quads (528 = 512 + 16 left a 2-way conflict)
 constexpr int WROW = 544;
@@ -78,9 +75,9 @@ constexpr int W2P = 32 * WROW;           // 17,408 per W2 plane
 constexpr int A1_PS = 108, A1_HALF = 4 * A1_PS;
 constexpr int A1P = 2 * A1_HALF * 16;    // 13,824 per a1 plane (400 pixels x 16 ic bf16 + pad)
 constexpr int L_XB = 0;
-constexpr int L_R1 = L_XB + 4 * XB_PLANE;   // 56,832
-constexpr int L_W2 = L_R1 + 3 * A1P;        // 98,304
-constexpr int L_END = L_W2 + 3 * W2P;       // 150,528
+constexpr int L_R1 = L_XB + 4 * XB_PLANE;   // 56,448
+constexpr int L_W2 = L_R1 + 3 * A1P;        // 97,920
+constexpr int L_END = L_W2 + 3 * W2P;       // 150,144
 static_assert(3 * W1P <= 3 * A1P, "W1 planes fit the a1 region");
 // PHI: gray tap rows + coefficient tables in the W2 region (W2 is split into it after the resize)
 constexpr int G_ROWS = 2 * DST;                       // 168 (output row, tap) source rows
@@ -92,16 +89,16 @@ constexpr int PHI_J = (PHI_TASKS + NT - 1) / NT;      // 4
 
 // LDS layout by envs per workgroup (EPW).  EPW = 1 is the layout above.  EPW = 2
 // (1,024 threads; waves 0-7 take env 0, waves 8-15 env 1, both share the weight
-// planes): conv1 phase  [screens e0 | screens e1 | W1 planes]       139,776 B;
+// planes): conv1 phase  [screens e0 | screens e1 | W1 planes]       139,008 B;
 //          conv2 phase  [a1 planes e0 | a1 planes e1 | W2 planes]  135,168 B
 // (W2 is split into the dead screen / W1 bytes after conv1's barrier).
 template <int EPW>
 struct Lay {
   static constexpr int XB(int el) { return el * 4 * XB_PLANE; }
-  static constexpr int W1 = EPW * 4 * XB_PLANE;                      // 56,832 / 113,664
+  static constexpr int W1 = EPW * 4 * XB_PLANE;                      // 56,448 / 112,896
   static constexpr int A1(int el) { return EPW == 1 ? W1 : el * 3 * A1P; }
-  static constexpr int W2 = EPW == 1 ? L_W2 : 2 * 3 * A1P;           // 98,304 / 82,944
-  static constexpr int END = EPW == 1 ? L_END : W1 + 3 * W1P;        // 150,528 / 139,776
+  static constexpr int W2 = EPW == 1 ? L_W2 : 2 * 3 * A1P;           // 97,920 / 82,944
+  static constexpr int END = EPW == 1 ? L_END : W1 + 3 * W1P;        // 150,144 / 139,008
   // a2 > 0 mask words (81 u32 per env) in bytes dead during conv2: the screens (EPW 1), past the W2
   // planes (EPW 2)
   static constexpr int MSK(int el) { return EPW == 1 ? 0 : W2 + 3 * W2P + el * 336; }
@@ -153,13 +150,6 @@ __device__ inline void w1_load(const float* W1, bool rgb, int tid, float4& w1a, 
   w1a = w1p[0];
   w1b = w1p[1];
 }
-// conv1's k order: k-step s, lane group g take the 8 kx of input plane k_plane(s, g), kernel row k_row(s, g)
-// (a bijection of (s, g) onto the 32 (plane, row) pairs); the W1 planes are stored in that order, the
-// fragment of (s, g) at slot 4 s + g of its oc row
-__device__ inline int k_plane(int s, int g) { return 2 * (s >> 2) + (g & 1); }
-__device__ inline int k_row(int s, int g) { return 2 * (s & 3) + (g >> 1); }
-__device__ inline int k_slot(int c, int ky) { return 16 * (c >> 1) + 4 * (ky >> 1) + 2 * (ky & 1) + (c & 1); }
-
 __device__ inline void w1_split_store(uint8_t* lds, int tid, float4 w1a, float4 w1b, bool rgb = false, int base = L_R1) {
   const int w1oc = tid >> 5, w1k = (8 * tid) & 255;
   if (rgb && w1k < 64) w1a = w1b = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -168,7 +158,7 @@ __device__ inline void w1_split_store(uint8_t* lds, int tid, float4 w1a, float4 
   split3_pack(w1a.z, w1a.w, ph.y, pm.y, pl.y);
   split3_pack(w1b.x, w1b.y, ph.z, pm.z, pl.z);
   split3_pack(w1b.z, w1b.w, ph.w, pm.w, pl.w);
-  uint8_t* d = lds + base + w1oc * WROW + k_slot(w1k >> 6, (w1k >> 3) & 7) * 16;
+  uint8_t* d = lds + base + w1oc * WROW + w1k * 2;
   *reinterpret_cast<uint4*>(d) = ph;
   *reinterpret_cast<uint4*>(d + W1P) = pm;
   *reinterpret_cast<uint4*>(d + 2 * W1P) = pl;
@@ -257,9 +247,9 @@ conv_fwd_kernel(ConvFwdArgs a) {
   f32x4 big[TJ], sml[TJ];
 #pragma unroll
   for (int j = 0; j < TJ; ++j) big[j] = sml[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // k-step s of every tile; lane group g: the 8 kx of plane k_plane(s, g), kernel row k_row(s, g)
+  // k-step s of every tile; W1 fragments of lane (oc = col, g): k = 8 (4 s + g) + 0..7
   auto conv1_step = [&](int s, bf16x8 wh, bf16x8 wm, bf16x8 wl) {
-    const int off = k_plane(s, g) * XB_PLANE + k_row(s, g) * XB_ROW;
+    const int u = 4 * s + g, off = (u >> 3) * XB_PLANE + (u & 7) * XB_ROW;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const bf16x8 xa = lds_load8_a8(lds, baseX[j] + off);
@@ -344,9 +334,9 @@ conv_fwd_kernel(ConvFwdArgs a) {
     }
     w1_split_store(lds, tid, w1a, w1b);
     __syncthreads();
-    // ---- conv1 k-steps over input planes 0..1 on the matrix cores (k_plane: steps 0..3)
+    // ---- conv1 k-steps over input planes 0..2 on the matrix cores
 #pragma unroll
-    for (int s = 0; s < ((ARL_ABLATE & 1) ? 0 : 4); ++s) {
+    for (int s = 0; s < ((ARL_ABLATE & 1) ? 0 : 6); ++s) {
       bf16x8 wh, wm, wl;
       w1_frag(s, wh, wm, wl);
       conv1_step(s, wh, wm, wl);
@@ -401,9 +391,9 @@ conv_fwd_kernel(ConvFwdArgs a) {
     }
     __syncthreads();   // plane 3 complete, the gray rows dead
     w2_split_store(lds, tid, w2v);   // conv2 reads it after the barrier in front of conv2
-    // ---- conv1's last k-steps (input planes 2 and 3)
+    // ---- conv1's last k-steps (input plane 3)
 #pragma unroll
-    for (int s = 4; s < ((ARL_ABLATE & 1) ? 0 : 8); ++s) {
+    for (int s = 6; s < ((ARL_ABLATE & 1) ? 0 : 8); ++s) {
       bf16x8 wh, wm, wl;
       w1_frag(s, wh, wm, wl);
       conv1_step(s, wh, wm, wl);
@@ -455,7 +445,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
       bf16x8 wh[2], wm[2], wl[2], xa[2][TJ];
       auto load = [&](int s, int b) {
         w1_frag(s, wh[b], wm[b], wl[b]);
-        const int off = k_plane(s, g) * XB_PLANE + k_row(s, g) * XB_ROW;
+        const int u = 4 * s + g, off = (u >> 3) * XB_PLANE + (u & 7) * XB_ROW;
 #pragma unroll
         for (int j = 0; j < TJ; ++j) xa[b][j] = lds_load8_a8(lds, baseX[j] + off);
       };
