@@ -99,6 +99,17 @@ __device__ inline void mfma_x3_t(bf16x8 a, bf16x8 bh, bf16x8 bm, bf16x8 bl, f32x
   big = mfma_bf16(bh, a, big);
 }
 
+// mfma_x6 with the operands' roles swapped (the same products and k order, the transposed tile)
+__device__ inline void mfma_x6_t(bf16x8 ah, bf16x8 am, bf16x8 al, bf16x8 bh, bf16x8 bm, bf16x8 bl, f32x4& big,
+                                 f32x4& small) {
+  small = mfma_bf16(bh, al, small);
+  small = mfma_bf16(bm, am, small);
+  small = mfma_bf16(bl, ah, small);
+  small = mfma_bf16(bh, am, small);
+  small = mfma_bf16(bm, ah, small);
+  big = mfma_bf16(bh, ah, big);
+}
+
 // both split: big += Ah.Bh; small += Al.Bh + Am.Bm + Ah.Bl + Am.Bh + Ah.Bm
 __device__ inline void mfma_x6(bf16x8 ah, bf16x8 am, bf16x8 al, bf16x8 bh, bf16x8 bm, bf16x8 bl, f32x4& big,
                                f32x4& small) {

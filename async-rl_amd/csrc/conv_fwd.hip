@@ -225,7 +225,9 @@ conv_fwd_kernel(ConvFwdArgs a) {
 #endif
   // conv1 runs transposed (mfma_x3_t): lane (g, col) holds oc 4g..4g+3 of position tile * 16 + col
   const float bias1[4] = {a.b1[4 * g], a.b1[4 * g + 1], a.b1[4 * g + 2], a.b1[4 * g + 3]};
-  const float bias2 = a.b2[16 * (w8 & 1) + col];
+  // conv2 runs transposed too (mfma_x6_t): lane (g, col) holds oc 16 nt + 4 g + r of position 16 m + col
+  const float bias2[4] = {a.b2[16 * (w8 & 1) + 4 * g], a.b2[16 * (w8 & 1) + 4 * g + 1], a.b2[16 * (w8 & 1) + 4 * g + 2],
+                          a.b2[16 * (w8 & 1) + 4 * g + 3]};
   const int64_t ks = a.ctl[CTL_STEP] + a.t;
   const int rs = (int)(ks % a.R);
   // conv1 tiles w, w + 8, w + 16 (and 24 on wave 0): 25 tiles over 8 waves in one
@@ -541,8 +543,8 @@ conv_fwd_kernel(ConvFwdArgs a) {
         const int b = s & 1;
         if (s + 1 < 8) load(s + 1, b ^ 1);
         __builtin_amdgcn_sched_barrier(0);
-        mfma_x6(aA[b][0], aA[b][1], aA[b][2], w2[b][0], w2[b][1], w2[b][2], bigA, smlA);
-        if (hasB) mfma_x6(aB[b][0], aB[b][1], aB[b][2], w2[b][0], w2[b][1], w2[b][2], bigB, smlB);
+        mfma_x6_t(aA[b][0], aA[b][1], aA[b][2], w2[b][0], w2[b][1], w2[b][2], bigA, smlA);
+        if (hasB) mfma_x6_t(aB[b][0], aB[b][1], aB[b][2], w2[b][0], w2[b][1], w2[b][2], bigB, smlB);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -560,53 +562,44 @@ conv_fwd_kernel(ConvFwdArgs a) {
       const int offA = a1A(tap);
       const bf16x8 ahA = lds_load<bf16x8>(lds, offA), amA = lds_load<bf16x8>(lds, offA + A1P),
                    alA = lds_load<bf16x8>(lds, offA + 2 * A1P);
-      mfma_x6(ahA, amA, alA, w2h[0], w2m[0], w2l[0], bigA, smlA);
+      mfma_x6_t(ahA, amA, alA, w2h[0], w2m[0], w2l[0], bigA, smlA);
       if (hasB) {
         const int offB = a1B(tap);
         const bf16x8 ahB = lds_load<bf16x8>(lds, offB), amB = lds_load<bf16x8>(lds, offB + A1P),
                      alB = lds_load<bf16x8>(lds, offB + 2 * A1P);
-        mfma_x6(ahB, amB, alB, w2h[0], w2m[0], w2l[0], bigB, smlB);
+        mfma_x6_t(ahB, amB, alB, w2h[0], w2m[0], w2l[0], bigB, smlB);
       }
     }
 #endif
     CF_STAMP();   // 6: conv2 MFMAs issued
     float* a2g = a.a2 + (int64_t)e * A2;
-    const float b = bias2;   // b2[oc]
-    // a2 > 0 -> bit k = oc * 81 + p of the env's mask words: a lane's 4 positions 16 m + 4 g + r are 4
-    // consecutive bits, lanes g = 0..3 of one oc a 16-bit run, or'd into the LDS words by lane g = 0
-    // (one or two ors per oc and tile, no two lanes on one word; stored after a barrier)
+    // a2 > 0 -> bit k = oc * 81 + p of the env's mask words: for each r the 16 lanes of group g hold 16
+    // consecutive positions of one oc, a 16-bit run of the wave's ballot, or'd into the LDS words by the
+    // group's lane 0 (one or two ors, no two lanes of a wave on one word; stored after a barrier)
     const bool mk = a.a2m != nullptr;
-    auto mask_or = [&](unsigned nib, int m) {
-      nib <<= 4 * g;
-      nib |= __shfl_xor(nib, 16);
-      nib |= __shfl_xor(nib, 32);
-      if (g == 0 && nib != 0u) {
-        const int k = oc * C2_P + 16 * m, sh = k & 31;
-        __hip_atomic_fetch_or(msk + (k >> 5), nib << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (sh > 16)
-          __hip_atomic_fetch_or(msk + (k >> 5) + 1, nib >> (32 - sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    };
-    unsigned nibA = 0u;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int p = 16 * mA + g * 4 + r;
-      const float v = fmaxf(__fadd_rn(__fadd_rn(bigA[r], smlA[r]), b), 0.f);
-      if (valid && p < C2_P) a2g[oc * C2_P + p] = v;
-      if (p < C2_P && v > 0.f) nibA |= 1u << r;
-    }
-    if (mk) mask_or(nibA, mA);
-    if (hasB) {
-      unsigned nibB = 0u;
+    auto tile_out = [&](const f32x4& big, const f32x4& sml, int m) {
+      const int p = 16 * m + col;
+      const bool pin = p < C2_P;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int p = 16 * mB + g * 4 + r;
-        const float v = fmaxf(__fadd_rn(__fadd_rn(bigB[r], smlB[r]), b), 0.f);
-        if (valid && p < C2_P) a2g[oc * C2_P + p] = v;
-        if (p < C2_P && v > 0.f) nibB |= 1u << r;
+        const int o = 16 * nt + 4 * g + r;
+        const float v = fmaxf(__fadd_rn(__fadd_rn(big[r], sml[r]), bias2[r]), 0.f);
+        if (valid && pin) a2g[o * C2_P + p] = v;
+        if (mk) {   // (block-uniform)
+          const unsigned long long bal = __ballot(pin && v > 0.f);
+          const unsigned run = (unsigned)(bal >> (16 * g)) & 0xffffu;
+          if (col == 0 && run != 0u) {
+            const int k = o * C2_P + 16 * m, sh = k & 31;
+            __hip_atomic_fetch_or(msk + (k >> 5), run << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (sh > 16)
+              __hip_atomic_fetch_or(msk + (k >> 5) + 1, run >> (32 - sh), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+        }
       }
-      if (mk) mask_or(nibB, mB);
-    }
+    };
+    tile_out(bigA, smlA, mA);
+    if (hasB) tile_out(bigB, smlB, mB);
     if (mk) {   // (block-uniform)
       __syncthreads();
       if (valid && t8 < A2W) a.a2m[(int64_t)e * (A2W) + t8] = msk[t8];
