@@ -27,8 +27,9 @@ echo "prof ok" >> $O/status
 for ab in $AB; do
   case $ab in
     phidma) bash scripts/env_ab.sh ARL_PHI_DMA=0 ARL_PHI_DMA=1 "" 2 phidma || exit $? ;;
-    variants) bash scripts/gpu_variants.sh "--steps 100 --warmup 10 --kernel-reps 3 --copy-peak 0 --secondary none" 2 "$VARIANTS" > $O/variants.txt 2>&1 || exit $?
-              bash scripts/gpu_variants.sh "--workload c2 --steps 100 --warmup 10 --kernel-reps 3 --copy-peak 0" 2 "$VARIANTS" > $O/variants_c2.txt 2>&1 || exit $? ;;
+    variants) for w in ${VARWL:-c4 c2}; do
+                bash scripts/gpu_variants.sh "--workload $w --steps 100 --warmup 10 --kernel-reps 3 --copy-peak 0 --secondary none" 2 "$VARIANTS" > $O/variants_$w.txt 2>&1 || exit $?
+              done ;;
     varparity) for v in $VARIANTS; do
                  ASYNCRL_HIP_LIB=$PWD/async-rl_amd/csrc/build_var_$v/libasyncrl_hip.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "configs or window_matches or norm_fold" > $O/varparity_$v.log 2>&1 || exit $?
                done ;;
