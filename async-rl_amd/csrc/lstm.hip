@@ -35,15 +35,16 @@ namespace {
 constexpr int LBM = 32, LBN = 64, LT = 512, LW = LT / 64;
 constexpr int LKC = 128;                       // K chunk (columns)
 constexpr int LROWS = LBN + LBM;               // 96 staged rows: 64 of [Wu | Wl], then 32 of [x | h]
-// float4 per staged row (32 used).  ARL_LSTM_LD=34 (A/B knob): 34 = 2 mod 16, so the 8 + 8 rows of a
-// ds_read_b128 lane group's two 16-byte k quarters land on 16 distinct bank quads (33 = 1 mod 16 puts two
-// of them on one quad); the same for the BPTT kernel's dG rows (BA_LD)
+// float4 per staged row (32 used): 34 = 2 mod 16, so the 8 + 8 rows of a ds_read_b128 lane group's two
+// 16-byte k quarters land on 16 distinct bank quads (33 = 1 mod 16 puts two of them on one quad); the
+// same for the BPTT kernel's dG rows (BA_LD).  34 vs 33 at C3: lstm_gates 20.3 -> 19.2 us, lstm_bptt
+// 17.1 -> 16.8 us, window 1.151 -> 1.140 ms (profiles/r04/r4o)
 #ifndef ARL_LSTM_LD
-#define ARL_LSTM_LD 33
+#define ARL_LSTM_LD 34
 #endif
 constexpr int LLD = ARL_LSTM_LD;
-constexpr int LPIECES = (LROWS * LLD + 63) / 64;   // 50 LDS-DMA pieces (64 x 16 B) per chunk
-constexpr int LWPIECES = LBN * LLD / 64;       // 33: the W rows alone (XRED x chunks)
+constexpr int LPIECES = (LROWS * LLD + 63) / 64;   // 51 LDS-DMA pieces (64 x 16 B) per chunk
+constexpr int LWPIECES = LBN * LLD / 64;       // 34: the W rows alone (XRED x chunks)
 constexpr int LSTAGE4 = LPIECES * 64;          // float4 per stage (incl. the last piece's overhang)
 constexpr int LSTAGES = 3;
 constexpr int TLD = 68;                        // epilogue tile row stride (floats)
@@ -294,7 +295,7 @@ namespace {
 constexpr int BBM = 32, BBN = 32, BT = 512, BW = BT / 64;
 constexpr int BKC = 128;                                 // K chunk
 constexpr int BNCH = GATES / BKC;                        // 8 chunks
-constexpr int BA_LD = ARL_LSTM_LD;                       // 33 (34) float4 per dG row
+constexpr int BA_LD = ARL_LSTM_LD;                       // 34 float4 per dG row
 constexpr int BB_LD = BBN / 4 + 1;                       // 9 float4 per Wl row
 constexpr int BA_PC = (BBM * BA_LD + 63) / 64;           // 17 pieces
 constexpr int BB_PC = (BKC * BB_LD + 63) / 64;           // 18 pieces
