@@ -32,7 +32,7 @@ for name, lst in sorted(per.items(), key=lambda kv: -sum(d["cycles"] for d in kv
     avg = {k: sum(d[k] for d in lst) / n for k in lst[0]}
     if avg["mfma_insts"] == 0:
         continue
-    short = name.split("(")[0][:70]
+    short = name.replace("(anonymous namespace)::", "").split("(")[0][:90]
     out[short] = {"dispatches": n, "mfma_busy_frac": round(avg["util"], 4), "cycles": round(avg["cycles"]),
                   "mfma_insts": round(avg["mfma_insts"]), "valu_insts": round(avg["valu_insts"]),
                   "lds_insts": round(avg["lds_insts"]), "waves": round(avg["waves"])}
