@@ -74,6 +74,12 @@
 #ifndef ARL_S1_SPLIT
 #define ARL_S1_SPLIT 0
 #endif
+// static wave priority (A/B knob): the second-dispatched half of the workgroup (waves 4-7, the
+// arbitration losers when two waves share a SIMD, MI355X_MICROARCH.md "Two waves per SIMD" item 4)
+// at s_setprio 1 for the whole kernel
+#ifndef ARL_CB_PRIO
+#define ARL_CB_PRIO 0
+#endif
 #ifndef ARL_CB_STAMP
 #define ARL_CB_STAMP 0   // timing experiments only: s_memtime at every barrier into the slab (results wrong)
 #endif
@@ -317,6 +323,7 @@ conv_bwd_kernel(ConvBwdArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, col = lane & 15;
+  if (ARL_CB_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
 #if ARL_CB_STAMP
   __shared__ uint32_t stamp[32];
   const uint64_t t0 = __builtin_amdgcn_s_memtime();

@@ -55,6 +55,11 @@
 #define ARL_CF_PREFETCH 0
 #endif
 
+// static wave priority (A/B knob): the second-dispatched half of the workgroup's waves at s_setprio 1
+// (MI355X_MICROARCH.md "Two waves per SIMD" item 4)
+#ifndef ARL_CF_PRIO
+#define ARL_CF_PRIO 0
+#endif
 #ifndef ARL_CF_STAMP
 #define ARL_CF_STAMP 0   // timing experiments only: s_memtime at phase ends into a2 (results wrong)
 #endif
@@ -205,6 +210,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, col = lane & 15;
+  if (ARL_CF_PRIO && wave >= NT * EPW / 128) __builtin_amdgcn_s_setprio(1);
   // EPW = 2: waves 0-7 (threads 0-511) env slot 0, waves 8-15 slot 1; w8 / t8 index within the slot
   const int el = EPW == 1 ? 0 : wave >> 3;
   const int w8 = wave & 7, t8 = tid & (NT - 1);

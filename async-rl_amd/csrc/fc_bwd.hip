@@ -718,6 +718,12 @@ __device__ void job_heads(const FcBwdArgs& a, int jt, float* lds) {
   }
 }
 
+// static wave priority (A/B knob): 1 = job A (dW) workgroups at s_setprio 1, 2 = job B (da2) ones; a CU
+// holds two workgroups, whose waves pair up on its SIMDs (MI355X_MICROARCH.md "Two waves per SIMD")
+#ifndef ARL_FCB_PRIO
+#define ARL_FCB_PRIO 0
+#endif
+
 template <int MT, bool SPLIT, class SH>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2)))
 fc_bwd_kernel(FcBwdArgs a) {
@@ -726,8 +732,13 @@ fc_bwd_kernel(FcBwdArgs a) {
   const int b = a.b0 + blockIdx.x;
   const int na = Dims<SH>::NTA * a.Z;
   if (b < a.nc) job_heads(a, b, lds);   // first: the smallest, longest-latency jobs
-  else if (b < a.nc + na) job_dw<SPLIT, SH>(a, b - a.nc, lds, rst);
-  else job_da2<MT, SPLIT, SH>(a, b - a.nc - na, lds);
+  else if (b < a.nc + na) {
+    if (ARL_FCB_PRIO == 1) __builtin_amdgcn_s_setprio(1);
+    job_dw<SPLIT, SH>(a, b - a.nc, lds, rst);
+  } else {
+    if (ARL_FCB_PRIO == 2) __builtin_amdgcn_s_setprio(1);
+    job_da2<MT, SPLIT, SH>(a, b - a.nc - na, lds);
+  }
 }
 
 // ~800 samples per job A range, at most 16 ranges (bf16-split steps, sweep in

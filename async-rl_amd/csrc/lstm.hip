@@ -42,6 +42,11 @@ constexpr int LROWS = LBN + LBM;               // 96 staged rows: 64 of [Wu | Wl
 #ifndef ARL_LSTM_LD
 #define ARL_LSTM_LD 34
 #endif
+// static wave priority (A/B knob): waves 4-7 of the gate and BPTT workgroups at s_setprio 1
+// (MI355X_MICROARCH.md "Two waves per SIMD" item 4)
+#ifndef ARL_LSTM_PRIO
+#define ARL_LSTM_PRIO 0
+#endif
 constexpr int LLD = ARL_LSTM_LD;
 constexpr int LPIECES = (LROWS * LLD + 63) / 64;   // 51 LDS-DMA pieces (64 x 16 B) per chunk
 constexpr int LWPIECES = LBN * LLD / 64;       // 34: the W rows alone (XRED x chunks)
@@ -96,8 +101,9 @@ struct LstmGatesArgs {
 template <bool XRED>
 __global__ void __launch_bounds__(LT)
 lstm_gates_kernel(LstmGatesArgs a) {
-  __shared__ __attribute__((aligned(16))) float S[LSTAGES * LSTAGE4 * 4];   // 153,600 B
+  __shared__ __attribute__((aligned(16))) float S[LSTAGES * LSTAGE4 * 4];   // 156,672 B
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (ARL_LSTM_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
   constexpr int NTN = GATES / LBN;
   const int m0 = (blockIdx.x / NTN) * LBM, n0 = (blockIdx.x % NTN) * LBN;
 
@@ -339,6 +345,7 @@ __global__ void __launch_bounds__(BT)
 lstm_bptt_kernel(LstmBpttArgs a) {
   __shared__ __attribute__((aligned(16))) float S[BSTAGES * BSTAGE4 * 4];   // 143,360 B
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (ARL_LSTM_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
   constexpr int NTN = HID / BBN;
   const int m0 = (blockIdx.x / NTN) * BBM, u0 = (blockIdx.x % NTN) * BBN;
   const int pw = bptt_pieces(wave);
