@@ -60,6 +60,10 @@
 #ifndef ARL_CF_PRIO
 #define ARL_CF_PRIO 0
 #endif
+// a1 / a2 global stores non-temporal (A/B knob): nothing reads them before the window's backward
+#ifndef ARL_CF_NTST
+#define ARL_CF_NTST 0
+#endif
 #ifndef ARL_CF_STAMP
 #define ARL_CF_STAMP 0   // timing experiments only: s_memtime at phase ends into a2 (results wrong)
 #endif
@@ -499,7 +503,10 @@ conv_fwd_kernel(ConvFwdArgs a) {
                     : fmaxf(__fadd_rn(div255(__fadd_rn(big[j][r], sml[j][r])), bias1[r]), 0.f);
       if (valid && a.a1 != nullptr) {   // (null: the bootstrap slot, which no backward reads)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) a1g[(4 * g + r) * C1_P + p] = ov[r];
+        for (int r = 0; r < 4; ++r) {
+          if (ARL_CF_NTST) __builtin_nontemporal_store(ov[r], a1g + (4 * g + r) * C1_P + p);
+          else a1g[(4 * g + r) * C1_P + p] = ov[r];
+        }
       }
       uint2 ph, pm, pl;
       split3_pack(ov[0], ov[1], ph.x, pm.x, pl.x);
@@ -590,7 +597,10 @@ conv_fwd_kernel(ConvFwdArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int o = 16 * nt + 4 * g + r;
         const float v = fmaxf(__fadd_rn(__fadd_rn(big[r], sml[r]), bias2[r]), 0.f);
-        if (valid && pin) a2g[o * C2_P + p] = v;
+        if (valid && pin) {
+          if (ARL_CF_NTST) __builtin_nontemporal_store(v, a2g + o * C2_P + p);
+          else a2g[o * C2_P + p] = v;
+        }
         if (mk) {   // (block-uniform)
           const unsigned long long bal = __ballot(pin && v > 0.f);
           const unsigned run = (unsigned)(bal >> (16 * g)) & 0xffffu;

@@ -69,6 +69,10 @@ constexpr int BK = 32;                  // K chunk (rows of a stage)
 #ifndef ARL_FCB_AJ
 #define ARL_FCB_AJ 128
 #endif
+// job B's da2 stores with the non-temporal cache policy (A/B knob)
+#ifndef ARL_FCB_NTST
+#define ARL_FCB_NTST 0
+#endif
 constexpr int AJ = ARL_FCB_AJ, AK = 8192 / ARL_FCB_AJ;
 constexpr int AWN = AK / 32;            // job A waves along k (64: 2, 32: 1)
 constexpr int STAGE = BK * (AJ + AK) > 8192 ? BK * (AJ + AK) : 8192;   // floats per LDS stage
@@ -651,7 +655,8 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
         if constexpr (SPLIT) v += sml[i][u][e];
         o[u] = (mb[i] >> (4 * e + u)) & 1u ? v : 0.f;
       }
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), out, kin ? (row * NB + k) * 4 : OOB, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), out, kin ? (row * NB + k) * 4 : OOB, 0,
+                                              ARL_FCB_NTST ? 2 : 0);
     }
 }
 
