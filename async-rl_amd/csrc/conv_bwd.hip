@@ -80,6 +80,10 @@
 #ifndef ARL_CB_PRIO
 #define ARL_CB_PRIO 0
 #endif
+// the per-workgroup slab stores non-temporal (A/B knob)
+#ifndef ARL_CB_NTST
+#define ARL_CB_NTST 0
+#endif
 #ifndef ARL_CB_STAMP
 #define ARL_CB_STAMP 0   // timing experiments only: s_memtime at every barrier into the slab (results wrong)
 #endif
@@ -315,6 +319,11 @@ __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_b
 __device__ inline bf16x8 frag_from_pairs(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   return __builtin_bit_cast(bf16x8, (u32x4{p0, p1, p2, p3}));
+}
+
+__device__ inline void slab_store(float* p, float v) {
+  if (ARL_CB_NTST) __builtin_nontemporal_store(v, p);
+  else *p = v;
 }
 
 __global__ void __launch_bounds__(NT)
@@ -663,9 +672,9 @@ conv_bwd_kernel(ConvBwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #if ARL_S1_SPLIT
-        out[(16 * mt + g * 4 + r) * 256 + 16 * (2 * wave + j) + col] = __fadd_rn(acc1[mt][j][r], sml1[mt][j][r]);
+        slab_store(out + (16 * mt + g * 4 + r) * 256 + 16 * (2 * wave + j) + col, __fadd_rn(acc1[mt][j][r], sml1[mt][j][r]));
 #else
-        out[(16 * mt + g * 4 + r) * 256 + 16 * (2 * wave + j) + col] = acc1[mt][j][r];
+        slab_store(out + (16 * mt + g * 4 + r) * 256 + 16 * (2 * wave + j) + col, acc1[mt][j][r]);
 #endif
   // dW1^T: tile a, C row g*4 + r -> ky = 4 (w & 1) + (row >> 2), kx = 4 a + (row & 3)
 #pragma unroll
@@ -674,7 +683,7 @@ conv_bwd_kernel(ConvBwdArgs a) {
     for (int r = 0; r < 4; ++r) {
       const int row = g * 4 + r;
       const int ky = 4 * (wave & 1) + (row >> 2), kx = 4 * a_ + (row & 3);
-      out[SLAB_W1 + ((wave >> 1) * 64 + ky * 8 + kx) * 16 + col] = __fadd_rn(big3[a_][r], sml3[a_][r]);
+      slab_store(out + SLAB_W1 + ((wave >> 1) * 64 + ky * 8 + kx) * 16 + col, __fadd_rn(big3[a_][r], sml3[a_][r]));
     }
   }
   float* red = reinterpret_cast<float*>(lds + L_RED);

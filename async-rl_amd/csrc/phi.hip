@@ -39,6 +39,15 @@ struct PhiShared {
   int16_t yb0[BAND], yb1[BAND];
 };
 
+// the resized plane's store into the ring (A/B knob ARL_PHI_NTST: non-temporal)
+#ifndef ARL_PHI_NTST
+#define ARL_PHI_NTST 0
+#endif
+__device__ inline void ring_store(uint32_t* p, uint32_t v) {
+  if (ARL_PHI_NTST) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 // Computes output rows [dy0, dy0+BAND) of one env's screen into `out`
 // (row stride 84).  cur/prev: the env's two RGB frames (HWC, uint8).
 // non-temporal loads of the frame pairs (A/B knob, off: phi_ring 10.1 -> 13.0 us at C2, 19.1 -> 23.7 us
@@ -108,7 +117,7 @@ __device__ inline void phi_band(const uint8_t* __restrict__ cur, const uint8_t* 
       const int v = resize_vpass(r0, r1, b0, b1, mode);
       packed |= (uint32_t)v << (8 * j);
     }
-    *reinterpret_cast<uint32_t*>(out + (size_t)(dy0 + ly) * DST + q * 4) = packed;
+    ring_store(reinterpret_cast<uint32_t*>(out + (size_t)(dy0 + ly) * DST + q * 4), packed);
   }
 }
 
@@ -176,7 +185,7 @@ __device__ inline void phi_band_dma(const uint8_t* __restrict__ cur, const uint8
       const int r1 = (int)sh.gray[ly][1][sx] * a0 + (int)sh.gray[ly][1][sx1] * a1;
       packed |= (uint32_t)resize_vpass(r0, r1, b0, b1, mode) << (8 * j);
     }
-    *reinterpret_cast<uint32_t*>(out + (size_t)(dy0 + ly) * DST + q * 4) = packed;
+    ring_store(reinterpret_cast<uint32_t*>(out + (size_t)(dy0 + ly) * DST + q * 4), packed);
   }
 }
 
