@@ -47,6 +47,10 @@ constexpr int LROWS = LBN + LBM;               // 96 staged rows: 64 of [Wu | Wl
 #ifndef ARL_LSTM_PRIO
 #define ARL_LSTM_PRIO 0
 #endif
+// the saved gate pre-activations (read by the window's BPTT) stored non-temporal (A/B knob)
+#ifndef ARL_LSTM_NTST
+#define ARL_LSTM_NTST 0
+#endif
 constexpr int LLD = ARL_LSTM_LD;
 constexpr int LPIECES = (LROWS * LLD + 63) / 64;   // 51 LDS-DMA pieces (64 x 16 B) per chunk
 constexpr int LWPIECES = LBN * LLD / 64;       // 34: the W rows alone (XRED x chunks)
@@ -252,7 +256,12 @@ lstm_gates_kernel(LstmGatesArgs a) {
   const int row = tid >> 4, u = tid & 15, m = m0 + row, n = n0 + 4 * u;
   if (m >= a.n) return;
   const float4 g = *reinterpret_cast<const float4*>(T + row * TLD + 4 * u);   // bias added above
-  *reinterpret_cast<float4*>(a.gates + (int64_t)m * GATES + n) = g;
+  if (ARL_LSTM_NTST) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(f4v{g.x, g.y, g.z, g.w}, reinterpret_cast<f4v*>(a.gates + (int64_t)m * GATES + n));
+  } else {
+    *reinterpret_cast<float4*>(a.gates + (int64_t)m * GATES + n) = g;
+  }
   if (!a.cell) return;
   const int64_t i = (int64_t)m * HID + (n >> 2);
   const float ag = tanhf(g.x), ig = lstm_sigm(g.y), fg = lstm_sigm(g.z), og = lstm_sigm(g.w);
