@@ -5,7 +5,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/final4
+O=gpurun_out/${FTAG:-final4}
 mkdir -p $O
 case $1 in
   suite)
@@ -19,6 +19,6 @@ case $1 in
     (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$O/prof" -o c4 -- python3 "$GRAFT_REPO_ROOT/bench.py" --cpu-seconds 0 --copy-peak 0 > "$GRAFT_REPO_ROOT/$O/bench_prof.log" 2>&1) || exit $?
     echo "prof ok" >> $O/status ;;
   configs)
-    bash scripts/gpu_configs.sh final4cfg ${WL:-c4 c3 c2 c5} > $O/configs.log 2>&1 || exit $?
+    bash scripts/gpu_configs.sh ${FTAG:-final4}cfg ${WL:-c4 c3 c2 c5} > $O/configs.log 2>&1 || exit $?
     echo "configs ok" >> $O/status ;;
 esac
