@@ -62,7 +62,8 @@
 #endif
 // a1 / a2 global stores non-temporal: nothing reads them before the window's backward, and they leave
 // no dirty lines in the L2s for the kernel's end to write back.  C4 median 0.4994-0.4998 -> 0.4947-0.4948 ms,
-// C3 1.147-1.151 -> 1.122-1.133 ms, conv_fwd 16.7-17.2 -> 16.0-16.3 us at C4 (2 interleaved reps, r4r)
+// C3 1.147-1.151 -> 1.122-1.133 ms, conv_fwd 16.7-17.2 -> 16.0-16.3 us at C4 (2 interleaved reps, r4r).
+// ARL_CF_NTST=2 (A/B): a1 only -- a2 is read by the next launch (fc_fwd)
 #ifndef ARL_CF_NTST
 #define ARL_CF_NTST 1
 #endif
@@ -600,7 +601,7 @@ conv_fwd_kernel(ConvFwdArgs a) {
         const int o = 16 * nt + 4 * g + r;
         const float v = fmaxf(__fadd_rn(__fadd_rn(big[r], sml[r]), bias2[r]), 0.f);
         if (valid && pin) {
-          if (ARL_CF_NTST) __builtin_nontemporal_store(v, a2g + o * C2_P + p);
+          if (ARL_CF_NTST == 1) __builtin_nontemporal_store(v, a2g + o * C2_P + p);
           else a2g[o * C2_P + p] = v;
         }
         if (mk) {   // (block-uniform)
