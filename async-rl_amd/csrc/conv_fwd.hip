@@ -60,12 +60,13 @@
 #ifndef ARL_CF_PRIO
 #define ARL_CF_PRIO 0
 #endif
-// a1 / a2 global stores non-temporal: nothing reads them before the window's backward, and they leave
-// no dirty lines in the L2s for the kernel's end to write back.  C4 median 0.4994-0.4998 -> 0.4947-0.4948 ms,
-// C3 1.147-1.151 -> 1.122-1.133 ms, conv_fwd 16.7-17.2 -> 16.0-16.3 us at C4 (2 interleaved reps, r4r).
-// ARL_CF_NTST=2 (A/B): a1 only -- a2 is read by the next launch (fc_fwd)
+// a1 global stores non-temporal (ARL_CF_NTST=2): nothing reads a1 before the window's backward, and the
+// stores leave no dirty lines in the L2s for the kernel's end to write back.  a2 keeps ordinary stores: the
+// next launch (fc_fwd) reads it.  0: both ordinary; 1: both non-temporal (C4 median 0.4994-0.4998 ->
+// 0.4947-0.4948 ms, r4r; fc_fwd 9.5 -> 10.5 us); 2 vs 1: C4 0.4854-0.4855 -> 0.4772-0.4774 ms, C3
+// 1.1142-1.1148 -> 1.1075-1.1095, C2 0.3119-0.3123 -> 0.3059-0.3064 (2 interleaved reps each, r4u)
 #ifndef ARL_CF_NTST
-#define ARL_CF_NTST 1
+#define ARL_CF_NTST 2
 #endif
 #ifndef ARL_CF_STAMP
 #define ARL_CF_STAMP 0   // timing experiments only: s_memtime at phase ends into a2 (results wrong)
