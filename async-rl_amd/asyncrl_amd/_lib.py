@@ -51,6 +51,7 @@ SIGNATURES = {
     "arl_net_buffer": (c_int, [c_void_p, ctypes.c_char_p, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
     "arl_net_bind": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "arl_net_reset": (c_int, [c_void_p, c_void_p]),
+    "arl_net_set_pool": (c_int, [c_void_p, c_int, c_void_p, c_i64]),
     "arl_observe": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int, c_void_p]),
     "arl_observe_rgb": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_i64, c_int, c_int,
                                 c_void_p]),
@@ -65,8 +66,6 @@ SIGNATURES = {
     "arl_observe_envs": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_i64,
                                  c_int, c_int, c_void_p]),
     "arl_act_envs": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
-    "arl_observe_act_envs": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int,
-                                     c_int, c_void_p]),
     "arl_run_stage": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "arl_stamps_begin": (c_int, [c_void_p, c_int]),
     "arl_stamps_sparse": (c_int, [c_void_p, c_int]),
@@ -97,8 +96,8 @@ for _name, (_res, _args) in SIGNATURES.items():
     _fn.restype = _res
     _fn.argtypes = _args
 
-if lib.arl_abi_version() != 2:
-    raise ImportError(f"asyncrl_amd: {LIB_PATH} has ABI {lib.arl_abi_version()}, expected 2 (rebuild it)")
+if lib.arl_abi_version() != 3:
+    raise ImportError(f"asyncrl_amd: {LIB_PATH} has ABI {lib.arl_abi_version()}, expected 3 (rebuild it)")
 
 ARCH_FF = 0
 ARCH_LSTM = 1
@@ -107,11 +106,12 @@ ARCH_RGB = 16        # flag for FF / LSTM: the ViZDoom models (train_a3c_doom.py
 ARCH_STACK = 32      # flag for FF / LSTM: observations are whole 4-screen stacks (ALE.state, ale.py:91-94)
 ARCH_STATES = 64     # flag for FF / LSTM: observations are f32 (4, 84, 84) states, phi's output (a3c.py:34,73)
 FWD_KEEP_STATE = 16  # arl_forward_states mode bit: LSTM keep_same_state (a3c_ale.py:57-60)
-ABI_VERSION = 2
+ABI_VERSION = 3
 ACT_CONV_ONLY = 4      # arl_act_envs mode bits (env-group staggering)
 ACT_AFTER_CONV = 8
 ENV_GROUP_ALIGN = 32   # arl_observe_envs / arl_act_envs: e0 % ENV_GROUP_ALIGN == 0
-LEARN_RETURNS, LEARN_HEADS_DW, LEARN_TRUNK, LEARN_GATES_REDUCE, LEARN_FC_REDUCE, LEARN_CONV = range(6)
+LEARN_RETURNS, LEARN_TRUNK, LEARN_CONV = range(3)
+POOL_FRAMES, POOL_REWARDS, POOL_DONES = range(3)   # arl_net_set_pool kinds
 # window timeline stages (arl_stamps_*): arl_run_stage's 1..11, then the stamp-only ones
 STAGE_NAMES = {1: "conv_fwd", 2: "fc_fwd", 3: "policy", 4: "fc_bwd", 5: "conv_bwd", 6: "returns", 7: "conv_reduce",
                8: "grad_sqnorm", 9: "lstm_gates", 10: "lstm_bptt", 11: "lstm_wgrad", 12: "phi", 13: "rmsprop",

@@ -51,33 +51,25 @@ from .net import DeviceNet, init_like_torch
 from . import serializers
 from .policy_output import SoftmaxPolicyOutput
 
-# env groups: chain g starts after chain g-1's first kernel (ARL_GROUP_STAGGER=0: together)
-STAGGER = os.environ.get("ARL_GROUP_STAGGER", "1") != "0"
-# env groups: the chains' launches are issued (captured) step-interleaved --
-# step t of chain 0, of chain 1, ..., then step t + 1 -- so a graph replay
-# hands every chain's first launches to the device early; ARL_GROUP_ORDER=chain
-# issues chain 0 whole, then chain 1, ... (the A arm)
-GROUP_ORDER = os.environ.get("ARL_GROUP_ORDER", "interleave")
-# > 1 rank: split the gradient all-reduce around the conv backward (ARL_OVERLAP_ALLREDUCE=0: one call)
+# > 1 rank: split the gradient all-reduce around the conv backward (ARL_OVERLAP_ALLREDUCE=0: one call,
+# the A arm of the 2-rank rehearsal)
 OVERLAP_ALLREDUCE = os.environ.get("ARL_OVERLAP_ALLREDUCE", "1") != "0"
-# one rank: GradientClipping's norm from the learner's conv reduce (ARL_NORM_FOLD=0: grad_sqnorm launch)
-NORM_FOLD = os.environ.get("ARL_NORM_FOLD", "1") != "0"
 # a single-chain window without collectives as one C call (arl_run_window: the same launches without a
 # host round trip per step); ARL_WINDOW_C=0 issues them step by step from Python (the A arm)
 WINDOW_C = os.environ.get("ARL_WINDOW_C", "1") != "0"
 
 def _is_dqn_phi(phi) -> bool:
-    """phi is dqn_phi (dqn_phi.py:4-17): this package's, the reference's own
-    function of that name, or a functools.partial / wrapper of one (marked by
-    __wrapped__).  Its output is the uint8 screens / 255, which the conv
-    kernels apply bit-exactly, so the ring keeps the uint8 screens."""
-    seen = 0
-    while phi is not None and seen < 8:
-        if phi is _device_dqn_phi or getattr(phi, "__name__", None) == "dqn_phi":
-            return True
-        phi = getattr(phi, "func", None) or getattr(phi, "__wrapped__", None)
-        seen += 1
-    return False
+    """phi IS dqn_phi (dqn_phi.py:4-17): this package's function object, or the
+    reference module's own (module dqn_phi, qualified name dqn_phi).  Its
+    output is the uint8 screens / 255, which the conv kernels apply
+    bit-exactly, so the ring keeps the uint8 screens.  Matched by identity
+    only: a wrapper, partial or look-alike of the same name may change the
+    output, so it takes the general path (phi's f32 output on an
+    ARCH_STATES ring), which is always exact."""
+    if phi is _device_dqn_phi:
+        return True
+    return (callable(phi) and getattr(phi, "__module__", None) == "dqn_phi"
+            and getattr(phi, "__qualname__", None) == "dqn_phi" and not hasattr(phi, "__wrapped__"))
 
 
 def _to_device_f32(state, device) -> torch.Tensor:
@@ -253,7 +245,7 @@ class A3C:
         self._vcoef = v_loss_coef * scale
         self.net.set_loss(pi_loss_coef * scale, keep_loss_scale_same)
         # no all-reduce between learn and update: the clip norm comes from the learner's conv reduce
-        self.net.set_norm_fold(not self.collectives and NORM_FOLD)
+        self.net.set_norm_fold(not self.collectives)
         self.t = 0          # env-steps taken (per env)
         self.t_start = 0    # a3c.py:56,152 (reference-contract act)
         self._episode_start = True
@@ -428,7 +420,7 @@ class A3C:
         64-row FC tiles, C4 0.497 vs 0.509-0.518 ms; profiles/r03/r3l)."""
         net, T = self.net, self.t_max
         groups = net.env_groups(net.default_env_groups() if env_groups is None else env_groups)
-        if (WINDOW_C and len(groups) == 1 and not split_update and not self.collectives and not net.fused_observe
+        if (WINDOW_C and len(groups) == 1 and not split_update and not self.collectives
                 and net.arch == net.base_arch and net.base_arch in (ARCH_FF, ARCH_LSTM)):
             # one C call: T x (observe, act), bootstrap, learn, clip + RMSProp, advance (arl_run_window)
             net.run_window(pair_pool, reward_pool, done_pool, pool_len, first, self.resize_mode, self.gamma, self.beta,
@@ -444,27 +436,21 @@ class A3C:
                 s.wait_stream(main)                  # fork before any chain is issued
             chains = [self._chain_steps(pair_pool, reward_pool, done_pool, pool_len, first,
                                         main if g == 0 else side[g - 1], envs) for g, envs in enumerate(groups)]
+            # the chains' launches are issued (captured) step-interleaved -- step t of chain 0, of chain 1,
+            # ..., then step t + 1 -- so a graph replay hands every chain's first launches to the device early
             started = [None] * len(chains)
-            if GROUP_ORDER == "chain":
-                for g, c in enumerate(chains):
-                    if g > 0 and started[g - 1] is not None:
+            live = list(range(len(chains)))
+            step = 0
+            while live:
+                for g in list(live):
+                    if step == 0 and g > 0 and started[g - 1] is not None:
                         side[g - 1].wait_event(started[g - 1])   # stagger: after chain g-1's first kernel
-                    for ev in c:
-                        if ev is not None:
-                            started[g] = ev
-            else:
-                live = list(range(len(chains)))
-                step = 0
-                while live:
-                    for g in list(live):
-                        if step == 0 and g > 0 and started[g - 1] is not None:
-                            side[g - 1].wait_event(started[g - 1])   # stagger: after chain g-1's first kernel
-                        ev = next(chains[g], StopIteration)
-                        if ev is StopIteration:
-                            live.remove(g)
-                        elif ev is not None:
-                            started[g] = ev
-                    step += 1
+                    ev = next(chains[g], StopIteration)
+                    if ev is StopIteration:
+                        live.remove(g)
+                    elif ev is not None:
+                        started[g] = ev
+                step += 1
             for s in side:
                 main.wait_stream(s)
             stream = main
@@ -482,8 +468,7 @@ class A3C:
 
     def _forward_chain(self, pair_pool, reward_pool, done_pool, pool_len, first, stream, envs):
         """T x (observe, act) + the bootstrap observe / act for envs (all if
-        None) on `stream`; each observe + act is one launch shorter where the
-        net fuses them (DeviceNet.observe_act)."""
+        None) on `stream`."""
         for _ in self._chain_steps(pair_pool, reward_pool, done_pool, pool_len, first, stream, envs):
             pass
 
@@ -494,11 +479,11 @@ class A3C:
         observation), later ones None."""
         net, T = self.net, self.t_max
         ev = None
-        stagger = envs is not None and STAGGER
+        stagger = envs is not None   # env groups: chain g starts after chain g-1's first kernel
         for t in range(T + 1):
             obs = t > 0 or first
             if stagger and ev is None:
-                if obs and not net.fused_observe:      # the first kernel is the observation
+                if obs:                                # the first kernel is the observation
                     net.observe(t, pair_pool, reward_pool, done_pool, pool_len, force_reset=(t == 0),
                                 resize_mode=self.resize_mode, stream=stream, envs=envs)
                     ev = torch.cuda.Event()
@@ -506,11 +491,7 @@ class A3C:
                     net.act(t, stream=stream, envs=envs)
                     yield ev
                     continue
-                if obs:
-                    net.observe_act(t, pair_pool, reward_pool, done_pool, pool_len, force_reset=(t == 0),
-                                    resize_mode=self.resize_mode, mode=1 | ACT_CONV_ONLY, stream=stream, envs=envs)
-                else:
-                    net.act(t, mode=1 | ACT_CONV_ONLY, stream=stream, envs=envs)
+                net.act(t, mode=1 | ACT_CONV_ONLY, stream=stream, envs=envs)
                 ev = torch.cuda.Event()
                 ev.record(stream)
                 net.act(t, mode=1 | ACT_AFTER_CONV, stream=stream, envs=envs)

@@ -10,14 +10,13 @@ compute is in libasyncrl_hip.so.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import numpy as np
 import torch
 
 from ._lib import (ARCH_FF, ARCH_FF_NATURE, ARCH_LSTM, ARCH_RGB, ARCH_STACK, ARCH_STATES, ENV_GROUP_ALIGN, FWD_KEEP_STATE,
-                   LEARN_CONV, LEARN_FC_REDUCE, LEARN_GATES_REDUCE, LEARN_HEADS_DW, LEARN_RETURNS, LEARN_TRUNK,
-                   RESIZE_SCALAR, STAGE_HOST, STAGE_NAMES, check, lib, ptr, stream_handle)
+                   POOL_DONES, POOL_FRAMES, POOL_REWARDS, RESIZE_SCALAR, STAGE_HOST, STAGE_NAMES, check, lib, ptr,
+                   stream_handle)
 
 
 def param_shapes(arch: int, n_actions: int):
@@ -53,20 +52,10 @@ def init_like_torch(arch: int, n_actions: int, rng: np.random.Generator):
     return out
 
 
-# learner side stream for the weight-gradient reduces (ARL_LEARN_FORK=1).  Off by
-# default: measured slower on every config (C2 0.413 -> 0.449 ms, C3 1.543 ->
-# 1.609, C4 0.641 -> 0.676): each cross-stream edge of the window graph costs
-# more on the critical path than the ~19 us of reduces it hides.
-LEARN_FORK = os.environ.get("ARL_LEARN_FORK", "0") == "1"
-# observe + act of a step in one launch (phi fused into the conv forward, conv_fwd_kernel<true>).
-# Off by default: measured slower than phi_ring_kernel + conv_fwd_kernel at C2 / C4
-FUSE_OBS = os.environ.get("ARL_FUSE_OBS", "0") == "1"
-
-
 
 def check_pools(pool_len: int, *pools):
-    """pool_len against each pool's leading dimension: the C ABI sees only
-    pointers, so a pool_len past a pool's end would read past its buffer."""
+    """pool_len against each pool's leading dimension (the C ABI checks it
+    again against the extents registered with arl_net_set_pool)."""
     if pool_len < 1:
         raise ValueError(f"pool_len must be >= 1, got {pool_len}")
     for p in pools:
@@ -147,6 +136,13 @@ class DeviceNet:
         return t.view(shape) if shape is not None else t
 
     # ------------------------------------------------------------ hot path
+    def set_pools(self, frames=None, rewards=None, dones=None):
+        """Register the input pools' extents with the net (arl_net_set_pool):
+        the C ABI refuses an observation whose pools it does not know."""
+        for kind, t in ((POOL_FRAMES, frames), (POOL_REWARDS, rewards), (POOL_DONES, dones)):
+            if t is not None:
+                check(lib.arl_net_set_pool(self._h, kind, ptr(t), t.numel() * t.element_size()), "arl_net_set_pool")
+
     def reset(self, stream=None):
         check(lib.arl_net_reset(self._h, stream_handle(stream)), "arl_net_reset")
 
@@ -156,6 +152,7 @@ class DeviceNet:
         RGB net (arch | ARCH_RGB) the screens (pool_len, n, H, W, 3) instead.
         envs=(e0, ne): only envs [e0, e0 + ne) (arl_observe_envs)."""
         check_pools(pool_len, pair_pool, reward_pool, done_pool)
+        self.set_pools(pair_pool, reward_pool, done_pool)
         if (self.stack or self.states) and envs is None:
             self.observe_stack(t, pair_pool, reward_pool, done_pool, pool_len, force_reset, stream)
             return
@@ -181,6 +178,7 @@ class DeviceNet:
         84, 84) f32 states, phi's output (arl_observe_states).  None ingests
         only the reward / done of step t (a terminal observation)."""
         check_pools(pool_len, stack_pool, reward_pool, done_pool)
+        self.set_pools(stack_pool, reward_pool, done_pool)
         if self.states:
             if stack_pool is not None and stack_pool.dtype != torch.float32:
                 raise ValueError("observe_stack: an ARCH_STATES net takes float32 states")
@@ -215,27 +213,13 @@ class DeviceNet:
             return
         check(lib.arl_act_mode(self._h, t, mode, stream_handle(stream)), "arl_act_mode")
 
-    @property
-    def fused_observe(self) -> bool:
-        """observe + act of a step as one launch (arl_observe_act_envs): frame-pair
-        nets with the NIPS head, when enabled (ARL_FUSE_OBS=1 or the instance
-        attribute fuse_obs = True)."""
-        return getattr(self, "fuse_obs", FUSE_OBS) and not (self.rgb or self.stack or self.states or self.arch == ARCH_FF_NATURE)
-
     def observe_act(self, t: int, pair_pool: torch.Tensor, reward_pool=None, done_pool=None, pool_len: int = 1,
                     force_reset: bool = False, resize_mode: int = RESIZE_SCALAR, mode: int = 1, stream=None,
                     envs=None):
-        """observe(t, ...) then act(t, mode) of envs (all if None), fused into
-        one conv launch where the net allows it (fused_observe)."""
-        if not self.fused_observe:
-            self.observe(t, pair_pool, reward_pool, done_pool, pool_len, force_reset, resize_mode, stream, envs)
-            self.act(t, mode, stream, envs)
-            return
-        check_pools(pool_len, pair_pool, reward_pool, done_pool)
-        e0, ne = envs if envs is not None else (0, -1)
-        check(lib.arl_observe_act_envs(self._h, t, e0, ne, ptr(pair_pool), ptr(reward_pool), ptr(done_pool), pool_len,
-                                       int(force_reset), resize_mode, mode, stream_handle(stream)),
-              "arl_observe_act_envs")
+        """observe(t, ...) then act(t, mode) of envs (all if None).  (phi fused into the
+        conv launch was built bit-identical and measured slower: DESIGN.md.)"""
+        self.observe(t, pair_pool, reward_pool, done_pool, pool_len, force_reset, resize_mode, stream, envs)
+        self.act(t, mode, stream, envs)
 
     def default_env_groups(self) -> int:
         """Forward chains per window that measured fastest on one MI355X:
@@ -266,36 +250,9 @@ class DeviceNet:
         """One window stage alone on the current workspace (timing / profiling)."""
         check(lib.arl_run_stage(self._h, self.STAGES[stage], t, stream_handle(stream)), "arl_run_stage")
 
-    def learn(self, gamma=0.99, beta=1e-2, v_loss_coef=0.5, clip_reward=True, stream=None, fork=None):
-        """Gradient of the window (arl_learn).  fork (default: LEARN_FORK)
-        runs the weight-gradient reduces that nothing downstream reads (heads
-        dW, LSTM gate and FC reduces) on a side stream, concurrently with the
-        heads -> FC -> conv backward chain (arl_learn_part); the streams join
-        before this returns, so the result is identical either way."""
-        fork = LEARN_FORK if fork is None else fork
-        if not fork or self.arch == ARCH_FF_NATURE:
-            check(lib.arl_learn(self._h, gamma, beta, v_loss_coef, int(clip_reward), stream_handle(stream)),
-                  "arl_learn")
-            return
-        main = stream if stream is not None else torch.cuda.current_stream(self.device)
-        side = getattr(self, "_learn_side", None)
-        if side is None:
-            side = self._learn_side = torch.cuda.Stream(device=self.device)
-
-        def part(p, s):
-            check(lib.arl_learn_part(self._h, p, gamma, beta, v_loss_coef, int(clip_reward), s.cuda_stream),
-                  "arl_learn_part")
-
-        part(LEARN_RETURNS, main)
-        side.wait_stream(main)
-        part(LEARN_HEADS_DW, side)
-        part(LEARN_TRUNK, main)
-        side.wait_stream(main)
-        if self.base_arch == ARCH_LSTM:
-            part(LEARN_GATES_REDUCE, side)
-        part(LEARN_FC_REDUCE, side)
-        part(LEARN_CONV, main)
-        main.wait_stream(side)
+    def learn(self, gamma=0.99, beta=1e-2, v_loss_coef=0.5, clip_reward=True, stream=None):
+        """Gradient of the window (arl_learn)."""
+        check(lib.arl_learn(self._h, gamma, beta, v_loss_coef, int(clip_reward), stream_handle(stream)), "arl_learn")
 
     def learn_parts(self, parts, gamma=0.99, beta=1e-2, v_loss_coef=0.5, clip_reward=True, stream=None):
         """arl_learn_part for each part in order on one stream (NIPS heads)."""
@@ -320,6 +277,7 @@ class DeviceNet:
         act), the bootstrap, learn, clip + RMSProp and the advance -- the
         launches of observe / act / learn / optimize(advance=True) in order."""
         check_pools(pool_len, pair_pool, reward_pool, done_pool)
+        self.set_pools(pair_pool, reward_pool, done_pool)
         check(lib.arl_run_window(self._h, ptr(pair_pool), ptr(reward_pool), ptr(done_pool), pool_len, int(first),
                                  resize_mode, gamma, beta, v_loss_coef, int(clip_reward), lr0, int(total_steps),
                                  int(n_total), alpha, eps, clip, stream_handle(stream)), "arl_run_window")

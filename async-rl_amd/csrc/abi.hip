@@ -12,6 +12,11 @@
 struct arl_net {
   arl::Net net;
   bool bound = false;
+  struct Pool {
+    uintptr_t base = 0;
+    int64_t bytes = 0;
+  };
+  Pool pools[3][8];   // registered input pools per kind (arl_net_set_pool)
 };
 
 namespace {
@@ -167,6 +172,44 @@ int arl_net_reset(arl_net* h, void* s) {
   return hip_status(e, "net_reset");
 }
 
+int arl_net_set_pool(arl_net* h, int kind, const void* pool, int64_t bytes) {
+  if (!h) return fail(ARL_EINVAL, "null net");
+  if (kind < ARL_POOL_FRAMES || kind > ARL_POOL_DONES) return fail(ARL_EINVAL, "set_pool: unknown pool kind");
+  if (!pool || bytes < 0) return fail(ARL_EINVAL, "set_pool: null pool / bytes < 0");
+  const uintptr_t b = reinterpret_cast<uintptr_t>(pool);
+  arl_net::Pool* tab = h->pools[kind];
+  int slot = -1;
+  for (int i = 0; i < 8; ++i)
+    if (tab[i].base == b) slot = i;
+  if (slot < 0) {   // a free slot, else replace the oldest registration (slots shift down)
+    for (int i = 0; i < 8 && slot < 0; ++i)
+      if (tab[i].bytes == 0) slot = i;
+    if (slot < 0) {
+      for (int i = 0; i < 7; ++i) tab[i] = tab[i + 1];
+      slot = 7;
+    }
+  }
+  tab[slot].base = bytes > 0 ? b : 0;
+  tab[slot].bytes = bytes;
+  return ARL_OK;
+}
+
+// a non-null pool must lie inside a registered pool of its kind with pool_len * rows * unit bytes
+// before that pool's end (0 = ok)
+static int check_pool(const arl_net* h, int kind, const void* pool, int64_t pool_len, int64_t unit, const char* what) {
+  if (!pool) return 0;
+  const uintptr_t p = reinterpret_cast<uintptr_t>(pool);
+  for (const arl_net::Pool& r : h->pools[kind]) {
+    if (r.bytes <= 0 || p < r.base || p >= r.base + (uintptr_t)r.bytes) continue;
+    const int64_t room = (int64_t)(r.base + (uintptr_t)r.bytes - p);
+    if (unit > 0 && pool_len > room / unit)
+      return fail(ARL_EINVAL, std::string("observe: pool_len ") + std::to_string(pool_len) + " exceeds the " + what +
+                                  " pool (" + std::to_string(room / unit) + " entries registered)");
+    return 0;
+  }
+  return fail(ARL_EINVAL, std::string("observe: the ") + what + " pool is not registered (arl_net_set_pool)");
+}
+
 // validates an observation and fills its ring arguments (0 = ok)
 static int ring_args(arl_net* h, int t, const uint8_t* pool, const float* reward_pool, const uint8_t* done_pool,
                      int64_t pool_len, int force_reset, int mode, int H, int W, int e0, int ne, arl::RingArgs& a) {
@@ -176,6 +219,13 @@ static int ring_args(arl_net* h, int t, const uint8_t* pool, const float* reward
     return fail(ARL_EINVAL, "observe: need the frame pool and pool_len >= 1");
   if (!aligned(pool, 16)) return fail(ARL_EINVAL, "observe: the frame pool must be 16-byte aligned");
   if (n.N > 65535) return fail(ARL_EINVAL, "observe: n_envs > 65535");
+  const int64_t frame_unit = n.layout == arl::FRAMES_RGB ? (int64_t)H * W * 3
+                             : n.layout == arl::FRAMES_STACK ? 4 * arl::PLANE
+                             : n.layout == arl::FRAMES_STATES ? 16 * arl::PLANE
+                                                             : arl::PAIR;
+  if (int rc = check_pool(h, ARL_POOL_FRAMES, pool, pool_len, frame_unit * n.N, "frame")) return rc;
+  if (int rc = check_pool(h, ARL_POOL_REWARDS, reward_pool, pool_len, 4 * (int64_t)n.N, "reward")) return rc;
+  if (int rc = check_pool(h, ARL_POOL_DONES, done_pool, pool_len, (int64_t)n.N, "done")) return rc;
   a.pair_pool = pool;
   a.reward_pool = reward_pool;
   a.done_pool = done_pool;
@@ -321,28 +371,6 @@ int arl_act_envs(arl_net* h, int t, int e0, int ne, int mode, void* s) {
   return hip_status(arl::net_act(h->net, t, mode, S(s), e0, ne), "act");
 }
 
-int arl_observe_act_envs(arl_net* h, int t, int e0, int ne, const uint8_t* pair_pool, const float* reward_pool,
-                         const uint8_t* done_pool, int64_t pool_len, int force_reset, int resize_mode, int mode,
-                         void* s) {
-  NEED_BOUND(h);
-  const arl::Net& n = h->net;
-  if (n.rgb || n.stack || n.states || n.arch == arl::ARCH_FF_NATURE)
-    return fail(ARL_ESTATE, "observe_act: frame-pair nets with the NIPS head only (use arl_observe + arl_act)");
-  if (ne < 0) {
-    e0 = 0;
-    ne = n.N;
-  }
-  if (int rc = check_env_range(n, e0, ne)) return rc;
-  if (resize_mode < 0 || resize_mode > (ARL_RESIZE_SIMD | ARL_RESIZE_CROP)) return fail(ARL_EINVAL, "bad resize_mode");
-  const int part = mode & ~3;
-  if (mode < 0 || (mode & 3) > 2 || (part != 0 && part != ARL_ACT_CONV_ONLY))
-    return fail(ARL_EINVAL, "observe_act: mode must be 0 / 1 / 2, optionally | ARL_ACT_CONV_ONLY");
-  arl::RingArgs a;
-  if (int rc = ring_args(h, t, pair_pool, reward_pool, done_pool, pool_len, force_reset, resize_mode, 0, 0, e0, ne, a))
-    return rc;
-  return hip_status(arl::net_act(h->net, t, mode, S(s), e0, ne, &a), "observe_act");
-}
-
 int arl_run_stage(arl_net* h, int stage, int t, void* s) {
   NEED_BOUND(h);
   if (stage < ARL_STAGE_CONV_FWD || (stage > ARL_STAGE_LSTM_WGRAD && stage != ARL_STAGE_RMSPROP))
@@ -446,6 +474,10 @@ int arl_run_window(arl_net* h, const uint8_t* pair_pool, const float* reward_poo
   if (n.rgb || n.stack || n.states || n.arch == arl::ARCH_FF_NATURE)
     return fail(ARL_ESTATE, "run_window: frame-pair nets with the NIPS head only (FF / LSTM)");
   if (resize_mode < 0 || resize_mode > (ARL_RESIZE_SIMD | ARL_RESIZE_CROP)) return fail(ARL_EINVAL, "bad resize_mode");
+  {   // every observation of the window reads the same pools: check them before the first launch
+    arl::RingArgs a;
+    if (int rc = ring_args(h, 0, pair_pool, reward_pool, done_pool, pool_len, 0, resize_mode, 0, 0, 0, -1, a)) return rc;
+  }
   for (int t = 0; t <= n.T; ++t) {
     if (t > 0 || first) {   // slot 0 of a continuing window: the previous window's bootstrap observation
       const int rc = observe_common(h, t, pair_pool, reward_pool, done_pool, pool_len, t == 0 ? 1 : 0, resize_mode, 0,
@@ -496,14 +528,10 @@ int arl_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, doubl
   if (clip > 0 && !parts) return fail(ARL_EINVAL, "rmsprop: clip needs norm_partials scratch");
   hipError_t e = hipSuccess;
   const int blocks = 256;
-  if (clip > 0) {   // the scratch's arrival ticket, armed per call (arl_internal.hpp NORM_TICKET)
-    e = hipMemsetAsync(parts + arl::NORM_TICKET, 0, sizeof(int), S(s));
-    if (e == hipSuccess) e = arl::launch_grad_sqnorm(g, n, parts, blocks, S(s));
-  }
+  if (clip > 0) e = arl::launch_grad_sqnorm(g, n, parts, blocks, S(s));
   if (e == hipSuccess)
-    e = arl::launch_rmsprop(p, ms, g, n, lr, alpha, eps,
-                            clip > 0 ? parts + (arl::norm_ticket() ? arl::NORM_RESULT : 0) : nullptr,
-                            (clip > 0 && !arl::norm_ticket()) ? blocks : 0, (float)clip, nullptr, 0, 0, 0, S(s));
+    e = arl::launch_rmsprop(p, ms, g, n, lr, alpha, eps, clip > 0 ? parts : nullptr, blocks, (float)clip, nullptr, 0,
+                            0, 0, S(s));
   return hip_status(e, "rmsprop");
 }
 

@@ -139,9 +139,6 @@ struct Net {
   // LSTM recurrent state of pi_and_v on explicit states (A3CLSTM.pi_and_v, a3c_ale.py:55-63):
   // h, c (n, 256), the step's outputs hn, cn, and reset flags (1 = state is None)
   int64_t w_eval_h = 0, w_eval_c = 0, w_eval_hn = 0, w_eval_cn = 0, w_eval_reset = 0;
-  // per-job weight-gradient slabs (heads, FC, LSTM gates) of the NIPS learner;
-  // the conv slab is `slab`
-  int64_t w_slab_heads = 0, w_slab_fc = 0, w_slab_lstm = 0;
   int64_t slab_floats;
   int norm_blocks;
   // bound pointers
@@ -157,11 +154,9 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
 // mode: 0 none, 1 sample, 2 greedy, | ACT_CONV_ONLY / ACT_AFTER_CONV (env-group staggering:
 // the step split after its conv launch); envs [e0, e0 + ne) (ne < 0: all)
 constexpr int ACT_CONV_ONLY = 4, ACT_AFTER_CONV = 8;
-// obs != null (FRAMES_RING nets, not with ACT_AFTER_CONV): the observation of step t is fused
-// into the conv launch (launch_phi_conv_fwd) -- arl_observe + arl_act in one step
-hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0 = 0, int ne = -1, const RingArgs* obs = nullptr);
-// learner parts (net_learn_part); see net.hip for which may run concurrently
-enum { LEARN_RETURNS = 0, LEARN_HEADS_DW, LEARN_TRUNK, LEARN_GATES_REDUCE, LEARN_FC_REDUCE, LEARN_CONV, LEARN_PARTS };
+hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0 = 0, int ne = -1);
+// learner parts (net_learn_part), in this order on one stream
+enum { LEARN_RETURNS = 0, LEARN_TRUNK, LEARN_CONV, LEARN_PARTS };
 hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s);
 hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s);
 // advance: also end the window, folded into the update kernel (arl_learn
@@ -224,16 +219,12 @@ hipError_t launch_heads_bwd(const float* dl, const float* dv, const float* Wpi, 
 hipError_t launch_conv_fwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int t,
                            const float* W1, const float* b1, const float* W2, const float* b2, float* a1, float* a2,
                            hipStream_t s, int layout = FRAMES_RING, int e0 = 0, int ne = -1, uint32_t* a2m = nullptr);
-// phi_ring_kernel + conv_fwd_kernel in one launch (one workgroup per env of ring.e0 + [0, ring.ne))
-hipError_t launch_phi_conv_fwd(const RingArgs& ring, const float* W1, const float* b1, const float* W2,
-                               const float* b2, float* a1, float* a2, hipStream_t s, uint32_t* a2m = nullptr);
 // the gradient's squared norm folded into the conv slab reduce (parts == null: not folded)
 struct NormFold {
-  double* parts;            // NORM_SCRATCH f64: conv_norm_parts(rest_blocks) partials, result, ticket
+  double* parts;            // NORM_SCRATCH f64: conv_norm_parts(rest_blocks) partials
   const float* g;           // the flat gradient
   int64_t rest_begin, rest_end;   // floats of g outside the conv tensors (final before the reduce)
   int rest_blocks;
-  int finish = 1;           // norm_finish's ticket (norm_ticket())
 };
 int conv_norm_parts(int rest_blocks);
 hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const int64_t* ctl, int n, int R, int S,
@@ -270,11 +261,10 @@ inline PolicyArgs make_policy_args(const float* Wpi, const float* bpi, const flo
 constexpr int FC_SPLIT = 8;   // fc forward split-K (one slice per XCD)
 int fc_fwd_tiles(int n);      // tickets needed for n envs
 bool fc_fwd_big(int n);       // launches over n envs run fc_fwd_big_kernel's 64-row tiles
-bool fc_fwd_heads(int n);     // ... and an FF step's heads run in its ticket tail
-// heads != null (FF, fc_fwd_heads(n)): the split-K reduce + relu -> hfc and the policy / value heads
-// with the draw in the same launch (policy_fc_kernel's work); tickets and hfc required
+// tickets == null: split-K partials only (the consumer reduces them); else the last-arriver reduce
+// + bias + relu -> hfc in the same launch
 hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b, float* slab, int* tickets,
-                         float* hfc, hipStream_t s, const PolicyArgs* heads = nullptr);
+                         float* hfc, hipStream_t s);
 // FC backward (fc_bwd.hip): dW / db straight into the gradient, da2 = (dfc W) * (a2 > 0)
 // weight gradients of the policy / value heads (a3c.py:126-130 through
 // policy.py / v_function.py Linear layers): rows a < A from dlogits, row A
@@ -326,57 +316,11 @@ struct AdvanceArgs {
   float* cbuf;
   int T, n;
 };
-// GradientClipping's squared norm: f64 partials [0, nparts) of the launch that sums
-// them (grad_sqnorm_kernel, or reduce_conv_bwd_kernel with a NormFold), whose last block
-// leaves the total in [NORM_RESULT]; [NORM_TICKET] is its arrival counter (an int, zero
-// before the first launch, re-armed by each)
-constexpr int NORM_MAX_PARTS = 1000, NORM_RESULT = 1000, NORM_TICKET = 1001, NORM_SCRATCH = 1024;
-// Cross-workgroup hand-off of the norm partials (MI355X_MICROARCH.md, "Valid forms", table
-// row 1): lane 0 of each block stores its partial sc1 (agent-scope relaxed atomic store =
-// write-through), drains it (s_waitcnt vmcnt(0)) and then adds to ONE unsharded ticket; the
-// block whose add returned nparts - 1 is the last, its wave 0 loads every partial sc1 and sums
-// them in index order (lane l: l, l + 64, ...; then the lanes in xor-tree order, a fixed
-// order), writes the squared norm to parts[NORM_RESULT] and re-arms the ticket.  The next
-// launch on the stream (rmsprop_kernel) reads the result after the kernel boundary.
-__device__ inline void norm_finish(double mine, int b, int nparts, double* parts, bool finish = true) {
-  if (!finish) {   // (ARL_NORM_TICKET=0: the partials only; rmsprop_kernel re-reduces them in every block)
-    if (threadIdx.x == 0) parts[b] = mine;
-    return;
-  }
-  __shared__ int last;
-  int* ticket = reinterpret_cast<int*>(parts + NORM_TICKET);
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(parts + b), __double_as_longlong(mine),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nparts - 1;
-  }
-  __syncthreads();
-  if (!last || threadIdx.x >= 64) return;
-  double t = 0.0;
-  for (int base = 0; base < nparts; base += 8 * 64) {   // 8 loads a lane in flight before the sums
-    unsigned long long v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      v[k] = __hip_atomic_load(reinterpret_cast<unsigned long long*>(parts + min(base + (int)threadIdx.x + 64 * k, nparts - 1)),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (base + (int)threadIdx.x + 64 * k < nparts) t += __longlong_as_double((long long)v[k]);
-  }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o);
-  if (threadIdx.x == 0) {
-    parts[NORM_RESULT] = t;
-    __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// the norm's hand-off: partials only, every rmsprop_kernel block re-reduces them (default); with
-// ARL_NORM_TICKET=1 the norm launch's last block leaves the total (norm_finish; measured slower)
-bool norm_ticket();
-// norm_sq: &partials[NORM_RESULT] (nparts = 0), or the partials themselves (nparts > 0, re-reduced);
-// null: no clip
+// GradientClipping's squared norm: f64 partials [0, nparts) (nparts <= NORM_MAX_PARTS) of the launch
+// that sums them (grad_sqnorm_kernel, or reduce_conv_bwd_kernel with a NormFold), one per block;
+// every block of the update kernel re-reduces them in block order
+constexpr int NORM_MAX_PARTS = 1000, NORM_SCRATCH = 1024;
+// norm_sq: the norm's partials [0, nparts), re-reduced by every block; null: no clip
 hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, double alpha, double eps,
                           const double* norm_sq, int nparts, float clip, const int64_t* ctl,
                           int64_t total_steps, int64_t n_total, int t_max, hipStream_t s,

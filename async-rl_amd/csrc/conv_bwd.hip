@@ -43,51 +43,6 @@
 #include "bf16split.hpp"
 #include "conv_slab.hpp"
 
-#ifndef ARL_ABLATE
-#define ARL_ABLATE 0   // timing experiments only (bits: 8 step 1, 16 step 2, 32 step 3, 64 prefetch loads)
-#endif
-// loop unrolling of steps 1-3 (A/B knobs)
-#ifndef ARL_S1_UNROLL
-#define ARL_S1_UNROLL 21   // fully unrolled: 65.9 vs 71.6 us at 3, 70.6 at 7 (253 VGPRs, no spill)
-#endif
-#ifndef ARL_S2_UNROLL
-#define ARL_S2_UNROLL 1
-#endif
-#ifndef ARL_S3_UNROLL
-#define ARL_S3_UNROLL 3
-#endif
-// LDS operands of steps 2 / 3 read ahead of their MFMAs (one LDS wait per step-2 tile / per group of
-// three step-3 k-steps instead of one or two per k-step; A/B knobs, off: with ARL_S1_UNROLL=7 (21
-// spills) conv_bwd 67.8 -> 70.7 us at C2, step 3's 75-76 us, profiles/r03/r3q)
-#ifndef ARL_S2_PREFETCH
-#define ARL_S2_PREFETCH 0
-#endif
-#ifndef ARL_S3_PREFETCH
-#define ARL_S3_PREFETCH 0
-#endif
-// (1) on bf16 splits (A/B knob, off): C = da2 [oc][p'] x im2col(a1)^T with positions p' = 10 oy + ox
-// (ox 9 a zero column, 96 padded) over a1 split phase planes, so 8 consecutive positions of one
-// (ic, ky, kx) column are 8 consecutive bf16 (5 dword reads + v_alignbyte); 72 instead of 84 MFMA
-// issues a wave at half the cycles each, but the per-sample convert pass (a1 -> phase planes), its
-// barrier and the da1 pad re-zeroing cost more: conv_bwd 66.7-67.4 -> 68.6-69.0 us at C2,
-// 119.7-120.7 -> 121.3-122.0 at C4 (parity green, profiles/r03/r3w).  Default: exact-f32 16x16x4
-#ifndef ARL_S1_SPLIT
-#define ARL_S1_SPLIT 0
-#endif
-// static wave priority (A/B knob): the second-dispatched half of the workgroup (waves 4-7, the
-// arbitration losers when two waves share a SIMD, MI355X_MICROARCH.md "Two waves per SIMD" item 4)
-// at s_setprio 1 for the whole kernel
-#ifndef ARL_CB_PRIO
-#define ARL_CB_PRIO 0
-#endif
-// the per-workgroup slab stores non-temporal (A/B knob)
-#ifndef ARL_CB_NTST
-#define ARL_CB_NTST 0
-#endif
-#ifndef ARL_CB_STAMP
-#define ARL_CB_STAMP 0   // timing experiments only: s_memtime at every barrier into the slab (results wrong)
-#endif
-
 namespace arl {
 
 namespace {
@@ -112,25 +67,10 @@ constexpr int L_XPH = L_D1 + 3 * D1P;      // [ic][y][b][XR]                    
 constexpr int L_D2 = L_XPH + 4 * 84 * 4 * XR;   // da2 split grid, 3 x D2P          24,576
 constexpr int L_MASK = L_D2 + 3 * D2P;     // a1 > 0, u16 of 16 channel bits per pixel 800
 constexpr int L_A1 = L_MASK + 800;         // a1 f32 [16][20][A1R]                  30,720
-#if ARL_S1_SPLIT
-// (1)'s operands: da2 split planes [3][oc][p'] (row 208 B = 13 16-byte slots: the 16 rows a b128
-// lane group reads land on distinct slots), written by commit_a; a1 split phase planes
-// [3][ic][y & 1][x & 1][Y][X] (10 x 10, 224 B each: reads run up to 11 elements past the 100)
-// written from the DMA'd a1 by the convert pass into the da1 region, dead until (2) writes da1
-constexpr int DA_ROW = 208;
-constexpr int DAP = 32 * DA_ROW;           // 6,656 per plane
-constexpr int L_DA = L_A1 + C1_OC * A1C * 4;    // 3 x DAP                               19,968
-constexpr int L_END = L_DA + 3 * DAP;      // 155,936
-constexpr int PH_B = 224;                  // bytes per phase plane (112 bf16)
-constexpr int PHP = 64 * PH_B;             // 14,336 per split plane (16 ic x 4 phases)
-constexpr int L_PH = L_D1;
-static_assert(3 * PHP <= 3 * D1P && L_DA % 16 == 0, "phase planes in the da1 region");
-#else
 constexpr int D2F_LD = 48;                 // da2 f32 [p][oc] row stride
 constexpr int L_D2F = L_A1 + C1_OC * A1C * 4;   // da2 f32 [81][D2F_LD]             15,552
 constexpr int L_END = L_D2F + 81 * D2F_LD * 4;  // 151,520
 static_assert(L_D2F % 16 == 0, "alignment");
-#endif
 constexpr int L_RED = 0;                   // end: f32 [16][128] (after the last sample)
 static_assert(L_END <= 160 * 1024, "LDS");
 static_assert(L_XPH % 16 == 0 && L_D2 % 16 == 0 && L_A1 % 16 == 0 && L_MASK % 8 == 0, "alignment");
@@ -176,7 +116,6 @@ __device__ inline void grid_item(int i, int& grp, int& cell, bool& v, int& p) {
 }
 
 __device__ inline void prefetch_a(const ConvBwdArgs& a, int s, PrefetchA& r) {
-  if (ARL_ABLATE & 64) return;
   const int tid = threadIdx.x;
   const float* g2 = a.da2 + (int64_t)s * A2;
 #pragma unroll
@@ -195,7 +134,6 @@ __device__ inline void prefetch_a(const ConvBwdArgs& a, int s, PrefetchA& r) {
 // dword (20), loaded as dwords 17..20 so no read passes the row.  The plane
 // base is uniform (scalar address + one offset VGPR per item).
 __device__ inline void prefetch_x(const ConvBwdArgs& a, int64_t step0, int s, PrefetchX& r) {
-  if (ARL_ABLATE & 64) return;
   const int tid = threadIdx.x;
   const int t = s / a.n, e = s - t * a.n;
   const int64_t ks = step0 + t;
@@ -224,7 +162,6 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // re-reads column 4)
 constexpr int A1_PIECES = C1_OC * 20 * (A1R / 4) / 64;   // 30 pieces of 1 KB
 __device__ inline void dma_a1(const ConvBwdArgs& a, int s, uint8_t* lds) {
-  if (ARL_ABLATE & 64) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float* g1 = a.a1 + (int64_t)s * A1;
 #pragma unroll
@@ -261,24 +198,10 @@ __device__ inline void commit_a(const PrefetchA& r, uint8_t* lds, float (&b2a)[8
       *reinterpret_cast<uint4*>(dd + D2P) = make_uint4(m[0], m[1], m[2], m[3]);
       *reinterpret_cast<uint4*>(dd + 2 * D2P) = make_uint4(l[0], l[1], l[2], l[3]);
       if (v) {
-#if ARL_S1_SPLIT
-        const int cy = cell / 11, pp = (cy - 1) * 10 + (cell - cy * 11 - 1);   // p' = 10 oy + ox
-        uint8_t* da = lds + L_DA + (8 * grp) * DA_ROW + 2 * pp;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int sh = 16 * (k & 1);
-          *reinterpret_cast<uint16_t*>(da + k * DA_ROW) = (uint16_t)(h[k >> 1] >> sh);
-          *reinterpret_cast<uint16_t*>(da + k * DA_ROW + DAP) = (uint16_t)(m[k >> 1] >> sh);
-          *reinterpret_cast<uint16_t*>(da + k * DA_ROW + 2 * DAP) = (uint16_t)(l[k >> 1] >> sh);
-          b2a[k] = __fadd_rn(b2a[k], d[k]);
-        }
-        (void)p;
-#else
         float* f = reinterpret_cast<float*>(lds + L_D2F) + p * D2F_LD + 8 * grp;
         reinterpret_cast<float4*>(f)[0] = make_float4(d[0], d[1], d[2], d[3]);
         reinterpret_cast<float4*>(f)[1] = make_float4(d[4], d[5], d[6], d[7]);
         (void)b2a;
-#endif
       }
     }
   }
@@ -296,7 +219,7 @@ __device__ inline void commit_x(const PrefetchX& r, uint8_t* lds) {
   for (int c = 0; c < PX; ++c) {
     uint4 v = r.x[c];
     if (q == 5) v = make_uint4(v.w, 0, 0, 0);
-    if ((ARL_ABLATE & 64) || c < 4 - nv) v = make_uint4(0, 0, 0, 0);
+    if (c < 4 - nv) v = make_uint4(0, 0, 0, 0);
     const uint32_t lo01 = __builtin_amdgcn_perm(v.y, v.x, 0x05010400u);
     const uint32_t hi01 = __builtin_amdgcn_perm(v.y, v.x, 0x07030602u);
     const uint32_t lo23 = __builtin_amdgcn_perm(v.w, v.z, 0x05010400u);
@@ -321,10 +244,7 @@ __device__ inline bf16x8 frag_from_pairs(uint32_t p0, uint32_t p1, uint32_t p2, 
   return __builtin_bit_cast(bf16x8, (u32x4{p0, p1, p2, p3}));
 }
 
-__device__ inline void slab_store(float* p, float v) {
-  if (ARL_CB_NTST) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
+__device__ inline void slab_store(float* p, float v) { *p = v; }
 
 __global__ void __launch_bounds__(NT)
 conv_bwd_kernel(ConvBwdArgs a) {
@@ -332,29 +252,13 @@ conv_bwd_kernel(ConvBwdArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, col = lane & 15;
-  if (ARL_CB_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
-#if ARL_CB_STAMP
-  __shared__ uint32_t stamp[32];
-  const uint64_t t0 = __builtin_amdgcn_s_memtime();
-  int nst = 0;
-#define CB_STAMP() do { if (tid == 0 && nst < 30) stamp[nst] = (uint32_t)(__builtin_amdgcn_s_memtime() - t0); ++nst; } while (0)
-#else
-#define CB_STAMP() do {} while (0)
-#endif
   const float* a1s = reinterpret_cast<const float*>(lds + L_A1);
-#if ARL_S1_SPLIT
-  // the da1 / phase-plane region and the da2 [oc][p'] planes zeroed once: the phase-plane reads run
-  // past a plane into finite bytes, and commit_a never writes the [oc][p'] pad positions
-  for (int i = tid; i < 3 * D1P / 16; i += NT) reinterpret_cast<uint4*>(lds + L_D1)[i] = make_uint4(0, 0, 0, 0);
-  for (int i = tid; i < 3 * DAP / 16; i += NT) reinterpret_cast<uint4*>(lds + L_DA)[i] = make_uint4(0, 0, 0, 0);
-#else
   const float* d2f = reinterpret_cast<const float*>(lds + L_D2F);
   // zero the da1 pad columns X 20..23 once: (2) writes only X < 20
   for (int i = tid; i < 3 * 16 * 20; i += NT) {
     const int pl = i / 320, r = i - pl * 320;
     *reinterpret_cast<uint2*>(lds + L_D1 + pl * D1P + (r / 20) * D1_OC + (r % 20) * D1_ROW + 40) = make_uint2(0, 0);
   }
-#endif
 
   // (2) W2 fragments of this wave's parity class: lane (ic = col, g), k-step
   // ks = (dy, dx), k = oc = 8 g + j -> W2[oc][ic][py + 2 dy][px + 2 dx]
@@ -383,11 +287,6 @@ conv_bwd_kernel(ConvBwdArgs a) {
   }
   float b2sum = 0.f, b1s[4] = {0.f, 0.f, 0.f, 0.f};   // b1s[rr]: channel 4 g + rr
   float b2a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // split (1): bias sums of this thread's da2 item
-#if ARL_S1_SPLIT
-  f32x4 sml1[2][2];   // (1)'s small terms
-#pragma unroll
-  for (int i = 0; i < 2; ++i) sml1[0][i] = sml1[1][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#endif
 
   // (3): wave w -> screen ic = w >> 1, ky = 4 kyq + (col >> 2) with kyq = w & 1,
   // kx = 4 a + (col & 3) (tile a = 0, 1); A row base of lane (phase row b = col & 3)
@@ -402,85 +301,15 @@ conv_bwd_kernel(ConvBwdArgs a) {
   dma_a1(a, blockIdx.x, lds);
   for (int s = blockIdx.x; s < a.S; s += G) {
     lds_barrier();                 // B0: the previous sample is done with every region
-    CB_STAMP();
     commit_a(pa, lds, b2a);
     commit_x(px_, lds);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this sample's a1 DMA has landed
     lds_barrier();                 // B1
-    CB_STAMP();
     {
       const int sn = min(s + G, a.S - 1);   // unconditional: the registers are redefined here
       prefetch_a(a, sn, pa);                // in flight during (1)-(3)
       prefetch_x(a, step0, sn, px_);
     }
-#if ARL_S1_SPLIT
-    // ---- a1 -> split phase planes ([3][ic][y & 1][x & 1][Y][X]): item (ic, phase, quad) = 4
-    // consecutive L = 10 Y + X of one phase plane, one 8-byte store per split plane; then a1 > 0 per
-    // pixel as 16 channel bits (threads < 400)
-    for (int it = tid; it < C1_OC * 4 * 25; it += NT) {
-      const int ic = it / 100, r = it - 100 * ic, ph = r / 25, q = r - 25 * ph;
-      const int py = ph >> 1, pxx = ph & 1;
-      float v[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int L = 4 * q + k, Y = L / 10, X = L - 10 * Y;
-        v[k] = a1s[ic * A1C + (2 * Y + py) * A1R + 2 * X + pxx];
-      }
-      uint2 h, m, l;
-      split3_pack(v[0], v[1], h.x, m.x, l.x);
-      split3_pack(v[2], v[3], h.y, m.y, l.y);
-      uint8_t* d = lds + L_PH + (ic * 4 + ph) * PH_B + 8 * q;
-      *reinterpret_cast<uint2*>(d) = h;
-      *reinterpret_cast<uint2*>(d + PHP) = m;
-      *reinterpret_cast<uint2*>(d + 2 * PHP) = l;
-    }
-    if (tid < C1_P) {
-      const float* ap = a1s + (tid / 20) * A1R + tid % 20;
-      uint32_t m = 0;
-#pragma unroll
-      for (int ic = 0; ic < C1_OC; ++ic) m |= (ap[ic * A1C] > 0.f ? 1u : 0u) << ic;
-      reinterpret_cast<uint16_t*>(lds + L_MASK)[tid] = (uint16_t)m;
-    }
-    lds_barrier();                 // B1b: the phase planes are complete
-    CB_STAMP();
-    // ---- (1) conv2 weight gradient, bf16 splits: wave w owns n-tiles (ic) 2w, 2w+1 x both m-tiles
-    // (oc); k = p' = 10 oy + ox over 3 k-steps of 32.  Lane (col, g): A = the [oc][p'] planes, row
-    // oc = 16 mt + col, 8 positions from 32 ks + 8 g (one b128); B = phase plane (ic, ky & 1, kx & 1)
-    // of (ky, kx) = divmod(col, 4) from element 32 ks + 8 g + d, d = 10 (ky >> 1) + (kx >> 1):
-    // 5 dwords and 4 v_alignbyte (d odd: a 2-byte shift).  Same C layout as the f32 path.
-    if (!(ARL_ABLATE & 8)) {
-      const int ky = col >> 2, kx = col & 3;
-      const int pb = L_PH + (2 * (ky & 1) + (kx & 1)) * PH_B + 2 * (8 * g + 10 * (ky >> 1) + (kx >> 1));
-      const int ab = L_DA + col * DA_ROW + 16 * g;
-#pragma unroll
-      for (int ks = 0; ks < 3; ++ks) {
-        bf16x8 av[2][3], bv[2][3];
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-          for (int h = 0; h < 3; ++h) av[mt][h] = lds_load<bf16x8>(lds, ab + mt * 16 * DA_ROW + h * DAP + 64 * ks);
-#pragma unroll
-        for (int jn = 0; jn < 2; ++jn)
-#pragma unroll
-          for (int h = 0; h < 3; ++h) {
-            const int a = pb + (2 * wave + jn) * 4 * PH_B + h * PHP + 64 * ks;
-            const int a4 = a & ~3, sh = a & 3;
-            uint32_t w[5];
-#pragma unroll
-            for (int q = 0; q < 5; ++q) w[q] = lds_load<uint32_t>(lds, a4 + 4 * q);
-            bv[jn][h] = frag_from_pairs(__builtin_amdgcn_alignbyte(w[1], w[0], sh),
-                                        __builtin_amdgcn_alignbyte(w[2], w[1], sh),
-                                        __builtin_amdgcn_alignbyte(w[3], w[2], sh),
-                                        __builtin_amdgcn_alignbyte(w[4], w[3], sh));
-          }
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-          for (int jn = 0; jn < 2; ++jn)
-            mfma_x6(av[mt][0], av[mt][1], av[mt][2], bv[jn][0], bv[jn][1], bv[jn][2], acc1[mt][jn], sml1[mt][jn]);
-      }
-    }
-#else
     // ---- (1) conv2 weight gradient + bias; wave w: n-tiles (ic) 2w, 2w+1 x both m-tiles
     {
       // 16 chunks of <= 6 positions, summed in order: the six reads in flight together
@@ -500,8 +329,8 @@ conv_bwd_kernel(ConvBwdArgs a) {
       // instead of a division per k-step; same k order
       const float* b0 = a1s + (2 * wave) * A1C + (col >> 2) * A1R + (col & 3);
       int ox = g, boff = 2 * g, doff = g * D2F_LD;   // oy = 0
-#pragma unroll ARL_S1_UNROLL
-      for (int ps = 0; ps < ((ARL_ABLATE & 8) ? 0 : 21); ++ps) {
+#pragma unroll
+      for (int ps = 0; ps < 21; ++ps) {   // fully unrolled: 65.9 vs 71.6 us at 3 (253 VGPRs, no spill)
         const bool pv = 4 * ps + g < C2_P;
         const float af0 = pv ? d2f[doff + col] : 0.f;
         const float af1 = pv ? d2f[doff + 16 + col] : 0.f;
@@ -527,17 +356,8 @@ conv_bwd_kernel(ConvBwdArgs a) {
       for (int ic = 0; ic < C1_OC; ++ic) m |= (ap[ic * A1C] > 0.f ? 1u : 0u) << ic;
       reinterpret_cast<uint16_t*>(lds + L_MASK)[tid] = (uint16_t)m;
     }
-#endif
     lds_barrier();                 // B2: a1 and the mask are consumed
-    CB_STAMP();
     dma_a1(a, min(s + G, a.S - 1), lds);   // next sample's a1, in flight during (2)-(3)
-#if ARL_S1_SPLIT
-    // the da1 pad columns X 20..23 back to 0 ((2) writes only X < 20; (3) reads them)
-    for (int i = tid; i < 3 * 16 * 20; i += NT) {
-      const int pl = i / 320, r = i - pl * 320;
-      *reinterpret_cast<uint2*>(lds + L_D1 + pl * D1P + (r / 20) * D1_OC + (r % 20) * D1_ROW + 40) = make_uint2(0, 0);
-    }
-#endif
     // ---- (2) da1 = convT(da2, W2) * (a1 > 0) -> da1 split planes.
     {
       // C^T form: rows = ic (A = the W2 fragments), columns = 16 grid cells
@@ -545,7 +365,7 @@ conv_bwd_kernel(ConvBwdArgs a) {
       // past the grid are computed and dropped.  Lane (col, g) ends up with
       // channels ic = 4 g + rr of one position.  Waves w < 4: tiles 0-3, w >= 4: 4-6.
       const int mt0 = wave < 4 ? 0 : 4, mt1 = wave < 4 ? 4 : 7;
-#pragma unroll ARL_S2_UNROLL
+#pragma unroll 1
       for (int mt = mt0; mt < mt1; ++mt) {
         const int cell = 12 + 16 * mt + col;
         // the position, its a1 > 0 mask and the da1 address first (clamped for dropped
@@ -555,31 +375,20 @@ conv_bwd_kernel(ConvBwdArgs a) {
         const int oy = keep ? 2 * (cy - 1) + py : 0, ox = keep ? 2 * (cx - 1) + px : 0;
         const uint32_t m = reinterpret_cast<const uint16_t*>(lds + L_MASK)[oy * 20 + ox];
         f32x4 big = {0.f, 0.f, 0.f, 0.f}, sml = big;
-        // the tile's B fragments of all four k-steps read first (12 b128 in flight, one LDS
-        // wait), then its 24 MFMAs -- read per k-step they left two exposed LDS waits a k-step
-        bf16x8 bh[4], bm[4], bl[4];
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           const int dcell = (ks >> 1) * 11 + (ks & 1);
           const int o = L_D2 + d2_slot(cell < 121 ? cell - dcell : 0, g);
-          bh[ks] = lds_load<bf16x8>(lds, o);
-          bm[ks] = lds_load<bf16x8>(lds, o + D2P);
-          bl[ks] = lds_load<bf16x8>(lds, o + 2 * D2P);
-          if (!ARL_S2_PREFETCH && !(ARL_ABLATE & 16))
-            mfma_x6(w2h[ks], w2m[ks], w2l[ks], bh[ks], bm[ks], bl[ks], big, sml);
-        }
-        if (ARL_S2_PREFETCH) {
-          __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs (the scheduler sinks them)
-#pragma unroll
-          for (int ks = 0; ks < ((ARL_ABLATE & 16) ? 0 : 4); ++ks)
-            mfma_x6(w2h[ks], w2m[ks], w2l[ks], bh[ks], bm[ks], bl[ks], big, sml);
+          const bf16x8 bh = lds_load<bf16x8>(lds, o), bm = lds_load<bf16x8>(lds, o + D2P),
+                       bl = lds_load<bf16x8>(lds, o + 2 * D2P);
+          mfma_x6(w2h[ks], w2m[ks], w2l[ks], bh, bm, bl, big, sml);
         }
         if (keep) {
           uint8_t* d = lds + L_D1 + (4 * g) * D1_OC + oy * D1_ROW + ox * 2;
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             float v = __fadd_rn(big[rr], sml[rr]);
-            if (!(ARL_ABLATE & 256) && !((m >> (4 * g + rr)) & 1)) v = 0.f;
+            if (!((m >> (4 * g + rr)) & 1)) v = 0.f;
             b1s[rr] = __fadd_rn(b1s[rr], v);
             uint32_t h, mm, l;
             split3(v, h, mm, l);
@@ -591,52 +400,12 @@ conv_bwd_kernel(ConvBwdArgs a) {
       }
     }
     lds_barrier();                 // B3
-    CB_STAMP();
     // ---- (3) conv1 weight gradient: k-step ks, quarter g -> group Gk = 4 ks + g
     // = (oy, X0 = 8 c): 8 positions (oy, X0..X0+7).  Tile a = rows (ky, kx =
     // 4 a + (col & 3)): the a = 0 and a = 1 fragments of a lane are pixels
     // X0..X0+7 and X0+1..X0+8 of one phase row, converted once and packed twice.
-#if ARL_S3_PREFETCH
-    // groups of three k-steps: every LDS operand of the group read first, one wait, then the
-    // pixel conversions and 18 MFMAs (same k order)
-    for (int k0 = 0; k0 < ((ARL_ABLATE & 32) ? 0 : 15); k0 += 3) {
-      bf16x8 bh[3], bm[3], bl[3];
-      uint2 lo[3];
-      uint32_t nx[3];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int Gk = 4 * (k0 + j) + g, oy = Gk / 3, c = Gk - 3 * oy;
-        const int ob = L_D1 + col * D1_OC + oy * D1_ROW + 16 * c;
-        bh[j] = lds_load<bf16x8>(lds, ob);
-        bm[j] = lds_load<bf16x8>(lds, ob + D1P);
-        bl[j] = lds_load<bf16x8>(lds, ob + 2 * D1P);
-        const int oa = xrow3 + oy * 16 * XR + 8 * c;
-        lo[j] = lds_load<uint2>(lds, oa);
-        nx[j] = lds_load<uint32_t>(lds, oa + 8);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        uint32_t f[9];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          f[k] = __float_as_uint((float)((lo[j].x >> (8 * k)) & 0xffu));
-          f[4 + k] = __float_as_uint((float)((lo[j].y >> (8 * k)) & 0xffu));
-        }
-        f[8] = __float_as_uint((float)(nx[j] & 0xffu));
-#pragma unroll
-        for (int a_ = 0; a_ < 2; ++a_) {
-          const bf16x8 xa = frag_from_pairs(__builtin_amdgcn_perm(f[a_ + 1], f[a_], 0x07060302u),
-                                            __builtin_amdgcn_perm(f[a_ + 3], f[a_ + 2], 0x07060302u),
-                                            __builtin_amdgcn_perm(f[a_ + 5], f[a_ + 4], 0x07060302u),
-                                            __builtin_amdgcn_perm(f[a_ + 7], f[a_ + 6], 0x07060302u));
-          mfma_x3(xa, bh[j], bm[j], bl[j], big3[a_], sml3[a_]);
-        }
-      }
-    }
-#else
-#pragma unroll ARL_S3_UNROLL
-    for (int ks = 0; ks < ((ARL_ABLATE & 32) ? 0 : 15); ++ks) {
+#pragma unroll 3
+    for (int ks = 0; ks < 15; ++ks) {
       const int Gk = 4 * ks + g, oy = Gk / 3, c = Gk - 3 * oy;
       const int ob = L_D1 + col * D1_OC + oy * D1_ROW + 16 * c;
       const bf16x8 bh = lds_load<bf16x8>(lds, ob), bm = lds_load<bf16x8>(lds, ob + D1P),
@@ -660,7 +429,6 @@ conv_bwd_kernel(ConvBwdArgs a) {
         mfma_x3(xa, bh, bm, bl, big3[a_], sml3[a_]);
       }
     }
-#endif
   }
   // ---- partial slab of this workgroup
   float* out = a.slab + (int64_t)blockIdx.x * SLAB;
@@ -671,11 +439,7 @@ conv_bwd_kernel(ConvBwdArgs a) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-#if ARL_S1_SPLIT
-        slab_store(out + (16 * mt + g * 4 + r) * 256 + 16 * (2 * wave + j) + col, __fadd_rn(acc1[mt][j][r], sml1[mt][j][r]));
-#else
         slab_store(out + (16 * mt + g * 4 + r) * 256 + 16 * (2 * wave + j) + col, acc1[mt][j][r]);
-#endif
   // dW1^T: tile a, C row g*4 + r -> ky = 4 (w & 1) + (row >> 2), kx = 4 a + (row & 3)
 #pragma unroll
   for (int a_ = 0; a_ < 2; ++a_) {
@@ -688,32 +452,6 @@ conv_bwd_kernel(ConvBwdArgs a) {
   }
   float* red = reinterpret_cast<float*>(lds + L_RED);
   __syncthreads();
-#if ARL_CB_STAMP
-  CB_STAMP();
-  if (tid == 0) {
-    uint32_t* o = reinterpret_cast<uint32_t*>(out) + SLAB_W1;
-    o[0] = nst;
-    o[1] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
-    o[2] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
-    o[3] = (uint32_t)t0;
-    o[4] = (uint32_t)(t0 >> 32);
-    for (int k = 0; k < nst && k < 30; ++k) o[8 + k] = stamp[k];
-  }
-#endif
-#if ARL_S1_SPLIT
-  // conv2 bias: item thread i (oc group i / 121) holds 8 channel sums; channel oc adds its group's
-  // 121 cells in order
-  if (tid < GI)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) red[tid * 8 + k] = b2a[k];
-  __syncthreads();
-  if (tid < 32) {
-    float t = 0.f;
-    for (int c = 0; c < 121; ++c) t = __fadd_rn(t, red[((tid >> 3) * 121 + c) * 8 + (tid & 7)]);
-    out[SLAB_B2 + tid] = t;
-  }
-  (void)b2sum;
-#else
   red[tid] = b2sum;                  // lane's oc = tid & 31
   __syncthreads();
   if (tid < 32) {
@@ -722,7 +460,6 @@ conv_bwd_kernel(ConvBwdArgs a) {
     out[SLAB_B2 + tid] = t;
   }
   (void)b2a;
-#endif
   __syncthreads();
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) red[(4 * g + rr) * 128 + wave * 16 + col] = b1s[rr];
@@ -741,9 +478,8 @@ conv_bwd_kernel(ConvBwdArgs a) {
 // null): every conv block also leaves the f64 sum of squares of the 64
 // gradient values it wrote in parts[block], and rest_blocks extra blocks sum
 // the squares of g[rest_begin, rest_end) -- the gradient the FC / heads / LSTM
-// backward has already finished -- into parts[nconv + b]; the optimizer then
-// reads their sum, which the last block to finish leaves in parts[NORM_RESULT]
-// (norm_finish, arl_internal.hpp), instead of a separate grad_sqnorm launch.
+// backward has already finished -- into parts[nconv + b]; every block of the
+// update kernel then sums the partials, instead of a separate grad_sqnorm launch.
 constexpr int RED_O = 64, RED_Z = 16;
 constexpr int RED_BLOCKS = (SLAB + RED_O - 1) / RED_O;   // 193
 __device__ inline double block_sum_f64_1024(double x, double* sh) {   // 1,024 threads, fixed order
@@ -776,7 +512,7 @@ reduce_conv_bwd_kernel(const float* __restrict__ slab, int G, float* __restrict_
       t += (double)v * v;
     }
     t = block_sum_f64_1024(t, shn);
-    norm_finish(t, RED_BLOCKS + b, RED_BLOCKS + nf.rest_blocks, nf.parts, nf.finish != 0);
+    if (threadIdx.x == 0) nf.parts[RED_BLOCKS + b] = t;
     return;
   }
   const int ol = threadIdx.x & (RED_O - 1), zg = threadIdx.x / RED_O;
@@ -804,11 +540,12 @@ reduce_conv_bwd_kernel(const float* __restrict__ slab, int G, float* __restrict_
   }
   if (nf.parts != nullptr) {   // (block-uniform)
     sq = block_sum_f64_1024(sq, shn);
-    norm_finish(sq, blockIdx.x, RED_BLOCKS + nf.rest_blocks, nf.parts, nf.finish != 0);
+    if (threadIdx.x == 0) nf.parts[blockIdx.x] = sq;
   }
 }
 
 int conv_norm_parts(int rest_blocks) { return RED_BLOCKS + rest_blocks; }
+static_assert(RED_BLOCKS + 64 <= NORM_MAX_PARTS, "the folded norm's partials fit the scratch");
 
 // workgroups (= slab slices): one per CU on the 256-CU part, at most one per sample
 int conv_bwd_blocks(int S) { return S < 256 ? S : 256; }

@@ -25,14 +25,7 @@
 #include <cstdlib>
 
 #include "arl_internal.hpp"
-#include "policy_rows.hpp"
 
-#ifndef ARL_ABLATE
-#define ARL_ABLATE 0   // timing experiments only (bits: 128 staging, 256 ticket/reduce, 512 MFMA)
-#endif
-#ifndef ARL_FC_HEADS_DEFAULT
-#define ARL_FC_HEADS_DEFAULT 0
-#endif
 
 namespace arl {
 
@@ -86,12 +79,8 @@ __device__ inline void fc_wait_vm(int n) {   // s_waitcnt vmcnt(n), n wave-unifo
   }
 }
 
-// The MFMAs of one staged chunk.  ARL_FC_PREFETCH=1 (A/B knob, off): every fragment read first, one LDS
-// wait per chunk -- 9.7 -> 10.5 us at 512 envs, 19.6 -> 21-22.8 us at 1,024 (profiles/r03/r3s); the
-// default reads per 16-k group, each group's reads waited for right before its four MFMAs
-#ifndef ARL_FC_PREFETCH
-#define ARL_FC_PREFETCH 0
-#endif
+// The MFMAs of one staged chunk: fragments read per 16-k group, each group's reads waited for right
+// before its four MFMAs (reading every fragment first measured slower: 9.7 -> 10.5 us at 512 envs, r3s)
 template <int G>
 __device__ inline f32x4 fc_chunk_mfma(const float* Ar, const float* B0, f32x4 c0) {
   f32x4 av[G], bv[G];
@@ -99,14 +88,6 @@ __device__ inline f32x4 fc_chunk_mfma(const float* Ar, const float* B0, f32x4 c0
   for (int s = 0; s < G; ++s) {
     av[s] = *reinterpret_cast<const f32x4*>(Ar + 16 * s);
     bv[s] = *reinterpret_cast<const f32x4*>(B0 + 16 * s);
-    if (!ARL_FC_PREFETCH)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s][r], bv[s][r], c0, 0, 0, 0);
-  }
-  if (ARL_FC_PREFETCH) {
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int s = 0; s < G; ++s)
 #pragma unroll
       for (int r = 0; r < 4; ++r) c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s][r], bv[s][r], c0, 0, 0, 0);
   }
@@ -127,7 +108,7 @@ fc_fwd_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, 
   // chunk c -> row i / ld, float4 column min(i % ld, w - 1) of the chunk
 #pragma unroll
   for (int c = 0; c < FCH; ++c) {
-    for (int it = wave; it < ((ARL_ABLATE & 128) ? 0 : ch_pieces(c)); it += FW) {
+    for (int it = wave; it < ch_pieces(c); it += FW) {
       const int i = min(it * 64 + lane, FROWS * ch_ld(c) - 1);
       const int r = i / ch_ld(c), cc = min(i - r * ch_ld(c), ch_w(c) - 1);
       const float* src = r < FBM ? a2 + (int64_t)min(m0 + r, n - 1) * A2   // rows past n: any valid row, never stored
@@ -148,15 +129,15 @@ fc_fwd_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, 
     int later = 0;
 #pragma unroll
     for (int c2 = c + 1; c2 < FCH; ++c2) later += ch_wave_pieces(c2, wave);
-    if (!(ARL_ABLATE & 128)) fc_wait_vm(later);
+    fc_wait_vm(later);
     // LDS-only barrier: __syncthreads()'s fence would drain vmcnt, i.e. wait for the later chunks too
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     const float* Ar = S + 4 * ch_base(c) + (ms * 16 + col) * 4 * ch_ld(c) + 4 * q;
     const float* B0 = S + 4 * ch_base(c) + (FBM + ns * 16 + col) * 4 * ch_ld(c) + 4 * q;
     constexpr int G16[FCH] = {7, 7, 6};   // whole 16-k groups per chunk
     // lane quarter q holds k = 16 s + 4 q + r
-    if (!(ARL_ABLATE & 512)) c0 = G16[c] == 7 ? fc_chunk_mfma<7>(Ar, B0, c0) : fc_chunk_mfma<6>(Ar, B0, c0);
-    if (c == FCH - 1 && !(ARL_ABLATE & 512)) {   // tail k = 320 + q (chunk column 96 + q)
+    c0 = G16[c] == 7 ? fc_chunk_mfma<7>(Ar, B0, c0) : fc_chunk_mfma<6>(Ar, B0, c0);
+    if (c == FCH - 1) {   // tail k = 320 + q (chunk column 96 + q)
       c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ar[96 - 3 * q], B0[96 - 3 * q], c0, 0, 0, 0);
     }
   }
@@ -174,7 +155,7 @@ fc_fwd_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, 
       __hip_atomic_store(part + (int64_t)m * HID + n0 + ns * 16 + col, c0[r], __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
   }
-  if ((ARL_ABLATE & 256) || tickets == nullptr) return;
+  if (tickets == nullptr) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0)
@@ -236,8 +217,7 @@ __host__ __device__ constexpr int g_wave_pieces(int c, int w) { return (g_pieces
 
 __global__ void __launch_bounds__(GT)
 fc_fwd_big_kernel(const float* __restrict__ a2, int n, const float* __restrict__ W, float* __restrict__ slab,
-                  int* __restrict__ tickets, const float* __restrict__ bias, float* __restrict__ hfc,
-                  int* __restrict__ row_tickets, PolicyArgs pa) {
+                  int* __restrict__ tickets, const float* __restrict__ bias, float* __restrict__ hfc) {
   __shared__ __attribute__((aligned(16))) float S[2 * GBUF4 * 4];   // 118,784 B
   __shared__ int is_last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -313,65 +293,6 @@ fc_fwd_big_kernel(const float* __restrict__ a2, int n, const float* __restrict__
   o[2] = fmaxf(__fadd_rn(acc[2], b.z), 0.f); o[3] = fmaxf(__fadd_rn(acc[3], b.w), 0.f);
   if (mrow < n) *reinterpret_cast<f32x4*>(hfc + (int64_t)mrow * HID + ccol) = o;
   if (tid == 0) __hip_atomic_store(&tickets[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (row_tickets == nullptr) return;
-  // FF heads (row_tickets != null): this tile's 64 columns are the heads' K quarter kq = n0 / 64 --
-  // policy_rows16's wave kq -- so waves 0-3 form the quarter's partial logits / value of 16 rows each
-  // (heads_quarter: the same MFMA sequence) from the tile in LDS and store them over the tile's
-  // consumed split-0 partials; the last of the row block's 4 column tiles (second ticket) sums the
-  // quarters in wave order + bias and runs the softmax / draw of its 64 rows (heads_row_out).
-  static_assert(FBN * 4 == HID && GBM == 64, "one heads K quarter per column tile, 4 row groups of 16");
-  constexpr int HL = FBN + 4;   // LDS row stride (floats): the 16 rows a lane group reads start on distinct banks
-  constexpr int KW = HID / 4, NS = KW / 16, NTM = HeadsPrefetch<HID>::NTM;
-  const int kq = n0 / FBN, A = pa.A;
-  HeadsPrefetch<HID> pf;
-  if (wave < 4) pf = heads_prefetch<HID>(pa, kq);
-  float* hl = S;
-  *reinterpret_cast<f32x4*>(hl + (tid >> 4) * HL + 4 * (tid & 15)) = o;
-  __syncthreads();
-  if (wave < 4) {
-    f32x4 hv[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) hv[s] = *reinterpret_cast<const f32x4*>(hl + (16 * wave + col) * HL + 16 * s + 4 * q);
-#pragma unroll
-    for (int nt = 0; nt < NTM; ++nt) {
-      if (16 * nt > A) break;   // wave-uniform
-      const int j = 16 * nt + col;
-      const f32x4 c = heads_quarter(hv, pf.wv, nt, j <= A);
-      if (j <= A) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + 16 * wave + 4 * q + r;
-          if (m < n)
-            __hip_atomic_store(slab + (int64_t)m * HID + n0 + j, c[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const int rb = m0 / GBM;
-  if (tid == 0)
-    is_last = __hip_atomic_fetch_add(&row_tickets[rb], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == HID / FBN - 1;
-  __syncthreads();
-  if (!is_last) return;
-  constexpr int ZL = MAXA + 2;
-  float* zs = S + GBM * HL;    // [64][ZL]
-  float* ez = zs + GBM * ZL;   // [64][ZL]
-  for (int i = tid; i < GBM * (A + 1); i += GT) {
-    const int r = i / (A + 1), j = i - r * (A + 1);
-    const float* src = slab + (int64_t)min(m0 + r, n - 1) * HID + j;
-    float pq[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) pq[w] = __hip_atomic_load(src + KW * w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const float z = __fadd_rn(__fadd_rn(pq[0], pq[1]), __fadd_rn(pq[2], pq[3]));
-    zs[r * ZL + j] = __fadd_rn(z, j < A ? pa.bpi[j] : pa.bv[0]);
-  }
-  __syncthreads();
-  if (tid < GBM && m0 + tid < n) {
-    const int64_t step = pa.mode == 1 ? pa.ctl[CTL_STEP] + pa.step_off : 0;
-    heads_row_out(zs + tid * ZL, ez + tid * ZL, m0 + tid, pa, step);
-  }
-  if (tid == 0) __hip_atomic_store(&row_tickets[rb], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 int fc_fwd_tiles(int n) { return ((n + FBM - 1) / FBM) * (HID / FBN); }
@@ -384,24 +305,14 @@ bool fc_fwd_big(int n) {
   return (big && (big[0] == '0' || big[0] == '1')) ? big[0] == '1' : n >= 512;
 }
 
-bool fc_fwd_heads(int n) {
-  // FF heads in fc_fwd_big_kernel's ticket tail instead of policy_fc_kernel (ARL_FC_HEADS=0 / 1)
-  static const char* e = getenv("ARL_FC_HEADS");
-  const bool on = (e && (e[0] == '0' || e[0] == '1')) ? e[0] == '1' : ARL_FC_HEADS_DEFAULT;
-  return on && n >= 128 && fc_fwd_big(n);
-}
-
 hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b, float* slab, int* tickets,
-                         float* hfc, hipStream_t s, const PolicyArgs* heads) {
+                         float* hfc, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  if (heads != nullptr && (tickets == nullptr || hfc == nullptr || !fc_fwd_heads(n) || heads->A + 1 > FBN))
-    return hipErrorInvalidValue;
   if (fc_fwd_big(n)) {
-    // its 64-row tiles use the first half of the 32-row tiles' tickets, the heads' row-block
-    // tickets the next ceil(n / 64) (within the ceil(n / 32) * 4 from n >= 128)
+    // its 64-row tiles use the first half of the 32-row tiles' tickets
     const int tiles = ((n + GBM - 1) / GBM) * (HID / FBN);
     hipLaunchKernelGGL(fc_fwd_big_kernel, dim3((unsigned)(tiles * FSPLIT)), dim3(GT), 0, s, a2, n, W, slab, tickets, b,
-                       hfc, heads != nullptr ? tickets + tiles : nullptr, heads != nullptr ? *heads : PolicyArgs{});
+                       hfc);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(fc_fwd_kernel, dim3((unsigned)(fc_fwd_tiles(n) * FSPLIT)), dim3(FT), 0, s, a2, n, W, b, slab,

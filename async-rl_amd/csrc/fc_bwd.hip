@@ -10,15 +10,11 @@
 //     (write-through stores, drained) and then takes a ticket; the holder of
 //     the last ticket sums the Z partials in range order -- deterministic
 //     whatever the arrival order -- straight into the flat gradient (its own
-//     from registers, rounded as published).  No workgroup waits on another
-//     (ARL_FC_BWD_SPIN=1: ticket first, the last range waits for the others'
-//     partials and never publishes its own -- writes 20.8 -> 18.2 MiB, but
-//     38.5 -> 41.6 us at C2, profiles/r02/rejected/fcb_spin/).  MFMA
+//     from registers, rounded as published).  No workgroup waits on another.  MFMA
 //     accumulators restart every 128 samples; those sums add in f64.  db
 //     rides on the k-tile 0 workgroups: their n-wave-0 lanes add the A
 //     fragments they already hold.
-//   job B (da2): 64 (s) x 128 (k) tiles over K = 256 (128 x 128 on the
-//     exact-f32 path), ReLU mask in the
+//   job B (da2): 64 (s) x 128 (k) tiles over K = 256, ReLU mask in the
 //     epilogue (mask bits prefetched during the k loop, float4 buffer stores).
 //   job C (optional): the policy / value heads' weight gradients, a small
 //     f64 VALU reduction over S that runs beside A and B instead of as two
@@ -27,9 +23,8 @@
 // 32 KB stages (K chunks of 32; the next chunk in flight while the current one
 // feeds the MFMAs).  A chunk is one 16x16x32 bf16 k-step per tile pair on exact
 // bf16 splits of the f32 fragments (bf16split.hpp: 6 MFMAs, f32-accurate; job B
-// keeps the 5 small terms in their own accumulator); ARL_FC_BWD_F32=1 runs the
-// exact-f32 v_mfma_f32_16x16x4_f32 steps instead.  256 threads, each wave a
-// 64 x 32 (job A) or 32 x 64 (job B; 64 x 64 on the f32 path) block of 16 x 16 tiles.
+// keeps the 5 small terms in their own accumulator).  256 threads, each wave a
+// 64 x 32 (job A) or 32 x 64 (job B) block of 16 x 16 tiles.
 // Fragment reads are wide: one lane's 16-byte read of 4 consecutive m (or n)
 // feeds 4 MFMA tiles whose rows (columns) interleave with stride 4 (8-byte
 // reads: 2 tiles, stride 2).  Job B's A operand is stored k-contiguous and is
@@ -47,7 +42,6 @@
 #include <stdint.h>
 
 #include <algorithm>
-#include <cstdlib>
 
 #include "arl_internal.hpp"
 #include "bf16split.hpp"
@@ -63,17 +57,8 @@ constexpr int OOB = 0x7ffffff0;         // a buffer offset past every range: the
 constexpr int NT = 256;                 // 4 waves
 constexpr int NW = NT / 64;
 constexpr int BK = 32;                  // K chunk (rows of a stage)
-// job A tile: AJ j x AK k (AJ AK = 8192).  ARL_FCB_AJ=256 (A/B knob): tiles spanning every j of the FC,
-// 256 x 32, so each a2 column block is streamed once instead of once per j tile (the dfc rows, L2-resident,
-// twice as wide); the waves then split j only (64 j x 32 k each)
-#ifndef ARL_FCB_AJ
-#define ARL_FCB_AJ 128
-#endif
-// job B's da2 stores with the non-temporal cache policy (A/B knob)
-#ifndef ARL_FCB_NTST
-#define ARL_FCB_NTST 0
-#endif
-constexpr int AJ = ARL_FCB_AJ, AK = 8192 / ARL_FCB_AJ;
+// job A tile: AJ j x AK k (tiles over all 256 j, a2 streamed once, measured slower: r4p)
+constexpr int AJ = 128, AK = 64;
 constexpr int AWN = AK / 32;            // job A waves along k (64: 2, 32: 1)
 constexpr int STAGE = BK * (AJ + AK) > 8192 ? BK * (AJ + AK) : 8192;   // floats per LDS stage
 constexpr int AKEY = AK == 64 ? 1 : 0;  // job A's X image: 64-float rows need the 8 * (row & 1) key, 32-float
@@ -92,8 +77,7 @@ static_assert(BK * (AJ + AK) <= STAGE && 128 * BK + BK * BN <= STAGE, "stage siz
 //   Chainer's LSTM gates = upward(x) + lateral(h)): dY = dG (S x 1024), X =
 //   [x | h_prev] (S x 512; h_prev rows of samples whose env reset at that step
 //   read 0, as the forward saw them), dW = [upward W | lateral W], db = the
-//   upward bias; dX = dfc = (dG Wu) * (hfc > 0).  Replaces the generic dual
-//   GEMM + slab reduce of round 2 (ARL_LSTM_WGRAD=gemm keeps it).
+//   upward bias; dX = dfc = (dG Wu) * (hfc > 0).
 struct ShapeFC {
   static constexpr int J = HID, KW = A2, KW1 = A2, NB = A2;
   static constexpr bool kLstm = false;
@@ -119,7 +103,7 @@ constexpr int RST_MAX = 1024;           // LSTM job A: reset flags of a sample r
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-// XCD-aware job order (ARL_FC_BWD_XCD=0: plain order, A/B timing only).
+// XCD-aware job order.
 // Workgroups are dealt round-robin over the 8 XCDs (b % 8 share one XCD and
 // its L2; which XCD is not fixed, MI355X_MICROARCH.md), so job b of n gets
 // linear work index xcd_order(b, n): every XCD takes one contiguous range of
@@ -181,14 +165,9 @@ struct FcBwdArgs {
   float* gb;          // (256) / LSTM upward b (1024)
   float* da2;         // dX: (S, 2592) / LSTM dfc (S, 256)
   float* part;        // (NTA, Z, PART) published job A partials (slot z = range z)
-  int* tick;          // (2 NTA): arrival tickets per tile, then ready counts (spin)
+  int* tick;          // (NTA): arrival tickets per tile
   HeadsDW hd;         // job C (hd.dl null: none)
   int nc;             // job C workgroups
-  int b0;             // first job index of this launch (timing experiments)
-  int abl;            // ARL_FC_BWD_ABL bits (timing experiments only): 1 no MFMA, 2 no staging,
-                      // 4 no job A reduction (wrong dW), 8 no job A k loop
-  int spin;           // job A reduce: ticket first, the last range waits for the others' partials
-  int xcd;            // XCD-aware job order (xcd_order)
   // LSTM only
   const float* hprev;      // h_prev (S, 256): the carry-in h of each sample's step (hbuf slot t)
   const uint8_t* reset;    // (S): the env reset at that step (its h_prev reads 0)
@@ -200,43 +179,22 @@ struct FcBwdArgs {
 };
 
 // ---------------------------------------------------------------- job A: dW, db
-// range z's partial of `tile` into its slot: write-through sc1 stores; the
-// (u = 0, 1) pair of a lane is 8 contiguous bytes, one 64-bit store, so a
-// quarter-wave writes 128 contiguous bytes (whole sectors)
-__device__ inline void publish_dw(const FcBwdArgs& a, int tile, int z, const double (&s)[4][2][4], const double (&sb)[4],
-                                  bool bias, int wm, int wn, int q, int col) {
-  float* dst = a.part + ((int64_t)tile * a.Z + z) * PART;
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      __hip_atomic_store(reinterpret_cast<uint64_t*>(dst + (wm * 64 + 16 * q + 4 * e + t) * AK + wn * 32 + 2 * col),
-                         pack2((float)s[t][0][e], (float)s[t][1][e]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (bias && q == 0)
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-      __hip_atomic_store(dst + AJ * AK + wm * 64 + 4 * col + t, (float)sb[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <bool SPLIT, class SH>
+template <class SH>
 __device__ void job_dw(const FcBwdArgs& a, int job, float* lds, uint8_t* rst) {
   using D = Dims<SH>;
   constexpr int NTA = D::NTA;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, col = lane & 15;
   const int wm = wave / AWN, wn = wave % AWN;   // wave: 64 j x 32 k
-  int tile = job % NTA, z = job / NTA;
-  if (a.xcd) {   // linear order (z, kt, jt), jt fastest
-    const int lin = xcd_order(job, NTA * a.Z);
-    z = lin / NTA;
-    const int r = lin - z * NTA;
-    tile = (r % D::NJA) * D::NKA + r / D::NJA;
-  }
+  // linear order (z, kt, jt), jt fastest, dealt to the XCDs in contiguous ranges
+  const int lin = xcd_order(job, NTA * a.Z);
+  const int z = lin / NTA;
+  const int tile = ((lin - z * NTA) % D::NJA) * D::NKA + (lin - z * NTA) / D::NJA;
   const int kt = tile % D::NKA, jt = tile / D::NKA;
   const int j0 = jt * AJ, k0 = kt * AK;
   const int r0 = z * a.kpz, r1 = min(a.S, r0 + a.kpz);
   const bool bias = kt == 0 && wn == 0;
-  const int nchunks = (a.abl & 8) ? 0 : max(0, (r1 - r0 + BK - 1) / BK);
+  const int nchunks = max(0, (r1 - r0 + BK - 1) / BK);
   // X columns of this k tile: FC a2; LSTM x = hfc (k < 256) or h_prev (k >= 256, the
   // range's reset flags staged in LDS first: a reset sample's row is DMA'd from the zero row)
   const bool hpart = SH::kLstm && k0 >= SH::KW1;   // block-uniform
@@ -258,7 +216,6 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds, uint8_t* rst) {
       for (int e = 0; e < 4; ++e) s[t][u][e] = 0.0;
   }
   auto issue = [&](int c) {
-    if (a.abl & 2) return;
     float* st = lds + (c & 1) * STAGE;
     stage_tile<BK, AJ, 0>(st, a.dfc, SH::J, r0 + c * BK, r1 - 1, j0);       // dY[s][j0 .. j0+127]
     if (SH::kLstm && hpart)
@@ -287,7 +244,7 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds, uint8_t* rst) {
         for (int u = 0; u < 2; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
       bs = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    if (!(a.abl & 1)) {
+    {
       // every fragment of the chunk first (counted LDS waits), then the MFMAs
       f32x4 av[BK / 4];
       f32x2 bv[BK / 4];
@@ -302,9 +259,8 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds, uint8_t* rst) {
         for (int ks = 0; ks < BK / 4; ++ks)
           if (4 * ks + q >= kvalid) av[ks] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      if constexpr (SPLIT) {
-        // one 16x16x32 bf16 step per tile pair: element i of lane (col, q)
-        // is sample 4 i + q, the same rows the f32 steps below read
+      {
+        // one 16x16x32 bf16 step per tile pair: element i of lane (col, q) is sample 4 i + q
         bf16x8 bh[2], bm[2], bl[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -326,16 +282,6 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds, uint8_t* rst) {
         if (bias)
 #pragma unroll
           for (int ks = 0; ks < BK / 4; ++ks) bs += av[ks];
-      } else {
-#pragma unroll
-        for (int ks = 0; ks < BK / 4; ++ks) {
-#pragma unroll
-          for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-              acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[ks][t], bv[ks][u], acc[t][u], 0, 0, 0);
-          if (bias) bs += av[ks];
-        }
       }
     }
     if (c % FLUSH == FLUSH - 1 || c == nchunks - 1) {
@@ -360,27 +306,7 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds, uint8_t* rst) {
     }
   }
   auto pidx = [&](int t, int u, int e) { return (wm * 64 + 16 * q + 4 * e + t) * AK + wn * 32 + 2 * col + u; };
-  if (a.Z > 1 && !(a.abl & 4) && a.spin) {
-    // ticket first: ranges holding tickets 0 .. Z-2 publish and count
-    // themselves in ready[tile]; the last waits for that count (every range it
-    // waits on has taken its ticket, so is resident and already publishing)
-    // and its own partial never leaves registers
-    int* flag = reinterpret_cast<int*>(lds);   // the stages are free after the k loop's last barrier
-    if (tid == 0) *flag = __hip_atomic_fetch_add(&a.tick[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (*flag < a.Z - 1) {
-      publish_dw(a, tile, z, s, sb, bias, wm, wn, q, col);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
-      __syncthreads();
-      if (tid == 0) __hip_atomic_fetch_add(&a.tick[NTA + tile], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-    if (tid == 0)
-      while (__hip_atomic_load(&a.tick[NTA + tile], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < a.Z - 1)
-        __builtin_amdgcn_s_sleep(1);
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // every slot load below is sc1
-  } else if (a.Z > 1 && !(a.abl & 4)) {
+  if (a.Z > 1) {
     // every range publishes into its slot (write-through sc1 stores, drained),
     // then takes a ticket; the holder of the last ticket sums the slots.
     // Ordering: this is the hand-off MI355X_MICROARCH.md lists as valid on
@@ -488,15 +414,13 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds, uint8_t* rst) {
   if (bias && q == 0)
 #pragma unroll
     for (int t = 0; t < 4; ++t) a.gb[j0 + wm * 64 + 4 * col + t] = (float)ob[t];
-  if (a.Z > 1 && tid == 0 && !(a.abl & 4)) {   // re-arm for the next launch (a captured graph replays this one)
+  if (a.Z > 1 && tid == 0)   // re-arm for the next launch (a captured graph replays this one)
     __hip_atomic_store(&a.tick[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (a.spin) __hip_atomic_store(&a.tick[NTA + tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 // ---------------------------------------------------------------- job B: da2
 // MT m-tiles per wave: workgroup tiles of BMT = 32 MT samples x 128 k
-template <int MT, bool SPLIT, class SH>
+template <int MT, class SH>
 __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
   using D = Dims<SH>;
   constexpr int NKB = D::NKB, NB = SH::NB;
@@ -505,29 +429,25 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, col = lane & 15;
   const int wm = wave >> 1, wn = wave & 1;   // wave: 16 MT s x 64 k
-  int kt = tile % NKB, st = tile / NKB;
-  if (a.xcd) {   // linear order (kt, st), st fastest
-    const int nst = (a.S + BMT - 1) / BMT;
-    const int lin = xcd_order(tile, nst * NKB);
-    kt = lin / nst;
-    st = lin - kt * nst;
-  }
+  // linear order (kt, st), st fastest, dealt to the XCDs in contiguous ranges
+  const int nst = (a.S + BMT - 1) / BMT;
+  const int lin = xcd_order(tile, nst * NKB);
+  const int kt = lin / nst, st = lin - kt * nst;
   const int s0 = st * BMT, k0 = kt * BN;
   constexpr int NCH = D::NCHB;               // chunks of 32 j: FC 8, LSTM 32
   auto issue = [&](int c) {
-    if (a.abl & 2) return;
     float* sg = lds + (c & 1) * STAGE;
     stage_tile<BMT, BK, 2>(sg, a.dfc + c * BK, SH::J, s0, a.S - 1, 0);                  // dY[s][j]
     stage_tile<BK, BN, 0>(sg + BMT * BK, a.W + (int64_t)c * BK * NB, NB, 0, BK - 1, k0);  // W[j][k0..k0+127]
   };
   f32x4 acc[MT][4];                          // m-tile i: rows 16 i + col; n-tile u: cols 4 col + u
-  f32x4 sml[SPLIT ? MT : 1][4];              // split path: the 5 small terms (acc: the h.h term)
+  f32x4 sml[MT][4];                          // the 5 small terms (acc: the h.h term)
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[i][u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int i = 0; i < (SPLIT ? MT : 1); ++i)
+  for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int u = 0; u < 4; ++u) sml[i][u] = f32x4{0.f, 0.f, 0.f, 0.f};
   // ReLU mask of the tile (a2 > 0), one bit per output element -- bit 4e + u
@@ -583,7 +503,7 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
     barrier_lds();
     const float* As = lds + (c & 1) * STAGE;
     const float* Bs = As + BMT * BK;
-    if (!(a.abl & 1)) {
+    {
       // every fragment of the chunk first (counted LDS waits), then the MFMAs
       f32x4 av[BK / 16][MT], bv[BK / 16][4];
 #pragma unroll
@@ -597,7 +517,7 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
         for (int r = 0; r < 4; ++r)   // k = 16 g + 4 q + r on both operands
           bv[g][r] = *reinterpret_cast<const f32x4*>(Bs + (16 * g + 4 * q + r) * BN + wn * 64 + 4 * col);
       }
-      if constexpr (SPLIT) {
+      {
         // one 16x16x32 bf16 step per tile pair: element 4 g + r of lane
         // (col, q) is k = 16 g + 4 q + r on both operands
         bf16x8 bh[4], bm[4], bl[4];
@@ -622,16 +542,6 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
 #pragma unroll
           for (int u = 0; u < 4; ++u) mfma_x6(ah, am, al, bh[u], bm[u], bl[u], acc[i][u], sml[i][u]);
         }
-      } else {
-#pragma unroll
-        for (int g = 0; g < BK / 16; ++g)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int i = 0; i < MT; ++i)
-#pragma unroll
-              for (int u = 0; u < 4; ++u)
-                acc[i][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][i][r], bv[g][r][u], acc[i][u], 0, 0, 0);
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -651,12 +561,10 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
       f32x4 o;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        float v = acc[i][u][e];
-        if constexpr (SPLIT) v += sml[i][u][e];
+        const float v = acc[i][u][e] + sml[i][u][e];
         o[u] = (mb[i] >> (4 * e + u)) & 1u ? v : 0.f;
       }
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), out, kin ? (row * NB + k) * 4 : OOB, 0,
-                                              ARL_FCB_NTST ? 2 : 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), out, kin ? (row * NB + k) * 4 : OOB, 0, 0);
     }
 }
 
@@ -723,34 +631,21 @@ __device__ void job_heads(const FcBwdArgs& a, int jt, float* lds) {
   }
 }
 
-// static wave priority (A/B knob): 1 = job A (dW) workgroups at s_setprio 1, 2 = job B (da2) ones; a CU
-// holds two workgroups, whose waves pair up on its SIMDs (MI355X_MICROARCH.md "Two waves per SIMD")
-#ifndef ARL_FCB_PRIO
-#define ARL_FCB_PRIO 0
-#endif
-
-template <int MT, bool SPLIT, class SH>
+template <int MT, class SH>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2)))
 fc_bwd_kernel(FcBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];   // 64 KB (72 KB with ARL_FCB_AJ=256)
+  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];   // 64 KB
   __shared__ uint8_t rst[SH::kLstm ? RST_MAX : 4];                 // LSTM: a range's reset flags
-  const int b = a.b0 + blockIdx.x;
+  const int b = blockIdx.x;
   const int na = Dims<SH>::NTA * a.Z;
   if (b < a.nc) job_heads(a, b, lds);   // first: the smallest, longest-latency jobs
-  else if (b < a.nc + na) {
-    if (ARL_FCB_PRIO == 1) __builtin_amdgcn_s_setprio(1);
-    job_dw<SPLIT, SH>(a, b - a.nc, lds, rst);
-  } else {
-    if (ARL_FCB_PRIO == 2) __builtin_amdgcn_s_setprio(1);
-    job_da2<MT, SPLIT, SH>(a, b - a.nc - na, lds);
-  }
+  else if (b < a.nc + na) job_dw<SH>(a, b - a.nc, lds, rst);
+  else job_da2<MT, SH>(a, b - a.nc - na, lds);
 }
 
 // ~800 samples per job A range, at most 16 ranges (bf16-split steps, sweep in
 // profiles/r02/fcb_split/z_sweep.txt: best Z 2 / 3-5 / 6 at S 1280 / 2560 / 5120)
 int fc_bwd_ranges(int S) {
-  static const char* zs = getenv("ARL_FC_BWD_Z");   // timing experiments only
-  if (zs) return std::max(1, std::min(16, atoi(zs)));
   return std::max(1, std::min(16, (S + 400) / 800));
 }
 // LSTM: the same, with no range longer than the LDS reset table
@@ -761,7 +656,7 @@ int range_len(int S, int Z) { return ((S + Z - 1) / Z + BK - 1) / BK * BK; }
 int64_t fc_bwd_part_floats(int S) {
   return (int64_t)std::max(Dims<ShapeFC>::NTA * fc_bwd_ranges(S), Dims<ShapeLSTM>::NTA * lstm_wgrad_ranges(S)) * PART;
 }
-int fc_bwd_tickets() { return 2 * NTA_MAX; }   // arrival tickets, then ready counts (ARL_FC_BWD_SPIN)
+int fc_bwd_tickets() { return NTA_MAX; }   // arrival tickets
 
 // Job A's last k tile stages a2 columns 2560..2623 and job B's last one W
 // columns 2560..2687: the floats past a row's end are the next row's (a2 has
@@ -772,33 +667,15 @@ hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int 
   if (S <= 0) return hipSuccess;
   const int Z = fc_bwd_ranges(S);
   const int kpz = range_len(S, Z);
-  // ARL_FC_BWD_F32=1: the exact-f32 16x16x4 MFMA steps instead of the bf16 splits (A/B timing).
-  // Job B tiles: 64 samples (2 m-tiles a wave) on the split path, whose small-term
-  // accumulators leave no room for 4 m-tiles; 128 on the f32 path unless ARL_FC_BWD_BM=64.
-  static const char* f32 = getenv("ARL_FC_BWD_F32");
-  static const char* bm = getenv("ARL_FC_BWD_BM");
-  const bool split = !(f32 && atoi(f32) == 1);
-  const int MT = (split || (bm && atoi(bm) == 64)) ? 2 : 4, BMT = 32 * MT;
+  // job B tiles: 64 samples (2 m-tiles a wave; the small-term accumulators leave no room for 4)
+  constexpr int MT = 2, BMT = 32 * MT;
   using D = Dims<ShapeFC>;
   const int na = D::NTA * Z, nb = ((S + BMT - 1) / BMT) * D::NKB;
-  // ARL_FC_BWD_JOBS=a / b: launch one job alone; ARL_FC_BWD_ABL: ablations (timing experiments only)
-  static const char* only = getenv("ARL_FC_BWD_JOBS");
-  static const char* abl = getenv("ARL_FC_BWD_ABL");
   if (heads != nullptr && (heads->A < 1 || heads->dl == nullptr)) return hipErrorInvalidValue;
   const int nc = heads != nullptr ? NJC : 0;
-  const int b0 = (only && only[0] == 'b') ? nc + na : (only && only[0] == 'a') ? nc : 0;
-  const int grid = (only && only[0] == 'a') ? na : (only && only[0] == 'b') ? nb : nc + na + nb;
-  // ARL_FC_BWD_SPIN=1: ticket-first job A reduce (the last range's partial is never published)
-  static const char* spin = getenv("ARL_FC_BWD_SPIN");
-  static const char* mask = getenv("ARL_FC_BWD_MASK");   // "f32": job B reads a2 for its mask (A/B timing)
-  if (mask && mask[0] == 'f') a2m = nullptr;
-  static const char* xcd = getenv("ARL_FC_BWD_XCD");
-  FcBwdArgs args{dfc, a2, W, S, Z, kpz, gW, gb, da2, part, tick, heads ? *heads : HeadsDW{}, nc, b0,
-                 abl ? atoi(abl) : 0, (spin && atoi(spin) == 1) ? 1 : 0, (xcd && xcd[0] == '0') ? 0 : 1,
+  FcBwdArgs args{dfc, a2, W, S, Z, kpz, gW, gb, da2, part, tick, heads ? *heads : HeadsDW{}, nc,
                  nullptr, nullptr, nullptr, nullptr, a2m};
-  if (split) hipLaunchKernelGGL((fc_bwd_kernel<2, true, ShapeFC>), dim3(grid), dim3(NT), 0, s, args);
-  else if (MT == 2) hipLaunchKernelGGL((fc_bwd_kernel<2, false, ShapeFC>), dim3(grid), dim3(NT), 0, s, args);
-  else hipLaunchKernelGGL((fc_bwd_kernel<4, false, ShapeFC>), dim3(grid), dim3(NT), 0, s, args);
+  hipLaunchKernelGGL((fc_bwd_kernel<MT, ShapeFC>), dim3(nc + na + nb), dim3(NT), 0, s, args);
   return hipGetLastError();
 }
 
@@ -815,10 +692,8 @@ hipError_t launch_lstm_wgrad(const float* dG, const float* hfc, const float* hpr
   using D = Dims<ShapeLSTM>;
   constexpr int BMT = 64;
   const int na = D::NTA * Z, nb = ((S + BMT - 1) / BMT) * D::NKB;
-  static const char* xcd = getenv("ARL_FC_BWD_XCD");
-  FcBwdArgs args{dG, hfc, Wu, S, Z, kpz, gWu, gbu, dfc, part, tick, HeadsDW{}, 0, 0, 0, 0,
-                 (xcd && xcd[0] == '0') ? 0 : 1, hprev, reset, zero, gWl};
-  hipLaunchKernelGGL((fc_bwd_kernel<2, true, ShapeLSTM>), dim3(na + nb), dim3(NT), 0, s, args);
+  FcBwdArgs args{dG, hfc, Wu, S, Z, kpz, gWu, gbu, dfc, part, tick, HeadsDW{}, 0, hprev, reset, zero, gWl};
+  hipLaunchKernelGGL((fc_bwd_kernel<2, ShapeLSTM>), dim3(na + nb), dim3(NT), 0, s, args);
   return hipGetLastError();
 }
 

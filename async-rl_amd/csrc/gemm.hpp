@@ -22,17 +22,13 @@
 // f32-accurate) instead of 8 exact-f32 16x16x4 steps: 2.7x fewer matrix-pipe
 // cycles for more VALU / LDS reads.  Off: these GEMMs wait on their register
 // gathers and scalar LDS reads, not on the matrix pipe -- every GEMM on it took
-// the LSTM C3 window 1.316 -> 1.377 ms, the dual weight-gradient kernel alone
-// (ARL_GEMM2_SPLIT=1) 1.319 -> 1.374 ms (profiles/r02/gemm_split/).
+// the LSTM C3 window 1.316 -> 1.377 ms (profiles/r02/gemm_split/).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "bf16split.hpp"
 
-#ifndef ARL_GEMM2_SPLIT
-#define ARL_GEMM2_SPLIT 0   // A/B variant only (see above)
-#endif
 
 namespace arl {
 
@@ -360,11 +356,11 @@ gemm2_kernel(J1 j1, J2 j2) {
   const int g1 = j1.gx * j1.gy * j1.gz;
   if (b < g1) {
     const int x = b % j1.gx, y = (b / j1.gx) % j1.gy, z = b / (j1.gx * j1.gy);
-    gemm_tile<BM, BN, BK, WM, WN, AV1, BV1, NTH, decltype(j1.A), decltype(j1.B), decltype(j1.E), ARL_GEMM2_SPLIT>(j1.A, j1.B, j1.E, j1.M, j1.N, j1.K, j1.kps, x, y, z);
+    gemm_tile<BM, BN, BK, WM, WN, AV1, BV1, NTH, decltype(j1.A), decltype(j1.B), decltype(j1.E), false>(j1.A, j1.B, j1.E, j1.M, j1.N, j1.K, j1.kps, x, y, z);
   } else {
     b -= g1;
     const int x = b % j2.gx, y = (b / j2.gx) % j2.gy, z = b / (j2.gx * j2.gy);
-    gemm_tile<BM, BN, BK, WM, WN, AV2, BV2, NTH, decltype(j2.A), decltype(j2.B), decltype(j2.E), ARL_GEMM2_SPLIT>(j2.A, j2.B, j2.E, j2.M, j2.N, j2.K, j2.kps, x, y, z);
+    gemm_tile<BM, BN, BK, WM, WN, AV2, BV2, NTH, decltype(j2.A), decltype(j2.B), decltype(j2.E), false>(j2.A, j2.B, j2.E, j2.M, j2.N, j2.K, j2.kps, x, y, z);
   }
 }
 

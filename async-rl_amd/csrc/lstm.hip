@@ -39,20 +39,10 @@ constexpr int LROWS = LBN + LBM;               // 96 staged rows: 64 of [Wu | Wl
 // 16-byte k quarters land on 16 distinct bank quads (33 = 1 mod 16 puts two of them on one quad); the
 // same for the BPTT kernel's dG rows (BA_LD).  34 vs 33 at C3: lstm_gates 20.3 -> 19.2 us, lstm_bptt
 // 17.1 -> 16.8 us, window 1.151 -> 1.140 ms (profiles/r04/r4o)
-#ifndef ARL_LSTM_LD
-#define ARL_LSTM_LD 34
-#endif
-// static wave priority (A/B knob): waves 4-7 of the gate and BPTT workgroups at s_setprio 1
-// (MI355X_MICROARCH.md "Two waves per SIMD" item 4)
-#ifndef ARL_LSTM_PRIO
-#define ARL_LSTM_PRIO 0
-#endif
+constexpr int LSTM_LD = 34;
 // the saved gate pre-activations (read only by the window's BPTT) stored non-temporal, as conv_fwd's a1 / a2:
 // C3 median 1.1133 / 1.1144 -> 1.1091 / 1.1109 ms, lstm_gates 19.5 -> 19.1 us (2 interleaved reps, r4t)
-#ifndef ARL_LSTM_NTST
-#define ARL_LSTM_NTST 1
-#endif
-constexpr int LLD = ARL_LSTM_LD;
+constexpr int LLD = LSTM_LD;
 constexpr int LPIECES = (LROWS * LLD + 63) / 64;   // 51 LDS-DMA pieces (64 x 16 B) per chunk
 constexpr int LWPIECES = LBN * LLD / 64;       // 34: the W rows alone (XRED x chunks)
 constexpr int LSTAGE4 = LPIECES * 64;          // float4 per stage (incl. the last piece's overhang)
@@ -108,7 +98,6 @@ __global__ void __launch_bounds__(LT)
 lstm_gates_kernel(LstmGatesArgs a) {
   __shared__ __attribute__((aligned(16))) float S[LSTAGES * LSTAGE4 * 4];   // 156,672 B
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (ARL_LSTM_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
   constexpr int NTN = GATES / LBN;
   const int m0 = (blockIdx.x / NTN) * LBM, n0 = (blockIdx.x % NTN) * LBN;
 
@@ -257,11 +246,9 @@ lstm_gates_kernel(LstmGatesArgs a) {
   const int row = tid >> 4, u = tid & 15, m = m0 + row, n = n0 + 4 * u;
   if (m >= a.n) return;
   const float4 g = *reinterpret_cast<const float4*>(T + row * TLD + 4 * u);   // bias added above
-  if (ARL_LSTM_NTST) {
+  {
     typedef float f4v __attribute__((ext_vector_type(4)));
     __builtin_nontemporal_store(f4v{g.x, g.y, g.z, g.w}, reinterpret_cast<f4v*>(a.gates + (int64_t)m * GATES + n));
-  } else {
-    *reinterpret_cast<float4*>(a.gates + (int64_t)m * GATES + n) = g;
   }
   if (!a.cell) return;
   const int64_t i = (int64_t)m * HID + (n >> 2);
@@ -311,7 +298,7 @@ namespace {
 constexpr int BBM = 32, BBN = 32, BT = 512, BW = BT / 64;
 constexpr int BKC = 128;                                 // K chunk
 constexpr int BNCH = GATES / BKC;                        // 8 chunks
-constexpr int BA_LD = ARL_LSTM_LD;                       // 34 float4 per dG row
+constexpr int BA_LD = LSTM_LD;                       // 34 float4 per dG row
 constexpr int BB_LD = BBN / 4 + 1;                       // 9 float4 per Wl row
 constexpr int BA_PC = (BBM * BA_LD + 63) / 64;           // 17 pieces
 constexpr int BB_PC = (BKC * BB_LD + 63) / 64;           // 18 pieces
@@ -355,7 +342,6 @@ __global__ void __launch_bounds__(BT)
 lstm_bptt_kernel(LstmBpttArgs a) {
   __shared__ __attribute__((aligned(16))) float S[BSTAGES * BSTAGE4 * 4];   // 143,360 B
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (ARL_LSTM_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
   constexpr int NTN = HID / BBN;
   const int m0 = (blockIdx.x / NTN) * BBM, u0 = (blockIdx.x % NTN) * BBN;
   const int pw = bptt_pieces(wave);

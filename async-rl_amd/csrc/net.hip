@@ -7,16 +7,14 @@
 // F.lstm (interleaved a,i,f,o gates), a3c.py:129-130 (backward of the window
 // loss), a3c.py:144 (unchain_backward: truncated BPTT at the window edge).
 //
-// Every contraction runs through the fp32 MFMA implicit-GEMM template
-// (gemm.hpp).  Forward: conv1 M = 400*n rows (env, oy, ox) x 16 oc x K 256
-// gathered straight from the uint8 frame ring (stack order oldest->newest,
-// planes older than the env's last reset read as 0, /255 folded into the
-// gather); conv2 M = 81*n x 32 x 256 from conv1's activations; FC M = n x 256
-// x 2592 split over K into partial slabs + a bias/ReLU reduce.  Backward over
-// the whole window (S = T*n samples): weight gradients are split-K GEMMs whose
-// reduction axis is the sample (and position) axis, with a ones-column that
-// yields the bias gradient in the same pass; slabs are summed in f64 in slice
-// order (deterministic) straight into the flat gradient buffer.
+// The window's launches in order (the kernels live in their own files):
+// forward per step t: phi_ring (phi.hip) -> conv_fwd (conv_fwd.hip) -> fc_fwd
+// (fc.hip) -> policy_fc (FF) or the LSTM gate kernel + policy (lstm.hip,
+// policy.hip); learner: returns + heads dh (policy.hip), [LSTM BPTT + gate
+// weight gradients], fc_bwd (fc_bwd.hip), conv_bwd + its slab reduce
+// (conv_bwd.hip), then clip + RMSProp + the window advance (optim.hip).  The
+// f32-state forward (pi_and_v) and the ARCH_STATES / Nature convolutions run on
+// the generic implicit-GEMM template (gemm.hpp).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -51,188 +49,21 @@ struct Conv2A {         // A(m, k) = a1[s][ic][2oy+ky][2ox+kx], m = s*81 + p, k 
     return a1[(int64_t)s * A1 + ic * C1_P + (2 * oy + ky) * 20 + 2 * ox + kx];
   }
 };
-struct LstmGateA {      // A(m, k): [x | h_prev (0 after reset)]
-  const float* __restrict__ x; const float* __restrict__ h; const uint8_t* __restrict__ reset;
-  __device__ float load(int m, int k) const {
-    if (k < HID) return x[(int64_t)m * HID + k];
-    return reset[m] ? 0.f : h[(int64_t)m * HID + k - HID];
-  }
-  __device__ float4 load4(int m, int k) const {   // a 4-vector never straddles k = 256
-    if (k < HID) return *reinterpret_cast<const float4*>(x + (int64_t)m * HID + k);
-    if (reset[m]) return make_float4(0.f, 0.f, 0.f, 0.f);
-    return *reinterpret_cast<const float4*>(h + (int64_t)m * HID + k - HID);
-  }
-};
-struct LstmGateB {      // B(k, j) = [Wu^T ; Wl^T]
-  const float* __restrict__ wu; const float* __restrict__ wl;
-  __device__ float load(int k, int j) const {
-    return k < HID ? wu[(int64_t)j * HID + k] : wl[(int64_t)j * HID + k - HID];
-  }
-  __device__ float4 load4(int k, int j) const {
-    return k < HID ? *reinterpret_cast<const float4*>(wu + (int64_t)j * HID + k)
-                   : *reinterpret_cast<const float4*>(wl + (int64_t)j * HID + k - HID);
-  }
-};
-struct LstmWB {         // B(s, j) = [x (256) | h_prev (256, 0 after reset) | 1]: the gate weight gradient's
-                        // operand (upward W, lateral W, then the ones column for the upward bias)
-  const float* __restrict__ x; const float* __restrict__ h; const uint8_t* __restrict__ reset;
-  __device__ float load(int s, int j) const {
-    if (j < HID) return x[(int64_t)s * HID + j];
-    if (j < 2 * HID) return reset[s] ? 0.f : h[(int64_t)s * HID + j - HID];
-    return 1.f;
-  }
-  // 4 consecutive j (j % 4 == 0, j + 3 < 2 HID): one 16-byte load of x or h
-  __device__ float4 load4n(int s, int j) const {
-    if (j < HID) return *reinterpret_cast<const float4*>(x + (int64_t)s * HID + j);
-    if (reset[s]) return make_float4(0.f, 0.f, 0.f, 0.f);
-    return *reinterpret_cast<const float4*>(h + (int64_t)s * HID + j - HID);
-  }
-};
-struct MapLstmW {       // LstmWB's column order -> the flat gradient: upward W, lateral W, upward b
-  float* g; int64_t oU, oL, ob;
-  __device__ void put(int m, int n, float v) const {
-    if (n < HID) g[oU + (int64_t)m * HID + n] = v;
-    else if (n < 2 * HID) g[oL + (int64_t)m * HID + (n - HID)] = v;
-    else g[ob + m] = v;
-  }
-};
-
-constexpr int BPTT_SPLIT = 4;   // split-K of the BPTT dh GEMM (K = 1024)
-
-// ARL_FC_BWD=gemm: the round-1 FC backward (generic split-K GEMM pair + slab
-// reduce) instead of fc_bwd_kernel -- A/B timing only
-static const bool FC_BWD_GEMM = [] {
-  const char* e = getenv("ARL_FC_BWD");
-  return e != nullptr && e[0] == 'g';
-}();
-
-// ARL_RETURNS_SPLIT=1: returns and the heads' dh as two launches -- A/B timing only
-static const bool RETURNS_SPLIT = [] {
-  const char* e = getenv("ARL_RETURNS_SPLIT");
-  return e != nullptr && e[0] == '1';
-}();
-
-struct MapResetMask {   // split-K reduce target: out[m][n] = reset[m] ? 0 : v
-  float* out; const uint8_t* reset; int ld;
-  __device__ void put(int m, int n, float v) const { out[(int64_t)m * ld + n] = reset[m] ? 0.f : v; }
-};
-struct EpiResetMask {   // out[m][n] = reset[m] ? 0 : v
-  float* __restrict__ out; const uint8_t* __restrict__ reset; int ld;
-  __device__ void store(int m, int n, float v, int) const {
-    out[(int64_t)m * ld + n] = reset[m] ? 0.f : v;
-  }
-};
-
 #define ARL_TRY(x) do { hipError_t _e = (x); if (_e != hipSuccess) return _e; } while (0)
 
-// ---------------------------------------------------------------- elementwise
-__device__ inline float sigm(float x) { return __fdiv_rn(1.f, __fadd_rn(1.f, expf(-x))); }
-
-// Chainer F.lstm forward: a,i,f,o interleaved per unit (reshape(n, 256, 4))
-__global__ void lstm_cell_fwd_kernel(const float* __restrict__ gates, const float* __restrict__ c_prev,
-                                     const uint8_t* __restrict__ reset, float* __restrict__ c_out,
-                                     float* __restrict__ h_out, int64_t count) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // (m, j)
-  if (i >= count) return;
-  const int64_t m = i / HID;
-  const float4 g = reinterpret_cast<const float4*>(gates)[i];
-  const float a = tanhf(g.x), ig = sigm(g.y), fg = sigm(g.z), og = sigm(g.w);
-  const float cp = reset[m] ? 0.f : c_prev[i];
-  const float c = __fadd_rn(__fmul_rn(a, ig), __fmul_rn(fg, cp));
-  c_out[i] = c;
-  h_out[i] = __fmul_rn(og, tanhf(c));
-}
-
-// The LSTM gate GEMM's epilogue with the cell fused in (one launch per step):
-// the gate tile (BM rows x BN interleaved gate columns = BN / 4 units) gets the
-// bias, is written out (the backward reads it), and each (row, unit) runs
-// lstm_cell_fwd_kernel's arithmetic -- the same operations on the same values
-// (bit-identical).
-struct EpiLstmCell {
-  static constexpr bool kTile = true;
-  float* __restrict__ gates; const float* __restrict__ b; const float* __restrict__ c_prev;
-  const uint8_t* __restrict__ reset; float* __restrict__ c_out; float* __restrict__ h_out;
-  template <int BM, int BN, int NTH>
-  __device__ void tile(const float* T, int m0, int n0, int M, int) const {
-    for (int it = threadIdx.x; it < BM * (BN / 4); it += NTH) {
-      const int ml = it / (BN / 4), u = it - ml * (BN / 4), m = m0 + ml, n = n0 + 4 * u;
-      if (m >= M) continue;
-      const float4 bb = *reinterpret_cast<const float4*>(b + n);
-      const float4 v = *reinterpret_cast<const float4*>(T + ml * BN + 4 * u);
-      const float4 g = make_float4(__fadd_rn(v.x, bb.x), __fadd_rn(v.y, bb.y), __fadd_rn(v.z, bb.z),
-                                   __fadd_rn(v.w, bb.w));
-      *reinterpret_cast<float4*>(gates + (int64_t)m * GATES + n) = g;
-      const int64_t i = (int64_t)m * HID + (n >> 2);
-      const float a = tanhf(g.x), ig = sigm(g.y), fg = sigm(g.z), og = sigm(g.w);
-      const float cp = reset[m] ? 0.f : c_prev[i];
-      const float c = __fadd_rn(__fmul_rn(a, ig), __fmul_rn(fg, cp));
-      c_out[i] = c;
-      h_out[i] = __fmul_rn(og, tanhf(c));
-    }
-  }
-};
-
-// ARL_LSTM_SPLIT=1: the LSTM cell as its own launches (forward: after the gate
-// GEMM; backward: after the BPTT reduce) -- A/B timing only
-static const bool LSTM_SPLIT = [] {
-  const char* e = getenv("ARL_LSTM_SPLIT");
-  return e != nullptr && e[0] == '1';
-}();
-
-// ARL_LSTM_GEMM=generic: the round-2 gate GEMM (generic gather template, EpiLstmCell) instead of
-// lstm_gates_kernel (lstm.hip) -- A/B timing only
-// ARL_LSTM_BPTT=generic: the BPTT step as the split-K GEMM + reduce/cell
-// launches (the A/B arm for lstm.hip's fused lstm_bptt_kernel)
-static const bool LSTM_BPTT_GENERIC = [] {
-  const char* e = getenv("ARL_LSTM_BPTT");
-  return e != nullptr && e[0] == 'g';
-}();
-static const bool LSTM_GEMM_GENERIC = [] {
-  const char* e = getenv("ARL_LSTM_GEMM");
-  return e != nullptr && e[0] == 'g';
-}();
 // Where the LSTM step's FC split-K partials are reduced: in the gate kernel's staging (XRED) for
 // launches under 512 envs, by the FC's last-arriver ticket for 512 and more (fc_fwd_big_kernel's
 // tail; the gate kernel then stages hfc: every one of its 16 column-tile workgroups of a row block
 // otherwise re-reads the block's 8 partial slabs -- C3 1.185 -> 1.160 ms, profiles/r03/r3aa).
-// ARL_LSTM_XRED=1 / 0 forces one form (A/B timing).
+// ARL_LSTM_XRED=1 / 0 forces one form (the bitwise arm of test_lstm_fc_ticket_big_tiles_identical).
 static const int LSTM_XRED_ENV = [] {
   const char* e = getenv("ARL_LSTM_XRED");
   return e == nullptr ? -1 : (e[0] != '0' ? 1 : 0);
 }();
-static bool lstm_xred(int launch_envs) {
-  if (LSTM_GEMM_GENERIC) return false;
-  return LSTM_XRED_ENV >= 0 ? LSTM_XRED_ENV == 1 : launch_envs < 512;
-}
-// ARL_LSTM_WGRAD=gemm: the gate weight gradients + dfc as the round-2 generic dual GEMM into the LSTM
-// slab (+ the LEARN_GATES_REDUCE reduce) instead of fc_bwd.hip's ShapeLSTM kernel -- A/B timing only
-static const bool LSTM_WGRAD_GEMM = [] {
-  const char* e = getenv("ARL_LSTM_WGRAD");
-  return e != nullptr && e[0] == 'g';
-}();
+static bool lstm_xred(int launch_envs) { return LSTM_XRED_ENV >= 0 ? LSTM_XRED_ENV == 1 : launch_envs < 512; }
 
-// gates = [x | h] [Wu ; Wl]^T + b, then the cell: c_out, h_out (rows [0, n))
-template <class AOp, class BOp>
-static hipError_t lstm_gates_cell(const AOp& A, const BOp& B, const float* bias, float* gates, const float* c_prev,
-                                  const uint8_t* reset, float* c_out, float* h_out, int n, hipStream_t s) {
-  if (!LSTM_GEMM_GENERIC) {   // lstm.hip: LDS-DMA staged tile, the cell in the epilogue (or its own launch)
-    ARL_TRY(launch_lstm_gates(A.x, A.h, A.reset, B.wu, B.wl, bias, gates, c_prev, c_out, h_out, n, !LSTM_SPLIT, s));
-    if (!LSTM_SPLIT) return hipSuccess;
-    const int64_t cnt = (int64_t)n * HID;
-    hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, gates, c_prev,
-                       reset, c_out, h_out, cnt);
-    return hipGetLastError();
-  }
-  if (!LSTM_SPLIT)
-    return launch_gemm<32, 64, 32, 2, 2, GK, GK>(A, B, EpiLstmCell{gates, bias, c_prev, reset, c_out, h_out}, n, GATES,
-                                                 2 * HID, 1, s);
-  const hipError_t e = launch_gemm<32, 64, 32, 2, 2, GK, GK>(A, B, EpiBias{gates, bias, GATES}, n, GATES, 2 * HID, 1, s);
-  if (e != hipSuccess) return e;
-  const int64_t cnt = (int64_t)n * HID;
-  hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, gates, c_prev, reset,
-                     c_out, h_out, cnt);
-  return hipGetLastError();
-}
+// ---------------------------------------------------------------- elementwise
+__device__ inline float sigm(float x) { return __fdiv_rn(1.f, __fadd_rn(1.f, expf(-x))); }
 
 // F.lstm backward of element i = (m, unit) at step t: dh = dL/dh_t (heads +
 // carried), dcn in: dc carried from t+1 (first: none), out: dc carried to t-1.
@@ -266,24 +97,6 @@ __global__ void lstm_cell_bwd_kernel(const float* __restrict__ gates, const floa
   const int64_t m = i / HID;
   const float dh = first ? dH[i] : __fadd_rn(dH[i], dhn[i]);
   lstm_cell_bwd_elem(gates, c_t, c_prev, reset[m] != 0, dh, dcn, dG, first != 0, i);
-}
-
-// The BPTT split-K reduce of step t (dh_{t-1} = (dG_t Wl) * (no reset at t),
-// reduce_grad_kernel + MapResetMask) fused with the cell backward of step t-1:
-// the carried dh never leaves registers.  Same f64 sum order as
-// reduce_grad_kernel for splits <= 4 (((s0 + s1) + s2) + s3), bit-identical.
-__global__ void lstm_dh_cell_bwd_kernel(const float* __restrict__ slab, int splits, const uint8_t* __restrict__ reset_t,
-                                        const float* __restrict__ gates, const float* __restrict__ c_t,
-                                        const float* __restrict__ c_prev, const uint8_t* __restrict__ reset,
-                                        const float* __restrict__ dH, float* __restrict__ dcn, float* __restrict__ dG,
-                                        int64_t count) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= count) return;
-  const int64_t m = i / HID;
-  double v = 0.0;
-  for (int z = 0; z < splits; ++z) v += (double)slab[(int64_t)z * count + i];
-  const float dhn = reset_t[m] ? 0.f : (float)v;
-  lstm_cell_bwd_elem(gates, c_t, c_prev, reset[m] != 0, __fadd_rn(dH[i], dhn), dcn, dG, false, i);
 }
 
 // dh[s][j] = sum_k dlogits[s][k] Wpi[k][j] + dv[s] Wv[j]; with mask: * (h > 0)
@@ -320,20 +133,6 @@ __global__ void advance_kernel(int64_t* ctl, int T, uint8_t* reset, int n, float
     ctl[CTL_STEP] += T;
     ctl[CTL_WINDOW] += 1;
   }
-}
-
-// ---------------------------------------------------------------- planning
-struct Plans {   // effective split counts (launch_gemm may shrink a request)
-  int heads_w, fc_w, lstm_w;
-};
-
-static Plans make_plans(const Net& net) {
-  const int S = net.T * net.N;
-  Plans p;
-  p.heads_w = effective_splits<32>(S, plan_splits(ceil_div(net.A + 1, 16) * ceil_div(HID + 1, 64), S, 32));
-  p.fc_w = effective_splits<32>(S, plan_splits(ceil_div(HID, 64) * ceil_div(A2 + 1, 64), S, 32));
-  p.lstm_w = effective_splits<32>(S, plan_splits(ceil_div(GATES, 64) * ceil_div(2 * HID + 1, 64), S, 32));
-  return p;
 }
 
 static int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
@@ -414,12 +213,9 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   // ---- workspace
   const int64_t n = n_envs, T = t_max, T1 = T + 1, S = T * n, A = n_actions;
   net.norm_blocks = 256;
-  Plans pl = make_plans(net);
   int64_t slab = 0;
   slab = std::max(slab, (int64_t)FC_SPLIT * n * HID);
-  slab = std::max(slab, (int64_t)pl.fc_w * HID * (A2 + 1));   // run_stage("fc_bwd") timing uses the main slab
   slab = std::max(slab, conv_bwd_slab_floats((int)S));
-  if (arch == ARCH_LSTM) slab = std::max(slab, (int64_t)BPTT_SPLIT * HID * n);
   if (NAT) slab = nature_slab_floats(net);
   if (sts) slab = std::max(slab, states_slab_floats(net));
   net.slab_floats = slab;
@@ -466,11 +262,6 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   net.w_da1 = buf("da1", NAT ? S * NA1 * 4 : sts ? S * A1 * 4 : 0);
   net.w_da3 = buf("da3", NAT ? S * NA3 * 4 : 0);
   net.w_slab = buf("slab", slab * 4);
-  if (!NAT) {   // per-job weight-gradient slabs of the NIPS learner
-    net.w_slab_heads = buf("slab_heads", (int64_t)pl.heads_w * (A + 1) * (HID + 1) * 4);
-    net.w_slab_fc = buf("slab_fc", (int64_t)pl.fc_w * HID * (A2 + 1) * 4);
-    net.w_slab_lstm = buf("slab_lstm", L ? (int64_t)pl.lstm_w * GATES * (2 * HID + 1) * 4 : 0);
-  }
   net.w_norm = buf("norm_partials", (int64_t)NORM_SCRATCH * 8);   // partials, result, ticket (arl_internal.hpp)
   net.w_tick = buf("tickets", (int64_t)fc_fwd_tiles((int)n) * 4);
   net.w_fcb_part = buf("fc_bwd_partials", NAT ? 0 : fc_bwd_part_floats((int)S) * 4);
@@ -517,7 +308,7 @@ static PolicyArgs slot_policy_args(const Net& net, int t, int mode) {
 // of window slot t.  Disjoint env ranges touch disjoint rows of every buffer
 // (the FC split-K slab and tickets included: e0 is a multiple of the FC's
 // 32-row tile), so ranges can run concurrently on separate streams.
-hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne, const RingArgs* obs) {
+hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne) {
   if (ne < 0) {
     e0 = 0;
     ne = net.N;
@@ -537,13 +328,7 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne, con
   float* a2 = net.at<float>(net.w_a2) + (int64_t)t * n * A2;
   float* hfc = net.at<float>(net.w_hfc) + ((int64_t)t * n + e0) * HID;
   const float* P = net.p;
-  if (obs != nullptr) {
-    if (net.layout != FRAMES_RING || (part & ACT_AFTER_CONV) || obs->e0 != e0 || obs->ne != ne)
-      return hipErrorInvalidValue;
-    ARL_TRY(launch_phi_conv_fwd(*obs, P + net.o_c1W, P + net.o_c1b, P + net.o_c2W, P + net.o_c2b, a1_bwd, a2, s,
-                                mask_bwd));
-    ARL_TRY(stamp(net, STAGE_CONV_FWD, s));
-  } else if (!(part & ACT_AFTER_CONV) && net.states) {
+  if (!(part & ACT_AFTER_CONV) && net.states) {
     if (e0 != 0 || ne != n) return hipErrorInvalidValue;   // one launch over all envs
     ARL_TRY(states_conv_fwd(net, t, a1, a2, s));
     ARL_TRY(stamp(net, STAGE_CONV_FWD, s));
@@ -556,69 +341,33 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne, con
   if (part & ACT_CONV_ONLY) return hipSuccess;
   const int64_t o = (int64_t)t * n + e0;
   float* fc_slab = net.at<float>(net.w_slab) + (int64_t)FC_SPLIT * e0 * HID;
+  const PolicyArgs pa = make_policy_args(P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
+                                         net.at<int64_t>(net.w_ctl), t, net.env_offset + e0, t < net.T ? mode : 0,
+                                         net.at<float>(net.w_logits) + o * A, net.at<float>(net.w_probs) + o * A,
+                                         net.at<float>(net.w_logp) + o * A, net.at<float>(net.w_v) + o,
+                                         net.at<float>(net.w_ent) + o, net.at<int32_t>(net.w_act) + o,
+                                         net.at<float>(net.w_logpa) + o);
   if (net.arch != ARCH_LSTM) {   // FF: split-K partials, reduce + relu + heads in one policy_fc launch
-    const PolicyArgs pa = make_policy_args(P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
-                                           net.at<int64_t>(net.w_ctl), t, net.env_offset + e0, t < net.T ? mode : 0,
-                                           net.at<float>(net.w_logits) + o * A, net.at<float>(net.w_probs) + o * A,
-                                           net.at<float>(net.w_logp) + o * A, net.at<float>(net.w_v) + o,
-                                           net.at<float>(net.w_ent) + o, net.at<int32_t>(net.w_act) + o,
-                                           net.at<float>(net.w_logpa) + o);
-    if (fc_fwd_heads(ne)) {   // ... or all of it in the FC launch's ticket tails
-      ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab,
-                            net.at<int>(net.w_tick) + fc_fwd_tiles(e0), hfc, s, &pa));
-      return stamp(net, STAGE_FC_FWD, s);
-    }
     ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab, nullptr, nullptr, s));
     ARL_TRY(stamp(net, STAGE_FC_FWD, s));
     ARL_TRY(launch_policy_fc(fc_slab, ne, P + net.o_fcb, hfc, pa, s));
     return stamp(net, STAGE_POLICY, s);
   }
-  // LSTM: the FC's split-K partials only, their reduce + bias + relu in the gate kernel's
-  // staging (lstm.hip XRED) or the FC's ticket reduce (lstm_xred)
+  // LSTM: the FC's split-K partials, reduced + bias + relu either in the gate kernel's staging (XRED) or
+  // by the FC's last-arriver ticket (lstm_xred); then the gates with the cell in their epilogue
   const bool xred = lstm_xred(ne);
   ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab,
                         xred ? nullptr : net.at<int>(net.w_tick) + fc_fwd_tiles(e0), xred ? nullptr : hfc, s));
   ARL_TRY(stamp(net, STAGE_FC_FWD, s));
-  const float* hpol = hfc;
-  if (xred) {
-    const int64_t r0 = (int64_t)t * n + e0;
-    const float* hprev = net.at<float>(net.w_hbuf) + r0 * HID;
-    float* hout = net.at<float>(net.w_hbuf) + (r0 + n) * HID;
-    float* cout = net.at<float>(net.w_cbuf) + (r0 + n) * HID;
-    const uint8_t* rs = net.at<uint8_t>(net.w_reset) + r0;
-    float* gates = net.at<float>(net.w_gates) + r0 * GATES;
-    const float* cprev = net.at<float>(net.w_cbuf) + r0 * HID;
-    ARL_TRY(launch_lstm_gates(nullptr, hprev, rs, P + net.o_luW, P + net.o_llW, P + net.o_lub, gates, cprev, cout,
-                              hout, ne, !LSTM_SPLIT, s, fc_slab, P + net.o_fcb, hfc));
-    ARL_TRY(stamp(net, STAGE_LSTM_GATES, s));
-    if (LSTM_SPLIT) {
-      const int64_t cnt = (int64_t)ne * HID;
-      hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, gates, cprev,
-                         rs, cout, hout, cnt);
-      ARL_TRY(hipGetLastError());
-      ARL_TRY(stamp(net, STAGE_LSTM_CELL, s));
-    }
-    hpol = hout;
-  } else if (net.arch == ARCH_LSTM) {
-    const int64_t r0 = (int64_t)t * n + e0;
-    float* gates = net.at<float>(net.w_gates) + r0 * GATES;
-    const float* hprev = net.at<float>(net.w_hbuf) + r0 * HID;
-    const float* cprev = net.at<float>(net.w_cbuf) + r0 * HID;
-    float* hout = net.at<float>(net.w_hbuf) + (r0 + n) * HID;
-    float* cout = net.at<float>(net.w_cbuf) + (r0 + n) * HID;
-    const uint8_t* rs = net.at<uint8_t>(net.w_reset) + r0;
-    // gates = [x | h] [Wu ; Wl]^T + b (split-K 2 + a bias reduce measured slower: 28.5 vs 27.7 us)
-    // the cell runs in the GEMM's epilogue (EpiLstmCell; ARL_LSTM_SPLIT=1: a separate launch)
-    ARL_TRY(lstm_gates_cell(LstmGateA{hfc, hprev, rs}, LstmGateB{P + net.o_luW, P + net.o_llW}, P + net.o_lub, gates,
-                            cprev, rs, cout, hout, ne, s));
-    ARL_TRY(stamp(net, STAGE_LSTM_GATES, s));
-    hpol = hout;
-  }
-  ARL_TRY(launch_policy(hpol, ne, P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
-                        net.at<int64_t>(net.w_ctl), t, net.env_offset + e0, t < net.T ? mode : 0,
-                        net.at<float>(net.w_logits) + o * A, net.at<float>(net.w_probs) + o * A,
-                        net.at<float>(net.w_logp) + o * A, net.at<float>(net.w_v) + o, net.at<float>(net.w_ent) + o,
-                        net.at<int32_t>(net.w_act) + o, net.at<float>(net.w_logpa) + o, s));
+  const int64_t r0 = (int64_t)t * n + e0;
+  float* hout = net.at<float>(net.w_hbuf) + (r0 + n) * HID;
+  ARL_TRY(launch_lstm_gates(xred ? nullptr : hfc, net.at<float>(net.w_hbuf) + r0 * HID,
+                            net.at<uint8_t>(net.w_reset) + r0, P + net.o_luW, P + net.o_llW, P + net.o_lub,
+                            net.at<float>(net.w_gates) + r0 * GATES, net.at<float>(net.w_cbuf) + r0 * HID,
+                            net.at<float>(net.w_cbuf) + (r0 + n) * HID, hout, ne, true, s, xred ? fc_slab : nullptr,
+                            xred ? P + net.o_fcb : nullptr, xred ? hfc : nullptr));
+  ARL_TRY(stamp(net, STAGE_LSTM_GATES, s));
+  ARL_TRY(launch_policy_args(hout, ne, pa, s, HID));
   return stamp(net, STAGE_POLICY, s);
 }
 
@@ -665,8 +414,7 @@ hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_
     float* hn = net.at<float>(net.w_eval_hn);
     float* cn = net.at<float>(net.w_eval_cn);
     uint8_t* rs = net.at<uint8_t>(net.w_eval_reset);
-    ARL_TRY(lstm_gates_cell(LstmGateA{hfc, eh, rs}, LstmGateB{P + net.o_luW, P + net.o_llW}, P + net.o_lub, gates, ec,
-                            rs, cn, hn, n, s));
+    ARL_TRY(launch_lstm_gates(hfc, eh, rs, P + net.o_luW, P + net.o_llW, P + net.o_lub, gates, ec, cn, hn, n, true, s));
     const int64_t cnt = (int64_t)n * HID;
     if (!keep) {
       ARL_TRY(hipMemcpyAsync(eh, hn, cnt * 4, hipMemcpyDeviceToDevice, s));
@@ -691,8 +439,7 @@ hipError_t net_reset_state(Net& net, int e0, int n, hipStream_t s) {
 // before the conv slab reduce
 static NormFold norm_fold_args(const Net& net) {
   if (!net.norm_fold) return NormFold{};
-  return NormFold{net.at<double>(net.w_norm), net.g, net.o_fcW, net.param_floats, net.norm_rest_blocks,
-                  norm_ticket() ? 1 : 0};
+  return NormFold{net.at<double>(net.w_norm), net.g, net.o_fcW, net.param_floats, net.norm_rest_blocks};
 }
 
 // the fused conv backward (per-sample slabs) and its slab reduce (with the folded clip norm's
@@ -725,101 +472,60 @@ hipError_t net_learn(Net& net, double gamma, float beta, float vcoef, int clip_r
   return hipSuccess;
 }
 
-// One part of the NIPS learner (LEARN_* in arl_internal.hpp).  Parts run in
-// order on one stream give net_learn; LEARN_HEADS_DW may run on a second
-// stream once LEARN_RETURNS is done, and LEARN_GATES_REDUCE / LEARN_FC_REDUCE
-// once LEARN_TRUNK is done, concurrently with the rest: nothing on the
-// critical path (dh -> FC -> conv backward) reads what they write.
-// LSTM gate weight gradients ([x | h | 1] operand, reset rows' h dropped) into
-// the LSTM slab and dfc = (dG Wu) * (hfc > 0), one dual-GEMM launch
+// LSTM gate weight gradients ([x | h_prev] operand, reset rows' h dropped) straight into the gradient
+// and dfc = (dG Wu) * (hfc > 0), one launch (fc_bwd.hip's ShapeLSTM)
 static hipError_t lstm_wgrad(Net& net, hipStream_t s) {
-  const int n = net.N, S = net.T * n;
-  const Plans pl = make_plans(net);
-  const float* dG = net.at<float>(net.w_dG);
-  const float* hfc = net.at<float>(net.w_hfc);
-  if (!LSTM_WGRAD_GEMM)   // straight into the gradient (no slab, no LEARN_GATES_REDUCE)
-    return launch_lstm_wgrad(dG, hfc, net.at<float>(net.w_hbuf), net.at<uint8_t>(net.w_reset),
-                             net.at<float>(net.w_zero), net.p + net.o_luW, S, net.g + net.o_luW, net.g + net.o_llW,
-                             net.g + net.o_lub, net.at<float>(net.w_dfc), net.at<float>(net.w_fcb_part),
-                             net.at<int>(net.w_fcb_tick), s);
-  return launch_gemm2<64, 64, 32, 2, 2, GM, GM, GK, GM>(
-      gemm_job<64, 32>(ColMajor{dG, GATES}, LstmWB{hfc, net.at<float>(net.w_hbuf), net.at<uint8_t>(net.w_reset)},
-                       EpiSlab{net.at<float>(net.w_slab_lstm), GATES, 2 * HID + 1}, GATES, 2 * HID + 1, S, pl.lstm_w,
-                       64),
-      gemm_job<64, 32>(RowMajor{dG, GATES}, RowMajor{net.p + net.o_luW, HID}, EpiMask{net.at<float>(net.w_dfc), hfc, HID},
-                       S, HID, GATES, 1, 64),
-      s);
+  const int S = net.T * net.N;
+  return launch_lstm_wgrad(net.at<float>(net.w_dG), net.at<float>(net.w_hfc), net.at<float>(net.w_hbuf),
+                           net.at<uint8_t>(net.w_reset), net.at<float>(net.w_zero), net.p + net.o_luW, S,
+                           net.g + net.o_luW, net.g + net.o_llW, net.g + net.o_lub, net.at<float>(net.w_dfc),
+                           net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s);
 }
 
+// the heads' weight gradients ride on the FC backward launch (its job C)
+static HeadsDW heads_dw(const Net& net) {
+  const float* hh = net.arch == ARCH_LSTM ? net.at<float>(net.w_hbuf) + (int64_t)net.N * HID : net.at<float>(net.w_hfc);
+  return HeadsDW{net.at<float>(net.w_dlogits), net.at<float>(net.w_dv), hh, net.A, net.g + net.o_piW,
+                 net.g + net.o_pib, net.g + net.o_vW, net.g + net.o_vb};
+}
+
+static hipError_t fc_backward(Net& net, hipStream_t s) {
+  const HeadsDW heads = heads_dw(net);
+  return launch_fc_bwd(net.at<float>(net.w_dfc), net.at<float>(net.w_a2), net.p + net.o_fcW, net.T * net.N,
+                       net.g + net.o_fcW, net.g + net.o_fcb, net.at<float>(net.w_da2), net.at<float>(net.w_fcb_part),
+                       net.at<int>(net.w_fcb_tick), s, &heads, a2_mask(net, 0));
+}
+
+// One part of the NIPS learner (LEARN_* in arl_internal.hpp), in order on one stream
 hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s) {
   if (net.arch == ARCH_FF_NATURE) return hipErrorInvalidValue;
-  if (part == LEARN_RETURNS) net.norm_ready = false;   // a new gradient: no folded norm until net_learn's reduce
-  const int n = net.N, T = net.T, A = net.A, S = T * n;
+  const int n = net.N, T = net.T, A = net.A;
   const float* P = net.p;
-  float* G = net.g;
-  float* slab = net.at<float>(net.w_slab);
-  float* slab_h = net.at<float>(net.w_slab_heads);
-  float* slab_f = net.at<float>(net.w_slab_fc);
-  const Plans pl = make_plans(net);
-  float* dl = net.at<float>(net.w_dlogits);
-  float* dv = net.at<float>(net.w_dv);
   const bool L = net.arch == ARCH_LSTM;
-  const float* hfc = net.at<float>(net.w_hfc);
-  const float* hheads = L ? net.at<float>(net.w_hbuf) + (int64_t)n * HID : hfc;   // h fed to pi / v
-  float* dfc = net.at<float>(net.w_dfc);
-  // 1. n-step returns + loss gradient wrt logits / v (a3c.py:82-126); also
-  //    snapshots the step counter for the optimizer's fused advance
-  //    and, in the same launch, the heads' backward dh (FF: dfc = dh * (hfc > 0))
-  if (part == LEARN_RETURNS && RETURNS_SPLIT) {
-    ARL_TRY(launch_returns(net.at<float>(net.w_rewards), net.at<uint8_t>(net.w_dones), net.at<float>(net.w_v),
-                           net.at<float>(net.w_probs), net.at<float>(net.w_logp), net.at<int32_t>(net.w_act), T, n, A,
-                           gamma, beta, vcoef, clip_reward, dl, dv, net.at<float>(net.w_loss), s,
-                           net.at<int64_t>(net.w_ctl), net.pi_coef, net.keep_scale));
-    ARL_TRY(launch_heads_bwd(dl, dv, P + net.o_piW, P + net.o_vW, A, HID, L ? nullptr : hfc,
-                             L ? net.at<float>(net.w_dh) : dfc, S, s));
-    return stamp(net, STAGE_RETURNS, s);
-  }
   if (part == LEARN_RETURNS) {
+    // n-step returns + loss gradient wrt logits / v (a3c.py:82-126); also snapshots the step counter for
+    // the optimizer's fused advance and, in the same launch, the heads' backward dh (FF: dfc = dh * (hfc > 0))
+    net.norm_ready = false;   // a new gradient: no folded norm until net_learn's reduce
     ARL_TRY(launch_returns_heads(net.at<float>(net.w_rewards), net.at<uint8_t>(net.w_dones), net.at<float>(net.w_v),
                                  net.at<float>(net.w_probs), net.at<float>(net.w_logp), net.at<int32_t>(net.w_act), T,
-                                 n, A, gamma, beta, vcoef, clip_reward, dl, dv, net.at<float>(net.w_loss), s,
-                                 net.at<int64_t>(net.w_ctl), net.pi_coef, net.keep_scale, P + net.o_piW, P + net.o_vW,
-                                 L ? nullptr : hfc, L ? net.at<float>(net.w_dh) : dfc));
+                                 n, A, gamma, beta, vcoef, clip_reward, net.at<float>(net.w_dlogits),
+                                 net.at<float>(net.w_dv), net.at<float>(net.w_loss), s, net.at<int64_t>(net.w_ctl),
+                                 net.pi_coef, net.keep_scale, P + net.o_piW, P + net.o_vW,
+                                 L ? nullptr : net.at<float>(net.w_hfc),
+                                 L ? net.at<float>(net.w_dh) : net.at<float>(net.w_dfc)));
     return stamp(net, STAGE_RETURNS, s);
   }
-  // heads: weight grads (ones column = bias) and dh.  With the fused FC
-  // backward the weight grads are its job C (LEARN_TRUNK): nothing here.
-  const HeadsDW heads{dl, dv, hheads, A, G + net.o_piW, G + net.o_pib, G + net.o_vW, G + net.o_vb};
-  if (part == LEARN_HEADS_DW) {
-    if (!FC_BWD_GEMM) return hipSuccess;
-    ARL_TRY((launch_gemm<16, 64, 32, 1, 4, GS, GM>(HeadsGA{dl, dv, A}, OnesColB{hheads, HID},
-                                                   EpiSlab{slab_h, A + 1, HID + 1}, A + 1, HID + 1, S, pl.heads_w,
-                                                   s)));
-    return launch_reduce_grad(slab_h, pl.heads_w, A + 1, HID + 1,
-                              MapHeads{G, net.o_piW, net.o_pib, net.o_vW, net.o_vb, A, HID}, s);
-  }
-  float* slab_l = net.at<float>(net.w_slab_lstm);
-  if (part == LEARN_GATES_REDUCE)
-    return (L && LSTM_WGRAD_GEMM) ? launch_reduce_grad(slab_l, pl.lstm_w, GATES, 2 * HID + 1,
-                                  MapLstmW{G, net.o_luW, net.o_llW, net.o_lub}, s)
-             : hipSuccess;
-  if (part == LEARN_FC_REDUCE)   // the FC weight gradient is written by fc_bwd_kernel (LEARN_TRUNK)
-    return FC_BWD_GEMM ? launch_reduce_grad(slab_f, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s)
-                       : hipSuccess;
-  const float* a2 = net.at<float>(net.w_a2);
-  float* da2 = net.at<float>(net.w_da2);
-  if (part == LEARN_CONV && net.states) {
-    ARL_TRY(states_conv_bwd(net, s));
-    return stamp(net, STAGE_CONV_BWD, s);
-  }
-  if (part == LEARN_CONV)
-    // fused conv backward per sample (conv_bwd.hip): conv2 dW/db,
-    // da1 = conv_transpose(da2, W2) * (a1 > 0) kept in LDS, conv1 dW/db
-    // straight from the frame ring; then its slab reduce
+  if (part == LEARN_CONV) {
+    if (net.states) {
+      ARL_TRY(states_conv_bwd(net, s));
+      return stamp(net, STAGE_CONV_BWD, s);
+    }
+    // fused conv backward per sample (conv_bwd.hip): conv2 dW/db, da1 = conv_transpose(da2, W2) * (a1 > 0)
+    // kept in LDS, conv1 dW/db straight from the frame ring; then its slab reduce
     return conv_backward(net, s, NormFold{});
+  }
   if (part != LEARN_TRUNK) return hipErrorInvalidValue;
-  // (the heads' dh was written by LEARN_RETURNS)
-  // 2. LSTM: truncated BPTT over the window, gate weight gradients, dfc
+  // LSTM: truncated BPTT over the window (a3c.py:144), then the gate weight gradients and dfc
   if (L) {
     const float* gates = net.at<float>(net.w_gates);
     const float* cbuf = net.at<float>(net.w_cbuf);
@@ -829,55 +535,25 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
     float* dcn = net.at<float>(net.w_dcn);
     const float* dH = net.at<float>(net.w_dh);
     const int64_t cnt = (int64_t)n * HID;
-    // step T-1's cell, then per step t: dh_{t-1} = (dG_t Wl) * (no reset at t) as a split-K GEMM
-    // (K = 1024 split 4 ways) and its reduce fused with step t-1's cell (lstm_dh_cell_bwd_kernel)
-    const unsigned cblocks = (unsigned)((cnt + 255) / 256);
-    const int splits = effective_splits<32>(GATES, BPTT_SPLIT);
-    static_assert(BPTT_SPLIT <= 4, "lstm_dh_cell_bwd_kernel sums in reduce_grad_kernel's order for <= 4 splits");
-    for (int t = T - 1; t >= 0; --t) {
-      const int64_t o = (int64_t)t * n;
-      if (t == T - 1 || LSTM_SPLIT) {
-        hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3(cblocks), dim3(256), 0, s, gates + o * GATES,
-                           cbuf + (o + n) * HID, cbuf + o * HID, rs + o, dH + o * HID, dhn, dcn, dG + o * GATES,
-                           t == T - 1 ? 1 : 0, cnt);
-        ARL_TRY(hipGetLastError());
-        ARL_TRY(stamp(net, STAGE_LSTM_CELL, s));
-      }
-      if (t > 0 && !LSTM_BPTT_GENERIC) {   // lstm.hip: dh GEMM + mask + step t-1's cell in one launch
-        const int64_t op = o - n;
-        ARL_TRY(launch_lstm_bptt(dG + o * GATES, P + net.o_llW, rs + o, gates + op * GATES, cbuf + (op + n) * HID,
-                                 cbuf + op * HID, rs + op, dH + op * HID, dcn, dG + op * GATES, dhn, n, !LSTM_SPLIT,
-                                 s));
-        ARL_TRY(stamp(net, STAGE_LSTM_BPTT, s));
-      } else if (t > 0) {
-        ARL_TRY((launch_gemm<32, 64, 32, 2, 2, GK, GM>(RowMajor{dG + o * GATES, GATES}, RowMajor{P + net.o_llW, HID},
-                                                       EpiSlab{slab, n, HID}, n, HID, GATES, BPTT_SPLIT, s)));
-        if (LSTM_SPLIT) {
-          ARL_TRY(launch_reduce_grad(slab, splits, n, HID, MapResetMask{dhn, rs + o, HID}, s));
-        } else {
-          const int64_t op = o - n;   // step t-1
-          hipLaunchKernelGGL(lstm_dh_cell_bwd_kernel, dim3(cblocks), dim3(256), 0, s, slab, splits, rs + o,
-                             gates + op * GATES, cbuf + (op + n) * HID, cbuf + op * HID, rs + op, dH + op * HID, dcn,
-                             dG + op * GATES, cnt);
-          ARL_TRY(hipGetLastError());
-        }
-        ARL_TRY(stamp(net, STAGE_LSTM_BPTT, s));
-      }
+    // step T-1's cell, then per step t: dh_{t-1} = (dG_t Wl) * (no reset at t) and step t-1's cell in one
+    // launch (lstm.hip)
+    const int64_t oT = (int64_t)(T - 1) * n;
+    hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, gates + oT * GATES,
+                       cbuf + (oT + n) * HID, cbuf + oT * HID, rs + oT, dH + oT * HID, dhn, dcn, dG + oT * GATES, 1, cnt);
+    ARL_TRY(hipGetLastError());
+    ARL_TRY(stamp(net, STAGE_LSTM_CELL, s));
+    for (int t = T - 1; t > 0; --t) {
+      const int64_t o = (int64_t)t * n, op = o - n;
+      ARL_TRY(launch_lstm_bptt(dG + o * GATES, P + net.o_llW, rs + o, gates + op * GATES, cbuf + (op + n) * HID,
+                               cbuf + op * HID, rs + op, dH + op * HID, dcn, dG + op * GATES, dhn, n, true, s));
+      ARL_TRY(stamp(net, STAGE_LSTM_BPTT, s));
     }
-    // gate weight gradients and dfc = (dG Wu) * (hfc > 0): independent, one launch
     ARL_TRY(lstm_wgrad(net, s));
     ARL_TRY(stamp(net, STAGE_LSTM_WGRAD, s));
   }
-  // 3. FC: dW + db straight into the gradient and da2 = (dfc W) * (a2 > 0),
-  //    one launch (fc_bwd.hip)
-  if (!FC_BWD_GEMM) {
-    ARL_TRY(launch_fc_bwd(dfc, a2, P + net.o_fcW, S, G + net.o_fcW, G + net.o_fcb, net.at<float>(net.w_da2),
-                          net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s, &heads, a2_mask(net, 0)));
-    return stamp(net, STAGE_FC_BWD, s);
-  }
-  ARL_TRY((launch_gemm2_nt<64, 64, 32, 2, 4, 512, GM, GM, GK, GM>(   // 8 waves, 2 sub-tiles each (ARL_FC_BWD=gemm)
-      gemm_job<64, 32>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab_f, HID, A2 + 1}, HID, A2 + 1, S, pl.fc_w, 64),
-      gemm_job<64, 32>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2}, EpiMask{da2, a2, A2}, S, A2, HID, 1, 64), s)));
+  // FC: dW + db straight into the gradient and da2 = (dfc W) * (a2 > 0), with the heads' weight
+  // gradients, one launch (fc_bwd.hip)
+  ARL_TRY(fc_backward(net, s));
   return stamp(net, STAGE_FC_BWD, s);
 }
 
@@ -910,30 +586,10 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
       const int64_t o = (int64_t)t * n;
       if (net.arch != ARCH_LSTM)
         return launch_policy_fc(slab, n, P + net.o_fcb, hfc + o * HID, slot_policy_args(net, t, 0), s);
-      const float* h = net.arch == ARCH_LSTM ? net.at<float>(net.w_hbuf) + (o + n) * HID : hfc + o * HID;
-      const int A = net.A;
-      return launch_policy(h, n, P + net.o_piW, P + net.o_pib, P + net.o_vW, P + net.o_vb, A, net.seed,
-                           net.at<int64_t>(net.w_ctl), t, net.env_offset, 0, net.at<float>(net.w_logits) + o * A,
-                           net.at<float>(net.w_probs) + o * A, net.at<float>(net.w_logp) + o * A,
-                           net.at<float>(net.w_v) + o, net.at<float>(net.w_ent) + o, nullptr, nullptr, s);
+      return launch_policy_args(net.at<float>(net.w_hbuf) + (o + n) * HID, n, slot_policy_args(net, t, 0), s, HID);
     }
-    case STAGE_FC_BWD: {
-      if (!FC_BWD_GEMM) {   // with the heads' weight gradients (job C), as in LEARN_TRUNK
-        const float* hh = net.arch == ARCH_LSTM ? net.at<float>(net.w_hbuf) + (int64_t)n * HID : hfc;
-        const HeadsDW heads{net.at<float>(net.w_dlogits), net.at<float>(net.w_dv), hh, net.A, G + net.o_piW,
-                            G + net.o_pib, G + net.o_vW, G + net.o_vb};
-        return launch_fc_bwd(net.at<float>(net.w_dfc), a2, P + net.o_fcW, S, G + net.o_fcW, G + net.o_fcb,
-                             net.at<float>(net.w_da2), net.at<float>(net.w_fcb_part), net.at<int>(net.w_fcb_tick), s,
-                             &heads, a2_mask(net, 0));
-      }
-      const Plans pl = make_plans(net);
-      const float* dfc = net.at<float>(net.w_dfc);
-      ARL_TRY((launch_gemm<64, 64, 32, 2, 2, GM, GM>(ColMajor{dfc, HID}, OnesColB{a2, A2}, EpiSlab{slab, HID, A2 + 1},
-                                                     HID, A2 + 1, S, pl.fc_w, s)));
-      ARL_TRY(launch_reduce_grad(slab, pl.fc_w, HID, A2 + 1, MapDense{G, net.o_fcW, net.o_fcb, -1, A2}, s));
-      return launch_gemm<64, 64, 32, 2, 2, GK, GM>(RowMajor{dfc, HID}, RowMajor{P + net.o_fcW, A2},
-                                                   EpiMask{net.at<float>(net.w_da2), a2, A2}, S, A2, HID, 1, s);
-    }
+    case STAGE_FC_BWD:   // with the heads' weight gradients (job C), as in LEARN_TRUNK
+      return fc_backward(net, s);
     case STAGE_CONV_BWD:
       return launch_conv_bwd(net.at<uint8_t>(net.w_frames), net.at<uint8_t>(net.w_nvalid),
                              net.at<int64_t>(net.w_ctl), n, net.R, S, net.at<float>(net.w_a1),
@@ -972,9 +628,9 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
       if (net.arch != ARCH_LSTM) return hipErrorInvalidValue;
       return lstm_wgrad(net, s);
     case STAGE_RMSPROP:   // the update kernel as a window runs it (clip 40 from the last norm the window left), lr 0
-      return launch_rmsprop(net.p, net.ms, net.g, net.param_floats, 0.0, 0.99, 0.1,
-                            net.at<double>(net.w_norm) + (norm_ticket() ? NORM_RESULT : 0),
-                            norm_ticket() ? 0 : (net.norm_ready ? conv_norm_parts(net.norm_rest_blocks) : net.norm_blocks), 40.f, nullptr, 0, 0, net.T, s);
+      return launch_rmsprop(net.p, net.ms, net.g, net.param_floats, 0.0, 0.99, 0.1, net.at<double>(net.w_norm),
+                            net.norm_ready ? conv_norm_parts(net.norm_rest_blocks) : net.norm_blocks, 40.f, nullptr, 0,
+                            0, net.T, s);
     default:
       return hipErrorInvalidValue;
   }
@@ -997,10 +653,8 @@ hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_tot
   const AdvanceArgs adv{net.at<int64_t>(net.w_ctl), net.at<uint8_t>(net.w_reset),
                         L ? net.at<float>(net.w_hbuf) : nullptr, L ? net.at<float>(net.w_cbuf) : nullptr, net.T,
                         net.N};
-  ARL_TRY(launch_rmsprop(net.p, net.ms, net.g, net.param_floats, lr0, alpha, eps,
-                         do_clip ? parts + (norm_ticket() ? NORM_RESULT : 0) : nullptr,
-                         (do_clip && !norm_ticket()) ? (folded ? conv_norm_parts(net.norm_rest_blocks) : net.norm_blocks) : 0,
-                         clip, total_steps > 0 ? net.at<int64_t>(net.w_ctl) : nullptr, total_steps,
+  ARL_TRY(launch_rmsprop(net.p, net.ms, net.g, net.param_floats, lr0, alpha, eps, do_clip ? parts : nullptr,
+                         folded ? conv_norm_parts(net.norm_rest_blocks) : net.norm_blocks, clip, total_steps > 0 ? net.at<int64_t>(net.w_ctl) : nullptr, total_steps,
                          n_total, net.T, s, fused ? &adv : nullptr));
   ARL_TRY(stamp(net, STAGE_RMSPROP, s));
   return advance && !fused ? net_advance(net, s) : hipSuccess;

@@ -11,9 +11,9 @@
 //     reduce_conv_bwd_kernel leaves the same partials, conv_bwd.hip), so the
 //     clip rate needs no host round trip and no extra launch;
 //   rmsprop_kernel: every block sums the partials in block order (their loads
-//     in flight with its first p / ms / g loads; ARL_NORM_TICKET=1: the norm
-//     launch's last-arriving block leaves the sum in partials[NORM_RESULT]
-//     instead, norm_finish -- measured slower), then 4 parameters per thread per
+//     in flight with its first p / ms / g loads; a last-arriving block of the
+//     norm launch leaving one f64 instead measured 2-4 us slower a window, r4c),
+//     then 4 parameters per thread per
 //     iteration: g' = clip ? g*f32(rate) : g; ms = ms*alpha; ms += (c*g')*g';
 //     p -= (lr*g') / sqrt(ms + eps) -- every op an explicit round-to-nearest
 //     f32 op in the reference's order (NumPy f32 semantics, no FMA), so the
@@ -22,7 +22,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <cstdlib>
 
 #include "arl_internal.hpp"
 
@@ -42,7 +41,7 @@ __device__ inline double block_sum_f64(double x, double* sh) {
 }
 
 __global__ void __launch_bounds__(256)
-grad_sqnorm_kernel(const float* __restrict__ g, int64_t n, double* __restrict__ partials, int finish) {
+grad_sqnorm_kernel(const float* __restrict__ g, int64_t n, double* __restrict__ partials) {
   __shared__ double sh[8];
   const int64_t n4 = n >> 2;
   float acc = 0.f;
@@ -57,7 +56,7 @@ grad_sqnorm_kernel(const float* __restrict__ g, int64_t n, double* __restrict__ 
     acc = __fadd_rn(acc, __fmul_rn(v, v));
   }
   const double t = block_sum_f64((double)acc, sh);
-  norm_finish(t, blockIdx.x, gridDim.x, partials, finish != 0);
+  if (threadIdx.x == 0) partials[blockIdx.x] = t;
 }
 
 struct RmsConst {   // (AdvanceArgs is declared in arl_internal.hpp)
@@ -79,10 +78,7 @@ __device__ inline void rms1(float& p, float& ms, float g, const RmsConst& c) {
   p = __fsub_rn(p, __fdiv_rn(__fmul_rn(c.lr, g), sqrtf(__fadd_rn(ms, c.eps))));  // p -= lr*g/sqrt(ms+eps)
 }
 
-// U float4 of p / ms / g per thread and pass, every load of a pass issued before the arithmetic
-// (U = 1: the grid covers the buffer in one pass; ARL_RMS_U=2: half the workgroups, two float4 a
-// thread in flight together -- A/B knob)
-template <int U>
+// one float4 of p / ms / g per thread and pass, the first pass's loads in flight with the norm's
 __global__ void __launch_bounds__(256)
 rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __restrict__ g, int64_t n, RmsConst c,
                const double* __restrict__ norm_sq, int nparts, float clip, AdvanceArgs adv) {
@@ -99,31 +95,25 @@ rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __res
   const float4* g4 = reinterpret_cast<const float4*>(g);
   const int64_t gsz = (int64_t)gridDim.x * blockDim.x;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  // the first pass's float4 of p / ms / g are in flight with the squared norm's load
-  float4 pv[U], mv[U], gv[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int64_t i = min(i0 + u * gsz, n4 - 1);   // (clamped: a duplicate, not stored)
-    pv[u] = p4[i];
-    mv[u] = m4[i];
-    gv[u] = g4[i];
+  // the first pass's float4 of p / ms / g are in flight with the squared norm's loads (n4 == 0: none;
+  // past the end: a clamped duplicate, never stored)
+  float4 pv, mv, gv;
+  if (n4 > 0) {
+    const int64_t i = min(i0, n4 - 1);
+    pv = p4[i];
+    mv = m4[i];
+    gv = g4[i];
   }
   float scale = 1.f;
   bool do_clip = false;
-  if (norm_sq != nullptr) {
-    double t;
-    if (nparts > 0) {   // re-reduce the partials (loads in flight with the first pass's)
-      t = 0.0;
-      double v[4];
+  if (norm_sq != nullptr) {   // re-reduce the partials [0, nparts) in block order (4 loads a thread in flight)
+    double t = 0.0, v[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = norm_sq[min((int)threadIdx.x + 256 * k, nparts - 1)];
+    for (int k = 0; k < 4; ++k) v[k] = norm_sq[min((int)threadIdx.x + 256 * k, nparts - 1)];
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if ((int)threadIdx.x + 256 * k < nparts) t += v[k];
-      t = block_sum_f64(t, sh);
-    } else {
-      t = *norm_sq;
-    }
+    for (int k = 0; k < 4; ++k)
+      if ((int)threadIdx.x + 256 * k < nparts) t += v[k];
+    t = block_sum_f64(t, sh);
     const double norm = sqrt(t);
     const double rate = (double)clip / norm;
     if (norm > 0.0 && rate < 1.0) {
@@ -131,31 +121,22 @@ rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __res
       scale = (float)rate;
     }
   }
-  for (int64_t ib = i0; ib < n4; ib += U * gsz) {
+  for (int64_t ib = i0; ib < n4; ib += gsz) {
     if (ib != i0) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t i = min(ib + u * gsz, n4 - 1);
-        pv[u] = p4[i];
-        mv[u] = m4[i];
-        gv[u] = g4[i];
-      }
+      pv = p4[ib];
+      mv = m4[ib];
+      gv = g4[ib];
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (do_clip) {
-        gv[u].x = __fmul_rn(gv[u].x, scale); gv[u].y = __fmul_rn(gv[u].y, scale);
-        gv[u].z = __fmul_rn(gv[u].z, scale); gv[u].w = __fmul_rn(gv[u].w, scale);
-      }
-      rms1(pv[u].x, mv[u].x, gv[u].x, c);
-      rms1(pv[u].y, mv[u].y, gv[u].y, c);
-      rms1(pv[u].z, mv[u].z, gv[u].z, c);
-      rms1(pv[u].w, mv[u].w, gv[u].w, c);
-      if (ib + u * gsz < n4) {
-        p4[ib + u * gsz] = pv[u];
-        m4[ib + u * gsz] = mv[u];
-      }
+    if (do_clip) {
+      gv.x = __fmul_rn(gv.x, scale); gv.y = __fmul_rn(gv.y, scale);
+      gv.z = __fmul_rn(gv.z, scale); gv.w = __fmul_rn(gv.w, scale);
     }
+    rms1(pv.x, mv.x, gv.x, c);
+    rms1(pv.y, mv.y, gv.y, c);
+    rms1(pv.z, mv.z, gv.z, c);
+    rms1(pv.w, mv.w, gv.w, c);
+    p4[ib] = pv;
+    m4[ib] = mv;
   }
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
     const int64_t j = (n4 << 2) + threadIdx.x;
@@ -186,24 +167,16 @@ static int stream_blocks(int64_t n) {
   return (int)b;
 }
 
-bool norm_ticket() {
-  static const bool on = [] {   // off by default: C4 0.4983-0.5000 vs 0.5014-0.5022 ms, C2 0.3108-0.3118 vs
-    const char* e = getenv("ARL_NORM_TICKET");   // 0.3140-0.3155 (r4c): the ticket adds 3.3 us to the conv
-    return e != nullptr && e[0] == '1';          // reduce, the re-reduce costs the update 0.5 us
-  }();
-  return on;
-}
-
 hipError_t launch_grad_sqnorm(const float* g, int64_t n, double* partials, int blocks, hipStream_t s) {
-  if (blocks < 1 || blocks > 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(grad_sqnorm_kernel, dim3(blocks), dim3(256), 0, s, g, n, partials, norm_ticket() ? 1 : 0);
+  if (blocks < 1 || blocks > NORM_MAX_PARTS) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(grad_sqnorm_kernel, dim3(blocks), dim3(256), 0, s, g, n, partials);
   return hipGetLastError();
 }
 
 hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double lr, double alpha, double eps,
                           const double* norm_sq, int nparts, float clip, const int64_t* ctl,
                           int64_t total_steps, int64_t n_total, int t_max, hipStream_t s, const AdvanceArgs* adv) {
-  if (nparts > 1024) return hipErrorInvalidValue;
+  if (norm_sq != nullptr && (nparts < 1 || nparts > NORM_MAX_PARTS)) return hipErrorInvalidValue;
   if (n <= 0) return hipSuccess;
   // each Python-float hyperparameter meets the f32 arrays as f32(value)
   RmsConst c;
@@ -219,16 +192,7 @@ hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double
   c.ctl_idx = adv != nullptr ? CTL_STEP_SNAP : CTL_STEP;
   AdvanceArgs a{};
   if (adv != nullptr) a = *adv;
-  static const bool u2 = [] {
-    const char* e = getenv("ARL_RMS_U");
-    return e != nullptr && e[0] == '2';
-  }();
-  if (u2)
-    hipLaunchKernelGGL(rmsprop_kernel<2>, dim3((stream_blocks(n) + 1) / 2), dim3(256), 0, s, p, ms, g, n, c, norm_sq,
-                       nparts, clip, a);
-  else
-    hipLaunchKernelGGL(rmsprop_kernel<1>, dim3(stream_blocks(n)), dim3(256), 0, s, p, ms, g, n, c, norm_sq, nparts,
-                       clip, a);
+  hipLaunchKernelGGL(rmsprop_kernel, dim3(stream_blocks(n)), dim3(256), 0, s, p, ms, g, n, c, norm_sq, nparts, clip, a);
   return hipGetLastError();
 }
 

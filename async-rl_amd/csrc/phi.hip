@@ -20,9 +20,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <cstdlib>
-#include <type_traits>
-
 #include "arl_internal.hpp"
 #include "phi_ops.hpp"
 
@@ -39,22 +36,13 @@ struct PhiShared {
   int16_t yb0[BAND], yb1[BAND];
 };
 
-// the resized plane's store into the ring (A/B knob ARL_PHI_NTST: non-temporal)
-#ifndef ARL_PHI_NTST
-#define ARL_PHI_NTST 0
-#endif
-__device__ inline void ring_store(uint32_t* p, uint32_t v) {
-  if (ARL_PHI_NTST) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
+// the resized plane's store into the ring: an ordinary store (the next conv launch reads it; non-temporal
+// measured slower, r4r)
+__device__ inline void ring_store(uint32_t* p, uint32_t v) { *p = v; }
 
 // Computes output rows [dy0, dy0+BAND) of one env's screen into `out`
 // (row stride 84).  cur/prev: the env's two RGB frames (HWC, uint8).
-// non-temporal loads of the frame pairs (A/B knob, off: phi_ring 10.1 -> 13.0 us at C2, 19.1 -> 23.7 us
-// at 512 envs, C5 0.678 -> 0.884 ms; profiles/r03/r3x)
-#ifndef ARL_PHI_NT
-#define ARL_PHI_NT 0
-#endif
+// (non-temporal loads of the frame pairs measured slower: phi_ring 10.1 -> 13.0 us at C2, r3x)
 
 __device__ inline void phi_band(const uint8_t* __restrict__ cur, const uint8_t* __restrict__ prev,
                                 uint8_t* __restrict__ out, int dy0, int mode, PhiShared& sh) {
@@ -72,22 +60,10 @@ __device__ inline void phi_band(const uint8_t* __restrict__ cur, const uint8_t* 
     else resize_coeff(dy0 + ly, SRC_H, DST, o, b0, b1);
     int sy = o + tap;
     if (sy > SRC_H - 1) sy = SRC_H - 1;
-#if ARL_PHI_NT
-    // the frame pairs are read once a window: non-temporal loads keep them out of the caches
-    typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
-    const u32x4_* pc = reinterpret_cast<const u32x4_*>(cur + (size_t)sy * SRC_W * 3 + c * 48);
-    const u32x4_* pp = reinterpret_cast<const u32x4_*>(prev + (size_t)sy * SRC_W * 3 + c * 48);
-    u32x4_ v[6] = {__builtin_nontemporal_load(pc), __builtin_nontemporal_load(pc + 1), __builtin_nontemporal_load(pc + 2),
-                   __builtin_nontemporal_load(pp), __builtin_nontemporal_load(pp + 1), __builtin_nontemporal_load(pp + 2)};
-    c0 = make_uint4(v[0][0], v[0][1], v[0][2], v[0][3]); c1 = make_uint4(v[1][0], v[1][1], v[1][2], v[1][3]);
-    c2 = make_uint4(v[2][0], v[2][1], v[2][2], v[2][3]); p0 = make_uint4(v[3][0], v[3][1], v[3][2], v[3][3]);
-    p1 = make_uint4(v[4][0], v[4][1], v[4][2], v[4][3]); p2 = make_uint4(v[5][0], v[5][1], v[5][2], v[5][3]);
-#else
     const uint4* pc = reinterpret_cast<const uint4*>(cur + (size_t)sy * SRC_W * 3 + c * 48);
     const uint4* pp = reinterpret_cast<const uint4*>(prev + (size_t)sy * SRC_W * 3 + c * 48);
     c0 = pc[0]; c1 = pc[1]; c2 = pc[2];
     p0 = pp[0]; p1 = pp[1]; p2 = pp[2];
-#endif
   }
   if (tid < DST) {
     int o, a0, a1;
@@ -116,74 +92,6 @@ __device__ inline void phi_band(const uint8_t* __restrict__ cur, const uint8_t* 
       const int r1 = (int)sh.gray[ly][1][sx] * a0 + (int)sh.gray[ly][1][sx1] * a1;
       const int v = resize_vpass(r0, r1, b0, b1, mode);
       packed |= (uint32_t)v << (8 * j);
-    }
-    ring_store(reinterpret_cast<uint32_t*>(out + (size_t)(dy0 + ly) * DST + q * 4), packed);
-  }
-}
-
-// phi_band with the source rows staged by LDS-DMA (global_load_lds_dwordx4):
-// the band's 24 tap rows of both frames (23,040 B) land lane-linear in LDS --
-// each wave instruction a whole contiguous 1 KB, every row in flight before
-// the one wait, no VGPRs held by the loads -- then max + luminance read them
-// back (the same max_luminance16 on the same bytes: bit-identical).  A/B knob
-// ARL_PHI_DMA (see launch_phi_ring).
-constexpr int PHI_ROWB = SRC_W * 3;                 // 480 bytes per source row
-constexpr int PHI_DMA_BYTES = 2 * 2 * BAND * PHI_ROWB;   // [frame][row r = 2 ly + tap][480]: 23,040
-constexpr int PHI_DMA_CHUNKS = PHI_DMA_BYTES / 16;  // 1,440
-struct PhiDmaShared {
-  uint8_t raw[PHI_DMA_BYTES + 1024];   // + the last wave instruction's overhang
-  PhiShared sh;
-};
-
-__device__ inline void phi_band_dma(const uint8_t* __restrict__ cur, const uint8_t* __restrict__ prev,
-                                    uint8_t* __restrict__ out, int dy0, int mode, PhiDmaShared& d) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  PhiShared& sh = d.sh;
-  // chunk i -> frame f = i / 720, row r = (i % 720) / 30 (ly = r >> 1, tap = r & 1), 16-byte column c
-  constexpr int PER_FRAME = 2 * BAND * (PHI_ROWB / 16);   // 720
-  for (int it = wave; it * 64 < PHI_DMA_CHUNKS; it += 4) {
-    const int i = min(it * 64 + lane, PHI_DMA_CHUNKS - 1);   // the overhang re-reads the last chunk
-    const int f = i / PER_FRAME, rem = i - f * PER_FRAME, r = rem / 30, c = rem - r * 30;
-    int o, b0, b1;
-    if (mode & 2) resize_coeff(dy0 + (r >> 1) + CROP_TOP, SRC_H, CROP_H, o, b0, b1);
-    else resize_coeff(dy0 + (r >> 1), SRC_H, DST, o, b0, b1);
-    const int sy = min(o + (r & 1), SRC_H - 1);
-    __builtin_amdgcn_global_load_lds((f ? prev : cur) + (size_t)sy * PHI_ROWB + 16 * c,
-                                     (__attribute__((address_space(3))) void*)(d.raw + 1024 * it), 16, 0, 0);
-  }
-  if (tid < DST) {
-    int o, a0, a1;
-    resize_coeff(tid, SRC_W, DST, o, a0, a1);
-    sh.xofs[tid] = (int16_t)o; sh.xa0[tid] = (int16_t)a0; sh.xa1[tid] = (int16_t)a1;
-  } else if (tid >= 96 && tid < 96 + BAND) {
-    int o, b0, b1;
-    if (mode & 2) resize_coeff(dy0 + tid - 96 + CROP_TOP, SRC_H, CROP_H, o, b0, b1);
-    else resize_coeff(dy0 + tid - 96, SRC_H, DST, o, b0, b1);
-    sh.yofs[tid - 96] = (int16_t)o; sh.yb0[tid - 96] = (int16_t)b0; sh.yb1[tid - 96] = (int16_t)b1;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // max + luminance: task = (row r, 16-pixel chunk c) as phi_band's staging
-  if (tid < 2 * BAND * 10) {
-    const int r = tid / 10, c = tid - 10 * (tid / 10);
-    const uint4* pc = reinterpret_cast<const uint4*>(d.raw + r * PHI_ROWB + c * 48);
-    const uint4* pp = reinterpret_cast<const uint4*>(d.raw + PER_FRAME * 16 + r * PHI_ROWB + c * 48);
-    *reinterpret_cast<uint4*>(&sh.gray[r >> 1][r & 1][c * 16]) = max_luminance16(pc[0], pc[1], pc[2], pp[0], pp[1], pp[2]);
-  }
-  __syncthreads();
-  if (tid < BAND * (DST / 4)) {
-    const int ly = tid / (DST / 4), q = tid % (DST / 4);
-    const int b0 = sh.yb0[ly], b1 = sh.yb1[ly];
-    uint32_t packed = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int dx = q * 4 + j;
-      const int sx = sh.xofs[dx];
-      const int sx1 = sx + 1 < SRC_W ? sx + 1 : SRC_W - 1;
-      const int a0 = sh.xa0[dx], a1 = sh.xa1[dx];
-      const int r0 = (int)sh.gray[ly][0][sx] * a0 + (int)sh.gray[ly][0][sx1] * a1;
-      const int r1 = (int)sh.gray[ly][1][sx] * a0 + (int)sh.gray[ly][1][sx1] * a1;
-      packed |= (uint32_t)resize_vpass(r0, r1, b0, b1, mode) << (8 * j);
     }
     ring_store(reinterpret_cast<uint32_t*>(out + (size_t)(dy0 + ly) * DST + q * 4), packed);
   }
@@ -227,18 +135,16 @@ phi_stack_kernel(const uint8_t* __restrict__ pairs, const uint8_t* __restrict__ 
 // nvalid[slot][e] = reset ? 1 : min(nvalid[prev slot][e] + 1, 4).  Also
 // ingests the reward / done that arrived with this obs (a3c.py:69-70,75):
 // rewards[t-1], dones[t-1] (t >= 1) and reset_flags[t].
-template <bool DMA>
 __global__ void __launch_bounds__(256)
 phi_ring_kernel(RingArgs a) {
-  __shared__ typename std::conditional<DMA, PhiDmaShared, PhiShared>::type sh;
+  __shared__ PhiShared sh;
   const int e = a.e0 + blockIdx.y;
   const int64_t k = a.ctl[CTL_STEP] + a.t;
   const int slot = (int)(k % a.R);
   const int64_t pidx = k % a.pool_len;
   const uint8_t* pr = a.pair_pool + (pidx * a.n + e) * (int64_t)(2 * FRAME_BYTES);
   uint8_t* dst = a.frames + ((int64_t)slot * a.n + e) * PLANE;
-  if constexpr (DMA) phi_band_dma(pr, pr + FRAME_BYTES, dst, blockIdx.x * BAND, a.mode, sh);
-  else phi_band(pr, pr + FRAME_BYTES, dst, blockIdx.x * BAND, a.mode, sh);
+  phi_band(pr, pr + FRAME_BYTES, dst, blockIdx.x * BAND, a.mode, sh);
   if (blockIdx.x == 0 && threadIdx.x == 0) ring_obs_store(a, e, k, ring_obs_load(a, e, k));
 }
 
@@ -452,13 +358,7 @@ hipError_t launch_phi_stack(const uint8_t* pairs, const uint8_t* prev_stack, con
 }
 
 hipError_t launch_phi_ring(const RingArgs& a, hipStream_t s) {
-  // ARL_PHI_DMA=1: the source rows staged by LDS-DMA (phi_band_dma; A/B knob)
-  static const bool dma = [] {
-    const char* e = getenv("ARL_PHI_DMA");
-    return e != nullptr && e[0] == '1';
-  }();
-  if (dma) hipLaunchKernelGGL(phi_ring_kernel<true>, dim3(NBANDS, (unsigned)(a.ne < 0 ? a.n : a.ne)), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(phi_ring_kernel<false>, dim3(NBANDS, (unsigned)(a.ne < 0 ? a.n : a.ne)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(phi_ring_kernel, dim3(NBANDS, (unsigned)(a.ne < 0 ? a.n : a.ne)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

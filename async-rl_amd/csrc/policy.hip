@@ -58,10 +58,7 @@ hipError_t launch_policy_args(const float* h, int64_t n, const PolicyArgs& pa, h
 // PF_ROWS env rows per workgroup (1: 256 workgroups at 256 envs, each reading
 // 8 KB of partials; measured 4.33 us vs 4.57 at 2 rows, 4.62 at 4, 5.56 at 16,
 // where the reduce ran on 16 CUs)
-#ifndef ARL_PF_ROWS
-#define ARL_PF_ROWS 1
-#endif
-constexpr int PF_ROWS = ARL_PF_ROWS;
+constexpr int PF_ROWS = 1;
 __global__ void __launch_bounds__(256)
 policy_fc_kernel(const float* __restrict__ slab, int n, const float* __restrict__ fc_bias, float* __restrict__ hfc,
                  PolicyArgs pa) {
@@ -324,7 +321,7 @@ __device__ inline int rh_envs(int T) { return 1; }
 template <int AM, int RB>
 __global__ void __launch_bounds__(256)
 returns_heads_kernel(ReturnsArgs a, const float* __restrict__ Wpi, const float* __restrict__ Wv,
-                     const float* __restrict__ mask, float* __restrict__ dh, int abl) {
+                     const float* __restrict__ mask, float* __restrict__ dh) {
   __shared__ float lpi[64], lv[64];
   __shared__ float sdl[64 * (AM + 1)];
   if (a.ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) a.ctl[CTL_STEP_SNAP] = a.ctl[CTL_STEP];
@@ -365,10 +362,10 @@ returns_heads_kernel(ReturnsArgs a, const float* __restrict__ Wpi, const float* 
 #pragma unroll
   for (int k = 0; k <= AM; ++k)
     if (k <= A) w[k * HID + j] = k < A ? wc[k] : wc[AM];
-  if (on && !(abl & 2)) returns_compute(a, t, e, in, lpi[tid], lv[tid], sdl + tid * (A + 1));   // row tid = t * EB + el
+  if (on) returns_compute(a, t, e, in, lpi[tid], lv[tid], sdl + tid * (A + 1));   // row tid = t * EB + el
   __syncthreads();
   if (a.loss != nullptr && t == 0 && on) env_loss(a, lpi, lv, EB, el, e);
-  for (int r0 = 0; r0 < ((abl & 1) ? 0 : rows); r0 += RB) {
+  for (int r0 = 0; r0 < rows; r0 += RB) {
     if (r0 > 0) rows_from(r0);   // T > RB: the next RB rows
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
@@ -405,15 +402,13 @@ hipError_t launch_returns_heads(const float* rewards, const uint8_t* dones, cons
   const int EB = 1;   // rh_envs
   const ReturnsArgs ra{rewards, dones, v, probs, logp, act, T, n, A, gamma, beta, vcoef, pcoef, clip_reward,
                        keep_scale, dlogits, dv, loss, ctl_snap};
-  static const char* ab = getenv("ARL_RH_ABL");   // timing experiments only: 1 no dh, 2 no returns
   const dim3 grid((n + EB - 1) / EB), blk(256);
-  const int ablv = ab ? atoi(ab) : 0;
   if (T <= 8) {
-    if (A <= 4) hipLaunchKernelGGL((returns_heads_kernel<4, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh, ablv);
-    else if (A <= 8) hipLaunchKernelGGL((returns_heads_kernel<8, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh, ablv);
-    else hipLaunchKernelGGL((returns_heads_kernel<MAXA, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh, ablv);
+    if (A <= 4) hipLaunchKernelGGL((returns_heads_kernel<4, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh);
+    else if (A <= 8) hipLaunchKernelGGL((returns_heads_kernel<8, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh);
+    else hipLaunchKernelGGL((returns_heads_kernel<MAXA, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh);
   } else {
-    hipLaunchKernelGGL((returns_heads_kernel<MAXA, 32>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh, ablv);
+    hipLaunchKernelGGL((returns_heads_kernel<MAXA, 32>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh);
   }
   return hipGetLastError();
 }

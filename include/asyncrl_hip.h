@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define ARL_ABI_VERSION 2
+#define ARL_ABI_VERSION 3
 
 #define ARL_OK 0
 #define ARL_EINVAL 1   /* bad argument (shape, pointer, alignment) */
@@ -105,6 +105,21 @@ int arl_net_bind(arl_net* net, float* params, float* grads, float* ms, void* wor
 /* Reset the control block (step counters) and the frame ring; call once
  * before the first observation (async). */
 int arl_net_reset(arl_net* net, void* stream);
+
+/* Input pools (no reference counterpart: the reference's actors hand one frame
+ * at a time to A3C.act).  The observation calls below read entry (control-block
+ * step + t) % pool_len of caller-owned device pools, and a pointer carries no
+ * extent, so the net keeps the extent of every pool it may read: register each
+ * pool with its size in bytes before observing from it (kind ARL_POOL_FRAMES:
+ * the frame-pair / image / stack / state pool; ARL_POOL_REWARDS; ARL_POOL_DONES;
+ * up to 8 pools per kind, a later registration of the same base replaces the
+ * earlier one, bytes == 0 removes it).  An observation whose non-NULL pool is
+ * not inside a registered one, or whose pool_len entries of n_envs rows do not
+ * fit before its end, fails with ARL_EINVAL before anything is launched. */
+#define ARL_POOL_FRAMES 0
+#define ARL_POOL_REWARDS 1
+#define ARL_POOL_DONES 2
+int arl_net_set_pool(arl_net* net, int kind, const void* pool, int64_t bytes);
 
 /* Observation at window step t (0..t_max): phi of the env's frame pair into
  * the ring + stack bookkeeping + ingest of the reward/done that came with it
@@ -194,37 +209,21 @@ int arl_observe_envs(arl_net* net, int t, int e0, int ne, const uint8_t* pool, i
 #define ARL_ACT_AFTER_CONV 8
 int arl_act_envs(arl_net* net, int t, int e0, int ne, int mode, void* stream);
 
-/* arl_observe_envs + arl_act_envs of the same step in one call (frame-pair
- * nets with the NIPS head: FF, LSTM): the observation's phi, ring write and
- * bookkeeping run inside the conv launch (one workgroup per env reads its
- * frame pair, writes the new screen to the ring and convolves it from LDS),
- * so the step is one launch shorter.  Same results as the two calls
- * (ale.py:59-89 + a3c.py:154-164).  ne < 0: all envs.  mode as arl_act_envs,
- * optionally | ARL_ACT_CONV_ONLY (the rest of the step then follows with
- * arl_act_envs(.., mode | ARL_ACT_AFTER_CONV)). */
-int arl_observe_act_envs(arl_net* net, int t, int e0, int ne, const uint8_t* pair_pool, const float* reward_pool,
-                         const uint8_t* done_pool, int64_t pool_len, int force_reset, int resize_mode, int mode,
-                         void* stream);
-
 /* Window update, gradient part (a3c.py:82-130): n-step returns with R = 0 at
  * terminals, advantage / entropy / value loss gradient, backward through
  * heads, [LSTM BPTT], FC, conv2, conv1 -> grads (overwritten). */
 int arl_learn(arl_net* net, double gamma, double beta, double v_loss_coef, int clip_reward, void* stream);
 
-/* arl_learn in parts (NIPS FF / LSTM heads; not the Nature head): calling
- * parts 0..5 in order on one stream equals arl_learn.  Part 1 (heads weight
- * gradients) may run on a second stream once part 0 (returns + loss
- * gradient) is done, and parts 3 (LSTM gate reduce) and 4 (FC reduce) once
- * part 2 (heads dh, LSTM BPTT, FC dW + da2 GEMMs) is done, concurrently with
- * part 5 (conv backward); the gradient is complete when both streams are.
- * With the fused FC backward (the default) part 2's launch also writes the
- * heads weight gradients and the FC reduce, so parts 1 and 4 enqueue nothing. */
+/* arl_learn in parts (NIPS FF / LSTM heads; not the Nature head): parts 0..2
+ * in order on one stream equal arl_learn (without its folded clip norm).
+ * Part 0: returns + loss gradient + the heads' dh; part 1: LSTM BPTT and gate
+ * weight gradients, the FC backward (dW, db, da2) and the heads' weight
+ * gradients; part 2: the conv backward and its slab reduce, which write only
+ * the conv tensors [0, offset of "0/2/W") of the gradient -- everything after
+ * is final once part 1 is done (the N > 1 window all-reduces it meanwhile). */
 #define ARL_LEARN_RETURNS 0
-#define ARL_LEARN_HEADS_DW 1
-#define ARL_LEARN_TRUNK 2
-#define ARL_LEARN_GATES_REDUCE 3
-#define ARL_LEARN_FC_REDUCE 4
-#define ARL_LEARN_CONV 5
+#define ARL_LEARN_TRUNK 1
+#define ARL_LEARN_CONV 2
 int arl_learn_part(arl_net* net, int part, double gamma, double beta, double v_loss_coef, int clip_reward,
                    void* stream);
 
@@ -253,12 +252,12 @@ enum {
   ARL_STAGE_GRAD_SQNORM = 8,  /* squared-norm partials of the whole gradient (GradientClipping) */
   ARL_STAGE_LSTM_GATES = 9,   /* LSTM: the gate kernel of slot t (cell in its epilogue) */
   ARL_STAGE_LSTM_BPTT = 10,   /* LSTM: one truncated-BPTT step (dh GEMM + the previous step's cell backward) */
-  ARL_STAGE_LSTM_WGRAD = 11,  /* LSTM: the gate weight gradients + dfc (one dual-GEMM launch) */
+  ARL_STAGE_LSTM_WGRAD = 11,  /* LSTM: the gate weight gradients + dfc (one launch) */
   /* timeline-only stages (arl_stamps_*, not arl_run_stage) */
   ARL_STAGE_PHI = 12,         /* the observation (phi into the frame ring) */
   ARL_STAGE_RMSPROP = 13,     /* clip + RMSProp (+ the window advance); arl_run_stage: the update
                                  kernel alone, lr 0, clip 40 at the norm the last window left */
-  ARL_STAGE_LSTM_CELL = 14,   /* a separate LSTM cell launch */
+  ARL_STAGE_LSTM_CELL = 14,   /* the LSTM cell backward of the window's last step */
   ARL_STAGE_HOST = 15,        /* a caller's stamp (arl_stamp), e.g. after a collective */
   ARL_STAGE_OTHER = 16
 };
@@ -325,7 +324,7 @@ int arl_reset_state(arl_net* net, int64_t e0, int64_t n, void* stream);
 /* RMSpropAsync.update_one (rmsprop_async.py:23-38) on flat f32 arrays, with
  * optional Chainer GradientClipping (norm over g, scale if clip/norm < 1).
  * norm_partials: device f64[1024] scratch (needed when clip > 0): the norm
- * pass's partials, its result ([1000]) and its arrival ticket ([1001]). */
+ * pass's per-block partials. */
 int arl_rmsprop(float* param, float* ms, const float* grad, int64_t n, double lr, double alpha, double eps,
                 double clip, double* norm_partials, void* stream);
 

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round-5 GPU calls: bash scripts/gpu_r5.sh TAG step [step ...]
+#   steps: sweep (HBM copy sweep), pytest (-m gpu suite), smoke, bench (default line), prof (rocprof stats of
+#   the default bench), c3 / c2 / c5 (bench lines of the other workloads)
+# Each GPU step has its own time limit; the first failure ends the call.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+TAG=$1; shift
+O=gpurun_out/$TAG
+mkdir -p $O
+ok() { echo "== $1 rc=$2" | tee -a $O/status; [ "$2" -eq 0 ] || exit "$2"; }
+for st in "$@"; do
+  case $st in
+    sweep) timeout -k 10 120 ./scripts/copy_sweep > $O/copy_sweep.txt 2>&1; ok sweep $? ;;
+    pytest) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 240 --timeout-method thread -rf > $O/pytest.log 2>&1; ok pytest $? ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; ok smoke $? ;;
+    bench) timeout -k 10 600 python -u bench.py > $O/bench.log 2>&1; ok bench $?; tail -c 600 $O/bench.log ;;
+    prof) (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$O/prof" -o c4 -- python3 "$GRAFT_REPO_ROOT/bench.py" --cpu-seconds 0 --copy-peak 0 --secondary none > "$GRAFT_REPO_ROOT/$O/bench_prof.log" 2>&1); ok prof $? ;;
+    c2|c3|c5) timeout -k 10 400 python -u bench.py --workload $st --cpu-seconds 0 --secondary none > $O/bench_$st.log 2>&1; ok $st $? ;;
+    *) echo "unknown step $st"; exit 2 ;;
+  esac
+done
+exit 0

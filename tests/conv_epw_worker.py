@@ -2,8 +2,7 @@
 env group and saves a1, a2, the actions, the window-1 gradient and the
 parameters to an .npz (argv[1]).  test_gpu_parity.test_conv_fwd_two_envs_identical
 runs it under ARL_CONV_EPW=1 / 2 (conv_fwd.hip: one or two envs a workgroup,
-read once per process), ARL_FC_BIG, ARL_FC_HEADS and ARL_PHI_DMA (phi_ring_kernel's
-LDS-DMA staging) and compares the files bitwise."""
+read once per process), ARL_FC_BIG and ARL_WINDOW_C and compares the files bitwise."""
 import os
 import sys
 

@@ -1,10 +1,8 @@
 """Runs two LSTM windows (eager + graph-captured) and one pi_and_v call and
 saves actions, values, hidden states, gradients and parameters to an .npz
-(argv[1]); test_gpu_parity.test_lstm_fused_cell_identical runs it under
-the LSTM knobs (ARL_LSTM_SPLIT, ARL_LSTM_XRED, ARL_GROUP_ORDER) and compares
-the files bitwise.  argv[2] == "one": a single window, its gradients (flat and per tensor)
-and dfc only (test_lstm_bptt_kernel_matches_generic,
-test_lstm_wgrad_kernel_matches_gemm)."""
+(argv[1]); test_gpu_parity.test_lstm_fc_reduce_forms_identical runs it under
+ARL_LSTM_XRED and compares the files bitwise.  argv[2] == "one": a single window,
+its gradients (flat and per tensor) and dfc only."""
 import os
 import sys
 

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_errors():
     from asyncrl_amd._lib import lib
-    assert lib.arl_abi_version() == 2
+    assert lib.arl_abi_version() == 3
     h = ctypes.c_void_p()
     rc = lib.arl_net_create(ctypes.byref(h), 7, 4, 16, 5, 0, 0)
     assert rc == 1 and b"arch" in lib.arl_last_error()
@@ -153,3 +153,45 @@ def test_pool_len_checked_against_the_pools():
             check_pools(bad, pairs, rewards, None)
     with pytest.raises(ValueError):
         check_pools(8, pairs, torch.zeros(4, 2))
+
+
+def test_c_abi_rejects_pools_it_does_not_know():
+    """The C ABI itself bounds every pool read (arl_net_set_pool): with fake,
+    never-dereferenced device pointers on a bound handle, an unregistered pool
+    and a pool_len past a registered pool's end fail with ARL_EINVAL before any
+    launch -- arl_observe, arl_observe_envs and arl_run_window alike (no GPU
+    needed: the checks run on the host)."""
+    from asyncrl_amd._lib import POOL_DONES, POOL_FRAMES, POOL_REWARDS, lib
+    N, T, PAIR = 4, 5, 2 * 210 * 160 * 3
+    h = ctypes.c_void_p()
+    assert lib.arl_net_create(ctypes.byref(h), 0, 4, N, T, 0, 0) == 0
+    try:
+        fake = 1 << 40                                   # 256-byte aligned, never dereferenced
+        assert lib.arl_net_bind(h, fake, fake, fake, fake) == 0
+        pairs, rew, done = fake + (1 << 30), fake + (2 << 30), fake + (3 << 30)
+        EINVAL = 1
+        # unregistered pools
+        assert lib.arl_observe(h, 0, pairs, None, None, 8, 1, 0, None) == EINVAL
+        assert b"not registered" in lib.arl_last_error()
+        assert lib.arl_net_set_pool(h, 7, pairs, 64) == EINVAL        # unknown kind
+        assert lib.arl_net_set_pool(h, POOL_FRAMES, pairs, 8 * N * PAIR) == 0
+        assert lib.arl_net_set_pool(h, POOL_REWARDS, rew, 8 * N * 4) == 0
+        assert lib.arl_net_set_pool(h, POOL_DONES, done, 8 * N) == 0
+        # pool_len past a registered pool's end: refused, nothing launched
+        for call in (lambda L: lib.arl_observe(h, 1, pairs, rew, done, L, 0, 0, None),
+                     lambda L: lib.arl_observe_envs(h, 1, 0, N, pairs, 0, 0, rew, done, L, 0, 0, None),
+                     lambda L: lib.arl_run_window(h, pairs, rew, done, L, 1, 0, 0.99, 0.01, 0.5, 1, 7e-4, 0, 0,
+                                                  0.99, 0.1, 40.0, None)):
+            for bad in (9, 28):
+                assert call(bad) == EINVAL, bad
+                assert b"exceeds" in lib.arl_last_error()
+        # an interior pointer is checked against the room left before the pool's end
+        assert lib.arl_observe(h, 1, pairs + 4 * N * PAIR, rew, done, 5, 0, 0, None) == EINVAL
+        # a reward pool shorter than the frame pool
+        assert lib.arl_net_set_pool(h, POOL_REWARDS, rew, 4 * N * 4) == 0   # re-registered smaller
+        assert lib.arl_observe(h, 1, pairs, rew, done, 8, 0, 0, None) == EINVAL
+        assert b"reward" in lib.arl_last_error()
+        assert lib.arl_net_set_pool(h, POOL_REWARDS, rew, 0) == 0           # removed
+        assert lib.arl_observe(h, 1, pairs, rew, done, 1, 0, 0, None) == EINVAL
+    finally:
+        lib.arl_net_destroy(h)

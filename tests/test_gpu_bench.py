@@ -62,12 +62,18 @@ def test_bench_rccl_one_rank(gpu):
 
 
 def test_bench_window_timeline(gpu):
-    """The per-stage table is the window's own: sparsely stamped eager windows
-    give each stage's launches per window (phi T = 5, the forward stages T + 1,
-    the learner's launches once) and the stage shares add up to the unstamped
-    window within 5 %."""
-    r = subprocess.run([sys.executable, BENCH, "--gpus", "1"] + SMALL + ["--stamp-windows", "30"], capture_output=True,
-                       text=True, timeout=300, env=_env())
+    """The per-stage table is the window's own, and every fraction in the line
+    can fail: sparsely stamped eager windows of the default workload (C4, the
+    driver's) give each stage's launches per window (phi T = 5, the forward
+    stages T + 1, the learner's launches once); the RAW sparse shares (each
+    carries one event's cost) add up to within 8 % of the unstamped window;
+    with the measured copy peak on, no HBM stage exceeds the spec or the
+    measured peak, and no MFMA stage exceeds the ceiling of the instructions it
+    issues (frac, frac_issued <= 1)."""
+    args = ["--steps", "10", "--warmup", "3", "--cpu-seconds", "0", "--kernel-reps", "3", "--secondary", "none",
+            "--median-windows", "40", "--stamp-windows", "40"]
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "1"] + args, capture_output=True, text=True, timeout=300,
+                       env=_env())
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     d = _last_json(r.stdout)
     tl = d["timeline"]
@@ -77,17 +83,21 @@ def test_bench_window_timeline(gpu):
     share = sum(v["window_share_us"] for v in tl["stages"].values())
     assert abs(share / 1e3 - tl["sum_of_shares_ms"]) <= 0.01 * tl["sum_of_shares_ms"], tl
     assert min(v["samples"] for v in tl["stages"].values()) >= 4, tl
-    # an event between two launches exposes the dispatch of the second, which an unstamped stream
-    # overlaps with the first's tail: ~1 us a measured launch (C2 1.054 / 1.108, C4 1.065: r4f, r4g);
-    # the bench estimates it from the sum and takes it off every launch
-    assert 0.95 <= tl["sum_vs_unstamped_median"] <= 1.15, tl
-    assert 0.0 <= tl["exposure_us_per_launch"] < 2.5, tl
-    assert 0.99 <= tl["corrected_sum_vs_unstamped_median"] <= 1.01, tl
+    assert 0.97 <= tl["sum_vs_unstamped_median"] <= 1.08, tl
+    peak = d["hbm_copy_peak"]["GB/s"]
+    assert peak >= 6000, d["hbm_copy_peak"]
     for k, v in d["kernels"].items():
-        assert v["time_source"] == "window" or k not in want, (k, v)
-        if v.get("bound") == "hbm" and k in want:
-            assert v["frac"] <= 1.0 and v.get("frac_measured_peak", 0) <= 1.0, (k, v)
-    assert d["roofline"]["time_source"] == "window"
+        if k not in want:
+            continue
+        assert v["time_source"] == "window", (k, v)
+        assert v["frac"] <= 1.0 and v["standalone_frac"] <= 1.0, (k, v)
+        if v["bound"] == "hbm":
+            assert v["frac_measured_peak"] <= 1.0, (k, v)
+        if v["bound"] == "mfma":
+            assert v["issued"]["frac_issued"] <= 1.0 and v["issued"]["standalone_frac_issued"] <= 1.0, (k, v)
+            assert v["frac"] <= v["issued"]["frac_issued"] + 1e-6, (k, v)   # padding only adds issued cycles
+    ro = d["roofline"]
+    assert ro["time_source"] == "window" and ro["frac"] <= 1.0 and ro.get("frac_issued", 0) <= 1.0, ro
 
 
 def test_bench_secondary_workload(gpu):

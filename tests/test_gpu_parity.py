@@ -604,9 +604,9 @@ def test_env_groups_identical(gpu, arch, N, groups):
 
 
 @pytest.mark.parametrize("arch", ["ff", "lstm"])
-def test_learn_fork_identical(gpu, arch):
-    """DeviceNet.learn(fork=True) (weight-gradient reduces on a side stream,
-    arl_learn_part) gives the same gradient bits as arl_learn in one call."""
+def test_learn_parts_identical(gpu, arch):
+    """arl_learn_part 0..2 in order on one stream (the N > 1 window's split
+    learner) gives the same gradient bits as arl_learn in one call."""
     from asyncrl_amd import A3C, A3CFF, A3CLSTM, RMSpropAsync
     rng = np.random.default_rng(81)
     N, T, P = 48, 5, 7
@@ -618,9 +618,12 @@ def test_learn_fork_identical(gpu, arch):
     ag.run_window(dp, dr, dd, P, first=True, split_update=True)
     net = ag.net
     got = []
-    for fork in (False, True, False):
+    for parts in (False, True, False):
         net.grads.fill_(1234.5)            # padding between tensors keeps it
-        net.learn(fork=fork)
+        if parts:
+            net.learn_parts(range(3))
+        else:
+            net.learn()
         torch.cuda.synchronize()
         got.append(net.grads.clone())
     for name in net.layout:               # every tensor was written
@@ -629,75 +632,18 @@ def test_learn_fork_identical(gpu, arch):
     assert torch.equal(got[0], got[1]) and torch.equal(got[0], got[2])
 
 
-@pytest.mark.parametrize("arch,N,groups,resize_mode", [("ff", 96, 1, 0), ("ff", 256, 2, 0), ("ff", 64, 1, 1),
-                                                         ("ff", 64, 1, 2), ("lstm", 80, 2, 0)])
-def test_fused_observe_identical(gpu, arch, N, groups, resize_mode):
-    """observe + act fused into one conv launch (arl_observe_act_envs,
-    conv_fwd_kernel<true>) vs arl_observe + arl_act: bit-identical ring
-    planes, nvalid / reset / reward / done bookkeeping, conv activations,
-    actions, values, gradients and parameters over eager and graph-captured
-    windows, with env groups and every resize mode."""
-    from asyncrl_amd import A3C, A3CFF, A3CLSTM, GradientClipping, RMSpropAsync
-    rng = np.random.default_rng(97)
-    T, P = 5, 7
-    Model = A3CFF if arch == "ff" else A3CLSTM
-    pairs, rewards, dones = make_pools(rng, P, N, "uniform", p_done=0.15)
-    dp, dr, dd = dev(pairs, gpu), dev(rewards, gpu), dev(dones, gpu)
-
-    def mk(fuse):
-        m = Model(4, n_envs=N, t_max=T, seed=5, init_seed=6, frames="pairs")
-        m.net.fuse_obs = fuse
-        o = RMSpropAsync(lr=7e-4, eps=0.1, alpha=0.99).setup(m)
-        o.add_hook(GradientClipping(40))
-        return A3C(m, o, T, 0.99, resize_mode=resize_mode)
-
-    outs = []
-    for fuse in (False, True):
-        ag = mk(fuse)
-        assert ag.net.fused_observe == fuse
-        ag.run_window(dp, dr, dd, P, first=True, env_groups=groups)
-        ag.run_window(dp, dr, dd, P, env_groups=groups)
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            ag.run_window(dp, dr, dd, P, stream=s, env_groups=groups)
-        s.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
-            ag.run_window(dp, dr, dd, P, stream=s, env_groups=groups, split_update=True)
-        g.replay()
-        torch.cuda.synchronize()
-        net = ag.net
-        R = net.t_max + 4
-        o = {"frames": net.buffer("frames", torch.uint8, (R, N, 84, 84)).clone(),
-             "nvalid": net.buffer("nvalid", torch.uint8, (R, N)).clone(),
-             "reset": net.buffer("reset", torch.uint8, (T + 1, N)).clone(),
-             "rewards": net.buffer("rewards", torch.float32, (T, N)).clone(),
-             "dones": net.buffer("dones", torch.uint8, (T, N)).clone(),
-             "a1": net.buffer("a1", torch.float32, (T + 1, N, 6400)).clone(),
-             "a2": net.buffer("a2", torch.float32, (T + 1, N, 2592)).clone(),
-             "actions": net.buffer("actions", torch.int32, (T + 1, N)).clone(),
-             "v": net.buffer("v", torch.float32, (T + 1, N)).clone(),
-             "grads": net.grads.clone(), "params": net.params.clone(), "ms": net.ms.clone()}
-        outs.append(o)
-    assert int(outs[0]["nvalid"].min()) >= 1 and int(outs[0]["reset"][1:].sum()) > 0   # resets happened
-    for k in outs[0]:
-        assert torch.equal(outs[0][k], outs[1][k]), k
-
-
-def test_lstm_fused_cell_identical(gpu, tmp_path):
-    """The LSTM cell fused into the gate kernel's epilogue (forward, act and
-    pi_and_v) and into the BPTT step (backward) gives the same bits as the
-    cell as separate launches (ARL_LSTM_SPLIT=1); so do the FC forward's
-    ticket reduce instead of the reduce in the gate kernel's staging
-    (ARL_LSTM_XRED=0) and the env-group chains issued chain by chain
-    (ARL_GROUP_ORDER=chain): hidden / cell states, gates, actions, values,
-    gradients, parameters."""
+def test_lstm_fc_reduce_forms_identical(gpu, tmp_path):
+    """LSTM windows (two env groups, eager and graph-captured) with the FC
+    forward's split-K partials reduced in the gate kernel's staging (the
+    default under 512 envs a launch) and by the FC's last-arriver ticket
+    (ARL_LSTM_XRED=0): the same partials summed in the same order, so hidden /
+    cell states, gates, actions, values, gradients and parameters match bit
+    for bit."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     outs = []
-    for extra in ({}, {"ARL_LSTM_SPLIT": "1"}, {"ARL_LSTM_XRED": "0"}, {"ARL_GROUP_ORDER": "chain"}):
+    for extra in ({}, {"ARL_LSTM_XRED": "0"}):
         f = str(tmp_path / f"lstm_{len(outs)}.npz")
         env = dict(os.environ, **extra)
         subprocess.run([sys.executable, os.path.join(here, "lstm_split_worker.py"), f], env=env, check=True,
@@ -707,82 +653,6 @@ def test_lstm_fused_cell_identical(gpu, tmp_path):
     for o in outs[1:]:
         for k in outs[0].files:
             assert np.array_equal(outs[0][k], o[k]), k
-
-
-def test_lstm_bptt_kernel_matches_generic(gpu, tmp_path):
-    """The fused BPTT step (lstm.hip lstm_bptt_kernel: dh GEMM in two K
-    halves, reset mask, the previous step's cell backward) against the
-    split-K GEMM + f64 reduce + cell launches (ARL_LSTM_BPTT=generic): same
-    forward bits, window gradients within 1e-5 of each tensor's scale (both
-    sum exact f32 products; only the order differs)."""
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    outs = []
-    for extra in ({}, {"ARL_LSTM_BPTT": "generic"}):
-        f = str(tmp_path / f"bptt_{len(outs)}.npz")
-        env = dict(os.environ, **extra)
-        subprocess.run([sys.executable, os.path.join(here, "lstm_split_worker.py"), f, "one"], env=env, check=True,
-                       timeout=240)
-        outs.append(np.load(f))
-    assert np.array_equal(outs[0]["hbuf"], outs[1]["hbuf"])
-    assert float(np.abs(outs[0]["grads"]).max()) > 0
-    ok, err = close_normscaled(outs[1]["grads"], outs[0]["grads"], 1e-5)
-    assert ok, err
-
-
-def test_lstm_wgrad_kernel_matches_gemm(gpu, tmp_path):
-    """The LSTM gate weight gradients + dfc on fc_bwd.hip's ShapeLSTM kernel
-    (bf16-split MFMA steps, [x | h_prev] staged by LDS-DMA with reset rows read
-    from a zero row, straight into the gradient) against the round-2 generic
-    exact-f32 dual GEMM + slab reduce (ARL_LSTM_WGRAD=gemm): same forward bits,
-    dfc and every gradient tensor within 1e-5 of its own scale (both are
-    f32-accurate sums; only the order differs)."""
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    outs = []
-    for extra in ({}, {"ARL_LSTM_WGRAD": "gemm"}):
-        f = str(tmp_path / f"wgrad_{len(outs)}.npz")
-        env = dict(os.environ, **extra)
-        subprocess.run([sys.executable, os.path.join(here, "lstm_split_worker.py"), f, "one"], env=env, check=True,
-                       timeout=240)
-        outs.append(np.load(f))
-    new, old = outs
-    assert np.array_equal(new["hbuf"], old["hbuf"])
-    ok, err = close_normscaled(old["dfc"], new["dfc"], 1e-5)
-    assert ok, ("dfc", err)
-    names = [k for k in new.files if k.startswith("g.")]
-    assert any("lateral" in k for k in names) and any("upward" in k for k in names)
-    for k in names:
-        assert float(np.abs(old[k]).max()) > 0, k
-        ok, err = close_normscaled(old[k], new[k], 1e-5)
-        assert ok, (k, err)
-
-
-def test_fc_bwd_variants(gpu, tmp_path):
-    """FC backward knobs at S = 1,280 (two dW ranges): the ticket-first reduce
-    (ARL_FC_BWD_SPIN=1) sums the same partials in the same order, so every
-    bit matches the default; the exact-f32 16x16x4 steps (ARL_FC_BWD_F32=1)
-    and the default bf16-split steps are both f32-accurate, so the window
-    gradients agree to 1e-5 of each tensor's scale (close_normscaled)."""
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    outs = {}
-    for name, extra in (("default", {}), ("spin", {"ARL_FC_BWD_SPIN": "1"}), ("f32", {"ARL_FC_BWD_F32": "1"})):
-        f = str(tmp_path / f"fcb_{name}.npz")
-        env = dict(os.environ, **extra)
-        env.pop("ARL_FC_BWD_Z", None)
-        subprocess.run([sys.executable, os.path.join(here, "fc_bwd_worker.py"), f], env=env, check=True, timeout=240)
-        outs[name] = np.load(f)
-    d, sp, f32 = outs["default"], outs["spin"], outs["f32"]
-    assert float(np.abs(d["grads1"]).max()) > 0
-    for k in d.files:
-        assert np.array_equal(d[k], sp[k]), k
-    ok, err = close_normscaled(f32["grads1"], d["grads1"], 1e-5)
-    assert ok, err
-    assert not np.array_equal(f32["grads1"], d["grads1"])   # the knob did switch the k-steps
 
 
 def test_norm_fold_matches_grad_sqnorm(gpu):
@@ -818,49 +688,35 @@ def test_norm_fold_matches_grad_sqnorm(gpu):
 @pytest.mark.parametrize("n_envs", [75, 200, 512])
 def test_conv_fwd_two_envs_identical(gpu, tmp_path, n_envs):
     """The large-launch forms against the 256-env ones: conv_fwd.hip with two
-    envs a workgroup (EPW = 2: 16 waves sharing the weight planes), fc.hip's
-    64-row tiles (fc_fwd_big_kernel), the defaults from 512 envs a launch, and
-    the FF heads in fc_fwd_big_kernel's ticket tails (ARL_FC_HEADS: each
-    column tile forms its K quarter of the logits, the row block's last tile
-    sums them and draws; from 128 envs).  The per-tile k order is the same, so
-    a1, a2, hfc, the policy outputs and actions, the window gradient and the
-    updated parameters match bit for bit -- at an odd env count (the last conv
-    workgroup's second slot idle, a partial FC tile; too few envs for the fused
-    heads, which fall back), at 200 (a partial 64-row block) and at 512.  The
-    frame ring too, against phi_ring_kernel's LDS-DMA staging (ARL_PHI_DMA); and the
+    envs a workgroup (EPW = 2: 16 waves sharing the weight planes) and fc.hip's
+    64-row tiles (fc_fwd_big_kernel), the defaults from 512 envs a launch.  The
+    per-tile k order is the same, so a1, a2, hfc, the policy outputs and
+    actions, the window gradient and the updated parameters match bit for bit
+    -- at an odd env count (the last conv workgroup's second slot idle, a
+    partial FC tile), at 200 (a partial 64-row block) and at 512.  And the
     window as one C call (arl_run_window) against its launches issued step by
-    step from Python (ARL_WINDOW_C=0).  And every update block re-reducing the
-    clip norm's partials against the ticket hand-off (ARL_NORM_TICKET=1): the f64
-    sums run in another order, so that arm is held to 1e-6 relative."""
+    step from Python (ARL_WINDOW_C=0)."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     outs = []
     for i, arm in enumerate(({"ARL_CONV_EPW": "1", "ARL_FC_BIG": "0"}, {"ARL_CONV_EPW": "2", "ARL_FC_BIG": "0"},
-                             {"ARL_CONV_EPW": "1", "ARL_FC_BIG": "1", "ARL_FC_HEADS": "0"},
-                             {"ARL_CONV_EPW": "1", "ARL_FC_BIG": "1", "ARL_FC_HEADS": "1"},
-                             {"ARL_PHI_DMA": "1"}, {"ARL_WINDOW_C": "0"}, {"ARL_NORM_TICKET": "1"})):
+                             {"ARL_CONV_EPW": "1", "ARL_FC_BIG": "1"}, {"ARL_WINDOW_C": "0"})):
         f = str(tmp_path / f"arm_{i}.npz")
         env = dict(os.environ, **arm)
         subprocess.run([sys.executable, os.path.join(here, "conv_epw_worker.py"), f, str(n_envs)], env=env,
                        check=True, timeout=240)
         outs.append(np.load(f))
     assert float(np.abs(outs[0]["a2"]).max()) > 0
-    for o in outs[1:-1]:
+    for o in outs[1:]:
         for k in outs[0].files:
             assert np.array_equal(outs[0][k], o[k]), k
-    for k in outs[0].files:
-        np.testing.assert_allclose(outs[-1][k], outs[0][k], rtol=1e-6, atol=1e-7, err_msg=k)
 
 
 @pytest.mark.parametrize("arch,N", [("ff", 75), ("ff", 512), ("lstm", 80)])
 def test_a2_mask_bits_match_a2(gpu, arch, N):
     """conv_fwd.hip's a2 > 0 bits (the FC backward's ReLU mask, 81 words per
-    env-step, EPW 1 and 2) equal a2 > 0 in every sample slot of a window, and the
-    window gradient is the same bits whether fc_bwd.hip's job B reads them or
-    a2 itself (ARL_FC_BWD_MASK=f32, a fresh process)."""
-    import subprocess
-    import sys
+    env-step, EPW 1 and 2) equal a2 > 0 in every sample slot of a window."""
     from asyncrl_amd import A3C, A3CFF, A3CLSTM, GradientClipping, RMSpropAsync
     rng = np.random.default_rng(91)
     T, P = 5, 7
@@ -878,18 +734,6 @@ def test_a2_mask_bits_match_a2(gpu, arch, N):
     # slots 0..T-1 (the bootstrap slot T feeds no backward: its mask and a1 are not stored)
     assert np.array_equal(bits.reshape(T + 1, N, 2592)[:T].astype(bool), a2[:T] > 0)
     assert float(np.abs(a2[T]).max()) > 0
-    if arch == "ff" and N == 75:
-        here = os.path.dirname(os.path.abspath(__file__))
-        outs = []
-        for mask in ("", "f32"):
-            f = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"a2mask_{os.getpid()}_{mask or 'bits'}.npz")
-            env = dict(os.environ, ARL_FC_BWD_MASK=mask)
-            subprocess.run([sys.executable, os.path.join(here, "conv_epw_worker.py"), f, str(N)], env=env,
-                           check=True, timeout=240)
-            outs.append(dict(np.load(f)))
-            os.remove(f)
-        for k in outs[0]:
-            assert np.array_equal(outs[0][k], outs[1][k]), k
 
 
 def test_lstm_fc_ticket_big_tiles_identical(gpu, tmp_path):

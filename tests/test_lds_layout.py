@@ -147,7 +147,7 @@ LSTM_SRC = os.path.join(os.path.dirname(__file__), "..", "async-rl_amd", "csrc",
 
 
 def lstm_ld():
-    m = re.search(r"#ifndef ARL_LSTM_LD\s+#define ARL_LSTM_LD (\d+)", open(LSTM_SRC).read())
+    m = re.search(r"constexpr int LSTM_LD = (\d+);", open(LSTM_SRC).read())
     assert m
     return int(m.group(1))
 
