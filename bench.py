@@ -353,8 +353,8 @@ def init_dist(timeout_s: float = 300.0):
 def measure_copy_peak(dev, mib: int = 1024, reps: int = 10):
     """HBM stream-copy rate on this GPU (arl_stream_copy, every form: grid-
     stride with four 16-byte loads in flight per lane, 64 KB blocks per
-    workgroup with non-temporal accesses, and a one-shot grid of 32 KB
-    workgroups with default-policy / non-temporal accesses): a 1 GiB buffer
+    workgroup with non-temporal accesses, and a one-shot grid of one 16-byte
+    load + store a lane, default-policy / non-temporal): a 1 GiB buffer
     (4x the 256 MiB Infinity Cache) copied `reps` times per form and grid
     size; the best one's read + write bytes / time."""
     from asyncrl_amd._lib import check, lib, ptr
@@ -363,9 +363,9 @@ def measure_copy_peak(dev, mib: int = 1024, reps: int = 10):
     dst = torch.empty_like(src)
     s = torch.cuda.current_stream(dev)
     best, best_cfg, tried = 0.0, None, {}
-    forms = {0: "gridstride", 1: "blocks64k_nt", 2: "chunk32k", 3: "chunk32k_nt"}
+    forms = {0: "gridstride", 1: "blocks64k_nt", 2: "oneshot", 3: "oneshot_nt"}
     for mode in (0, 1, 2, 3):
-        for blocks in ((1024, 2048, 4096, 8192) if mode < 2 else (0,)):
+        for blocks in ((4096, 8192) if mode < 2 else (0,)):
             for _ in range(2):
                 check(lib.arl_stream_copy(ptr(src), ptr(dst), n, blocks, mode, s.cuda_stream), "arl_stream_copy")
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -356,8 +356,8 @@ int arl_returns_lossgrad(const float* rewards, const uint8_t* dones, const float
  * stream-copy peak the bench reports beside the 8 TB/s spec (SURVEY 8(d);
  * no reference counterpart).  mode 0: grid-stride, 4 loads in flight per lane;
  * mode 1: 64 KB blocks per workgroup, 16 non-temporal loads in flight per lane;
- * mode 2 / 3: a one-shot grid of bytes / 32 KB workgroups (`blocks` ignored), 8
- * lane-linear loads in flight per lane (3: non-temporal). */
+ * mode 2 / 3: a one-shot grid of bytes / 4 KB workgroups (`blocks` ignored), one
+ * 16-byte load and store per lane (3: non-temporal). */
 int arl_stream_copy(const void* src, void* dst, int64_t bytes, int blocks, int mode, void* stream);
 
 #ifdef __cplusplus
