@@ -51,6 +51,7 @@ SIGNATURES = {
     "arl_net_buffer": (c_int, [c_void_p, ctypes.c_char_p, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
     "arl_net_bind": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "arl_net_reset": (c_int, [c_void_p, c_void_p]),
+    "arl_net_params_changed": (c_int, [c_void_p]),
     "arl_net_set_pool": (c_int, [c_void_p, c_int, c_void_p, c_i64]),
     "arl_observe": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int, c_void_p]),
     "arl_observe_rgb": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_i64, c_int, c_int,

@@ -128,7 +128,7 @@ class A3CModel:
         arch = self.arch | (ARCH_STACK if frames == "stacks" else ARCH_STATES)
         net = DeviceNet(arch, self.n_actions, old.n_envs, old.t_max, env_offset=old.env_offset, seed=old.seed,
                         device=old.device)
-        net.params.copy_(old.params)
+        net.copy_params_from(old)
         net.ms.copy_(old.ms)
         self.net, self.frames = net, frames
 

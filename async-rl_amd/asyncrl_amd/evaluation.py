@@ -23,7 +23,7 @@ and every env's game restarts at the start of the evaluation.  The envs are
 left partway through episodes when it returns.
 The run uses (and overwrites) the model's lockstep workspace -- frame ring,
 step counter, LSTM state -- so evaluate on a model of its own (copy the
-trained parameters in: `eval_model.net.params.copy_(model.net.params)`), and
+trained parameters in: `eval_model.net.copy_params_from(model.net)`), and
 on a VecALE of its own: every env's game is restarted and left mid-episode,
 so a training learner stepping the same envs would carry its frame ring,
 LSTM state and n-step bootstrap across an unrelated game without a terminal

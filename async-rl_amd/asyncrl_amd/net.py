@@ -122,6 +122,18 @@ class DeviceNet:
         for name, (off, shape) in self.layout.items():
             a = np.asarray(arrays[name], dtype=np.float32).reshape(shape)
             self.param(name).copy_(torch.from_numpy(a))
+        self.params_changed()
+
+    def params_changed(self) -> None:
+        """Tell the net its params were written from outside (arl_net_params_changed):
+        derived device state (the FC weight's split planes) is rebuilt before
+        the next forward.  load_params / copy_params_from call it."""
+        check(lib.arl_net_params_changed(self._h), "arl_net_params_changed")
+
+    def copy_params_from(self, other: "DeviceNet") -> None:
+        """copy_param.copy_param (copy_param.py): this net's params <- other's."""
+        self.params.copy_(other.params)
+        self.params_changed()
 
     def state_dict(self, flat: torch.Tensor | None = None) -> dict:
         flat = self.params if flat is None else flat

@@ -143,7 +143,14 @@ int arl_net_bind(arl_net* h, float* params, float* grads, float* ms, void* ws) {
   h->net.g = grads;
   h->net.ms = ms;
   h->net.ws = reinterpret_cast<char*>(ws);
+  h->net.planes_ok = false;
   h->bound = true;
+  return ARL_OK;
+}
+
+int arl_net_params_changed(arl_net* h) {
+  if (!h) return fail(ARL_EINVAL, "null net");
+  h->net.planes_ok = false;
   return ARL_OK;
 }
 

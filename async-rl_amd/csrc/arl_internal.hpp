@@ -118,6 +118,9 @@ struct Net {
   // nothing changes the gradient between arl_learn and the update, e.g. no all-reduce):
   // norm_ready = the last arl_learn left the partials, consumed by the next update
   bool norm_fold = false, norm_ready = false;
+  // the FC weight's split planes (w_fcplanes) match the params: false after bind / arl_net_params_changed;
+  // the next forward rebuilds them (fc_planes_kernel), every update keeps them current (rmsprop_kernel)
+  bool planes_ok = false;
   int norm_rest_blocks = 64;
   int hid;                 // width of the layer the heads read (256 NIPS / LSTM, 512 Nature)
   int env_offset;          // global id of env 0 on this rank (RNG stream)
@@ -134,7 +137,8 @@ struct Net {
   int64_t w_ctl, w_frames, w_nvalid, w_reset, w_rewards, w_dones, w_a1, w_a2, w_hfc, w_gates, w_hbuf,
       w_cbuf, w_logits, w_probs, w_logp, w_v, w_ent, w_logpa, w_act, w_dlogits, w_dv, w_dh, w_dfc,
       w_dG, w_dhn, w_dcn, w_da2, w_slab, w_norm, w_loss, w_tick, w_fcb_part = 0, w_fcb_tick = 0, w_zero = 0,
-      w_a2m = 0;   // (T+1, N, 81) a2 > 0 bits (ring-frame NIPS nets; 0: none)
+      w_a2m = 0,   // (T+1, N, 81) a2 > 0 bits (ring-frame NIPS nets; 0: none)
+      w_fcplanes = 0;   // FC_PLANES_BYTES: the FC weight's bf16 split planes (NIPS nets)
   int64_t w_a3 = 0, w_da1 = 0, w_da3 = 0;   // Nature head only (w_da1 also ARCH_STATES)
   // LSTM recurrent state of pi_and_v on explicit states (A3CLSTM.pi_and_v, a3c_ale.py:55-63):
   // h, c (n, 256), the step's outputs hn, cn, and reset flags (1 = state is None)
@@ -259,11 +263,43 @@ inline PolicyArgs make_policy_args(const float* Wpi, const float* bpi, const flo
 }
 
 constexpr int FC_SPLIT = 8;   // fc forward split-K (one slice per XCD)
+// The FC weight as three exact bf16 split planes (bf16split.hpp), the B operand of fc_fwd_kernel (fc.hip):
+// [3][256][FC_PLANE_LD] bf16; split z's 324 columns at z * FC_PLANE_SLICE (16-byte aligned slices, 4 pad
+// columns each), the first 320 of a slice permuted within each 32-block so that lane quarter g of a 16x16x32
+// fragment reads its 8 k as one 16-byte run: stored 8 g + 4 h + r holds column k = 16 h + 4 g + r.
+// Written by fc_planes_kernel (fc.hip) and, for every W the update changes, by rmsprop_kernel (optim.hip).
+constexpr int FC_PLANE_SLICE = A2 / FC_SPLIT + 4, FC_PLANE_LD = FC_SPLIT * FC_PLANE_SLICE;   // 328, 2624
+constexpr int64_t FC_PLANES_BYTES = (int64_t)3 * HID * FC_PLANE_LD * 2;
+__host__ __device__ constexpr int fc_plane_pos(int local) {   // stored position of slice column `local`
+  return local >= 320 ? local : (local & ~31) + 8 * ((local >> 2) & 3) + 4 * ((local >> 4) & 1) + (local & 3);
+}
+// 4 consecutive W elements (flat index e % 4 == 0 within the (256, 2592) tensor) -> 8 bytes per plane
+__device__ inline void fc_planes_store(uint16_t* planes, int e, float4 w) {
+  const int j = e / A2, k = e - j * A2, z = k / (A2 / FC_SPLIT), loc = k - z * (A2 / FC_SPLIT);
+  const int64_t o = (int64_t)j * FC_PLANE_LD + z * FC_PLANE_SLICE + fc_plane_pos(loc);   // 4 consecutive stored
+  const float v[4] = {w.x, w.y, w.z, w.w};
+  uint32_t h[4], m[4], l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t hb = __float_as_uint(v[i]) & 0xffff0000u;
+    const float r1 = __fsub_rn(v[i], __uint_as_float(hb));
+    const uint32_t mb = __float_as_uint(r1) & 0xffff0000u;
+    const float r2 = __fsub_rn(r1, __uint_as_float(mb));
+    h[i] = hb >> 16;
+    m[i] = mb >> 16;
+    l[i] = __float_as_uint(r2) >> 16;
+  }
+  constexpr int64_t P = (int64_t)HID * FC_PLANE_LD;
+  *reinterpret_cast<uint2*>(planes + o) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+  *reinterpret_cast<uint2*>(planes + P + o) = make_uint2(m[0] | (m[1] << 16), m[2] | (m[3] << 16));
+  *reinterpret_cast<uint2*>(planes + 2 * P + o) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
+}
+hipError_t launch_fc_planes(const float* W, uint16_t* planes, hipStream_t s);
 int fc_fwd_tiles(int n);      // tickets needed for n envs
 bool fc_fwd_big(int n);       // launches over n envs run fc_fwd_big_kernel's 64-row tiles
-// tickets == null: split-K partials only (the consumer reduces them); else the last-arriver reduce
-// + bias + relu -> hfc in the same launch
-hipError_t launch_fc_fwd(const float* a2, int n, const float* W, const float* b, float* slab, int* tickets,
+// Wp: the FC weight's split planes (FC_PLANE_LD above); tickets == null: split-K partials only (the
+// consumer reduces them); else the last-arriver reduce + bias + relu -> hfc in the same launch
+hipError_t launch_fc_fwd(const float* a2, int n, const uint16_t* Wp, const float* b, float* slab, int* tickets,
                          float* hfc, hipStream_t s);
 // FC backward (fc_bwd.hip): dW / db straight into the gradient, da2 = (dfc W) * (a2 > 0)
 // weight gradients of the policy / value heads (a3c.py:126-130 through
@@ -311,6 +347,8 @@ __device__ inline float div255(float x) {
 // are copied grid-stride by all workgroups (optim.hip).
 struct AdvanceArgs {
   int64_t* ctl;             // null: no advance
+  uint16_t* fc_planes;      // non-null: also rewrite the FC weight's split planes ([fc_w0, fc_w0 + 256 x 2592))
+  int64_t fc_w0;
   uint8_t* reset;           // (T+1, n): row T -> row 0
   float* hbuf;              // LSTM: (T+2, n, 256), row T -> row 0 (else null)
   float* cbuf;

@@ -16,10 +16,15 @@
 // registers (unconditional loads from clamped addresses: no load waits for
 // another) while the current one computes.
 //
-// (1) runs on v_mfma_f32_16x16x4_f32 (exact f32): M = 32 oc x N = 256 (ic,
-//     ky, kx) x K = 81; wave w owns n-tiles 2w, 2w+1 of both m-tiles.
-// (2) and (3) run on the bf16 matrix cores with exact bf16 splits of the f32
-//     operands (bf16split.hpp; f32-accurate):
+// All three run on the bf16 matrix cores with exact bf16 splits of the f32
+// operands (bf16split.hpp; f32-accurate):
+// (1) M = 32 oc x N = 256 (ic, ky, kx) x K = 81 positions p = 9 oy + ox (3
+//     k-steps of 32, positions past 80 zero on the A side); wave w owns n-tiles
+//     2w, 2w+1 of both m-tiles.  A = da2 split planes [oc][p], written at commit
+//     time; B = 8 consecutive positions of one (ic, ky, kx) column gathered from
+//     the f32 a1 rows and split in registers -- no convert pass, 6 MFMAs per
+//     tile pair and k-step (72 issues of 16 cycles a wave, was 84 exact-f32
+//     16x16x4 of 32).
 // (2) per parity class (py, px) = wave & 3: C^T = W2 (16 ic rows) x the da2
 //     split planes stored channel-last on an 11 x 11 grid with a zero border
 //     (16 consecutive grid cells per tile, 7 tiles; the shifted windows need
@@ -67,10 +72,13 @@ constexpr int L_XPH = L_D1 + 3 * D1P;      // [ic][y][b][XR]                    
 constexpr int L_D2 = L_XPH + 4 * 84 * 4 * XR;   // da2 split grid, 3 x D2P          24,576
 constexpr int L_MASK = L_D2 + 3 * D2P;     // a1 > 0, u16 of 16 channel bits per pixel 800
 constexpr int L_A1 = L_MASK + 800;         // a1 f32 [16][20][A1R]                  30,720
-constexpr int D2F_LD = 48;                 // da2 f32 [p][oc] row stride
-constexpr int L_D2F = L_A1 + C1_OC * A1C * 4;   // da2 f32 [81][D2F_LD]             15,552
-constexpr int L_END = L_D2F + 81 * D2F_LD * 4;  // 151,520
-static_assert(L_D2F % 16 == 0, "alignment");
+// (1)'s A operand: da2 split planes [3][oc][p] (row 208 B = 13 16-byte slots, an odd count, so the 16
+// rows a ds_read_b128 lane group reads land on distinct bank quads); positions 81..103 stay 0
+constexpr int DA_ROW = 208;
+constexpr int DAP = 32 * DA_ROW;           // 6,656 per plane
+constexpr int L_DA = L_A1 + C1_OC * A1C * 4;    // 3 x DAP                             19,968
+constexpr int L_END = L_DA + 3 * DAP;      // 155,936
+static_assert(L_DA % 16 == 0, "alignment");
 constexpr int L_RED = 0;                   // end: f32 [16][128] (after the last sample)
 static_assert(L_END <= 160 * 1024, "LDS");
 static_assert(L_XPH % 16 == 0 && L_D2 % 16 == 0 && L_A1 % 16 == 0 && L_MASK % 8 == 0, "alignment");
@@ -176,8 +184,8 @@ __device__ inline void dma_a1(const ConvBwdArgs& a, int s, uint8_t* lds) {
   }
 }
 
-// da2 f32 [p][oc] (split (1): the [oc][p'] split planes and the thread's bias sums b2a) and the
-// da2 split grid (border cells written as 0)
+// da2 of a sample: the split grid of (2) (border cells written as 0), the [oc][p] split planes of (1),
+// and the thread's running conv2 bias sums b2a (its item's 8 channels)
 __device__ inline void commit_a(const PrefetchA& r, uint8_t* lds, float (&b2a)[8]) {
   const int tid = threadIdx.x;
 #pragma unroll
@@ -198,10 +206,15 @@ __device__ inline void commit_a(const PrefetchA& r, uint8_t* lds, float (&b2a)[8
       *reinterpret_cast<uint4*>(dd + D2P) = make_uint4(m[0], m[1], m[2], m[3]);
       *reinterpret_cast<uint4*>(dd + 2 * D2P) = make_uint4(l[0], l[1], l[2], l[3]);
       if (v) {
-        float* f = reinterpret_cast<float*>(lds + L_D2F) + p * D2F_LD + 8 * grp;
-        reinterpret_cast<float4*>(f)[0] = make_float4(d[0], d[1], d[2], d[3]);
-        reinterpret_cast<float4*>(f)[1] = make_float4(d[4], d[5], d[6], d[7]);
-        (void)b2a;
+        uint8_t* da = lds + L_DA + (8 * grp) * DA_ROW + 2 * p;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int sh = 16 * (k & 1);
+          *reinterpret_cast<uint16_t*>(da + k * DA_ROW) = (uint16_t)(h[k >> 1] >> sh);
+          *reinterpret_cast<uint16_t*>(da + k * DA_ROW + DAP) = (uint16_t)(m[k >> 1] >> sh);
+          *reinterpret_cast<uint16_t*>(da + k * DA_ROW + 2 * DAP) = (uint16_t)(l[k >> 1] >> sh);
+          b2a[k] = __fadd_rn(b2a[k], d[k]);
+        }
       }
     }
   }
@@ -253,12 +266,13 @@ conv_bwd_kernel(ConvBwdArgs a) {
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, col = lane & 15;
   const float* a1s = reinterpret_cast<const float*>(lds + L_A1);
-  const float* d2f = reinterpret_cast<const float*>(lds + L_D2F);
-  // zero the da1 pad columns X 20..23 once: (2) writes only X < 20
+  // zero once: the da1 pad columns X 20..23 ((2) writes only X < 20) and the da2 [oc][p] planes (commit_a
+  // writes only p < 81; (1) reads positions up to 95 as zeros)
   for (int i = tid; i < 3 * 16 * 20; i += NT) {
     const int pl = i / 320, r = i - pl * 320;
     *reinterpret_cast<uint2*>(lds + L_D1 + pl * D1P + (r / 20) * D1_OC + (r % 20) * D1_ROW + 40) = make_uint2(0, 0);
   }
+  for (int i = tid; i < 3 * DAP / 16; i += NT) reinterpret_cast<uint4*>(lds + L_DA)[i] = make_uint4(0, 0, 0, 0);
 
   // (2) W2 fragments of this wave's parity class: lane (ic = col, g), k-step
   // ks = (dy, dx), k = oc = 8 g + j -> W2[oc][ic][py + 2 dy][px + 2 dx]
@@ -285,8 +299,8 @@ conv_bwd_kernel(ConvBwdArgs a) {
   for (int i = 0; i < 2; ++i) {
     acc1[0][i] = acc1[1][i] = big3[i] = sml3[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  float b2sum = 0.f, b1s[4] = {0.f, 0.f, 0.f, 0.f};   // b1s[rr]: channel 4 g + rr
-  float b2a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // split (1): bias sums of this thread's da2 item
+  float b1s[4] = {0.f, 0.f, 0.f, 0.f};   // b1s[rr]: channel 4 g + rr
+  float b2a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // conv2 bias sums of this thread's da2 item
 
   // (3): wave w -> screen ic = w >> 1, ky = 4 kyq + (col >> 2) with kyq = w & 1,
   // kx = 4 a + (col & 3) (tile a = 0, 1); A row base of lane (phase row b = col & 3)
@@ -310,42 +324,34 @@ conv_bwd_kernel(ConvBwdArgs a) {
       prefetch_a(a, sn, pa);                // in flight during (1)-(3)
       prefetch_x(a, step0, sn, px_);
     }
-    // ---- (1) conv2 weight gradient + bias; wave w: n-tiles (ic) 2w, 2w+1 x both m-tiles
+    // ---- (1) conv2 weight gradient; wave w: n-tiles (ic) 2w, 2w+1 x both m-tiles.  k-step ks, lane
+    // (col, g): positions p = 32 ks + 8 g + j, j = 0..7.  A: da2 planes row oc = 16 mt + col, one b128 a
+    // plane; B: a1[ic][2 oy + ky][2 ox + kx] of the lane's column (ky, kx) = divmod(col, 4) at those
+    // positions, 8 f32 LDS reads (offset 48 oy + 2 ox: the 8 positions wrap a row at most once; past
+    // position 80 they read finite bytes beyond the row block, times A's zeros), split in registers.
     {
-      // 16 chunks of <= 6 positions, summed in order: the six reads in flight together
-      // (positions past 80 re-read position 80 and are dropped)
-      const int oc = tid & 31, ch = tid >> 5;
-      float v[6];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) v[k] = d2f[min(ch * 6 + k, C2_P - 1) * D2F_LD + oc];
-      float t = 0.f;
-#pragma unroll
-      for (int k = 0; k < 6; ++k)
-        if (ch * 6 + k < C2_P) t = __fadd_rn(t, v[k]);
-      b2sum = __fadd_rn(b2sum, t);
-    }
-    {
-      // position p = 4 ps + g = (oy, ox) stepped incrementally (ox += 4, wrap at 9)
-      // instead of a division per k-step; same k order
       const float* b0 = a1s + (2 * wave) * A1C + (col >> 2) * A1R + (col & 3);
-      int ox = g, boff = 2 * g, doff = g * D2F_LD;   // oy = 0
 #pragma unroll
-      for (int ps = 0; ps < 21; ++ps) {   // fully unrolled: 65.9 vs 71.6 us at 3 (253 VGPRs, no spill)
-        const bool pv = 4 * ps + g < C2_P;
-        const float af0 = pv ? d2f[doff + col] : 0.f;
-        const float af1 = pv ? d2f[doff + 16 + col] : 0.f;
-        const float bf0 = b0[pv ? boff : 0], bf1 = b0[A1C + (pv ? boff : 0)];
-        ox += 4;
-        doff += 4 * D2F_LD;
-        boff += 8;
-        if (ox >= 9) {   // next row: 2 a1 rows down, back 18 columns
-          ox -= 9;
-          boff += 2 * A1R - 18;
+      for (int ks = 0; ks < 3; ++ks) {
+        const int p0 = 32 * ks + 8 * g, oy0 = p0 / 9, ox0 = p0 - 9 * oy0;
+        const int off0 = 48 * oy0 + 2 * ox0, wrap = 9 - ox0;   // j >= wrap: the next output row
+        bf16x8 av[2][3];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int h = 0; h < 3; ++h)
+            av[mt][h] = lds_load<bf16x8>(lds, L_DA + (16 * mt + col) * DA_ROW + h * DAP + 2 * p0);
+#pragma unroll
+        for (int jn = 0; jn < 2; ++jn) {
+          float x[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = b0[jn * A1C + off0 + 2 * j + (j >= wrap ? 30 : 0)];
+          bf16x8 bh, bm, bl;
+          split3_x8(x, bh, bm, bl);
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt)
+            acc1[mt][jn] = mfma_x6_acc(av[mt][0], av[mt][1], av[mt][2], bh, bm, bl, acc1[mt][jn]);
         }
-        acc1[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(af0, bf0, acc1[0][0], 0, 0, 0);
-        acc1[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(af1, bf0, acc1[1][0], 0, 0, 0);
-        acc1[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(af0, bf1, acc1[0][1], 0, 0, 0);
-        acc1[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(af1, bf1, acc1[1][1], 0, 0, 0);
       }
     }
     // a1 > 0 per pixel as 16 channel bits
@@ -452,14 +458,17 @@ conv_bwd_kernel(ConvBwdArgs a) {
   }
   float* red = reinterpret_cast<float*>(lds + L_RED);
   __syncthreads();
-  red[tid] = b2sum;                  // lane's oc = tid & 31
+  // conv2 bias: item thread i (oc group i / 121) holds 8 channel sums; channel oc adds its group's
+  // 121 cells in order
+  if (tid < GI)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[tid * 8 + k] = b2a[k];
   __syncthreads();
   if (tid < 32) {
     float t = 0.f;
-    for (int c = 0; c < NT / 32; ++c) t = __fadd_rn(t, red[c * 32 + tid]);
+    for (int c = 0; c < 121; ++c) t = __fadd_rn(t, red[((tid >> 3) * 121 + c) * 8 + (tid & 7)]);
     out[SLAB_B2 + tid] = t;
   }
-  (void)b2a;
   __syncthreads();
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) red[(4 * g + rr) * 128 + wave * 16 + col] = b1s[rr];

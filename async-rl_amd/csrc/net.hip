@@ -273,6 +273,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
   net.w_eval_cn = buf("eval_cn", L ? n * HID * 4 : 0);
   net.w_eval_reset = buf("eval_reset", L ? n : 0);
   net.w_zero = buf("zero_row", L ? ZERO_ROW_FLOATS * 4 : 0);
+  net.w_fcplanes = buf("fc_planes", NAT ? 0 : FC_PLANES_BYTES);
   net.ws_bytes = wo;
   return true;
 }
@@ -286,10 +287,20 @@ static uint32_t* a2_mask(const Net& net, int t) {
   return net.at<uint32_t>(net.w_a2m) + (int64_t)t * net.N * A2W;
 }
 
+// the FC weight's split planes (fc.hip): rebuilt from the params when they may have changed behind the
+// net's back (bind, arl_net_params_changed); every update keeps them current
+static hipError_t ensure_fc_planes(Net& net, hipStream_t s) {
+  if (net.planes_ok || net.arch == ARCH_FF_NATURE) return hipSuccess;
+  ARL_TRY(launch_fc_planes(net.p + net.o_fcW, net.at<uint16_t>(net.w_fcplanes), s));
+  net.planes_ok = true;
+  return hipSuccess;
+}
+static const uint16_t* fc_planes(const Net& net) { return net.at<uint16_t>(net.w_fcplanes); }
+
 // head after conv1 (conv2 -> fc) for n rows, activations at a1/a2/hfc
 static hipError_t fc_forward(const Net& net, int n, const float* a2, float* hfc, hipStream_t s) {
-  return launch_fc_fwd(a2, n, net.p + net.o_fcW, net.p + net.o_fcb, net.at<float>(net.w_slab),
-                       net.at<int>(net.w_tick), hfc, s);
+  return launch_fc_fwd(a2, n, fc_planes(net), net.p + net.o_fcb, net.at<float>(net.w_slab), net.at<int>(net.w_tick),
+                       hfc, s);
 }
 
 // policy / value heads of window slot t (rows n of env 0..n-1) reading h
@@ -320,6 +331,7 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne) {
   const int n = net.N, A = net.A;
   const int part = mode & (ACT_CONV_ONLY | ACT_AFTER_CONV);
   mode &= 3;
+  ARL_TRY(ensure_fc_planes(net, s));
   // the bootstrap slot T feeds only the FC / heads forward: no backward reads its a1 or a2 mask
   // (the ring-frame conv kernels skip those stores: 25.6 KB an env)
   float* a1 = net.at<float>(net.w_a1) + (int64_t)t * n * A1;
@@ -348,7 +360,7 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne) {
                                          net.at<float>(net.w_ent) + o, net.at<int32_t>(net.w_act) + o,
                                          net.at<float>(net.w_logpa) + o);
   if (net.arch != ARCH_LSTM) {   // FF: split-K partials, reduce + relu + heads in one policy_fc launch
-    ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab, nullptr, nullptr, s));
+    ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, fc_planes(net), P + net.o_fcb, fc_slab, nullptr, nullptr, s));
     ARL_TRY(stamp(net, STAGE_FC_FWD, s));
     ARL_TRY(launch_policy_fc(fc_slab, ne, P + net.o_fcb, hfc, pa, s));
     return stamp(net, STAGE_POLICY, s);
@@ -356,7 +368,7 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne) {
   // LSTM: the FC's split-K partials, reduced + bias + relu either in the gate kernel's staging (XRED) or
   // by the FC's last-arriver ticket (lstm_xred); then the gates with the cell in their epilogue
   const bool xred = lstm_xred(ne);
-  ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, P + net.o_fcW, P + net.o_fcb, fc_slab,
+  ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, fc_planes(net), P + net.o_fcb, fc_slab,
                         xred ? nullptr : net.at<int>(net.w_tick) + fc_fwd_tiles(e0), xred ? nullptr : hfc, s));
   ARL_TRY(stamp(net, STAGE_FC_FWD, s));
   const int64_t r0 = (int64_t)t * n + e0;
@@ -398,6 +410,7 @@ hipError_t net_forward_f32(Net& net, const float* x, int n, int mode, hipStream_
   float* a2 = net.at<float>(net.w_a2) + (int64_t)T * N * A2;
   float* hfc = net.at<float>(net.w_hfc) + (int64_t)T * N * HID;
   const float* P = net.p;
+  ARL_TRY(ensure_fc_planes(net, s));
   const int K1 = (net.rgb ? 3 : 4) * 64;
   ARL_TRY((launch_gemm<64, 16, 32, 4, 1>(Conv1F32A{x, K1 / 64}, WeightT{P + net.o_c1W, K1},
                                                       EpiConv{a1, P + net.o_c1b, C1_OC, C1_P}, n * C1_P, C1_OC, K1,
@@ -579,8 +592,9 @@ hipError_t net_stage(Net& net, int stage, int t, hipStream_t s) {
                              P + net.o_c2b, net.at<float>(net.w_a1) + (int64_t)t * n * A1, a2 + (int64_t)t * n * A2,
                              s, net.layout, 0, -1, a2_mask(net, t));
     case STAGE_FC_FWD:   // as in net_act: FF (and the LSTM's XRED gate kernel) reduce the partials downstream
+      ARL_TRY(ensure_fc_planes(net, s));
       if (net.arch != ARCH_LSTM || lstm_xred(n))
-        return launch_fc_fwd(a2 + (int64_t)t * n * A2, n, P + net.o_fcW, P + net.o_fcb, slab, nullptr, nullptr, s);
+        return launch_fc_fwd(a2 + (int64_t)t * n * A2, n, fc_planes(net), P + net.o_fcb, slab, nullptr, nullptr, s);
       return fc_forward(net, n, a2 + (int64_t)t * n * A2, hfc + (int64_t)t * n * HID, s);
     case STAGE_POLICY: {
       const int64_t o = (int64_t)t * n;
@@ -650,12 +664,16 @@ hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_tot
     ARL_TRY(stamp(net, STAGE_GRAD_SQNORM, s));
   }
   const bool L = net.arch == ARCH_LSTM;
-  const AdvanceArgs adv{net.at<int64_t>(net.w_ctl), net.at<uint8_t>(net.w_reset),
+  // the update rewrites the FC weight's split planes with the new W (all of them, so they are current
+  // afterwards even if they were not before)
+  uint16_t* planes = net.arch == ARCH_FF_NATURE ? nullptr : net.at<uint16_t>(net.w_fcplanes);
+  const AdvanceArgs adv{fused ? net.at<int64_t>(net.w_ctl) : nullptr, planes, net.o_fcW, net.at<uint8_t>(net.w_reset),
                         L ? net.at<float>(net.w_hbuf) : nullptr, L ? net.at<float>(net.w_cbuf) : nullptr, net.T,
                         net.N};
+  if (planes != nullptr) net.planes_ok = true;
   ARL_TRY(launch_rmsprop(net.p, net.ms, net.g, net.param_floats, lr0, alpha, eps, do_clip ? parts : nullptr,
                          folded ? conv_norm_parts(net.norm_rest_blocks) : net.norm_blocks, clip, total_steps > 0 ? net.at<int64_t>(net.w_ctl) : nullptr, total_steps,
-                         n_total, net.T, s, fused ? &adv : nullptr));
+                         n_total, net.T, s, &adv));
   ARL_TRY(stamp(net, STAGE_RMSPROP, s));
   return advance && !fused ? net_advance(net, s) : hipSuccess;
 }

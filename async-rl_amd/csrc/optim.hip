@@ -137,6 +137,8 @@ rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __res
     rms1(pv.w, mv.w, gv.w, c);
     p4[ib] = pv;
     m4[ib] = mv;
+    const int64_t e = 4 * ib - adv.fc_w0;   // the FC weight's split planes follow their f32 W (fc.hip)
+    if (adv.fc_planes != nullptr && e >= 0 && e < (int64_t)HID * A2) fc_planes_store(adv.fc_planes, (int)e, pv);
   }
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
     const int64_t j = (n4 << 2) + threadIdx.x;
@@ -147,7 +149,7 @@ rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __res
     p[j] = pt;
     ms[j] = mt;
   }
-  if (adv.ctl == nullptr) return;
+  if (adv.ctl == nullptr) return;   // (no window advance)
   for (int64_t i = i0; i < adv.n; i += gsz) adv.reset[i] = adv.reset[(int64_t)adv.T * adv.n + i];
   if (adv.hbuf != nullptr)
     for (int64_t i = i0; i < (int64_t)adv.n * HID; i += gsz) {
@@ -189,7 +191,7 @@ hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double
   c.n_total = n_total;
   c.t_max = t_max;
   c.ctl = ctl;
-  c.ctl_idx = adv != nullptr ? CTL_STEP_SNAP : CTL_STEP;
+  c.ctl_idx = (adv != nullptr && adv->ctl != nullptr) ? CTL_STEP_SNAP : CTL_STEP;
   AdvanceArgs a{};
   if (adv != nullptr) a = *adv;
   hipLaunchKernelGGL(rmsprop_kernel, dim3(stream_blocks(n)), dim3(256), 0, s, p, ms, g, n, c, norm_sq, nparts, clip, a);

@@ -102,6 +102,12 @@ int arl_net_buffer(const arl_net* net, const char* name, int64_t* offset, int64_
  * 16-byte aligned; grads must be zeroed once by the caller) and workspace. */
 int arl_net_bind(arl_net* net, float* params, float* grads, float* ms, void* workspace);
 
+/* The caller wrote the bound params (a checkpoint load, a copy from another
+ * model): derived device state is rebuilt before the next forward -- the FC
+ * weight's bf16 split planes, which every arl_optimize* keeps current
+ * (no reference counterpart; copy_param.py / serializers write params there). */
+int arl_net_params_changed(arl_net* net);
+
 /* Reset the control block (step counters) and the frame ring; call once
  * before the first observation (async). */
 int arl_net_reset(arl_net* net, void* stream);
