@@ -485,15 +485,26 @@ int arl_run_window(arl_net* h, const uint8_t* pair_pool, const float* reward_poo
     arl::RingArgs a;
     if (int rc = ring_args(h, 0, pair_pool, reward_pool, done_pool, pool_len, 0, resize_mode, 0, 0, 0, -1, a)) return rc;
   }
+  // FF: the learner's returns + heads backward run in the bootstrap step's policy launch
+  n.fuse_returns = n.arch == arl::ARCH_FF;
+  n.returns_done = false;
+  n.ret = arl::Net::ReturnsCfg{gamma, (float)beta, (float)vcoef, clip_reward};
   for (int t = 0; t <= n.T; ++t) {
     if (t > 0 || first) {   // slot 0 of a continuing window: the previous window's bootstrap observation
       const int rc = observe_common(h, t, pair_pool, reward_pool, done_pool, pool_len, t == 0 ? 1 : 0, resize_mode, 0,
                                     0, s);
-      if (rc != ARL_OK) return rc;
+      if (rc != ARL_OK) {
+        n.fuse_returns = false;
+        return rc;
+      }
     }
     const hipError_t e = arl::net_act(n, t, 1, S(s));   // (slot T: the bootstrap forward, no draw)
-    if (e != hipSuccess) return hip_status(e, "run_window: act");
+    if (e != hipSuccess) {
+      n.fuse_returns = false;
+      return hip_status(e, "run_window: act");
+    }
   }
+  n.fuse_returns = false;
   hipError_t e = arl::net_learn(n, gamma, (float)beta, (float)vcoef, clip_reward, S(s));
   if (e == hipSuccess) e = arl::net_optimize(n, lr0, total_steps, n_total, alpha, eps, (float)clip, S(s), true);
   return hip_status(e, "run_window");

@@ -121,6 +121,12 @@ struct Net {
   // the FC weight's split planes (w_fcplanes) match the params: false after bind / arl_net_params_changed;
   // the next forward rebuilds them (fc_planes_kernel), every update keeps them current (rmsprop_kernel)
   bool planes_ok = false;
+  // the learner's returns folded into the bootstrap step's policy launch (FF, arl_run_window):
+  // fuse_returns = on, with the learn arguments below, for the window's slot-T forward; returns_done = that
+  // launch ran, so the window's LEARN_RETURNS part is a no-op
+  struct ReturnsCfg { double gamma; float beta, vcoef; int clip_reward; };
+  bool fuse_returns = false, returns_done = false;
+  ReturnsCfg ret{};
   int norm_rest_blocks = 64;
   int hid;                 // width of the layer the heads read (256 NIPS / LSTM, 512 Nature)
   int env_offset;          // global id of env 0 on this rank (RNG stream)
@@ -383,5 +389,13 @@ hipError_t launch_returns_heads(const float* rewards, const uint8_t* dones, cons
                                 float vcoef, int clip_reward, float* dlogits, float* dv, float* loss, hipStream_t s,
                                 int64_t* ctl_snap, float pcoef, int keep_scale, const float* Wpi, const float* Wv,
                                 const float* mask, float* dh);
+// launch_policy_fc of the bootstrap slot (no draw) + launch_returns_heads for the same n envs, one launch
+// (policy.hip policy_fc_returns_kernel; v(s_T) handed over in LDS); bit-identical to the two launches
+hipError_t launch_policy_fc_returns(const float* slab, int n, const float* fc_bias, float* hfc, const PolicyArgs& pa,
+                                    const float* rewards, const uint8_t* dones, const float* v, const float* probs,
+                                    const float* logp, const int32_t* act, int T, double gamma, float beta,
+                                    float vcoef, int clip_reward, float* dlogits, float* dv, float* loss,
+                                    int64_t* ctl_snap, float pcoef, int keep_scale, const float* mask, float* dh,
+                                    hipStream_t s);
 
 }  // namespace arl

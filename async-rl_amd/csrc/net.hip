@@ -362,6 +362,19 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne) {
   if (net.arch != ARCH_LSTM) {   // FF: split-K partials, reduce + relu + heads in one policy_fc launch
     ARL_TRY(launch_fc_fwd(a2 + (int64_t)e0 * A2, ne, fc_planes(net), P + net.o_fcb, fc_slab, nullptr, nullptr, s));
     ARL_TRY(stamp(net, STAGE_FC_FWD, s));
+    if (t == net.T && net.fuse_returns && e0 == 0 && ne == n) {   // + the learner's returns (one env group)
+      const Net::ReturnsCfg& r = net.ret;
+      ARL_TRY(launch_policy_fc_returns(fc_slab, ne, P + net.o_fcb, hfc, pa, net.at<float>(net.w_rewards),
+                                       net.at<uint8_t>(net.w_dones), net.at<float>(net.w_v),
+                                       net.at<float>(net.w_probs), net.at<float>(net.w_logp),
+                                       net.at<int32_t>(net.w_act), net.T, r.gamma, r.beta, r.vcoef, r.clip_reward,
+                                       net.at<float>(net.w_dlogits), net.at<float>(net.w_dv),
+                                       net.at<float>(net.w_loss), net.at<int64_t>(net.w_ctl), net.pi_coef,
+                                       net.keep_scale, net.at<float>(net.w_hfc), net.at<float>(net.w_dfc), s));
+      net.returns_done = true;
+      net.norm_ready = false;   // a new gradient (as LEARN_RETURNS)
+      return stamp(net, STAGE_POLICY, s);
+    }
     ARL_TRY(launch_policy_fc(fc_slab, ne, P + net.o_fcb, hfc, pa, s));
     return stamp(net, STAGE_POLICY, s);
   }
@@ -516,6 +529,10 @@ hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vc
   const float* P = net.p;
   const bool L = net.arch == ARCH_LSTM;
   if (part == LEARN_RETURNS) {
+    if (net.returns_done) {   // the bootstrap policy launch ran it (net_act, fuse_returns)
+      net.returns_done = false;
+      return hipSuccess;
+    }
     // n-step returns + loss gradient wrt logits / v (a3c.py:82-126); also snapshots the step counter for
     // the optimizer's fused advance and, in the same launch, the heads' backward dh (FF: dfc = dh * (hfc > 0))
     net.norm_ready = false;   // a new gradient: no folded norm until net_learn's reduce

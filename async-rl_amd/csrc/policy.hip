@@ -309,74 +309,137 @@ returns_kernel(ReturnsArgs a) {
 
 // returns_kernel + the heads' backward (a3c.py:129-130 through policy.py /
 // v_function.py): dh[s][j] = sum_k dlogits[s][k] Wpi[k][j] + dv[s] Wv[j],
-// times (mask[s][j] > 0) when mask is given, for the EB envs x T steps of
-// the block (EB = 32 / T: at most 32 rows) -- the rows the block's own
-// threads just produced, handed over in LDS.  Thread j of the block owns
-// column j (HID = 256 = blockDim): its Wpi / Wv column and its mask entries
-// are loaded up front, beside the returns' own loads.
-__device__ inline int rh_envs(int T) { return 1; }
+// times (mask[s][j] > 0) when mask is given, for the T steps of one env per
+// block -- the rows the block's own threads just produced, handed over in
+// LDS.  Thread j of the block owns column j (HID = 256 = blockDim): its Wpi /
+// Wv column and its mask entries are loaded up front, beside the returns' own
+// loads.  rh_load issues every load of a block, rh_finish does the rest, so
+// the bootstrap step's policy launch can run both around its own work
+// (policy_fc_returns_kernel).
 // AM >= A actions, RB rows (steps) per pass: the register arrays (mask
 // entries, head-weight column, loaded probs / log-probs) are sized for the
 // window, e.g. 5 rows and 4 actions at C2 instead of 32 and 32
+template <int AM, int RB>
+struct RhState {
+  float mv[RB];
+  int64_t so[RB];
+  float wc[AM + 1];
+  RetIn<AM> in;
+};
+
+// mask entries of rows r0 .. r0 + RB - 1 (row r = step r of env e) for column j = threadIdx.x
+// (unconditional loads at clamped offsets: a load under a per-lane branch would wait for each one in turn)
+template <int AM, int RB>
+__device__ inline void rh_rows(const ReturnsArgs& a, const float* __restrict__ mask, int e, int r0,
+                               RhState<AM, RB>& st) {
+  const int j = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < RB; ++u) {
+    const int r = r0 + u;
+    st.so[u] = (r < a.T && e < a.n) ? ((int64_t)r * a.n + e) * HID + j : -1;
+  }
+#pragma unroll
+  for (int u = 0; u < RB; ++u) st.mv[u] = mask != nullptr ? mask[st.so[u] < 0 ? j : st.so[u]] : 1.f;
+}
+
+template <int AM, int RB>
+__device__ inline void rh_load(const ReturnsArgs& a, const float* __restrict__ Wpi, const float* __restrict__ Wv,
+                               const float* __restrict__ mask, int e, RhState<AM, RB>& st) {
+  const int T = a.T, A = a.A, j = threadIdx.x;
+  rh_rows(a, mask, e, 0, st);
+#pragma unroll
+  for (int k = 0; k <= AM; ++k) st.wc[k] = k < A ? Wpi[min(k, A - 1) * HID + j] : Wv[j];
+  returns_load(a, min((int)threadIdx.x, T - 1), min(e, a.n - 1), st.in);   // off threads: a valid step, discarded
+}
+
+// lpi / lv: 64 floats, sdl: 64 (AM + 1), w: (AM + 1) HID of LDS
+template <int AM, int RB>
+__device__ inline void rh_finish(const ReturnsArgs& a, const float* __restrict__ mask, float* __restrict__ dh, int e,
+                                 RhState<AM, RB>& st, float* lpi, float* lv, float* sdl, float* w) {
+  const int T = a.T, A = a.A;
+  const int tid = threadIdx.x, t = tid, j = tid;
+  const bool on = t < T && e < a.n;
+#pragma unroll
+  for (int k = 0; k <= AM; ++k)
+    if (k <= A) w[k * HID + j] = k < A ? st.wc[k] : st.wc[AM];   // thread j's own column
+  if (on) returns_compute(a, t, e, st.in, lpi[tid], lv[tid], sdl + tid * (A + 1));   // row tid = step t
+  __syncthreads();
+  if (a.loss != nullptr && t == 0 && on) env_loss(a, lpi, lv, 1, 0, e);
+  for (int r0 = 0; r0 < T; r0 += RB) {
+    if (r0 > 0) rh_rows(a, mask, e, r0, st);   // T > RB: the next RB rows
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      if (st.so[u] < 0) continue;
+      const float* d = sdl + (r0 + u) * (A + 1);
+      float acc = 0.f;
+      for (int k = 0; k < A; ++k) acc = __fadd_rn(acc, __fmul_rn(d[k], w[k * HID + j]));
+      acc = __fadd_rn(acc, __fmul_rn(d[A], w[A * HID + j]));
+      dh[st.so[u]] = st.mv[u] > 0.f ? acc : 0.f;
+    }
+  }
+}
+
 template <int AM, int RB>
 __global__ void __launch_bounds__(256)
 returns_heads_kernel(ReturnsArgs a, const float* __restrict__ Wpi, const float* __restrict__ Wv,
                      const float* __restrict__ mask, float* __restrict__ dh) {
   __shared__ float lpi[64], lv[64];
   __shared__ float sdl[64 * (AM + 1)];
+  __shared__ float w[(AM + 1) * HID];
   if (a.ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) a.ctl[CTL_STEP_SNAP] = a.ctl[CTL_STEP];
-  const int T = a.T, n = a.n, A = a.A;
-  const int EB = rh_envs(T), rows = T * EB;   // rows <= 64
-  const int tid = threadIdx.x, t = tid / EB, el = tid - t * EB;
-  const int e0 = blockIdx.x * EB;
-  const int e = e0 + el;
-  const bool on = t < T && e < n;
-  const int j = tid;
-  // this thread's mask entries and head-weight column, in flight during the returns
-  // (unconditional loads at clamped offsets: a load under a per-lane branch
-  // would wait for each one in turn)
-  float mv[RB];
-  int64_t so[RB];
-  auto rows_from = [&](int r0) {
+  RhState<AM, RB> st;
+  rh_load(a, Wpi, Wv, mask, blockIdx.x, st);
+  rh_finish(a, mask, dh, blockIdx.x, st, lpi, lv, sdl, w);
+}
+
+// The FF window's bootstrap step (slot T, no draw) with the learner's first
+// launch folded in: block e runs policy_fc_kernel's row e (the FC split-K
+// reduce + relu + heads), then returns_heads_kernel's env e, whose bootstrap
+// value v(s_T) is the row's own value head output, taken from LDS (the same
+// f32 the policy stores to v).  Every load of the returns part is issued
+// before the FC partials' loads.  Results are bit-identical to the two
+// launches: the same per-element arithmetic in the same order.
+template <int AM, int RB>
+__global__ void __launch_bounds__(256)
+policy_fc_returns_kernel(const float* __restrict__ slab, int n, const float* __restrict__ fc_bias,
+                         float* __restrict__ hfc, PolicyArgs pa, ReturnsArgs ra, const float* __restrict__ mask,
+                         float* __restrict__ dh) {
+  __shared__ float part[4][16][MAXA + 2];
+  __shared__ float zs[16][MAXA + 2];
+  __shared__ __attribute__((aligned(16))) float hl[HID];
+  __shared__ float lpi[64], lv[64];
+  __shared__ float sdl[64 * (AM + 1)];
+  __shared__ float w[(AM + 1) * HID];
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x;
+  const int e = blockIdx.x;
+  if (ra.ctl != nullptr && e == 0 && tid == 0) ra.ctl[CTL_STEP_SNAP] = ra.ctl[CTL_STEP];
+  RhState<AM, RB> st;
+  rh_load(ra, pa.Wpi, pa.Wv, mask, e, st);
+  const HeadsPrefetch<HID> pf = heads_prefetch<HID>(pa);
+  // policy_fc_kernel's row (PF_ROWS = 1): threads 0..63 hold one float4 column of the 8 partials
+  const int c = 4 * (tid & 63);
+  const int64_t m = min((int64_t)e, (int64_t)n - 1);
+  f32x4v p[FC_SPLIT];
 #pragma unroll
-    for (int u = 0; u < RB; ++u) {
-      const int r = r0 + u, l = r % EB;
-      const bool ok = r < rows && e0 + l < n;
-      so[u] = ok ? ((int64_t)(r / EB) * n + e0 + l) * HID + j : -1;
-    }
-    if (mask != nullptr) {
+  for (int z = 0; z < FC_SPLIT; ++z) p[z] = *reinterpret_cast<const f32x4v*>(slab + ((int64_t)z * n + m) * HID + c);
+  if (tid < HID / 4) {
+    f32x4v acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int u = 0; u < RB; ++u) mv[u] = mask[so[u] < 0 ? j : so[u]];
-    } else {
+    for (int z = 0; z < FC_SPLIT; ++z)
 #pragma unroll
-      for (int u = 0; u < RB; ++u) mv[u] = 1.f;
-    }
-  };
-  rows_from(0);
-  float wc[AM + 1];   // column j of Wpi / Wv (clamped offsets: every load issued together)
-#pragma unroll
-  for (int k = 0; k <= AM; ++k) wc[k] = k < A ? Wpi[min(k, A - 1) * HID + j] : Wv[j];
-  RetIn<AM> in;   // off threads load a valid step (t, e) and discard it
-  returns_load(a, min(t, T - 1), min(e, n - 1), in);
-  __shared__ float w[(AM + 1) * HID];   // thread j's own column
-#pragma unroll
-  for (int k = 0; k <= AM; ++k)
-    if (k <= A) w[k * HID + j] = k < A ? wc[k] : wc[AM];
-  if (on) returns_compute(a, t, e, in, lpi[tid], lv[tid], sdl + tid * (A + 1));   // row tid = t * EB + el
-  __syncthreads();
-  if (a.loss != nullptr && t == 0 && on) env_loss(a, lpi, lv, EB, el, e);
-  for (int r0 = 0; r0 < rows; r0 += RB) {
-    if (r0 > 0) rows_from(r0);   // T > RB: the next RB rows
-#pragma unroll
-    for (int u = 0; u < RB; ++u) {
-      if (so[u] < 0) continue;
-      const float* d = sdl + (r0 + u) * (A + 1);
-      float acc = 0.f;
-      for (int k = 0; k < A; ++k) acc = __fadd_rn(acc, __fmul_rn(d[k], w[k * HID + j]));
-      acc = __fadd_rn(acc, __fmul_rn(d[A], w[A * HID + j]));
-      dh[so[u]] = mv[u] > 0.f ? acc : 0.f;
-    }
+      for (int k = 0; k < 4; ++k) acc[k] = __fadd_rn(acc[k], p[z][k]);
+    const float4 b = *reinterpret_cast<const float4*>(fc_bias + c);
+    float4 o;
+    o.x = fmaxf(__fadd_rn(acc[0], b.x), 0.f); o.y = fmaxf(__fadd_rn(acc[1], b.y), 0.f);
+    o.z = fmaxf(__fadd_rn(acc[2], b.z), 0.f); o.w = fmaxf(__fadd_rn(acc[3], b.w), 0.f);
+    *reinterpret_cast<float4*>(hl + c) = o;
+    if (e < n) *reinterpret_cast<float4*>(hfc + (int64_t)e * HID + c) = o;
   }
+  __syncthreads();
+  policy_rows16<HID, false, true, 1>(hl, e, n, pa, part, zs, &pf);   // ends with a barrier
+  st.in.vboot = zs[0][pa.A];   // v(s_T) of env e (heads_row_out stored zs[0][A] to v)
+  rh_finish(ra, mask, dh, e, st, lpi, lv, sdl, w);
 }
 
 hipError_t launch_returns(const float* rewards, const uint8_t* dones, const float* v, const float* probs,
@@ -399,16 +462,41 @@ hipError_t launch_returns_heads(const float* rewards, const uint8_t* dones, cons
                                 const float* mask, float* dh) {
   if (n <= 0) return hipSuccess;
   if (T < 1 || T > 64 || A < 1 || A > MAXA) return hipErrorInvalidValue;
-  const int EB = 1;   // rh_envs
   const ReturnsArgs ra{rewards, dones, v, probs, logp, act, T, n, A, gamma, beta, vcoef, pcoef, clip_reward,
                        keep_scale, dlogits, dv, loss, ctl_snap};
-  const dim3 grid((n + EB - 1) / EB), blk(256);
+  const dim3 grid(n), blk(256);
   if (T <= 8) {
     if (A <= 4) hipLaunchKernelGGL((returns_heads_kernel<4, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh);
     else if (A <= 8) hipLaunchKernelGGL((returns_heads_kernel<8, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh);
     else hipLaunchKernelGGL((returns_heads_kernel<MAXA, 8>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh);
   } else {
     hipLaunchKernelGGL((returns_heads_kernel<MAXA, 32>), grid, blk, 0, s, ra, Wpi, Wv, mask, dh);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_policy_fc_returns(const float* slab, int n, const float* fc_bias, float* hfc, const PolicyArgs& pa,
+                                    const float* rewards, const uint8_t* dones, const float* v, const float* probs,
+                                    const float* logp, const int32_t* act, int T, double gamma, float beta,
+                                    float vcoef, int clip_reward, float* dlogits, float* dv, float* loss,
+                                    int64_t* ctl_snap, float pcoef, int keep_scale, const float* mask, float* dh,
+                                    hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int A = pa.A;
+  if (T < 1 || T > 64 || A < 1 || A > MAXA) return hipErrorInvalidValue;
+  const ReturnsArgs ra{rewards, dones, v, probs, logp, act, T, n, A, gamma, beta, vcoef, pcoef, clip_reward,
+                       keep_scale, dlogits, dv, loss, ctl_snap};
+  const dim3 grid(n), blk(256);
+  if (T <= 8) {
+    if (A <= 4)
+      hipLaunchKernelGGL((policy_fc_returns_kernel<4, 8>), grid, blk, 0, s, slab, n, fc_bias, hfc, pa, ra, mask, dh);
+    else if (A <= 8)
+      hipLaunchKernelGGL((policy_fc_returns_kernel<8, 8>), grid, blk, 0, s, slab, n, fc_bias, hfc, pa, ra, mask, dh);
+    else
+      hipLaunchKernelGGL((policy_fc_returns_kernel<MAXA, 8>), grid, blk, 0, s, slab, n, fc_bias, hfc, pa, ra, mask,
+                         dh);
+  } else {
+    hipLaunchKernelGGL((policy_fc_returns_kernel<MAXA, 32>), grid, blk, 0, s, slab, n, fc_bias, hfc, pa, ra, mask, dh);
   }
   return hipGetLastError();
 }

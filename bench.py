@@ -245,9 +245,9 @@ def mfma_cycles(stage, N, T, arch="ff"):
     S = N * T
     if stage == "conv_fwd":   # conv_fwd.hip: conv1 25 position tiles x 8 k-steps x 3 (mfma_x3_t); conv2 6 x 2
         return N * (25 * 8 * 3 + 6 * 2 * 8 * 6) * BF16_CYC   # tiles x 8 k-steps x 6 (mfma_x6_t)
-    if stage == "fc_fwd":     # fc.hip: 16 x 16 sub-tiles x 8 K slices x 81 f32 16x16x4 steps (324 k)
-        rows = _cdiv(N, 64) * 64 if fc_big(N) else _cdiv(N, 32) * 32
-        return (rows // 16) * (256 // 16) * 8 * 81 * F32_CYC
+    if stage == "fc_fwd":     # fc.hip: 16 x 16 sub-tiles x 8 K slices (324 k): 10 split k-steps x 6
+        rows = _cdiv(N, 64) * 64 if fc_big(N) else _cdiv(N, 32) * 32   # (mfma_x6) + one f32 16x16x4 tail
+        return (rows // 16) * (256 // 16) * 8 * (10 * 6 * BF16_CYC + F32_CYC)
     if stage in ("fc_bwd", "lstm_wgrad"):   # fc_bwd.hip: job A 4 waves x (4 x 2 tile pairs x 6) per 32-sample
         lstm = stage == "lstm_wgrad"         # chunk of each range; job B 4 waves x (2 x 4 x 6) per 32-j chunk
         nta = (1024 // 128) * (512 // 64) if lstm else (256 // 128) * _cdiv(2592, 64)
@@ -255,8 +255,9 @@ def mfma_cycles(stage, N, T, arch="ff"):
         job_a = nta * chunks * 4 * 48
         job_b = _cdiv(S, 64) * (_cdiv(256, 128) if lstm else _cdiv(2592, 128)) * (1024 // 32 if lstm else 256 // 32) * 4 * 48
         return (job_a + job_b) * BF16_CYC
-    if stage == "conv_bwd":   # conv_bwd.hip per sample: (1) 8 waves x 84 f32 16x16x4; (2) 28 tiles x 4 k-steps
-        return S * (8 * 84 * F32_CYC + 28 * 4 * 6 * BF16_CYC + 8 * 15 * 2 * 3 * BF16_CYC)   # x 6; (3) 8 x 15 x 2 x 3
+    if stage == "conv_bwd":   # conv_bwd.hip per sample, 6-term (mfma_x6) / 3-term (mfma_x3) splits:
+        # (1) 8 waves x 3 k-steps x 2 x 2 tiles x 6; (2) 28 tiles x 4 k-steps x 6; (3) 8 waves x 15 x 2 x 3
+        return S * (8 * 3 * 4 * 6 + 28 * 4 * 6 + 8 * 15 * 2 * 3) * BF16_CYC
     if stage == "lstm_gates":  # lstm.hip: 32-row tiles, K = 512 on f32 16x16x4
         return _cdiv(N, 32) * 32 * 1024 * 512 * 2 // 64
     if stage == "lstm_bptt":   # lstm.hip: 32-row tiles, N = 256, K = 1024 on f32 16x16x4
@@ -272,12 +273,12 @@ def mfma_ideal_cycles(stage, N, T):
     b3, b6, f = 3 / 1024, 6 / 1024, 1 / 64   # cycles per FLOP
     if stage == "conv_fwd":
         return N * (2 * 400 * 16 * 256 * b3 + 2 * 81 * 32 * 256 * b6)
-    if stage == "fc_fwd":
-        return N * FC_FWD_FLOP_PER_ENV * f
+    if stage == "fc_fwd":   # 320 of each K slice's 324 k on the split, the last 4 on f32
+        return N * FC_FWD_FLOP_PER_ENV * (320 * b6 + 4 * f) / 324
     if stage == "fc_bwd":
         return 2 * S * FC_FWD_FLOP_PER_ENV * b6
     if stage == "conv_bwd":
-        return S * (2 * 32 * 256 * 81 * f + 2 * 81 * 32 * 256 * b6 + 2 * 400 * 16 * 256 * b3)
+        return S * (2 * 32 * 256 * 81 * b6 + 2 * 81 * 32 * 256 * b6 + 2 * 400 * 16 * 256 * b3)
     if stage == "lstm_gates":
         return N * LSTM_GATES_FLOP_PER_ENV * f
     if stage == "lstm_bptt":
@@ -848,6 +849,7 @@ def main(a):
             # the learner's small HBM-bound launches (NIPS heads): returns + loss gradient + heads dh,
             # the conv backward's slab reduce, the gradient's squared norm (GradientClipping)
             None if nat else
+            # (FF one-call windows: folded into the bootstrap step's policy launch, policy_fc_returns_kernel)
             ("returns", "returns_heads_kernel", lambda i: net.run_stage("returns", stream=stream), 1, "hbm",
              returns_bytes(N, T, A, mask=not lstm)),
             None if nat else
@@ -866,6 +868,8 @@ def main(a):
             for name, kname, fn, calls, bound, work in filter(None, specs):
                 us_alone = timed(fn)
                 win = tl.get(name)
+                if win is None and timeline is not None:
+                    calls = 0   # not in the window (FF: the returns run in the bootstrap policy launch)
                 # the raw in-window interval (one event's cost included: a lower bound on the kernel's rate)
                 us = win["us_per_launch"] if win is not None else us_alone
                 cyc = mfma_cycles(name, N, T, arch) if (bound == "mfma" and arch in ("ff", "lstm")) else None
