@@ -484,6 +484,34 @@ def test_rmsprop_kernel_bitexact_vs_reference(gpu):
         assert (ms.cpu().numpy() == r["ms_out"][k]).all()
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 5])
+@pytest.mark.parametrize("clip", [False, True])
+def test_rmsprop_tiny_arrays_match_oracle(gpu, n, clip):
+    """update_one on arrays shorter than a float4 (the value-head bias has one
+    element): no float4 pass, the tail handled element-wise; bit-exact with the
+    oracle's f32 op sequence, the clip scale from the f64 norm."""
+    from asyncrl_amd import GradientClipping, RMSpropAsync
+    rng = np.random.default_rng(100 + n)
+    p = rng.standard_normal(n).astype(np.float32)
+    ms = np.abs(rng.standard_normal(n)).astype(np.float32) * 0.01
+    g = (rng.uniform(1.0, 2.0, n) * rng.choice([-1.0, 1.0], n) * (60.0 if clip else 1.0)).astype(np.float32)
+    opt = RMSpropAsync(lr=7e-4, alpha=0.99, eps=0.1)
+    if clip:
+        opt.add_hook(GradientClipping(40))
+    P, M, G = dev(p, gpu), dev(ms, gpu), dev(g, gpu)
+    opt.update_arrays(P, M, G)
+    gc = g
+    if clip:
+        (gc,), norm = O.clip_grads([g], 40.0, exact_norm=True)
+        assert norm > 40.0
+    p1, m1 = O.rmsprop_update(p, ms, gc, 7e-4)
+    if clip:   # the scale is one f32 rounding of the f64 norm on both sides
+        assert np.allclose(P.cpu().numpy(), p1, rtol=1e-6, atol=1e-7)
+        assert np.allclose(M.cpu().numpy(), m1, rtol=1e-6, atol=1e-9)
+    else:
+        assert (P.cpu().numpy() == p1).all() and (M.cpu().numpy() == m1).all()
+
+
 def test_rmsprop_clip_matches_oracle(gpu):
     from asyncrl_amd import GradientClipping, RMSpropAsync
     rng = np.random.default_rng(41)
