@@ -6,9 +6,11 @@
 // is chosen for one short dependency chain per workgroup:
 //   * split-K 8 ways, one K slice (324) per XCD (blockIdx % 8 = split): each
 //     XCD's L2 holds just its 324-column slice of a2 and W;
-//   * BM x 64 output tile per workgroup (BM = 32: 8 waves; BM = 64 for
-//     launches over >= 512 envs: 16 waves, so 512 envs are one workgroup per
-//     CU), one 16 x 16 output sub-tile per wave;
+//   * BM x 64 output tile per workgroup (BM = 32: 4 waves; BM = 64 for
+//     launches over >= 512 envs: 8 waves, so 512 envs are one workgroup per
+//     CU), two 16 x 16 output sub-tiles per wave along N, so one exact split
+//     of the wave's a2 fragment feeds both (fc_fwd 10.7 -> 9.9 us at C4
+//     against one sub-tile a wave, r5p);
 //   * the f32 products on the bf16 matrix cores: a2 (f32) is split exactly
 //     into three bf16 parts in registers, W comes pre-split as three bf16
 //     planes (fc_planes_kernel / the RMSProp kernel write them whenever W
@@ -51,7 +53,7 @@ __host__ __device__ constexpr int ck_b(int c) { return c < 3 ? 12 : 5; }    // B
 constexpr int A_LD = 26, B_LD = 14;                                            // 16-byte slots per row
 template <int BM>
 struct FcLay {
-  static constexpr int NT = BM * 16;                     // threads: one 16 x 16 sub-tile per wave
+  static constexpr int NT = BM * 8;                      // threads: two 16 x 16 sub-tiles per wave (along N)
   static constexpr int NW = NT / 64;
   static constexpr int A_SLOTS = BM * A_LD;
   static constexpr int B_PLANE = FBN * B_LD;             // slots per B plane
@@ -61,7 +63,7 @@ struct FcLay {
   static constexpr int PW_MAX = (PIECES + NW - 1) / NW;
 };
 static_assert(2 * FcLay<64>::BUF * 16 <= 160 * 1024 && 2 * FcLay<32>::BUF * 16 <= 160 * 1024, "LDS");
-static_assert(FcLay<64>::PW_MAX <= 12 && FcLay<32>::PW_MAX <= 12, "fc_wait_vm range");
+static_assert(FcLay<64>::PW_MAX <= 16 && FcLay<32>::PW_MAX <= 16, "fc_wait_vm range");
 }  // namespace
 
 __device__ inline void fc_wait_vm(int n) {   // s_waitcnt vmcnt(n), n wave-uniform, 0..12
@@ -79,6 +81,10 @@ __device__ inline void fc_wait_vm(int n) {   // s_waitcnt vmcnt(n), n wave-unifo
     case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
     case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
     case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
@@ -118,8 +124,11 @@ fc_fwd_kernel(const float* __restrict__ a2, int n, const uint16_t* __restrict__ 
   issue(0);
   issue(1);
   const int g = lane >> 4, col = lane & 15;
-  const int ms = wave % (BM / 16), ns = wave / (BM / 16);
-  f32x4 big = {0.f, 0.f, 0.f, 0.f}, sml = big;
+  // wave: m sub-tile ms, n sub-tiles 2 np and 2 np + 1 (one A split feeds both)
+  const int ms = wave % (BM / 16), np = wave / (BM / 16);
+  f32x4 big[2], sml[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) big[u] = sml[u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int c = 0; c < FCH; ++c) {
     // this wave's pieces of chunk c have landed (chunk c + 1's may still fly), then everyone's
@@ -127,7 +136,7 @@ fc_fwd_kernel(const float* __restrict__ a2, int n, const uint16_t* __restrict__ 
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     const uint8_t* buf = S + 16 * (c & 1) * LY::BUF;
     const float* Ar = reinterpret_cast<const float*>(buf) + (ms * 16 + col) * (4 * A_LD);
-    const uint8_t* Br = buf + 16 * (LY::A_SLOTS + (ns * 16 + col) * B_LD);
+    const uint8_t* Br0 = buf + 16 * (LY::A_SLOTS + (2 * np * 16 + col) * B_LD);
 #pragma unroll
     for (int s = 0; s < (c < 3 ? 3 : 1); ++s) {
       // lane quarter g: k = 32 s + 16 h + 4 g + r (element 4 h + r) on both sides
@@ -142,17 +151,24 @@ fc_fwd_kernel(const float* __restrict__ a2, int n, const uint16_t* __restrict__ 
       bf16x8 ah, am, al;
       split3_x8(x, ah, am, al);
       const int bo = 64 * s + 16 * g;
-      const bf16x8 bh = lds_load<bf16x8>(Br, bo), bm = lds_load<bf16x8>(Br, bo + 16 * LY::B_PLANE),
-                   bl = lds_load<bf16x8>(Br, bo + 32 * LY::B_PLANE);
-      mfma_x6(ah, am, al, bh, bm, bl, big, sml);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint8_t* Br = Br0 + 16 * 16 * B_LD * u;
+        const bf16x8 bh = lds_load<bf16x8>(Br, bo), bm = lds_load<bf16x8>(Br, bo + 16 * LY::B_PLANE),
+                     bl = lds_load<bf16x8>(Br, bo + 32 * LY::B_PLANE);
+        mfma_x6(ah, am, al, bh, bm, bl, big[u], sml[u]);
+      }
     }
     if (c == FCH - 1) {   // the slice's last 4 k (chunk columns 32 + g): exact f32, W rebuilt from its planes
       const float at = Ar[32 + g];
-      const uint16_t* bt = reinterpret_cast<const uint16_t*>(Br) + 32 + g;
-      const float wt = __fadd_rn(__fadd_rn(__uint_as_float((uint32_t)bt[0] << 16),
-                                           __uint_as_float((uint32_t)bt[8 * LY::B_PLANE] << 16)),
-                                 __uint_as_float((uint32_t)bt[16 * LY::B_PLANE] << 16));
-      sml = __builtin_amdgcn_mfma_f32_16x16x4f32(at, wt, sml, 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint16_t* bt = reinterpret_cast<const uint16_t*>(Br0 + 16 * 16 * B_LD * u) + 32 + g;
+        const float wt = __fadd_rn(__fadd_rn(__uint_as_float((uint32_t)bt[0] << 16),
+                                             __uint_as_float((uint32_t)bt[8 * LY::B_PLANE] << 16)),
+                                   __uint_as_float((uint32_t)bt[16 * LY::B_PLANE] << 16));
+        sml[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(at, wt, sml[u], 0, 0, 0);
+      }
     }
     if (c + 2 < FCH) {   // every wave is done reading buffer c & 1: chunk c + 2 goes there
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -167,12 +183,14 @@ fc_fwd_kernel(const float* __restrict__ a2, int n, const uint16_t* __restrict__ 
   // been acknowledged at device scope before the ticket is taken.
   float* part = slab + (int64_t)split * n * HID;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int m = m0 + ms * 16 + g * 4 + r;
-    if (m < n)
-      __hip_atomic_store(part + (int64_t)m * HID + n0 + ns * 16 + col, __fadd_rn(big[r], sml[r]), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-  }
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + ms * 16 + g * 4 + r;
+      if (m < n)
+        __hip_atomic_store(part + (int64_t)m * HID + n0 + (2 * np + u) * 16 + col, __fadd_rn(big[u][r], sml[u][r]),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   if (tickets == nullptr) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
