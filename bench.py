@@ -866,7 +866,14 @@ def main(a):
         kernels = {}
         with torch.cuda.stream(stream):
             for name, kname, fn, calls, bound, work in filter(None, specs):
+                # the update stage runs with lr 0 (p unchanged) but still rewrites the RMSProp statistics:
+                # time it on the live buffers, then put ms back (the line's params_finite / replica checks and
+                # any later window see the state the timed windows left)
+                ms_keep = net.ms.clone() if name == "rmsprop" else None
                 us_alone = timed(fn)
+                if ms_keep is not None:
+                    stream.synchronize()
+                    net.ms.copy_(ms_keep)
                 win = tl.get(name)
                 if win is None and timeline is not None:
                     calls = 0   # not in the window (FF: the returns run in the bootstrap policy launch)
