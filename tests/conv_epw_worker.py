@@ -42,7 +42,8 @@ def main(out, N):
              frames=net.buffer("frames").cpu().numpy(),
              actions=net.buffer("actions", torch.int32, (T + 1, N)).cpu().numpy(),
              **{k: net.buffer(k, torch.float32).cpu().numpy() for k in ("hfc", "logits", "probs", "logp", "v",
-                                                                       "entropy", "logp_a")})
+                                                                       "entropy", "logp_a", "dlogits", "dv",
+                                                                       "loss", "dfc")})
 
 
 if __name__ == "__main__":

@@ -713,7 +713,7 @@ def test_norm_fold_matches_grad_sqnorm(gpu):
     assert ok, err
 
 
-@pytest.mark.parametrize("n_envs", [75, 200, 512])
+@pytest.mark.parametrize("n_envs", [1, 33, 75, 200, 512])
 def test_conv_fwd_two_envs_identical(gpu, tmp_path, n_envs):
     """The large-launch forms against the 256-env ones: conv_fwd.hip with two
     envs a workgroup (EPW = 2: 16 waves sharing the weight planes) and fc.hip's
@@ -723,7 +723,10 @@ def test_conv_fwd_two_envs_identical(gpu, tmp_path, n_envs):
     -- at an odd env count (the last conv workgroup's second slot idle, a
     partial FC tile), at 200 (a partial 64-row block) and at 512.  And the
     window as one C call (arl_run_window) against its launches issued step by
-    step from Python (ARL_WINDOW_C=0)."""
+    step from Python (ARL_WINDOW_C=0): the C window runs the learner's returns
+    and heads backward inside the bootstrap policy launch
+    (policy_fc_returns_kernel), so dlogits / dv / the losses / dfc are compared
+    too -- also at 1 and 33 envs."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
