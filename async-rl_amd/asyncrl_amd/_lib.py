@@ -61,6 +61,7 @@ SIGNATURES = {
     "arl_truncate_window": (c_int, [c_void_p, c_int, c_void_p]),
     "arl_net_set_loss": (c_int, [c_void_p, c_double, c_int]),
     "arl_net_set_norm_fold": (c_int, [c_void_p, c_int]),
+    "arl_net_set_returns_fusion": (c_int, [c_void_p, c_int, c_double, c_double, c_double, c_int]),
     "arl_reset_state": (c_int, [c_void_p, c_i64, c_i64, c_void_p]),
     "arl_act": (c_int, [c_void_p, c_int, c_void_p]),
     "arl_act_mode": (c_int, [c_void_p, c_int, c_int, c_void_p]),

@@ -428,7 +428,15 @@ class A3C:
             self.t += T
             return
         if len(groups) == 1:
-            self._forward_chain(pair_pool, reward_pool, done_pool, pool_len, first, stream, None)
+            # FF: the learner's returns ride on the bootstrap policy launch (as arl_run_window does)
+            fuse = net.base_arch == ARCH_FF and net.arch != ARCH_FF_NATURE
+            if fuse:
+                net.set_returns_fusion(True, self.gamma, self.beta, self._vcoef, self.clip_reward)
+            try:
+                self._forward_chain(pair_pool, reward_pool, done_pool, pool_len, first, stream, None)
+            finally:
+                if fuse:
+                    net.set_returns_fusion(False)
         else:
             main = stream if stream is not None else torch.cuda.current_stream(net.device)
             side = self._side_streams(len(groups) - 1)

@@ -209,6 +209,15 @@ class DeviceNet:
         only when the gradient is not all-reduced between learn and update."""
         check(lib.arl_net_set_norm_fold(self._h, int(on)), "arl_net_set_norm_fold")
 
+    def set_returns_fusion(self, on: bool, gamma: float = 0.99, beta: float = 0.01, v_loss_coef: float = 0.5,
+                           clip_reward: bool = True):
+        """Run the learner's returns + heads backward inside the bootstrap
+        step's policy launch (arl_net_set_returns_fusion; FF nets, one launch
+        over all envs): the next act at t = t_max does them, and the window's
+        LEARN_RETURNS part is skipped.  Bit-identical to the separate launch."""
+        check(lib.arl_net_set_returns_fusion(self._h, int(on), gamma, beta, v_loss_coef, int(clip_reward)),
+              "arl_net_set_returns_fusion")
+
     def set_loss(self, pi_loss_coef: float = 1.0, keep_loss_scale_same: bool = False):
         check(lib.arl_net_set_loss(self._h, pi_loss_coef, int(keep_loss_scale_same)), "arl_net_set_loss")
 

@@ -323,6 +323,17 @@ int arl_net_set_norm_fold(arl_net* h, int on) {
   return ARL_OK;
 }
 
+int arl_net_set_returns_fusion(arl_net* h, int on, double gamma, double beta, double v_loss_coef, int clip_reward) {
+  if (!h) return fail(ARL_EINVAL, "null net");
+  arl::Net& n = h->net;
+  n.fuse_returns = on != 0 && n.arch == arl::ARCH_FF;
+  if (on) {   // (turning it off keeps returns_done: the window's learn still skips what the act ran)
+    n.returns_done = false;
+    n.ret = arl::Net::ReturnsCfg{gamma, (float)beta, (float)v_loss_coef, clip_reward};
+  }
+  return ARL_OK;
+}
+
 int arl_net_set_loss(arl_net* h, double pi_loss_coef, int keep_loss_scale_same) {
   if (!h) return fail(ARL_EINVAL, "null net");
   h->net.pi_coef = (float)pi_loss_coef;
@@ -486,6 +497,8 @@ int arl_run_window(arl_net* h, const uint8_t* pair_pool, const float* reward_poo
     if (int rc = ring_args(h, 0, pair_pool, reward_pool, done_pool, pool_len, 0, resize_mode, 0, 0, 0, -1, a)) return rc;
   }
   // FF: the learner's returns + heads backward run in the bootstrap step's policy launch
+  const bool fuse_was = n.fuse_returns;
+  const arl::Net::ReturnsCfg ret_was = n.ret;
   n.fuse_returns = n.arch == arl::ARCH_FF;
   n.returns_done = false;
   n.ret = arl::Net::ReturnsCfg{gamma, (float)beta, (float)vcoef, clip_reward};
@@ -494,17 +507,20 @@ int arl_run_window(arl_net* h, const uint8_t* pair_pool, const float* reward_poo
       const int rc = observe_common(h, t, pair_pool, reward_pool, done_pool, pool_len, t == 0 ? 1 : 0, resize_mode, 0,
                                     0, s);
       if (rc != ARL_OK) {
-        n.fuse_returns = false;
+        n.fuse_returns = fuse_was;
+        n.ret = ret_was;
         return rc;
       }
     }
     const hipError_t e = arl::net_act(n, t, 1, S(s));   // (slot T: the bootstrap forward, no draw)
     if (e != hipSuccess) {
-      n.fuse_returns = false;
+      n.fuse_returns = fuse_was;
+      n.ret = ret_was;
       return hip_status(e, "run_window: act");
     }
   }
-  n.fuse_returns = false;
+  n.fuse_returns = fuse_was;
+  n.ret = ret_was;
   hipError_t e = arl::net_learn(n, gamma, (float)beta, (float)vcoef, clip_reward, S(s));
   if (e == hipSuccess) e = arl::net_optimize(n, lr0, total_steps, n_total, alpha, eps, (float)clip, S(s), true);
   return hip_status(e, "run_window");

@@ -182,6 +182,15 @@ int arl_net_set_loss(arl_net* net, double pi_loss_coef, int keep_loss_scale_same
  * all-reduced across ranks); arl_learn_part never folds.  Default off. */
 int arl_net_set_norm_fold(arl_net* net, int on);
 
+/* The learner's returns + loss gradient + heads backward (arl_learn_part
+ * ARL_LEARN_RETURNS, a3c.py:82-130) folded into the bootstrap step's policy
+ * launch: with on != 0, the next arl_act / arl_act_mode at t == t_max over all
+ * envs of an FF net with the NIPS head runs them in that launch with these
+ * arguments, bit-identical, and the window's ARL_LEARN_RETURNS part (or
+ * arl_learn's first launch) is then skipped.  arl_run_window does this
+ * internally.  Host state of the handle; default off. */
+int arl_net_set_returns_fusion(arl_net* net, int on, double gamma, double beta, double v_loss_coef, int clip_reward);
+
 /* A3C.act forward + sample at window step t (a3c.py:154-164): pi_and_v of
  * the ring state, softmax policy output, Philox inverse-CDF action.  t ==
  * t_max is the bootstrap value of the window end (a3c.py:85, pre-update
