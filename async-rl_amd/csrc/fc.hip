@@ -96,7 +96,6 @@ fc_fwd_kernel(const float* __restrict__ a2, int n, const uint16_t* __restrict__ 
   using LY = FcLay<BM>;
   constexpr int NT = LY::NT, NW = LY::NW;
   __shared__ __attribute__((aligned(16))) uint8_t S[2 * LY::BUF * 16];
-  __shared__ int is_last;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int split = blockIdx.x % FSPLIT, tile = blockIdx.x / FSPLIT;
   constexpr int NTN = HID / FBN;
@@ -194,7 +193,8 @@ fc_fwd_kernel(const float* __restrict__ a2, int n, const uint16_t* __restrict__ 
   if (tickets == nullptr) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0)
+  int& is_last = *reinterpret_cast<int*>(S);   // the staging array (every read of it is done): no second
+  if (tid == 0)                                // __shared__ object, which would make the compiler drain the DMA
     is_last = __hip_atomic_fetch_add(&tickets[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == FSPLIT - 1;
   __syncthreads();
   if (!is_last) return;

@@ -420,7 +420,7 @@ __device__ void job_dw(const FcBwdArgs& a, int job, float* lds, uint8_t* rst) {
 
 // ---------------------------------------------------------------- job B: da2
 // MT m-tiles per wave: workgroup tiles of BMT = 32 MT samples x 128 k
-template <int MT, class SH>
+template <int MT, class SH, bool BITS>
 __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
   using D = Dims<SH>;
   constexpr int NKB = D::NKB, NB = SH::NB;
@@ -464,7 +464,8 @@ __device__ void job_da2(const FcBwdArgs& a, int tile, float* lds) {
   for (int i = 0; i < MT; ++i) mb[i] = 0u;
   f32x4 mraw[4];
   uint32_t mw[4];
-  const bool bits = !SH::kLstm && a.a2m != nullptr;   // block-uniform
+  constexpr bool bits = BITS;   // (compile-time: a runtime choice branches around every mask load, each waiting
+                                //  for all DMA in flight)
   const __amdgpu_buffer_rsrc_t mskw = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint32_t*>(bits ? a.a2m : nullptr) + (int64_t)s0 * A2W, 0, bits ? rows * A2W * 4 : 0, BUF_DWORD3);
   issue(0);
@@ -631,16 +632,18 @@ __device__ void job_heads(const FcBwdArgs& a, int jt, float* lds) {
   }
 }
 
-template <int MT, class SH>
+template <int MT, class SH, bool BITS>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2)))
 fc_bwd_kernel(FcBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];   // 64 KB
-  __shared__ uint8_t rst[SH::kLstm ? RST_MAX : 4];                 // LSTM: a range's reset flags
+  // 64 KB of stages + (LSTM) a range's reset flags in one __shared__ object: a second one beside the
+  // LDS-DMA staging makes the compiler drain every DMA in flight (vmcnt(0)) before a chunk's LDS reads
+  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE + (SH::kLstm ? RST_MAX / 4 : 0)];
+  uint8_t* rst = reinterpret_cast<uint8_t*>(lds + 2 * STAGE);
   const int b = blockIdx.x;
   const int na = Dims<SH>::NTA * a.Z;
   if (b < a.nc) job_heads(a, b, lds);   // first: the smallest, longest-latency jobs
   else if (b < a.nc + na) job_dw<SH>(a, b - a.nc, lds, rst);
-  else job_da2<MT, SH>(a, b - a.nc - na, lds);
+  else job_da2<MT, SH, BITS>(a, b - a.nc - na, lds);
 }
 
 // ~800 samples per job A range, at most 16 ranges (bf16-split steps, sweep in
@@ -675,7 +678,8 @@ hipError_t launch_fc_bwd(const float* dfc, const float* a2, const float* W, int 
   const int nc = heads != nullptr ? NJC : 0;
   FcBwdArgs args{dfc, a2, W, S, Z, kpz, gW, gb, da2, part, tick, heads ? *heads : HeadsDW{}, nc,
                  nullptr, nullptr, nullptr, nullptr, a2m};
-  hipLaunchKernelGGL((fc_bwd_kernel<MT, ShapeFC>), dim3(nc + na + nb), dim3(NT), 0, s, args);
+  if (a2m != nullptr) hipLaunchKernelGGL((fc_bwd_kernel<MT, ShapeFC, true>), dim3(nc + na + nb), dim3(NT), 0, s, args);
+  else hipLaunchKernelGGL((fc_bwd_kernel<MT, ShapeFC, false>), dim3(nc + na + nb), dim3(NT), 0, s, args);
   return hipGetLastError();
 }
 
@@ -693,7 +697,7 @@ hipError_t launch_lstm_wgrad(const float* dG, const float* hfc, const float* hpr
   constexpr int BMT = 64;
   const int na = D::NTA * Z, nb = ((S + BMT - 1) / BMT) * D::NKB;
   FcBwdArgs args{dG, hfc, Wu, S, Z, kpz, gWu, gbu, dfc, part, tick, HeadsDW{}, 0, hprev, reset, zero, gWl};
-  hipLaunchKernelGGL((fc_bwd_kernel<2, ShapeLSTM>), dim3(na + nb), dim3(NT), 0, s, args);
+  hipLaunchKernelGGL((fc_bwd_kernel<2, ShapeLSTM, false>), dim3(na + nb), dim3(NT), 0, s, args);
   return hipGetLastError();
 }
 
