@@ -7,7 +7,8 @@
 // their log-probs), a3c.py:69-70 (reward clip), a3c.py:82-126 (n-step
 // return, advantage, pi/v/entropy losses).
 //
-// policy_kernel: one 4-wave workgroup per 16 env rows.  The A logits and the
+// policy_kernel: one 4-wave workgroup per 4 env rows (C3 window 1.0642-1.0678 -> 1.0582-1.0588 ms
+// against 16 rows, 1.0635-1.0641 at 1 row, r5am).  The A logits and the
 // value are one small GEMM on the matrix cores: [16 rows x 256] . [256 x
 // (A + 1)] with v_mfma_f32_16x16x4_f32 (exact f32 products; each lane's h and
 // W fragments are 16-byte loads covering 4 k-steps, k permuted identically on
@@ -31,20 +32,21 @@
 namespace arl {
 
 // HW = hidden width (256: NIPS head / LSTM; 512: Nature head)
+constexpr int PK_ROWS = 4;   // env rows a workgroup (the MFMA tile's other rows repeat the last: bit-identical)
 template <int HW>
 __global__ void __launch_bounds__(256)
 policy_kernel(const float* __restrict__ h, int64_t n, PolicyArgs pa) {
   __shared__ float part[4][16][MAXA + 2];
   __shared__ float zs[16][MAXA + 2];
-  policy_rows16<HW, false>(h, (int64_t)blockIdx.x * 16, n, pa, part, zs);
+  policy_rows16<HW, false, false, PK_ROWS>(h, (int64_t)blockIdx.x * PK_ROWS, n, pa, part, zs);
 }
 
 hipError_t launch_policy_args(const float* h, int64_t n, const PolicyArgs& pa, hipStream_t s, int hid) {
   if (n <= 0) return hipSuccess;
   if (hid == 512)
-    hipLaunchKernelGGL(policy_kernel<512>, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, s, h, n, pa);
+    hipLaunchKernelGGL(policy_kernel<512>, dim3((unsigned)((n + PK_ROWS - 1) / PK_ROWS)), dim3(256), 0, s, h, n, pa);
   else if (hid == HID)
-    hipLaunchKernelGGL(policy_kernel<HID>, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, s, h, n, pa);
+    hipLaunchKernelGGL(policy_kernel<HID>, dim3((unsigned)((n + PK_ROWS - 1) / PK_ROWS)), dim3(256), 0, s, h, n, pa);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
