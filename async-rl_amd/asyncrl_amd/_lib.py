@@ -52,6 +52,8 @@ SIGNATURES = {
     "arl_net_bind": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "arl_net_reset": (c_int, [c_void_p, c_void_p]),
     "arl_net_params_changed": (c_int, [c_void_p]),
+    "arl_net_prepare": (c_int, [c_void_p, c_void_p]),
+    "arl_net_param_generation": (c_int, [c_void_p, ctypes.POINTER(c_u64), ctypes.POINTER(c_u64)]),
     "arl_net_set_pool": (c_int, [c_void_p, c_int, c_void_p, c_i64]),
     "arl_observe": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int, c_void_p]),
     "arl_observe_rgb": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_i64, c_int, c_int,
@@ -98,8 +100,8 @@ for _name, (_res, _args) in SIGNATURES.items():
     _fn.restype = _res
     _fn.argtypes = _args
 
-if lib.arl_abi_version() != 3:
-    raise ImportError(f"asyncrl_amd: {LIB_PATH} has ABI {lib.arl_abi_version()}, expected 3 (rebuild it)")
+if lib.arl_abi_version() != 4:
+    raise ImportError(f"asyncrl_amd: {LIB_PATH} has ABI {lib.arl_abi_version()}, expected 4 (rebuild it)")
 
 ARCH_FF = 0
 ARCH_LSTM = 1
@@ -108,7 +110,7 @@ ARCH_RGB = 16        # flag for FF / LSTM: the ViZDoom models (train_a3c_doom.py
 ARCH_STACK = 32      # flag for FF / LSTM: observations are whole 4-screen stacks (ALE.state, ale.py:91-94)
 ARCH_STATES = 64     # flag for FF / LSTM: observations are f32 (4, 84, 84) states, phi's output (a3c.py:34,73)
 FWD_KEEP_STATE = 16  # arl_forward_states mode bit: LSTM keep_same_state (a3c_ale.py:57-60)
-ABI_VERSION = 3
+ABI_VERSION = 4
 ACT_CONV_ONLY = 4      # arl_act_envs mode bits (env-group staggering)
 ACT_AFTER_CONV = 8
 ENV_GROUP_ALIGN = 32   # arl_observe_envs / arl_act_envs: e0 % ENV_GROUP_ALIGN == 0

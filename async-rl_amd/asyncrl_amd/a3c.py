@@ -57,6 +57,10 @@ OVERLAP_ALLREDUCE = os.environ.get("ARL_OVERLAP_ALLREDUCE", "1") != "0"
 # a single-chain window without collectives as one C call (arl_run_window: the same launches without a
 # host round trip per step); ARL_WINDOW_C=0 issues them step by step from Python (the A arm)
 WINDOW_C = os.environ.get("ARL_WINDOW_C", "1") != "0"
+# the step-by-step FF window runs the learner's returns inside the bootstrap policy launch, as the C
+# window does; ARL_FUSE_RETURNS=0 keeps the separate returns launch (the bitwise arm of
+# test_conv_fwd_two_envs_identical)
+FUSE_RETURNS = os.environ.get("ARL_FUSE_RETURNS", "1") != "0"
 
 def _is_dqn_phi(phi) -> bool:
     """phi IS dqn_phi (dqn_phi.py:4-17): this package's function object, or the
@@ -429,7 +433,7 @@ class A3C:
             return
         if len(groups) == 1:
             # FF: the learner's returns ride on the bootstrap policy launch (as arl_run_window does)
-            fuse = net.base_arch == ARCH_FF and net.arch != ARCH_FF_NATURE
+            fuse = FUSE_RETURNS and net.base_arch == ARCH_FF and net.arch != ARCH_FF_NATURE
             if fuse:
                 net.set_returns_fusion(True, self.gamma, self.beta, self._vcoef, self.clip_reward)
             try:
@@ -440,6 +444,7 @@ class A3C:
         else:
             main = stream if stream is not None else torch.cuda.current_stream(net.device)
             side = self._side_streams(len(groups) - 1)
+            net.prepare(main)                        # stale FC planes rebuilt before the chains fork
             for s in side:
                 s.wait_stream(main)                  # fork before any chain is issued
             chains = [self._chain_steps(pair_pool, reward_pool, done_pool, pool_len, first,

@@ -10,6 +10,7 @@ compute is in libasyncrl_hip.so.
 from __future__ import annotations
 
 import ctypes
+import weakref
 
 import numpy as np
 import torch
@@ -53,6 +54,25 @@ def init_like_torch(arch: int, n_actions: int, rng: np.random.Generator):
 
 
 
+# every live DeviceNet, so a writer of a flat tensor can find the nets whose params it aliases
+_NETS: "weakref.WeakSet[DeviceNet]" = weakref.WeakSet()
+
+
+def nets_aliasing(t: torch.Tensor):
+    """The live DeviceNets whose bound params overlap the memory of `t`."""
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        return []
+    lo = t.data_ptr()
+    hi = lo + t.numel() * t.element_size()
+    out = []
+    for n in list(_NETS):
+        p = n._params
+        b = p.data_ptr()
+        if p.device == t.device and lo < b + p.numel() * p.element_size() and b < hi:
+            out.append(n)
+    return out
+
+
 def check_pools(pool_len: int, *pools):
     """pool_len against each pool's leading dimension (the C ABI checks it
     again against the extents registered with arl_net_set_pool)."""
@@ -80,12 +100,14 @@ class DeviceNet:
         self._h = h
         P = lib.arl_net_param_floats(h)
         self.param_floats = P
-        self.params = torch.zeros(P, dtype=torch.float32, device=self.device)
+        self._params = torch.zeros(P, dtype=torch.float32, device=self.device)
         self.grads = torch.zeros(P, dtype=torch.float32, device=self.device)
         self.ms = torch.zeros(P, dtype=torch.float32, device=self.device)
         self.workspace = torch.zeros(lib.arl_net_workspace_bytes(h), dtype=torch.uint8, device=self.device)
-        check(lib.arl_net_bind(h, ptr(self.params), ptr(self.grads), ptr(self.ms), ptr(self.workspace)),
+        check(lib.arl_net_bind(h, ptr(self._params), ptr(self.grads), ptr(self.ms), ptr(self.workspace)),
               "arl_net_bind")
+        self._pver = self._params._version   # (binding bumped the net's parameter generation)
+        _NETS.add(self)
         self.layout = {}
         shapes = dict(param_shapes(arch, n_actions))
         name = ctypes.create_string_buffer(64)
@@ -108,6 +130,38 @@ class DeviceNet:
         return self._h
 
     # ------------------------------------------------------------ params
+    @property
+    def params(self) -> torch.Tensor:
+        """The bound flat f32 parameters (Chainer namedparams order).  In-place
+        writes through this tensor or a view of it are seen (torch's version
+        counter) and rebuild the FC weight planes before the next forward."""
+        return self._params
+
+    @params.setter
+    def params(self, value) -> None:
+        """net.params = x copies x into the bound memory (the C library keeps
+        its pointer) and bumps the parameter generation."""
+        self._params.copy_(torch.as_tensor(value, dtype=torch.float32, device=self.device).reshape(-1))
+        self.params_changed()
+
+    def _sync_params(self) -> None:
+        """Bump the parameter generation if torch's version counter of the
+        params moved since the last bump (an in-place write from Python)."""
+        if self._params._version != self._pver:
+            self.params_changed()
+
+    def prepare(self, stream=None) -> None:
+        """Make derived device state current on `stream` (arl_net_prepare):
+        before env-range chains fork from it and before a graph replay."""
+        self._sync_params()
+        check(lib.arl_net_prepare(self._h, stream_handle(stream)), "arl_net_prepare")
+
+    def param_generation(self):
+        """(param_gen, planes_gen) of the C net: the planes are current iff equal."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib.arl_net_param_generation(self._h, ctypes.byref(a), ctypes.byref(b)), "arl_net_param_generation")
+        return a.value, b.value
+
     def view(self, flat: torch.Tensor, name: str) -> torch.Tensor:
         off, shape = self.layout[name]
         return flat[off:off + int(np.prod(shape))].view(shape)
@@ -127,8 +181,11 @@ class DeviceNet:
     def params_changed(self) -> None:
         """Tell the net its params were written from outside (arl_net_params_changed):
         derived device state (the FC weight's split planes) is rebuilt before
-        the next forward.  load_params / copy_params_from call it."""
+        the next forward.  load_params / copy_params_from / the params setter /
+        RMSpropAsync.update_arrays on these params call it; other in-place
+        writes through the tensor are caught by its version counter."""
         check(lib.arl_net_params_changed(self._h), "arl_net_params_changed")
+        self._pver = self._params._version
 
     def copy_params_from(self, other: "DeviceNet") -> None:
         """copy_param.copy_param (copy_param.py): this net's params <- other's."""
@@ -229,6 +286,7 @@ class DeviceNet:
     def act(self, t: int, mode: int = 1, stream=None, envs=None):
         """mode: 0 forward only, 1 sampled action, 2 greedy (first argmax);
         envs=(e0, ne): only envs [e0, e0 + ne) (arl_act_envs)."""
+        self._sync_params()
         if envs is not None:
             check(lib.arl_act_envs(self._h, t, envs[0], envs[1], mode, stream_handle(stream)), "arl_act_envs")
             return
@@ -284,6 +342,7 @@ class DeviceNet:
     def optimize(self, lr0=7e-4, total_steps=0, n_total=0, alpha=0.99, eps=0.1, clip=40.0, stream=None,
                  advance=False):
         """Clip + RMSProp; advance=True also ends the window (arl_optimize_advance)."""
+        self._sync_params()
         if advance:
             check(lib.arl_optimize_advance(self._h, lr0, int(total_steps), int(n_total), alpha, eps, clip,
                                            stream_handle(stream)), "arl_optimize_advance")
@@ -299,6 +358,7 @@ class DeviceNet:
         launches of observe / act / learn / optimize(advance=True) in order."""
         check_pools(pool_len, pair_pool, reward_pool, done_pool)
         self.set_pools(pair_pool, reward_pool, done_pool)
+        self._sync_params()
         check(lib.arl_run_window(self._h, ptr(pair_pool), ptr(reward_pool), ptr(done_pool), pool_len, int(first),
                                  resize_mode, gamma, beta, v_loss_coef, int(clip_reward), lr0, int(total_steps),
                                  int(n_total), alpha, eps, clip, stream_handle(stream)), "arl_run_window")
@@ -314,6 +374,7 @@ class DeviceNet:
         if states.dtype != torch.float32 or tuple(states.shape[1:]) != (c, 84, 84):
             raise ValueError(f"forward_states: need (n, {c}, 84, 84) float32 states")
         m = mode | (FWD_KEEP_STATE if keep_same_state else 0)
+        self._sync_params()
         check(lib.arl_forward_states(self._h, ptr(states), n, m, stream_handle(stream)), "arl_forward_states")
 
     # ------------------------------------------------------------ window timeline (measurement)

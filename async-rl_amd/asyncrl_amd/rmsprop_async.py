@@ -12,6 +12,7 @@ from __future__ import annotations
 import torch
 
 from ._lib import check, lib, ptr, stream_handle
+from .net import nets_aliasing
 
 
 class GradientClipping:
@@ -82,3 +83,7 @@ class RMSpropAsync:
         check(lib.arl_rmsprop(ptr(param), ptr(ms), ptr(grad), param.numel(), self.lr, self.alpha, self.eps,
                               clip, ptr(self._scratch) if clip > 0 else None, stream_handle(stream)),
               "arl_rmsprop")
+        # the kernel wrote `param` behind torch's back: a net whose params it aliases rebuilds its
+        # derived FC planes before the next forward
+        for net in nets_aliasing(param):
+            net.params_changed()

@@ -143,14 +143,21 @@ int arl_net_bind(arl_net* h, float* params, float* grads, float* ms, void* ws) {
   h->net.g = grads;
   h->net.ms = ms;
   h->net.ws = reinterpret_cast<char*>(ws);
-  h->net.planes_ok = false;
+  ++h->net.param_gen;   // new parameter memory: derived state (the FC planes) is stale
   h->bound = true;
   return ARL_OK;
 }
 
 int arl_net_params_changed(arl_net* h) {
   if (!h) return fail(ARL_EINVAL, "null net");
-  h->net.planes_ok = false;
+  ++h->net.param_gen;
+  return ARL_OK;
+}
+
+int arl_net_param_generation(const arl_net* h, uint64_t* param_gen, uint64_t* planes_gen) {
+  if (!h) return fail(ARL_EINVAL, "null net");
+  if (param_gen) *param_gen = h->net.param_gen;
+  if (planes_gen) *planes_gen = h->net.planes_gen;
   return ARL_OK;
 }
 
@@ -159,6 +166,11 @@ int arl_net_params_changed(arl_net* h) {
     if (!(h)) return fail(ARL_EINVAL, "null net");                            \
     if (!(h)->bound) return fail(ARL_ESTATE, "net not bound (arl_net_bind)"); \
   } while (0)
+
+int arl_net_prepare(arl_net* h, void* s) {
+  NEED_BOUND(h);
+  return hip_status(arl::ensure_fc_planes(h->net, S(s)), "net_prepare");
+}
 
 int arl_net_reset(arl_net* h, void* s) {
   NEED_BOUND(h);
@@ -170,6 +182,7 @@ int arl_net_reset(arl_net* h, void* s) {
   if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_norm, 0, (size_t)arl::NORM_SCRATCH * 8, S(s));
   if (e == hipSuccess && n.w_fcb_tick)
     e = hipMemsetAsync(n.ws + n.w_fcb_tick, 0, (size_t)arl::fc_bwd_tickets() * 4, S(s));
+  n.returns_done = false;
   if (e == hipSuccess && n.arch == arl::ARCH_LSTM) {
     e = hipMemsetAsync(n.ws + n.w_hbuf, 0, (size_t)(n.T + 2) * n.N * arl::HID * 4, S(s));
     if (e == hipSuccess) e = hipMemsetAsync(n.ws + n.w_cbuf, 0, (size_t)(n.T + 2) * n.N * arl::HID * 4, S(s));
@@ -198,6 +211,10 @@ int arl_net_set_pool(arl_net* h, int kind, const void* pool, int64_t bytes) {
   }
   tab[slot].base = bytes > 0 ? b : 0;
   tab[slot].bytes = bytes;
+  // a registration overlapping the new one belongs to memory that was freed and reused: drop it
+  for (int i = 0; i < 8 && bytes > 0; ++i)
+    if (i != slot && tab[i].bytes > 0 && tab[i].base < b + (uintptr_t)bytes && b < tab[i].base + (uintptr_t)tab[i].bytes)
+      tab[i] = arl_net::Pool{};
   return ARL_OK;
 }
 
@@ -206,15 +223,19 @@ int arl_net_set_pool(arl_net* h, int kind, const void* pool, int64_t bytes) {
 static int check_pool(const arl_net* h, int kind, const void* pool, int64_t pool_len, int64_t unit, const char* what) {
   if (!pool) return 0;
   const uintptr_t p = reinterpret_cast<uintptr_t>(pool);
+  // the registration with the greatest base <= p whose range holds p: a stale, larger registration of a
+  // freed pool that also spans p never lends its room to a newer pool allocated inside it
+  const arl_net::Pool* best = nullptr;
   for (const arl_net::Pool& r : h->pools[kind]) {
     if (r.bytes <= 0 || p < r.base || p >= r.base + (uintptr_t)r.bytes) continue;
-    const int64_t room = (int64_t)(r.base + (uintptr_t)r.bytes - p);
-    if (unit > 0 && pool_len > room / unit)
-      return fail(ARL_EINVAL, std::string("observe: pool_len ") + std::to_string(pool_len) + " exceeds the " + what +
-                                  " pool (" + std::to_string(room / unit) + " entries registered)");
-    return 0;
+    if (!best || r.base > best->base) best = &r;
   }
-  return fail(ARL_EINVAL, std::string("observe: the ") + what + " pool is not registered (arl_net_set_pool)");
+  if (!best) return fail(ARL_EINVAL, std::string("observe: the ") + what + " pool is not registered (arl_net_set_pool)");
+  const int64_t room = (int64_t)(best->base + (uintptr_t)best->bytes - p);
+  if (unit > 0 && pool_len > room / unit)
+    return fail(ARL_EINVAL, std::string("observe: pool_len ") + std::to_string(pool_len) + " exceeds the " + what +
+                                " pool (" + std::to_string(room / unit) + " entries registered)");
+  return 0;
 }
 
 // validates an observation and fills its ring arguments (0 = ok)
@@ -309,6 +330,7 @@ int arl_truncate_window(arl_net* h, int t_len, void* s) {
   NEED_BOUND(h);
   arl::Net& n = h->net;
   if (t_len < 1 || t_len > n.T) return fail(ARL_EINVAL, "truncate_window: t_len out of [1, t_max]");
+  n.returns_done = false;   // a truncated window's learn runs its own returns
   if (t_len == n.T) return ARL_OK;
   const size_t rows = (size_t)(n.T - t_len) * n.N;
   hipError_t e = hipMemsetAsync(n.ws + n.w_dones + (size_t)t_len * n.N, 2, rows, S(s));
@@ -386,6 +408,9 @@ int arl_act_envs(arl_net* h, int t, int e0, int ne, int mode, void* s) {
     return fail(ARL_EINVAL, "act: mode must be 0 / 1 / 2, optionally | ARL_ACT_CONV_ONLY or ARL_ACT_AFTER_CONV");
   if (int rc = check_env_range(h->net, e0, ne)) return rc;
   if (part != 0 && h->net.arch == arl::ARCH_FF_NATURE) return fail(ARL_EINVAL, "act: Nature head has no conv split");
+  if (ne != h->net.N && !h->net.planes_current() && h->net.arch != arl::ARCH_FF_NATURE)
+    return fail(ARL_ESTATE, "act: the params changed since the FC weight planes were built; call arl_net_prepare on "
+                            "the stream the env-range chains fork from before issuing them");
   return hip_status(arl::net_act(h->net, t, mode, S(s), e0, ne), "act");
 }
 

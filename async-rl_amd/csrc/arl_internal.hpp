@@ -118,9 +118,13 @@ struct Net {
   // nothing changes the gradient between arl_learn and the update, e.g. no all-reduce):
   // norm_ready = the last arl_learn left the partials, consumed by the next update
   bool norm_fold = false, norm_ready = false;
-  // the FC weight's split planes (w_fcplanes) match the params: false after bind / arl_net_params_changed;
-  // the next forward rebuilds them (fc_planes_kernel), every update keeps them current (rmsprop_kernel)
-  bool planes_ok = false;
+  // parameter generations: every writer of the params the library does not make itself bumps param_gen
+  // (arl_net_bind, arl_net_params_changed); planes_gen = the generation the FC weight's split planes
+  // (w_fcplanes) were built from.  A forward over all envs rebuilds stale planes on its own stream
+  // (fc_planes_kernel); an env-range forward refuses them (arl_net_prepare first, before the streams
+  // fork); every in-window update rewrites all planes from the new W (rmsprop_kernel).
+  uint64_t param_gen = 1, planes_gen = 0;
+  bool planes_current() const { return planes_gen == param_gen; }
   // the learner's returns folded into the bootstrap step's policy launch (FF, arl_run_window):
   // fuse_returns = on, with the learn arguments below, for the window's slot-T forward; returns_done = that
   // launch ran, so the window's LEARN_RETURNS part is a no-op
@@ -165,6 +169,7 @@ bool net_init(Net& net, int arch, int n_actions, int n_envs, int t_max, int env_
 // the step split after its conv launch); envs [e0, e0 + ne) (ne < 0: all)
 constexpr int ACT_CONV_ONLY = 4, ACT_AFTER_CONV = 8;
 hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0 = 0, int ne = -1);
+hipError_t ensure_fc_planes(Net& net, hipStream_t s);   // rebuild the FC weight planes if stale (net.hip)
 // learner parts (net_learn_part), in this order on one stream
 enum { LEARN_RETURNS = 0, LEARN_TRUNK, LEARN_CONV, LEARN_PARTS };
 hipError_t net_learn_part(Net& net, int part, double gamma, float beta, float vcoef, int clip_reward, hipStream_t s);

@@ -287,12 +287,12 @@ static uint32_t* a2_mask(const Net& net, int t) {
   return net.at<uint32_t>(net.w_a2m) + (int64_t)t * net.N * A2W;
 }
 
-// the FC weight's split planes (fc.hip): rebuilt from the params when they may have changed behind the
-// net's back (bind, arl_net_params_changed); every update keeps them current
-static hipError_t ensure_fc_planes(Net& net, hipStream_t s) {
-  if (net.planes_ok || net.arch == ARCH_FF_NATURE) return hipSuccess;
+// the FC weight's split planes (fc.hip): rebuilt from the params when a writer bumped the parameter
+// generation since they were built (bind, arl_net_params_changed); every update keeps them current
+hipError_t ensure_fc_planes(Net& net, hipStream_t s) {
+  if (net.planes_current() || net.arch == ARCH_FF_NATURE) return hipSuccess;
   ARL_TRY(launch_fc_planes(net.p + net.o_fcW, net.at<uint16_t>(net.w_fcplanes), s));
-  net.planes_ok = true;
+  net.planes_gen = net.param_gen;
   return hipSuccess;
 }
 static const uint16_t* fc_planes(const Net& net) { return net.at<uint16_t>(net.w_fcplanes); }
@@ -331,7 +331,13 @@ hipError_t net_act(Net& net, int t, int mode, hipStream_t s, int e0, int ne) {
   const int n = net.N, A = net.A;
   const int part = mode & (ACT_CONV_ONLY | ACT_AFTER_CONV);
   mode &= 3;
+  // an env range forks from the caller's stream: stale planes rebuilt on one chain's stream would race
+  // the other chains' FC reads (the ABI refuses that case first, arl_act_envs)
+  if (ne != n && !net.planes_current()) return hipErrorNotReady;
   ARL_TRY(ensure_fc_planes(net, s));
+  // a fused bootstrap launch whose learn never followed (a dropped window) must not make a later
+  // window's learn skip its returns: any act of a window's step t < T starts a new window
+  if (t < net.T) net.returns_done = false;
   // the bootstrap slot T feeds only the FC / heads forward: no backward reads its a1 or a2 mask
   // (the ring-frame conv kernels skip those stores: 25.6 KB an env)
   float* a1 = net.at<float>(net.w_a1) + (int64_t)t * n * A1;
@@ -687,7 +693,7 @@ hipError_t net_optimize(Net& net, double lr0, int64_t total_steps, int64_t n_tot
   const AdvanceArgs adv{fused ? net.at<int64_t>(net.w_ctl) : nullptr, planes, net.o_fcW, net.at<uint8_t>(net.w_reset),
                         L ? net.at<float>(net.w_hbuf) : nullptr, L ? net.at<float>(net.w_cbuf) : nullptr, net.T,
                         net.N};
-  if (planes != nullptr) net.planes_ok = true;
+  if (planes != nullptr) net.planes_gen = net.param_gen;
   ARL_TRY(launch_rmsprop(net.p, net.ms, net.g, net.param_floats, lr0, alpha, eps, do_clip ? parts : nullptr,
                          folded ? conv_norm_parts(net.norm_rest_blocks) : net.norm_blocks, clip, total_steps > 0 ? net.at<int64_t>(net.w_ctl) : nullptr, total_steps,
                          n_total, net.T, s, &adv));

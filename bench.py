@@ -129,6 +129,10 @@ def parse():
                          "'secondary'; auto: c3 beside the default c4 line at N = 1; none disables")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="0 disables the CPU baseline leg")
     ap.add_argument("--kernel-reps", type=int, default=50)
+    ap.add_argument("--timed-diag", type=int, default=0,
+                    help="diagnostic (off by default): after the timed region, repeat its shape (sync, K windows, "
+                         "sync) this many times with a HIP event after every window, to attribute the gap between "
+                         "the timed mean and the per-window median (first window vs the rest, host edges)")
     return ap.parse_args()
 
 
@@ -570,6 +574,37 @@ def secondary_line(a, pkg, dev, workload):
     return out
 
 
+def timed_region_diag(a, window, stream):
+    """The timed region's shape again (synchronize, K windows, synchronize),
+    a.timed_diag times, with a HIP event recorded before the first window and
+    after each one: per repetition the host-timed mean, the event-timed
+    windows (first one apart), and the host time outside the events (launch
+    of the first kernel, the final synchronize).  Half the repetitions start
+    after a 20 ms idle sleep (a clock ramp would show in their first windows)."""
+    reps = []
+    for r in range(a.timed_diag):
+        if r % 2 == 1:
+            time.sleep(0.02)
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(stream):
+            evs[0].record(stream)
+            for i in range(a.steps):
+                window()
+                evs[i + 1].record(stream)
+        stream.synchronize()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(a.steps)]
+        reps.append({"idle_before_ms": 20 if r % 2 == 1 else 0, "host_mean_ms": round(1e3 * el / a.steps, 4),
+                     "event_mean_ms": round(float(np.mean(ms)), 4), "first_ms": round(ms[0], 4),
+                     "second_ms": round(ms[1], 4) if len(ms) > 1 else None,
+                     "rest_median_ms": round(float(np.median(ms[1:])), 4) if len(ms) > 1 else None,
+                     "outside_events_ms": round(1e3 * el - float(np.sum(ms)), 4)})
+    return reps
+
+
 def main(a):
     mp_ctx = None
     if a.cpu_seconds > 0 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
@@ -688,6 +723,8 @@ def main(a):
     units = N * T * world * a.steps
     value = units / elapsed
     ms_step = 1e3 * elapsed / a.steps
+
+    diag = timed_region_diag(a, window, stream) if a.timed_diag > 0 else None
 
     # per-window distribution (median over >= 100 windows): more
     # windows after the timed region, each between two HIP events on the bench
@@ -993,6 +1030,7 @@ def main(a):
             "allreduce_bytes_per_window": (4 * model.net.grads.numel()) if collectives else 0,
             "replicas_identical": replicas,
             "windows": windows, "timeline": timeline, "hbm_copy_peak": copy_peak,
+            **({"timed_region_diag": diag} if diag is not None else {}),
             "roofline": roof, "kernels": kernels, "cpu_baseline": cpu, "params_finite": finite,
             "secondary": secondary,
         }

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define ARL_ABI_VERSION 3
+#define ARL_ABI_VERSION 4
 
 #define ARL_OK 0
 #define ARL_EINVAL 1   /* bad argument (shape, pointer, alignment) */
@@ -102,11 +102,21 @@ int arl_net_buffer(const arl_net* net, const char* name, int64_t* offset, int64_
  * 16-byte aligned; grads must be zeroed once by the caller) and workspace. */
 int arl_net_bind(arl_net* net, float* params, float* grads, float* ms, void* workspace);
 
-/* The caller wrote the bound params (a checkpoint load, a copy from another
- * model): derived device state is rebuilt before the next forward -- the FC
- * weight's bf16 split planes, which every arl_optimize* keeps current
- * (no reference counterpart; copy_param.py / serializers write params there). */
+/* Parameter generations (ABI 4).  The FC forward reads the FC weight as bf16
+ * split planes derived from the bound params; every arl_optimize* /
+ * arl_run_window update keeps them current.  Any OTHER writer of the bound
+ * params -- a checkpoint load, a copy from another model (copy_param.py,
+ * serializers), arl_rmsprop on the params -- must bump the generation with
+ * arl_net_params_changed; arl_net_bind bumps it too.  A forward over all envs
+ * rebuilds stale planes on its own stream; arl_net_prepare rebuilds them on a
+ * given stream (call it on the stream env-range chains fork from, and before
+ * replaying a captured window after such a write: a replay has no rebuild);
+ * arl_act_envs over a proper env range refuses stale planes with ARL_ESTATE.
+ * arl_net_param_generation reads both generations (planes current iff equal).
+ * No reference counterpart: the reference's forward reads the f32 params. */
 int arl_net_params_changed(arl_net* net);
+int arl_net_prepare(arl_net* net, void* stream);
+int arl_net_param_generation(const arl_net* net, uint64_t* param_gen, uint64_t* planes_gen);
 
 /* Reset the control block (step counters) and the frame ring; call once
  * before the first observation (async). */

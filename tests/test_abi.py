@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_errors():
     from asyncrl_amd._lib import lib
-    assert lib.arl_abi_version() == 3
+    assert lib.arl_abi_version() == 4
     h = ctypes.c_void_p()
     rc = lib.arl_net_create(ctypes.byref(h), 7, 4, 16, 5, 0, 0)
     assert rc == 1 and b"arch" in lib.arl_last_error()
