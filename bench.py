@@ -528,21 +528,23 @@ def secondary_line(a, pkg, dev, workload):
     graph = None
     with torch.cuda.stream(stream):
         agent.run_window(pairs, rewards, dones, P, first=True, stream=stream)
-        for _ in range(max(0, a.warmup - 1)):
-            agent.run_window(pairs, rewards, dones, P, stream=stream)
-        if groups > 1:
+        if groups > 1:   # captured before the warmup windows, which then run right before the timed ones
+            agent.run_window(pairs, rewards, dones, P, stream=stream)   # (creates the side streams)
             stream.synchronize()
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, stream=stream):
                 agent.run_window(pairs, rewards, dones, P, stream=stream)
-            graph.replay()
-    stream.synchronize()
 
     def window():
         if graph is not None:
             graph.replay()
         else:
             agent.run_window(pairs, rewards, dones, P, stream=stream)
+
+    with torch.cuda.stream(stream):
+        for _ in range(max(0, a.warmup - 1)):
+            window()
+    stream.synchronize()
 
     torch.cuda.synchronize()
     t0 = time.perf_counter()

@@ -193,5 +193,38 @@ def test_c_abi_rejects_pools_it_does_not_know():
         assert b"reward" in lib.arl_last_error()
         assert lib.arl_net_set_pool(h, POOL_REWARDS, rew, 0) == 0           # removed
         assert lib.arl_observe(h, 1, pairs, rew, done, 1, 0, 0, None) == EINVAL
+        # a freed pool's stale, larger registration must not lend its room to a newer, smaller
+        # pool allocated inside it -- registering the new pool drops every overlapping registration
+        big, small = fake + (4 << 30), fake + (4 << 30) + 2 * N * PAIR
+        assert lib.arl_net_set_pool(h, POOL_REWARDS, rew, 8 * N * 4) == 0
+        assert lib.arl_net_set_pool(h, POOL_FRAMES, big, 8 * N * PAIR) == 0
+        assert lib.arl_net_set_pool(h, POOL_FRAMES, small, 2 * N * PAIR) == 0   # (big freed, memory reused)
+        assert lib.arl_observe(h, 1, small, rew, done, 3, 0, 0, None) == EINVAL
+        assert b"exceeds" in lib.arl_last_error()
+        assert lib.arl_observe(h, 1, big, rew, done, 1, 0, 0, None) == EINVAL  # the stale one is gone
+        assert b"not registered" in lib.arl_last_error()
+    finally:
+        lib.arl_net_destroy(h)
+
+
+def test_param_generation_without_device():
+    """ABI 4 parameter generations on a bound handle (fake, never-dereferenced pointers; no launch):
+    binding and arl_net_params_changed bump param_gen; the FC planes are stale until a forward or
+    arl_net_prepare rebuilds them, so an env-range act refuses to run."""
+    from asyncrl_amd._lib import lib
+    h = ctypes.c_void_p()
+    assert lib.arl_net_create(ctypes.byref(h), 0, 4, 64, 5, 0, 0) == 0
+    try:
+        pg, pl = ctypes.c_uint64(), ctypes.c_uint64()
+        assert lib.arl_net_param_generation(h, ctypes.byref(pg), ctypes.byref(pl)) == 0
+        g0 = pg.value
+        fake = 1 << 40
+        assert lib.arl_net_bind(h, fake, fake, fake, fake) == 0
+        assert lib.arl_net_param_generation(h, ctypes.byref(pg), ctypes.byref(pl)) == 0
+        assert pg.value == g0 + 1 and pl.value != pg.value
+        assert lib.arl_net_params_changed(h) == 0
+        assert lib.arl_net_param_generation(h, ctypes.byref(pg), None) == 0 and pg.value == g0 + 2
+        assert lib.arl_act_envs(h, 0, 0, 32, 1, None) == 3                     # ARL_ESTATE: stale planes
+        assert b"arl_net_prepare" in lib.arl_last_error()
     finally:
         lib.arl_net_destroy(h)
