@@ -57,24 +57,6 @@ __device__ inline uint32_t px_pair_bf16(uint32_t w, int b) {
 // residuals on the packed f32 adder (9 instructions a pair instead of 12).  Exact: x - RN(x) has <= 16
 // significant bits, its residual <= 8, so the third piece is exact in bf16 and x = h + m + l.  The pieces
 // differ from split3's (rounded, not truncated); the 6-term products are as exact
-#ifdef ARL_SPLIT_SCALAR
-// (experiment) the residuals as scalar v_sub_f32 (opaque to the SLP packer): packed f32 VALU between
-// MFMAs costs more than its issue slot (MI355X_MICROARCH.md, constants table)
-__device__ inline float sub_f32(float a, float b) {
-  float r;
-  asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-__device__ inline void split3_pack_rn(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l) {
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
-  h = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2{x0, x1}), b2));
-  const float r10 = sub_f32(x0, __uint_as_float(h << 16)), r11 = sub_f32(x1, __uint_as_float(h & 0xffff0000u));
-  m = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2{r10, r11}), b2));
-  const float r20 = sub_f32(r10, __uint_as_float(m << 16)), r21 = sub_f32(r11, __uint_as_float(m & 0xffff0000u));
-  l = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2{r20, r21}), b2));
-}
-#else
 __device__ inline void split3_pack_rn(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   typedef __bf16 b2 __attribute__((ext_vector_type(2)));
@@ -85,7 +67,6 @@ __device__ inline void split3_pack_rn(float x0, float x1, uint32_t& h, uint32_t&
   const f2 r2 = r1 - f2{__uint_as_float(m << 16), __uint_as_float(m & 0xffff0000u)};
   l = __builtin_bit_cast(uint32_t, __builtin_convertvector(r2, b2));
 }
-#endif
 
 // split 8 f32 (one lane's 8 k of a 16x16x32 fragment) into three bf16x8 planes (round-to-nearest pieces:
 // fc_bwd 64.3 -> 61.7 us, conv_bwd 106.8 -> 105.2 us in the C4 window against the truncating split, r5m)

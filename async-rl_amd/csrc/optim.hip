@@ -21,9 +21,7 @@
 // 20 bytes move per parameter (read p, g, ms; write p, ms) + 4 for the norm.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 
-#include <algorithm>
 
 #include "arl_internal.hpp"
 
@@ -164,104 +162,6 @@ rmsprop_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __res
   }
 }
 
-// U float4 of p / ms / g per thread, all 3 U loads issued before the norm re-reduce: block b owns the
-// contiguous float4 run [b * 256 U, (b + 1) * 256 U) (lane-consecutive within each of its U slices).
-// Grid-stride past the first pass (n4 > grid * 256 U).
-template <int U>
-__global__ void __launch_bounds__(256)
-rmsprop_u_kernel(float* __restrict__ p, float* __restrict__ ms, const float* __restrict__ g, int64_t n, RmsConst c,
-                 const double* __restrict__ norm_sq, int nparts, float clip, AdvanceArgs adv) {
-  __shared__ double sh[8];
-  if (c.ctl != nullptr && c.total > 0) {
-    const int64_t gt = (c.ctl[c.ctl_idx] + c.t_max) * c.n_total;
-    c.lr = (float)(((double)max(c.total - gt - 1, (int64_t)0) / (double)c.total) * c.lr0);
-  }
-  const int64_t n4 = n >> 2;
-  float4* p4 = reinterpret_cast<float4*>(p);
-  float4* m4 = reinterpret_cast<float4*>(ms);
-  const float4* g4 = reinterpret_cast<const float4*>(g);
-  const int64_t span = (int64_t)gridDim.x * 256 * U;
-  const int64_t b0 = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
-  float4 pv[U], mv[U], gv[U];
-  auto load = [&](int64_t base) {
-#pragma unroll
-    for (int k = 0; k < U; ++k) {   // clamped duplicates past the end, never stored
-      const int64_t i = min(base + 256 * k, n4 - 1);
-      pv[k] = p4[i];
-      mv[k] = m4[i];
-      gv[k] = g4[i];
-    }
-  };
-  if (n4 > 0) load(b0);
-  float scale = 1.f;
-  bool do_clip = false;
-  if (norm_sq != nullptr) {
-    double t = 0.0, v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = norm_sq[min((int)threadIdx.x + 256 * k, nparts - 1)];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if ((int)threadIdx.x + 256 * k < nparts) t += v[k];
-    t = block_sum_f64(t, sh);
-    const double norm = sqrt(t);
-    const double rate = (double)clip / norm;
-    if (norm > 0.0 && rate < 1.0) {
-      do_clip = true;
-      scale = (float)rate;
-    }
-  }
-  for (int64_t base = b0; base < n4; base += span) {
-    if (base != b0) load(base);
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const int64_t ib = base + 256 * k;
-      if (ib >= n4) break;
-      float4 gk = gv[k], pk = pv[k], mk = mv[k];
-      if (do_clip) {
-        gk.x = __fmul_rn(gk.x, scale); gk.y = __fmul_rn(gk.y, scale);
-        gk.z = __fmul_rn(gk.z, scale); gk.w = __fmul_rn(gk.w, scale);
-      }
-      rms1(pk.x, mk.x, gk.x, c);
-      rms1(pk.y, mk.y, gk.y, c);
-      rms1(pk.z, mk.z, gk.z, c);
-      rms1(pk.w, mk.w, gk.w, c);
-      p4[ib] = pk;
-      m4[ib] = mk;
-      const int64_t e = 4 * ib - adv.fc_w0;
-      if (adv.fc_planes != nullptr && e >= 0 && e < (int64_t)HID * A2) fc_planes_store(adv.fc_planes, (int)e, pk);
-    }
-  }
-  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x, gsz = (int64_t)gridDim.x * 256;
-  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
-    const int64_t j = (n4 << 2) + threadIdx.x;
-    float gt = g[j];
-    if (do_clip) gt = __fmul_rn(gt, scale);
-    float pt = p[j], mt = ms[j];
-    rms1(pt, mt, gt, c);
-    p[j] = pt;
-    ms[j] = mt;
-  }
-  if (adv.ctl == nullptr) return;   // (no window advance)
-  for (int64_t i = i0; i < adv.n; i += gsz) adv.reset[i] = adv.reset[(int64_t)adv.T * adv.n + i];
-  if (adv.hbuf != nullptr)
-    for (int64_t i = i0; i < (int64_t)adv.n * HID; i += gsz) {
-      adv.hbuf[i] = adv.hbuf[(int64_t)adv.T * adv.n * HID + i];
-      adv.cbuf[i] = adv.cbuf[(int64_t)adv.T * adv.n * HID + i];
-    }
-  if (i0 == 0) {
-    adv.ctl[CTL_STEP] += adv.T;
-    adv.ctl[CTL_WINDOW] += 1;
-  }
-}
-
-// RMSProp form (A/B): ARL_RMS_U = 1 (default: rmsprop_kernel, one float4 a thread, grid-stride), 2 or 4
-// (rmsprop_u_kernel)
-static const int RMS_U = [] {
-  const char* e = getenv("ARL_RMS_U");
-  const int u = e == nullptr ? 1 : atoi(e);
-  return u == 2 || u == 4 ? u : 1;
-}();
-
 static int stream_blocks(int64_t n) {
   int64_t b = (n / 4 + 255) / 256;
   if (b > 2048) b = 2048;
@@ -294,17 +194,6 @@ hipError_t launch_rmsprop(float* p, float* ms, const float* g, int64_t n, double
   c.ctl_idx = (adv != nullptr && adv->ctl != nullptr) ? CTL_STEP_SNAP : CTL_STEP;
   AdvanceArgs a{};
   if (adv != nullptr) a = *adv;
-  if (RMS_U > 1) {
-    int64_t blocks = (n / 4 + 256 * RMS_U - 1) / (256 * RMS_U);
-    blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, 2048));
-    if (RMS_U == 2)
-      hipLaunchKernelGGL(rmsprop_u_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, s, p, ms, g, n, c, norm_sq, nparts,
-                         clip, a);
-    else
-      hipLaunchKernelGGL(rmsprop_u_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, s, p, ms, g, n, c, norm_sq, nparts,
-                         clip, a);
-    return hipGetLastError();
-  }
   hipLaunchKernelGGL(rmsprop_kernel, dim3(stream_blocks(n)), dim3(256), 0, s, p, ms, g, n, c, norm_sq, nparts, clip, a);
   return hipGetLastError();
 }

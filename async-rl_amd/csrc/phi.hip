@@ -19,9 +19,6 @@
 // resize reads them back and writes 4 output pixels per thread as one u32.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
-
-#include <algorithm>
 
 #include "arl_internal.hpp"
 #include "phi_ops.hpp"
@@ -149,89 +146,6 @@ phi_ring_kernel(RingArgs a) {
   uint8_t* dst = a.frames + ((int64_t)slot * a.n + e) * PLANE;
   phi_band(pr, pr + FRAME_BYTES, dst, blockIdx.x * BAND, a.mode, sh);
   if (blockIdx.x == 0 && threadIdx.x == 0) ring_obs_store(a, e, k, ring_obs_load(a, e, k));
-}
-
-// Persistent form of phi_ring_kernel: G workgroups stream the launch's (env, band) items, item i =
-// (env i / 7, band i % 7), workgroup b taking items b, b + G, ...; the next item's frame-row loads (six
-// 16-byte loads a staging thread) are issued before the current item's max / luminance / resize, so a
-// workgroup always has one item's bytes in flight while it computes another.  The x resize table is
-// tabulated once per workgroup.  Same arithmetic and stores as phi_band: bit-identical.
-struct PhiRows {
-  uint4 c0, c1, c2, p0, p1, p2;
-};
-__device__ inline void phi_rows_load(const uint8_t* __restrict__ pr, int dy0, int mode, PhiRows& v) {
-  const int tid = threadIdx.x;
-  const int r = tid / 10, c = tid % 10;
-  const int ly = min(r >> 1, BAND - 1), tap = r & 1;   // (threads past the 240 stagers reload row 11)
-  int o, b0, b1;
-  if (mode & 2) resize_coeff(dy0 + ly + CROP_TOP, SRC_H, CROP_H, o, b0, b1);
-  else resize_coeff(dy0 + ly, SRC_H, DST, o, b0, b1);
-  int sy = o + tap;
-  if (sy > SRC_H - 1) sy = SRC_H - 1;
-  const uint4* pc = reinterpret_cast<const uint4*>(pr + (size_t)sy * SRC_W * 3 + c * 48);
-  const uint4* pp = reinterpret_cast<const uint4*>(pr + FRAME_BYTES + (size_t)sy * SRC_W * 3 + c * 48);
-  v.c0 = pc[0]; v.c1 = pc[1]; v.c2 = pc[2];
-  v.p0 = pp[0]; v.p1 = pp[1]; v.p2 = pp[2];
-}
-
-__global__ void __launch_bounds__(256)
-phi_ring_persist_kernel(RingArgs a, int nitems) {
-  __shared__ PhiShared sh;
-  const int tid = threadIdx.x;
-  const int64_t k = a.ctl[CTL_STEP] + a.t;
-  const int slot = (int)(k % a.R);
-  const int64_t pidx = k % a.pool_len;
-  const uint8_t* pool = a.pair_pool + pidx * a.n * (int64_t)(2 * FRAME_BYTES);
-  uint8_t* frames = a.frames + (int64_t)slot * a.n * PLANE;
-  auto item_env = [&](int i) { return a.e0 + i / NBANDS; };
-  auto item_dy0 = [&](int i) { return (i % NBANDS) * BAND; };
-  int item = blockIdx.x;
-  PhiRows cur, nxt;
-  if (item < nitems) phi_rows_load(pool + (int64_t)item_env(item) * (2 * FRAME_BYTES), item_dy0(item), a.mode, cur);
-  if (tid < DST) {
-    int o, a0, a1;
-    resize_coeff(tid, SRC_W, DST, o, a0, a1);
-    sh.xofs[tid] = (int16_t)o; sh.xa0[tid] = (int16_t)a0; sh.xa1[tid] = (int16_t)a1;
-  }
-  for (; item < nitems; item += gridDim.x) {
-    const int e = item_env(item), dy0 = item_dy0(item);
-    const int nx = min(item + (int)gridDim.x, nitems - 1);   // unconditional (clamped): in flight meanwhile
-    phi_rows_load(pool + (int64_t)item_env(nx) * (2 * FRAME_BYTES), item_dy0(nx), a.mode, nxt);
-    const bool obs = dy0 == 0 && tid == 0;
-    RingObs ob;
-    if (obs) ob = ring_obs_load(a, e, k);
-    if (tid >= 96 && tid < 96 + BAND) {
-      int o, b0, b1;
-      if (a.mode & 2) resize_coeff(dy0 + tid - 96 + CROP_TOP, SRC_H, CROP_H, o, b0, b1);
-      else resize_coeff(dy0 + tid - 96, SRC_H, DST, o, b0, b1);
-      sh.yofs[tid - 96] = (int16_t)o; sh.yb0[tid - 96] = (int16_t)b0; sh.yb1[tid - 96] = (int16_t)b1;
-    }
-    if (tid < 2 * BAND * 10) {
-      const int r = tid / 10, c = tid % 10;
-      *reinterpret_cast<uint4*>(&sh.gray[r >> 1][r & 1][c * 16]) =
-          max_luminance16(cur.c0, cur.c1, cur.c2, cur.p0, cur.p1, cur.p2);
-    }
-    __syncthreads();
-    if (tid < BAND * (DST / 4)) {
-      const int ly = tid / (DST / 4), q = tid % (DST / 4);
-      const int b0 = sh.yb0[ly], b1 = sh.yb1[ly];
-      uint32_t packed = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int dx = q * 4 + j;
-        const int sx = sh.xofs[dx];
-        const int sx1 = sx + 1 < SRC_W ? sx + 1 : SRC_W - 1;
-        const int a0 = sh.xa0[dx], a1 = sh.xa1[dx];
-        const int r0 = (int)sh.gray[ly][0][sx] * a0 + (int)sh.gray[ly][0][sx1] * a1;
-        const int r1 = (int)sh.gray[ly][1][sx] * a0 + (int)sh.gray[ly][1][sx1] * a1;
-        packed |= (uint32_t)resize_vpass(r0, r1, b0, b1, a.mode) << (8 * j);
-      }
-      ring_store(reinterpret_cast<uint32_t*>(frames + (int64_t)e * PLANE + (size_t)(dy0 + ly) * DST + q * 4), packed);
-    }
-    if (obs) ring_obs_store(a, e, k, ob);
-    __syncthreads();   // the next item rewrites the gray rows and the y table
-    cur = nxt;
-  }
 }
 
 // ---------------------------------------------------------------- RGB (Doom)
@@ -443,22 +357,8 @@ hipError_t launch_phi_stack(const uint8_t* pairs, const uint8_t* prev_stack, con
   return hipGetLastError();
 }
 
-// ARL_PHI_PERSIST=k (A/B): the persistent form with k workgroups a CU (256 CUs); unset / 0: one workgroup
-// per (band, env)
-static const int PHI_PERSIST = [] {
-  const char* e = getenv("ARL_PHI_PERSIST");
-  return e == nullptr ? 0 : atoi(e);
-}();
-
 hipError_t launch_phi_ring(const RingArgs& a, hipStream_t s) {
-  const int ne = a.ne < 0 ? a.n : a.ne;
-  if (PHI_PERSIST > 0) {
-    const int items = NBANDS * ne;
-    const int grid = std::min(items, 256 * PHI_PERSIST);
-    hipLaunchKernelGGL(phi_ring_persist_kernel, dim3(grid), dim3(256), 0, s, a, items);
-    return hipGetLastError();
-  }
-  hipLaunchKernelGGL(phi_ring_kernel, dim3(NBANDS, (unsigned)ne), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(phi_ring_kernel, dim3(NBANDS, (unsigned)(a.ne < 0 ? a.n : a.ne)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
