@@ -604,8 +604,35 @@ __device__ inline void prefetch_x_ws(const ConvBwdArgs& a, int r0, int s, int ty
   }
 }
 
+// D2 and DA of one sample together (conv_bwd_ws2_kernel): one grid item, one split
+__device__ inline void commit_d2_da(const float (&r)[8], uint8_t* lds, int ty, float (&b2a)[8]) {
+  int grp, cell, p;
+  bool v;
+  const int i = opaque(ty);
+  grid_item(i, grp, cell, v, p);
+  if (i >= GI) return;
+  uint32_t h[4], m[4], l[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) split3_pack(v ? r[2 * k] : 0.f, v ? r[2 * k + 1] : 0.f, h[k], m[k], l[k]);
+  uint8_t* dd = lds + L2_D2 + d2_slot(cell, grp);
+  *reinterpret_cast<uint4*>(dd) = make_uint4(h[0], h[1], h[2], h[3]);
+  *reinterpret_cast<uint4*>(dd + D2P) = make_uint4(m[0], m[1], m[2], m[3]);
+  *reinterpret_cast<uint4*>(dd + 2 * D2P) = make_uint4(l[0], l[1], l[2], l[3]);
+  if (!v) return;
+  uint8_t* da = lds + L2_DA + (8 * grp) * DA_ROW + 2 * p;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int sh = 16 * (k & 1);
+    *reinterpret_cast<uint16_t*>(da + k * DA_ROW) = (uint16_t)(h[k >> 1] >> sh);
+    *reinterpret_cast<uint16_t*>(da + k * DA_ROW + DAP) = (uint16_t)(m[k >> 1] >> sh);
+    *reinterpret_cast<uint16_t*>(da + k * DA_ROW + 2 * DAP) = (uint16_t)(l[k >> 1] >> sh);
+    b2a[k] = __fadd_rn(b2a[k], r[k]);
+  }
+}
+
 // screens -> phase rows (commit_x with the Y thread index ty)
-__device__ inline void commit_x_ws(const PrefetchX& r, uint8_t* lds, int ty) {
+__device__ inline void commit_x_ws(const PrefetchX& r, uint8_t* lds, int ty_) {
+  const int ty = opaque(ty_);
   const int nv = __shfl(r.nv, 0);
   if (ty >= 504) return;
   const int y = ty / 6, q = ty - 6 * (ty / 6);
@@ -672,7 +699,7 @@ __device__ inline void step1_wave(const uint8_t* lds, int wy, int lane_, f32x4 (
 // phase stamps (diagnostic builds only: make variant DEFS=-DARL_CB_WS_STAMP): workgroups 0-7, wave 0 (X) and
 // wave 8 (Y), shader clock at the start / end of each phase's work, sample k < 15; k = 15 the prologue
 #ifdef ARL_CB_WS_STAMP
-__device__ uint64_t g_cb_stamps[8][2][16][4];
+__device__ uint64_t g_cb_stamps[8][2][16][6];
 #define CB_STAMP(role, k, j)                                                               \
   do {                                                                                     \
     if (b < 8 && lane == 0 && (wave & 7) == 0 && (k) < 16)                                 \
@@ -691,7 +718,7 @@ __global__ void __launch_bounds__(NT2)
 conv_bwd_ws_kernel(ConvBwdArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[L2_END];
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: SGPR values
   const int g = lane >> 4, col = lane & 15;
   const int b = blockIdx.x, G = a.G;
   const int n = (a.S - 1 - b) / G + 1;   // samples b, b + G, ... of this workgroup
@@ -929,11 +956,12 @@ conv_bwd_ws_kernel(ConvBwdArgs a) {
 
 // ---------------------------------------------------------------------------
 // Wave-specialised form without the skew (conv_bwd_ws2_kernel): both halves work on sample s_k.
-//   P_k  X: (2) of s_k, the a1 > 0 test read straight from A1 (no mask pass)
-//        Y: (1) of s_k; screens of s_k -> XPH (or X, CB_XPH_X)
+//   P_k  X: the a1 > 0 bits of its (2) tiles, read straight from A1 (no mask pass), then an LDS arrival
+//           count; (2) of s_k; screens of s_k -> XPH (planes CB_XPH_X0 .. 3; Y commits the others)
+//        Y: (1) of s_k; once the 8 X arrivals of s_k are in, its own two a1 channels of s_{k+1} by LDS-DMA
 //   Q_k  X: (3) of s_k
-//        Y: a1 of s_{k+1} by LDS-DMA, da2 of s_{k+1} -> D2 and DA; waits for the DMA before the barrier
-// No fill phase and no mask buffers; the a1 DMA has one Q phase to land.
+//        Y: da2 of s_{k+1} -> D2 and DA; waits for its DMA before the barrier
+// No fill phase and no mask buffers; the a1 DMA is in flight from the end of (1) to the end of Q_k.
 namespace {
 constexpr int L3_D1 = 0;
 constexpr int L3_XPH = L3_D1 + 3 * D1P;
@@ -944,40 +972,129 @@ constexpr int L3_END = L3_DA + 3 * DAP;   // 155,520
 static_assert(L3_END <= 160 * 1024 && L3_A1 == L2_A1 && L3_DA == L2_DA && L3_D2 == L2_D2 && L3_XPH == L2_XPH,
               "the shared helpers address the L2_ regions");
 }  // namespace
+#ifndef CB_XPH_X0
+#define CB_XPH_X0 4   // screens planes X commits: CB_XPH_X0 .. 3 (4: none)
+#endif
+#ifndef CB_DMA_X
+#define CB_DMA_X 0    // 1: the X waves issue the a1 DMA of s_{k+1} at Q_k's start and wait for it after (3)
+#endif
+#ifndef CB_W2_LDS
+#define CB_W2_LDS 1   // 1: W2 staged through LDS by coalesced loads (the fragments' direct loads touch a 64-B
+                      // segment per lane: 64 L2 requests per instruction)
+#endif
+// W2 staging in the da1 region before the first sample: (oc, ic, tap) at oc * W2S_OC + ic * W2S_IC + tap; the
+// fragment reads (lanes: ic = col, oc = 8 g + j) hit 32 distinct banks (W2S_IC = 17, 8 W2S_OC = 16 mod 32)
+constexpr int W2S_IC = 17, W2S_OC = 16 * W2S_IC + 2;   // 274 floats
+static_assert(32 * W2S_OC * 4 <= 3 * D1P, "W2 staging fits the da1 region");
+
+// screens planes [C0, C0 + NC) of sample s (prefetch_x_ws restricted to those planes)
+template <int NC>
+struct PrefetchXn {
+  uint4 x[NC > 0 ? NC : 1];
+  int nv;
+};
+template <int C0, int NC>
+__device__ inline void prefetch_xn(const ConvBwdArgs& a, int r0, int s, int ty_, PrefetchXn<NC>& r) {
+  const int ty = opaque(ty_);
+  const int t = s / a.n, e = s - t * a.n;
+  const int rs = (r0 + t) % a.R;
+  r.nv = a.nvalid[(int64_t)rs * a.n + min(e + (ty & 63), a.n - 1)];
+  const int it = ty < 504 ? ty : 0;
+  const int y = it / 6, q = it - 6 * (it / 6);
+  const int off = y * 84 + (q < 5 ? 16 * q : 68);
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const int c = C0 + j;
+    const int64_t pl = a.layout == FRAMES_STACK ? ((int64_t)rs * a.n + e) * 4 + c
+                       : a.layout == FRAMES_RGB ? ((int64_t)rs * a.n + e) * 3 + (c > 0 ? c - 1 : 0)
+                                                : (int64_t)((rs + a.R - 3 + c) % a.R) * a.n + e;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.frames + pl * PLANE + off);
+    r.x[j] = make_uint4(src[0], src[1], src[2], src[3]);
+  }
+}
+template <int C0, int NC>
+__device__ inline void commit_xn(const PrefetchXn<NC>& r, uint8_t* lds, int ty_) {
+  const int ty = opaque(ty_);
+  const int nv = __shfl(r.nv, 0);
+  if (ty >= 504) return;
+  const int y = ty / 6, q = ty - 6 * (ty / 6);
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const int c = C0 + j;
+    uint4 v = r.x[j];
+    if (q == 5) v = make_uint4(v.w, 0, 0, 0);
+    if (c < 4 - nv) v = make_uint4(0, 0, 0, 0);
+    const uint32_t lo01 = __builtin_amdgcn_perm(v.y, v.x, 0x05010400u);
+    const uint32_t hi01 = __builtin_amdgcn_perm(v.y, v.x, 0x07030602u);
+    const uint32_t lo23 = __builtin_amdgcn_perm(v.w, v.z, 0x05010400u);
+    const uint32_t hi23 = __builtin_amdgcn_perm(v.w, v.z, 0x07030602u);
+    uint8_t* d = lds + L2_XPH + (c * 84 + y) * 4 * XR + 4 * q;
+    *reinterpret_cast<uint32_t*>(d) = __builtin_amdgcn_perm(lo23, lo01, 0x05040100u);
+    *reinterpret_cast<uint32_t*>(d + XR) = __builtin_amdgcn_perm(lo23, lo01, 0x07060302u);
+    *reinterpret_cast<uint32_t*>(d + 2 * XR) = __builtin_amdgcn_perm(hi23, hi01, 0x05040100u);
+    *reinterpret_cast<uint32_t*>(d + 3 * XR) = __builtin_amdgcn_perm(hi23, hi01, 0x07060302u);
+  }
+}
 
 __global__ void __launch_bounds__(NT2)
 conv_bwd_ws2_kernel(ConvBwdArgs a) {
+  constexpr int XC0 = CB_XPH_X0, XNC = 4 - CB_XPH_X0;   // screens planes of X: [XC0, 4); of Y: [0, XC0)
   __shared__ __attribute__((aligned(16))) uint8_t lds[L3_END];
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: SGPR values
   const int g = lane >> 4, col = lane & 15;
   const int b = blockIdx.x, G = a.G;
   const int n = (a.S - 1 - b) / G + 1;
   auto smp = [&](int k) { return b + min(k, n - 1) * G; };
-  for (int i = tid; i < 3 * 16 * 20; i += NT2) {
-    const int pl = i / 320, r = i - pl * 320;
-    *reinterpret_cast<uint2*>(lds + L3_D1 + pl * D1P + (r / 20) * D1_OC + (r % 20) * D1_ROW + 40) = make_uint2(0, 0);
-  }
+  auto zero_d1_pads = [&](int t0, int nt) {
+    for (int i = t0; i < 3 * 16 * 20; i += nt) {
+      const int pl = i / 320, r = i - pl * 320;
+      *reinterpret_cast<uint2*>(lds + L3_D1 + pl * D1P + (r / 20) * D1_OC + (r % 20) * D1_ROW + 40) = make_uint2(0, 0);
+    }
+  };
+  if (!CB_W2_LDS) zero_d1_pads(tid, NT2);
   for (int i = tid; i < 3 * DAP / 16; i += NT2) reinterpret_cast<uint4*>(lds + L3_DA)[i] = make_uint4(0, 0, 0, 0);
   if (tid < 4 * A1R / 4)
     reinterpret_cast<uint4*>(lds + L3_A1 + C1_OC * A1C * 4)[tid] = make_uint4(0, 0, 0, 0);
   float* out = a.slab + (int64_t)b * SLAB;
   float* red = reinterpret_cast<float*>(lds + L_RED);
   float* red1 = red + GI * 8;
-  const int r0 = (int)(a.ctl[CTL_STEP] % a.R);
 
   if (wave < 8) {
     // ================================================================ X: (2) and (3)
     const int wx = wave;
     const int cls = wx & 3, py = cls >> 1, px = cls & 1;
+    float* w2s = reinterpret_cast<float*>(lds + L3_D1);
+    if (CB_W2_LDS) {   // W2 (32 x 16 x 16 f32): 4 float4 a thread, coalesced
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int f = tid + 512 * j, oc = f >> 6, ic = (f >> 2) & 15, t4 = (f & 3) * 4;
+        const float4 w = reinterpret_cast<const float4*>(a.W2)[f];
+        float* d = w2s + oc * W2S_OC + ic * W2S_IC + t4;
+        d[0] = w.x;
+        d[1] = w.y;
+        d[2] = w.z;
+        d[3] = w.w;
+      }
+    }
+    PrefetchXn<XNC> pxr;
+    int r0 = 0;
+    if constexpr (XNC > 0) {
+      r0 = (int)(a.ctl[CTL_STEP] % a.R);
+      prefetch_xn<XC0, XNC>(a, r0, smp(0), tid, pxr);
+    }
+    if (CB_W2_LDS) lds_barrier();   // #0: W2 staged
     bf16x8 w2h[4], w2m[4], w2l[4];
     {
       const float* w2src = a.W2 + (8 * g * 16 + col) * 16 + py * 4 + px;
+      const float* w2l_ = w2s + (8 * g) * W2S_OC + col * W2S_IC + py * 4 + px;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         float v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = w2src[j * 256 + (ks >> 1) * 8 + 2 * (ks & 1)];
+        for (int j = 0; j < 8; ++j)
+          v[j] = CB_W2_LDS ? w2l_[j * W2S_OC + (ks >> 1) * 8 + 2 * (ks & 1)]
+                           : w2src[j * 256 + (ks >> 1) * 8 + 2 * (ks & 1)];
         uint32_t h[4], m[4], l[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) split3_pack(v[2 * j], v[2 * j + 1], h[j], m[j], l[j]);
@@ -991,63 +1108,58 @@ conv_bwd_ws2_kernel(ConvBwdArgs a) {
     for (int i = 0; i < 2; ++i) big3[i] = sml3[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     float b1s[4] = {0.f, 0.f, 0.f, 0.f};
     const int xrow3 = L3_XPH + (((wx >> 1) * 84 + 4 * (wx & 1) + (col >> 2)) * 4 + (col & 3)) * XR;
-#if CB_XPH_X
-    PrefetchX pxr;
-    prefetch_x_ws(a, r0, smp(0), tid, pxr);
-#endif
+    const int mt0 = wx < 4 ? 0 : 4, mt1 = wx < 4 ? 4 : 7;
+    if (CB_W2_LDS) {
+      lds_barrier();   // #0b: every X wave has its W2 fragments; the da1 pads are re-zeroed over the staging
+      zero_d1_pads(tid, NT2 / 2);
+    }
     CB_STAMP(0, 15, 0);
     lds_barrier();   // #1: zeroed pads, D2 / DA / A1 of s_0
     CB_STAMP(0, 15, 1);
     for (int k = 0; k < n; ++k) {
       // ---- P_k: (2) of s_k
       CB_STAMP(0, k, 0);
-#if CB_XPH_X
-      commit_x_ws(pxr, lds, tid);
-#endif
-      {
-        const float* a1m = reinterpret_cast<const float*>(lds + L3_A1) + (4 * g) * A1C;
-        const int mt0 = wx < 4 ? 0 : 4, mt1 = wx < 4 ? 4 : 7;
+      if constexpr (XNC > 0) commit_xn<XC0, XNC>(pxr, lds, tid);
+      const float* a1m = reinterpret_cast<const float*>(lds + L3_A1) + (4 * g) * A1C;
 #pragma unroll 1
-        for (int mt = mt0; mt < mt1; ++mt) {
-          const int cell = 12 + 16 * mt + col;
-          const int cy = cell / 11, cx = cell - cy * 11;
-          const bool keep = cell < 121 && cx != 0;
-          const int oy = keep ? 2 * (cy - 1) + py : 0, ox = keep ? 2 * (cx - 1) + px : 0;
-          const float* ap = a1m + oy * A1R + ox;
-          const float m0 = ap[0], m1 = ap[A1C], m2 = ap[2 * A1C], m3 = ap[3 * A1C];   // a1 of channels 4 g + rr
-          f32x4 big = {0.f, 0.f, 0.f, 0.f}, sml = big;
+      for (int mt = mt0; mt < mt1; ++mt) {
+        const int cell = 12 + 16 * mt + col;
+        const int cy = cell / 11, cx = cell - cy * 11;
+        const bool keep = cell < 121 && cx != 0;
+        const int oy = keep ? 2 * (cy - 1) + py : 0, ox = keep ? 2 * (cx - 1) + px : 0;
+        const float* ap = a1m + oy * A1R + ox;   // a1 of channels 4 g + rr: the > 0 test of (2)
+        const float m0 = ap[0], m1 = ap[A1C], m2 = ap[2 * A1C], m3 = ap[3 * A1C];
+        const uint32_t m = (m0 > 0.f ? 1u : 0u) | (m1 > 0.f ? 2u : 0u) | (m2 > 0.f ? 4u : 0u) | (m3 > 0.f ? 8u : 0u);
+        f32x4 big = {0.f, 0.f, 0.f, 0.f}, sml = big;
 #pragma unroll
-          for (int ks = 0; ks < 4; ++ks) {
-            const int dcell = (ks >> 1) * 11 + (ks & 1);
-            const int o = L3_D2 + d2_slot(cell < 121 ? cell - dcell : 0, g);
-            const bf16x8 bh = lds_load<bf16x8>(lds, o), bm = lds_load<bf16x8>(lds, o + D2P),
-                         bl = lds_load<bf16x8>(lds, o + 2 * D2P);
-            mfma_x6(w2h[ks], w2m[ks], w2l[ks], bh, bm, bl, big, sml);
-          }
-          if (keep) {
-            const float mv[4] = {m0, m1, m2, m3};
-            uint8_t* d = lds + L3_D1 + (4 * g) * D1_OC + oy * D1_ROW + ox * 2;
+        for (int ks = 0; ks < 4; ++ks) {
+          const int dcell = (ks >> 1) * 11 + (ks & 1);
+          const int o = L3_D2 + d2_slot(cell < 121 ? cell - dcell : 0, g);
+          const bf16x8 bh = lds_load<bf16x8>(lds, o), bm = lds_load<bf16x8>(lds, o + D2P),
+                       bl = lds_load<bf16x8>(lds, o + 2 * D2P);
+          mfma_x6(w2h[ks], w2m[ks], w2l[ks], bh, bm, bl, big, sml);
+        }
+        if (keep) {
+          uint8_t* d = lds + L3_D1 + (4 * g) * D1_OC + oy * D1_ROW + ox * 2;
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-              float v = __fadd_rn(big[rr], sml[rr]);
-              if (!(mv[rr] > 0.f)) v = 0.f;
-              b1s[rr] = __fadd_rn(b1s[rr], v);
-              uint32_t h, mm, l;
-              split3(v, h, mm, l);
-              *reinterpret_cast<uint16_t*>(d + rr * D1_OC) = (uint16_t)h;
-              *reinterpret_cast<uint16_t*>(d + rr * D1_OC + D1P) = (uint16_t)mm;
-              *reinterpret_cast<uint16_t*>(d + rr * D1_OC + 2 * D1P) = (uint16_t)l;
-            }
+          for (int rr = 0; rr < 4; ++rr) {
+            float v = __fadd_rn(big[rr], sml[rr]);
+            if (!((m >> rr) & 1)) v = 0.f;
+            b1s[rr] = __fadd_rn(b1s[rr], v);
+            uint32_t h, mm, l;
+            split3(v, h, mm, l);
+            *reinterpret_cast<uint16_t*>(d + rr * D1_OC) = (uint16_t)h;
+            *reinterpret_cast<uint16_t*>(d + rr * D1_OC + D1P) = (uint16_t)mm;
+            *reinterpret_cast<uint16_t*>(d + rr * D1_OC + 2 * D1P) = (uint16_t)l;
           }
         }
       }
-#if CB_XPH_X
-      prefetch_x_ws(a, r0, smp(k + 1), tid, pxr);
-#endif
+      if constexpr (XNC > 0) prefetch_xn<XC0, XNC>(a, r0, smp(k + 1), tid, pxr);
       CB_STAMP(0, k, 1);
       lds_barrier();
-      // ---- Q_k: (3) of s_k
+      // ---- Q_k: (3) of s_k (CB_DMA_X: a1 of s_{k+1} -> A1 by this wave's LDS-DMA meanwhile)
       CB_STAMP(0, k, 2);
+      if (CB_DMA_X && k + 1 < n) dma_a1_wave(a, smp(k + 1), lds, wx, lane);
 #pragma unroll CB_S3_UNROLL
       for (int ks = 0; ks < 15; ++ks) {
         const int Gk = 4 * ks + g, oy = Gk / 3, c = Gk - 3 * oy;
@@ -1074,6 +1186,7 @@ conv_bwd_ws2_kernel(ConvBwdArgs a) {
         }
       }
       CB_STAMP(0, k, 3);
+      if (CB_DMA_X && k + 1 < n) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // a1 of s_{k+1} has landed
       lds_barrier();
     }
 #pragma unroll
@@ -1089,47 +1202,46 @@ conv_bwd_ws2_kernel(ConvBwdArgs a) {
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) red1[(4 * g + rr) * 128 + wx * 16 + col] = b1s[rr];
   } else {
-    // ================================================================ Y: (1), the commits
+    // ================================================================ Y: (1), the commits, the a1 DMA
     const int ty = tid - NT2 / 2, wy = wave - 8;
     f32x4 acc1[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) acc1[0][i] = acc1[1][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     float b2a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float pa[8];
+    PrefetchXn<XC0> pxr;
     CB_STAMP(1, 15, 0);
     dma_a1_wave(a, smp(0), lds, wy, lane);
     load_da2(a, smp(0), ty, pa);
-#if !CB_XPH_X
-    PrefetchX pxr;
-    prefetch_x_ws(a, r0, smp(0), ty, pxr);
-#endif
+    int r0 = 0;
+    if constexpr (XC0 > 0) {
+      r0 = (int)(a.ctl[CTL_STEP] % a.R);   // after the loads that do not need it
+      prefetch_xn<0, XC0>(a, r0, smp(0), ty, pxr);
+    }
     CB_STAMP(1, 15, 1);
+    if (CB_W2_LDS) lds_barrier();   // #0
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     CB_STAMP(1, 15, 2);
-    commit_d2(pa, lds, ty);
-    commit_da(pa, lds, ty, b2a);
+    commit_d2_da(pa, lds, ty, b2a);
     CB_STAMP(1, 15, 3);
+    if (CB_W2_LDS) lds_barrier();   // #0b
     lds_barrier();   // #1
     for (int k = 0; k < n; ++k) {
       // ---- P_k
       CB_STAMP(1, k, 0);
       load_da2(a, smp(k + 1), ty, pa);   // for Q_k
-#if !CB_XPH_X
-      commit_x_ws(pxr, lds, ty);
-#endif
+      if constexpr (XC0 > 0) commit_xn<0, XC0>(pxr, lds, ty);
       step1_wave(lds, wy, lane, acc1);
-#if !CB_XPH_X
-      prefetch_x_ws(a, r0, smp(k + 1), ty, pxr);
-#endif
+      if constexpr (XC0 > 0) prefetch_xn<0, XC0>(a, r0, smp(k + 1), ty, pxr);
       CB_STAMP(1, k, 1);
       lds_barrier();
       // ---- Q_k
       CB_STAMP(1, k, 2);
       if (k + 1 < n) {
-        dma_a1_wave(a, smp(k + 1), lds, wy, lane);
-        commit_d2(pa, lds, ty);
-        commit_da(pa, lds, ty, b2a);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // a1 of s_{k+1} has landed
+        if (!CB_DMA_X) dma_a1_wave(a, smp(k + 1), lds, wy, lane);
+        commit_d2_da(pa, lds, ty, b2a);
+        CB_STAMP(1, k, 5);
+        if (!CB_DMA_X) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // a1 of s_{k+1} has landed
       }
       CB_STAMP(1, k, 3);
       lds_barrier();

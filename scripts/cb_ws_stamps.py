@@ -31,7 +31,7 @@ pairs, rewards, dones = synth_pools(N, P, 0, dev)
 for i in range(6):
     ag.run_window(pairs, rewards, dones, P, first=(i == 0))
 torch.cuda.synchronize()
-buf = np.zeros((8, 2, 16, 4), np.uint64)
+buf = np.zeros((8, 2, 16, 6), np.uint64)
 f = _lib.lib.arl_debug_cb_stamps
 f.argtypes = [ctypes.c_void_p]
 assert f(buf.ctypes.data) == 0
@@ -45,7 +45,8 @@ for k in range(min(n, 15)):
     q_end = X[:, k + 1, 0] if k + 1 < min(n, 15) else X[:, k, 3]
     rows.append({"k": k, "P": int(np.median(p_len)), "X_P_work": int(np.median(X[:, k, 1] - X[:, k, 0])),
                  "Y_P_work": int(np.median(Y[:, k, 1] - Y[:, k, 0])), "Q": int(np.median(q_end - X[:, k, 2])),
-                 "X_Q_work": int(np.median(X[:, k, 3] - X[:, k, 2])), "Y_Q_work": int(np.median(Y[:, k, 3] - Y[:, k, 2]))})
+                 "X_Q_work": int(np.median(X[:, k, 3] - X[:, k, 2])), "Y_Q_work": int(np.median(Y[:, k, 3] - Y[:, k, 2])),
+                 "Y_S1_end": int(np.median(Y[:, k, 4] - Y[:, k, 0])), "Y_slot5": int(np.median(Y[:, k, 5] - Y[:, k, 0]))})
 pro = {"to_b1": int(np.median(X[:, 15, 1] - X[:, 15, 0])), "fill_b2": int(np.median(X[:, 15, 2] - X[:, 15, 1])),
        "b3": int(np.median(X[:, 15, 3] - X[:, 15, 2])),
        "Y_issue": int(np.median(Y[:, 15, 1] - Y[:, 15, 0])), "Y_wait": int(np.median(Y[:, 15, 2] - Y[:, 15, 1])),
