@@ -9,12 +9,15 @@
 // Reference: a3c.py:129-130 (total_loss.backward through Chainer's
 // Convolution2D backward: im2col + tensordot for gW, col2im for gx).
 //
-// One 512-thread workgroup per CU (8 waves, 2 per SIMD); every operand of a
-// sample has its own LDS region (151 KB), so a sample is four
-// barrier-separated phases: commit, (1) + mask, (2), (3).  Workgroup b handles
-// samples b, b + G, ...; the next sample's a1 / da2 / screens are loaded into
-// registers (unconditional loads from clamped addresses: no load waits for
-// another) while the current one computes.
+// One workgroup per CU; every operand of a sample has its own LDS region
+// (152 KB).  Workgroup b handles samples b, b + G, ...  Two forms, bit-identical:
+// * conv_bwd_ws_kernel (the default, below): 1,024 threads; waves 0-7 run (2)
+//   and (3), waves 8-15 run (1) and the commits, two barriers a sample;
+// * conv_bwd_kernel (ARL_CB_WS=0, the test arm): 512 threads (8 waves, 2 per
+//   SIMD), a sample in four barrier-separated phases: commit, (1) + mask, (2),
+//   (3); the next sample's a1 / da2 / screens are loaded into registers
+//   (unconditional loads from clamped addresses: no load waits for another)
+//   while the current one computes.
 //
 // All three run on the bf16 matrix cores with exact bf16 splits of the f32
 // operands (bf16split.hpp; f32-accurate):
@@ -481,54 +484,47 @@ conv_bwd_kernel(ConvBwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Wave-specialised form: 1,024 threads, 4 waves a SIMD.  Waves 0-7 ("X") run
-// (2) and (3) of sample s_k; waves 8-15 ("Y") run (1) of sample s_{k+1}, the
-// a1 > 0 mask of s_{k+1} and every commit, so the two halves of a SIMD's waves
-// issue different steps.  Two barriers a sample:
-//   P_k  X: (2) of s_k (D2, mask buffer k & 1 -> D1)
-//        Y: screens of s_k -> XPH; mask of s_{k+1} -> mask buffer (k + 1) & 1;
-//           (1) of s_{k+1} (DA, A1); its own two a1 channels of s_{k+2} by LDS-DMA
+// The default form, conv_bwd_ws_kernel: 1,024 threads, 4 waves a SIMD, wave-specialised.  Waves 0-7 ("X")
+// run (2) and (3), waves 8-15 ("Y") run (1) and every commit, so each SIMD's four waves issue two different
+// steps at once.  Two barriers a sample s_k:
+//   P_k  X: (2) of s_k (D2 -> D1), the a1 > 0 test read straight from A1 (no mask pass)
+//        Y: (1) of s_k (DA, A1); screens of s_k -> XPH; loads da2 of s_{k+1} and the screens of s_{k+1}
 //   Q_k  X: (3) of s_k (D1, XPH)
-//        Y: da2 of s_{k+1} -> D2 (split grid), da2 of s_{k+2} -> DA (split planes)
-// Y wave w owns a1 channels 2w, 2w + 1: it alone computes their mask bits
-// (byte w of a pixel's 8-byte mask entry), reads them in (1) and DMAs the next
-// sample's into them, so the a1 hand-off needs no workgroup barrier and the
-// DMA has a whole phase pair to land.  Every accumulator sees the same
-// products in the same order as conv_bwd_kernel (per-wave tiles unchanged):
-// the slabs are bit-identical.
+//        Y: a1 of s_{k+1} -> A1 by LDS-DMA (nobody reads A1 in Q), da2 of s_{k+1} -> D2 and DA; waits for
+//           the DMA before the barrier
+// W2 is staged once through LDS by coalesced loads (the fragment-order global loads touched one 64-byte
+// segment a lane: 64 L2 requests an instruction, ~20k cycles of prologue).  Every accumulator sees the
+// same products in the same order as conv_bwd_kernel (per-wave tiles unchanged), so the slabs are
+// bit-identical to it (ARL_CB_WS=0 runs conv_bwd_kernel: the bitwise test arm).
 namespace {
 constexpr int NT2 = 1024;
-constexpr int A1W = 2 * A1C * 4;                 // bytes of a Y wave's two a1 channels (3,840)
+constexpr int A1W = 2 * A1C * 4;                 // bytes of one Y wave's two a1 channels (3,840)
 constexpr int A1W_PIECES = A1W / 16;             // 240 16-byte DMA pieces
-constexpr int MASKB = C1_P * 8;                  // one mask buffer: 400 pixels x 8 bytes
-constexpr int L2_D1 = 0;                         // da1 split planes                       47,616
-constexpr int L2_XPH = L2_D1 + 3 * D1P;          // screens by column phase                 32,256
-constexpr int L2_D2 = L2_XPH + 4 * 84 * 4 * XR;  // da2 split grid                          24,576
-constexpr int L2_A1 = L2_D2 + 3 * D2P;           // a1 f32 [16][20][A1R] + 4 zero rows       31,104
-constexpr int L2_DA = L2_A1 + C1_OC * A1C * 4 + 4 * A1R * 4;   // da2 [oc][p] split planes   19,968
-constexpr int L2_MASK = L2_DA + 3 * DAP;         // 2 mask buffers                          6,400
-constexpr int L2_END = L2_MASK + 2 * MASKB;      // 162,112
-static_assert(L2_END <= 160 * 1024, "LDS");
-static_assert(L2_A1 % 16 == 0 && L2_DA % 16 == 0 && L2_MASK % 8 == 0, "alignment");
+constexpr int LW_D1 = 0;                         // da1 split planes                     47,616
+constexpr int LW_XPH = LW_D1 + 3 * D1P;          // screens by column phase               32,256
+constexpr int LW_D2 = LW_XPH + 4 * 84 * 4 * XR;  // da2 split grid                        24,576
+constexpr int LW_A1 = LW_D2 + 3 * D2P;           // a1 f32 [16][20][A1R] + 4 zero rows     31,104
+constexpr int LW_DA = LW_A1 + C1_OC * A1C * 4 + 4 * A1R * 4;   // da2 [oc][p] split planes 19,968
+constexpr int LW_END = LW_DA + 3 * DAP;          // 155,520
+static_assert(LW_END <= 160 * 1024, "LDS");
+static_assert(LW_A1 % 16 == 0 && LW_DA % 16 == 0 && LW_XPH % 16 == 0 && LW_D2 % 16 == 0, "alignment");
 static_assert(GI <= NT2 / 2, "one da2 item per Y thread");
-#ifndef CB_XPH_X
-#define CB_XPH_X 0
-#endif
-#ifndef CB_S3_UNROLL
-#define CB_S3_UNROLL 3
-#endif
+// W2 staging in the da1 region before the first sample: (oc, ic, tap) at oc * W2S_OC + ic * W2S_IC + tap;
+// the fragment reads (lanes: ic = col, oc = 8 g + j) hit 32 distinct banks (W2S_IC = 17, 8 W2S_OC = 16 mod 32)
+constexpr int W2S_IC = 17, W2S_OC = 16 * W2S_IC + 2;   // 274 floats
+static_assert(32 * W2S_OC * 4 <= 3 * D1P, "W2 staging fits the da1 region");
 }  // namespace
 
-// Y wave wy: its two a1 channels of sample s by LDS-DMA (piece i = (channel, row, 16-byte column))
 __device__ inline int opaque(int x) {   // a value the compiler cannot hoist work on out of the sample loop
   asm volatile("" : "+v"(x));
   return x;
 }
 
+// Y wave wy: its two a1 channels of sample s by LDS-DMA (piece i = (channel, row, 16-byte column))
 __device__ inline void dma_a1_wave(const ConvBwdArgs& a, int s, uint8_t* lds, int wy, int lane_) {
   const int lane = opaque(lane_);
   const float* g1 = a.a1 + (int64_t)s * A1 + (2 * wy) * C1_P;
-  uint8_t* dst = lds + L2_A1 + wy * A1W;
+  uint8_t* dst = lds + LW_A1 + wy * A1W;
 #pragma unroll
   for (int ii = 0; ii < (A1W_PIECES + 63) / 64; ++ii) {
     const int i = ii * 64 + lane;
@@ -550,7 +546,8 @@ __device__ inline void load_da2(const ConvBwdArgs& a, int s, int ty, float (&d)[
   for (int k = 0; k < 8; ++k) d[k] = src[k * C2_P];
 }
 
-__device__ inline void commit_d2(const float (&r)[8], uint8_t* lds, int ty) {
+// D2 and DA of one sample (commit_a with the Y thread index): one grid item, one split
+__device__ inline void commit_d2_da(const float (&r)[8], uint8_t* lds, int ty, float (&b2a)[8]) {
   int grp, cell, p;
   bool v;
   const int i = opaque(ty);
@@ -559,21 +556,12 @@ __device__ inline void commit_d2(const float (&r)[8], uint8_t* lds, int ty) {
   uint32_t h[4], m[4], l[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) split3_pack(v ? r[2 * k] : 0.f, v ? r[2 * k + 1] : 0.f, h[k], m[k], l[k]);
-  uint8_t* dd = lds + L2_D2 + d2_slot(cell, grp);
+  uint8_t* dd = lds + LW_D2 + d2_slot(cell, grp);
   *reinterpret_cast<uint4*>(dd) = make_uint4(h[0], h[1], h[2], h[3]);
   *reinterpret_cast<uint4*>(dd + D2P) = make_uint4(m[0], m[1], m[2], m[3]);
   *reinterpret_cast<uint4*>(dd + 2 * D2P) = make_uint4(l[0], l[1], l[2], l[3]);
-}
-
-__device__ inline void commit_da(const float (&r)[8], uint8_t* lds, int ty, float (&b2a)[8]) {
-  int grp, cell, p;
-  bool v;
-  grid_item(opaque(ty), grp, cell, v, p);
   if (!v) return;
-  uint32_t h[4], m[4], l[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) split3_pack(r[2 * k], r[2 * k + 1], h[k], m[k], l[k]);
-  uint8_t* da = lds + L2_DA + (8 * grp) * DA_ROW + 2 * p;
+  uint8_t* da = lds + LW_DA + (8 * grp) * DA_ROW + 2 * p;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int sh = 16 * (k & 1);
@@ -584,8 +572,7 @@ __device__ inline void commit_da(const float (&r)[8], uint8_t* lds, int ty, floa
   }
 }
 
-// prefetch_x with the Y thread index ty (0..511)
-// r0 = the window's first step modulo the ring length
+// prefetch_x with the Y thread index ty (0..511); r0 = the window's first step modulo the ring length
 __device__ inline void prefetch_x_ws(const ConvBwdArgs& a, int r0, int s, int ty_, PrefetchX& r) {
   const int ty = opaque(ty_);
   const int t = s / a.n, e = s - t * a.n;
@@ -604,32 +591,6 @@ __device__ inline void prefetch_x_ws(const ConvBwdArgs& a, int r0, int s, int ty
   }
 }
 
-// D2 and DA of one sample together (conv_bwd_ws2_kernel): one grid item, one split
-__device__ inline void commit_d2_da(const float (&r)[8], uint8_t* lds, int ty, float (&b2a)[8]) {
-  int grp, cell, p;
-  bool v;
-  const int i = opaque(ty);
-  grid_item(i, grp, cell, v, p);
-  if (i >= GI) return;
-  uint32_t h[4], m[4], l[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) split3_pack(v ? r[2 * k] : 0.f, v ? r[2 * k + 1] : 0.f, h[k], m[k], l[k]);
-  uint8_t* dd = lds + L2_D2 + d2_slot(cell, grp);
-  *reinterpret_cast<uint4*>(dd) = make_uint4(h[0], h[1], h[2], h[3]);
-  *reinterpret_cast<uint4*>(dd + D2P) = make_uint4(m[0], m[1], m[2], m[3]);
-  *reinterpret_cast<uint4*>(dd + 2 * D2P) = make_uint4(l[0], l[1], l[2], l[3]);
-  if (!v) return;
-  uint8_t* da = lds + L2_DA + (8 * grp) * DA_ROW + 2 * p;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int sh = 16 * (k & 1);
-    *reinterpret_cast<uint16_t*>(da + k * DA_ROW) = (uint16_t)(h[k >> 1] >> sh);
-    *reinterpret_cast<uint16_t*>(da + k * DA_ROW + DAP) = (uint16_t)(m[k >> 1] >> sh);
-    *reinterpret_cast<uint16_t*>(da + k * DA_ROW + 2 * DAP) = (uint16_t)(l[k >> 1] >> sh);
-    b2a[k] = __fadd_rn(b2a[k], r[k]);
-  }
-}
-
 // screens -> phase rows (commit_x with the Y thread index ty)
 __device__ inline void commit_x_ws(const PrefetchX& r, uint8_t* lds, int ty_) {
   const int ty = opaque(ty_);
@@ -645,7 +606,7 @@ __device__ inline void commit_x_ws(const PrefetchX& r, uint8_t* lds, int ty_) {
     const uint32_t hi01 = __builtin_amdgcn_perm(v.y, v.x, 0x07030602u);
     const uint32_t lo23 = __builtin_amdgcn_perm(v.w, v.z, 0x05010400u);
     const uint32_t hi23 = __builtin_amdgcn_perm(v.w, v.z, 0x07030602u);
-    uint8_t* d = lds + L2_XPH + (c * 84 + y) * 4 * XR + 4 * q;
+    uint8_t* d = lds + LW_XPH + (c * 84 + y) * 4 * XR + 4 * q;
     *reinterpret_cast<uint32_t*>(d) = __builtin_amdgcn_perm(lo23, lo01, 0x05040100u);
     *reinterpret_cast<uint32_t*>(d + XR) = __builtin_amdgcn_perm(lo23, lo01, 0x07060302u);
     *reinterpret_cast<uint32_t*>(d + 2 * XR) = __builtin_amdgcn_perm(hi23, hi01, 0x05040100u);
@@ -653,25 +614,12 @@ __device__ inline void commit_x_ws(const PrefetchX& r, uint8_t* lds, int ty_) {
   }
 }
 
-// Y wave wy: a1 > 0 bits of its channels 2wy (bit 0) and 2wy + 1 (bit 1) -> byte wy of each pixel's entry
-__device__ inline void mask_wave(uint8_t* lds, int buf, int wy, int lane_) {
-  const int lane = opaque(lane_);
-  const float* a1s = reinterpret_cast<const float*>(lds + L2_A1) + (2 * wy) * A1C;
-  uint8_t* m = lds + L2_MASK + buf * MASKB + wy;
-#pragma unroll
-  for (int it = 0; it < (C1_P + 63) / 64; ++it) {
-    const int px = it * 64 + lane;
-    if (px < C1_P) {
-      const int o = (px / 20) * A1R + px % 20;
-      m[px * 8] = (uint8_t)((a1s[o] > 0.f ? 1u : 0u) | (a1s[o + A1C] > 0.f ? 2u : 0u));
-    }
-  }
-}
-
-// (1) of one sample on Y wave wy (conv_bwd_kernel's step (1) with wave -> wy)
+// (1) of one sample on Y wave wy (conv_bwd_kernel's step (1) with wave -> wy).  Positions past 80 read up to
+// 4 rows past the wave's second channel (the next channel's rows, or the zero rows after channel 15) times A's
+// zeros.
 __device__ inline void step1_wave(const uint8_t* lds, int wy, int lane_, f32x4 (&acc1)[2][2]) {
   const int lane = opaque(lane_), g = lane >> 4, col = lane & 15;
-  const float* b0 = reinterpret_cast<const float*>(lds + L2_A1) + (2 * wy) * A1C + (col >> 2) * A1R + (col & 3);
+  const float* b0 = reinterpret_cast<const float*>(lds + LW_A1) + (2 * wy) * A1C + (col >> 2) * A1R + (col & 3);
 #pragma unroll
   for (int ks = 0; ks < 3; ++ks) {
     const int p0 = 32 * ks + 8 * g, oy0 = p0 / 9, ox0 = p0 - 9 * oy0;
@@ -681,7 +629,7 @@ __device__ inline void step1_wave(const uint8_t* lds, int wy, int lane_, f32x4 (
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int h = 0; h < 3; ++h)
-        av[mt][h] = lds_load<bf16x8>(lds, L2_DA + (16 * mt + col) * DA_ROW + h * DAP + 2 * p0);
+        av[mt][h] = lds_load<bf16x8>(lds, LW_DA + (16 * mt + col) * DA_ROW + h * DAP + 2 * p0);
 #pragma unroll
     for (int jn = 0; jn < 2; ++jn) {
       float x[8];
@@ -696,8 +644,9 @@ __device__ inline void step1_wave(const uint8_t* lds, int wy, int lane_, f32x4 (
   }
 }
 
-// phase stamps (diagnostic builds only: make variant DEFS=-DARL_CB_WS_STAMP): workgroups 0-7, wave 0 (X) and
-// wave 8 (Y), shader clock at the start / end of each phase's work, sample k < 15; k = 15 the prologue
+// phase stamps (diagnostic builds only: make variant DEFS=-DARL_CB_WS_STAMP, scripts/cb_ws_stamps.py):
+// workgroups 0-7, wave 0 (X) and wave 8 (Y), shader clock at the start / end of each phase's work, sample
+// k < 15; k = 15 the prologue
 #ifdef ARL_CB_WS_STAMP
 __device__ uint64_t g_cb_stamps[8][2][16][6];
 #define CB_STAMP(role, k, j)                                                               \
@@ -716,22 +665,18 @@ extern "C" int arl_debug_cb_stamps(uint64_t* host) {
 
 __global__ void __launch_bounds__(NT2)
 conv_bwd_ws_kernel(ConvBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[L2_END];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LW_END];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: SGPR values
   const int g = lane >> 4, col = lane & 15;
   const int b = blockIdx.x, G = a.G;
   const int n = (a.S - 1 - b) / G + 1;   // samples b, b + G, ... of this workgroup
   auto smp = [&](int k) { return b + min(k, n - 1) * G; };
-  // zero once: the da1 pad columns X 20..23, the da2 [oc][p] planes (positions past 80 stay 0), and the
-  // 4 rows after a1 channel 15 ((1) reads up to 4 rows past a channel, times A's zeros)
-  for (int i = tid; i < 3 * 16 * 20; i += NT2) {
-    const int pl = i / 320, r = i - pl * 320;
-    *reinterpret_cast<uint2*>(lds + L2_D1 + pl * D1P + (r / 20) * D1_OC + (r % 20) * D1_ROW + 40) = make_uint2(0, 0);
-  }
-  for (int i = tid; i < 3 * DAP / 16; i += NT2) reinterpret_cast<uint4*>(lds + L2_DA)[i] = make_uint4(0, 0, 0, 0);
+  // zero once: the da2 [oc][p] planes (positions past 80 stay 0) and the 4 rows after a1 channel 15; the
+  // da1 pad columns X 20..23 after the W2 staging (below)
+  for (int i = tid; i < 3 * DAP / 16; i += NT2) reinterpret_cast<uint4*>(lds + LW_DA)[i] = make_uint4(0, 0, 0, 0);
   if (tid < 4 * A1R / 4)
-    reinterpret_cast<uint4*>(lds + L2_A1 + C1_OC * A1C * 4)[tid] = make_uint4(0, 0, 0, 0);
+    reinterpret_cast<uint4*>(lds + LW_A1 + C1_OC * A1C * 4)[tid] = make_uint4(0, 0, 0, 0);
   float* out = a.slab + (int64_t)b * SLAB;
   float* red = reinterpret_cast<float*>(lds + L_RED);   // after the last sample: b2a [GI][8], then b1s
   float* red1 = red + GI * 8;
@@ -740,14 +685,27 @@ conv_bwd_ws_kernel(ConvBwdArgs a) {
     // ================================================================ X: (2) and (3)
     const int wx = wave;
     const int cls = wx & 3, py = cls >> 1, px = cls & 1;
+    float* w2s = reinterpret_cast<float*>(lds + LW_D1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {   // W2 (32 x 16 x 16 f32): 4 float4 a thread, coalesced
+      const int f = tid + 512 * j, oc = f >> 6, ic = (f >> 2) & 15, t4 = (f & 3) * 4;
+      const float4 w = reinterpret_cast<const float4*>(a.W2)[f];
+      float* d = w2s + oc * W2S_OC + ic * W2S_IC + t4;
+      d[0] = w.x;
+      d[1] = w.y;
+      d[2] = w.z;
+      d[3] = w.w;
+    }
+    lds_barrier();   // #0: W2 staged
+    // (2) W2 fragments of this wave's parity class: lane (ic = col, g), k-step ks = (dy, dx), k = oc = 8 g + j
     bf16x8 w2h[4], w2m[4], w2l[4];
     {
-      const float* w2src = a.W2 + (8 * g * 16 + col) * 16 + py * 4 + px;
+      const float* w2f = w2s + (8 * g) * W2S_OC + col * W2S_IC + py * 4 + px;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         float v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = w2src[j * 256 + (ks >> 1) * 8 + 2 * (ks & 1)];
+        for (int j = 0; j < 8; ++j) v[j] = w2f[j * W2S_OC + (ks >> 1) * 8 + 2 * (ks & 1)];
         uint32_t h[4], m[4], l[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) split3_pack(v[2 * j], v[2 * j + 1], h[j], m[j], l[j]);
@@ -760,358 +718,12 @@ conv_bwd_ws_kernel(ConvBwdArgs a) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) big3[i] = sml3[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     float b1s[4] = {0.f, 0.f, 0.f, 0.f};
-    const int xrow3 = L2_XPH + (((wx >> 1) * 84 + 4 * (wx & 1) + (col >> 2)) * 4 + (col & 3)) * XR;
-#if CB_XPH_X
-    const int r0 = (int)(a.ctl[CTL_STEP] % a.R);
-    PrefetchX pxr;
-    prefetch_x_ws(a, r0, smp(0), tid, pxr);
-#endif
-    CB_STAMP(0, 15, 0);
-    lds_barrier();   // #1: zeroed pads, D2 / DA of s_0
-    CB_STAMP(0, 15, 1);
-    lds_barrier();   // #2: (1) and the mask of s_0 (Y)
-    CB_STAMP(0, 15, 2);
-    lds_barrier();   // #3: DA of s_1 (Y)
-    CB_STAMP(0, 15, 3);
-    for (int k = 0; k < n; ++k) {
-      // ---- P_k: (2) of s_k
-      CB_STAMP(0, k, 0);
-#if CB_XPH_X
-      commit_x_ws(pxr, lds, tid);
-#endif
-      {
-        const uint8_t* mk = lds + L2_MASK + (k & 1) * MASKB + 2 * g;
-        const int mt0 = wx < 4 ? 0 : 4, mt1 = wx < 4 ? 4 : 7;
-#pragma unroll 1
-        for (int mt = mt0; mt < mt1; ++mt) {
-          const int cell = 12 + 16 * mt + col;
-          const int cy = cell / 11, cx = cell - cy * 11;
-          const bool keep = cell < 121 && cx != 0;
-          const int oy = keep ? 2 * (cy - 1) + py : 0, ox = keep ? 2 * (cx - 1) + px : 0;
-          const uint32_t c16 = *reinterpret_cast<const uint16_t*>(mk + (oy * 20 + ox) * 8);
-          const uint32_t m = (c16 & 3u) | ((c16 >> 6) & 0xcu);   // bit rr: channel 4 g + rr
-          f32x4 big = {0.f, 0.f, 0.f, 0.f}, sml = big;
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks) {
-            const int dcell = (ks >> 1) * 11 + (ks & 1);
-            const int o = L2_D2 + d2_slot(cell < 121 ? cell - dcell : 0, g);
-            const bf16x8 bh = lds_load<bf16x8>(lds, o), bm = lds_load<bf16x8>(lds, o + D2P),
-                         bl = lds_load<bf16x8>(lds, o + 2 * D2P);
-            mfma_x6(w2h[ks], w2m[ks], w2l[ks], bh, bm, bl, big, sml);
-          }
-          if (keep) {
-            uint8_t* d = lds + L2_D1 + (4 * g) * D1_OC + oy * D1_ROW + ox * 2;
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-              float v = __fadd_rn(big[rr], sml[rr]);
-              if (!((m >> rr) & 1)) v = 0.f;
-              b1s[rr] = __fadd_rn(b1s[rr], v);
-              uint32_t h, mm, l;
-              split3(v, h, mm, l);
-              *reinterpret_cast<uint16_t*>(d + rr * D1_OC) = (uint16_t)h;
-              *reinterpret_cast<uint16_t*>(d + rr * D1_OC + D1P) = (uint16_t)mm;
-              *reinterpret_cast<uint16_t*>(d + rr * D1_OC + 2 * D1P) = (uint16_t)l;
-            }
-          }
-        }
-      }
-#if CB_XPH_X
-      prefetch_x_ws(a, r0, smp(k + 1), tid, pxr);
-#endif
-      CB_STAMP(0, k, 1);
-      lds_barrier();
-      // ---- Q_k: (3) of s_k
-      CB_STAMP(0, k, 2);
-#pragma unroll CB_S3_UNROLL
-      for (int ks = 0; ks < 15; ++ks) {
-        const int Gk = 4 * ks + g, oy = Gk / 3, c = Gk - 3 * oy;
-        const int ob = L2_D1 + col * D1_OC + oy * D1_ROW + 16 * c;
-        const bf16x8 bh = lds_load<bf16x8>(lds, ob), bm = lds_load<bf16x8>(lds, ob + D1P),
-                     bl = lds_load<bf16x8>(lds, ob + 2 * D1P);
-        const int oa = xrow3 + oy * 16 * XR + 8 * c;
-        const uint2 lo = lds_load<uint2>(lds, oa);
-        const uint32_t nx = lds_load<uint32_t>(lds, oa + 8);
-        uint32_t f[9];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          f[q] = __float_as_uint((float)((lo.x >> (8 * q)) & 0xffu));
-          f[4 + q] = __float_as_uint((float)((lo.y >> (8 * q)) & 0xffu));
-        }
-        f[8] = __float_as_uint((float)(nx & 0xffu));
-#pragma unroll
-        for (int a_ = 0; a_ < 2; ++a_) {
-          const bf16x8 xa = frag_from_pairs(__builtin_amdgcn_perm(f[a_ + 1], f[a_], 0x07060302u),
-                                            __builtin_amdgcn_perm(f[a_ + 3], f[a_ + 2], 0x07060302u),
-                                            __builtin_amdgcn_perm(f[a_ + 5], f[a_ + 4], 0x07060302u),
-                                            __builtin_amdgcn_perm(f[a_ + 7], f[a_ + 6], 0x07060302u));
-          mfma_x3(xa, bh, bm, bl, big3[a_], sml3[a_]);
-        }
-      }
-      CB_STAMP(0, k, 3);
-      lds_barrier();
-    }
-#pragma unroll
-    for (int a_ = 0; a_ < 2; ++a_) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = g * 4 + r;
-        const int ky = 4 * (wx & 1) + (row >> 2), kx = 4 * a_ + (row & 3);
-        slab_store(out + SLAB_W1 + ((wx >> 1) * 64 + ky * 8 + kx) * 16 + col, __fadd_rn(big3[a_][r], sml3[a_][r]));
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) red1[(4 * g + rr) * 128 + wx * 16 + col] = b1s[rr];
-  } else {
-    // ================================================================ Y: (1), the mask, the commits
-    const int ty = tid - NT2 / 2, wy = wave - 8;
-    f32x4 acc1[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) acc1[0][i] = acc1[1][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float b2a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float pa[8], sa[8];
-    CB_STAMP(1, 15, 0);
-#if !CB_XPH_X
-    PrefetchX pxr;
-    const int r0 = (int)(a.ctl[CTL_STEP] % a.R);
-#endif
-    dma_a1_wave(a, smp(0), lds, wy, lane);
-    load_da2(a, smp(0), ty, pa);
-#if !CB_XPH_X
-    prefetch_x_ws(a, r0, smp(0), ty, pxr);
-#endif
-    CB_STAMP(1, 15, 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    CB_STAMP(1, 15, 2);
-    commit_d2(pa, lds, ty);
-    commit_da(pa, lds, ty, b2a);
-    load_da2(a, smp(1), ty, pa);
-    CB_STAMP(1, 15, 3);
-    lds_barrier();   // #1
-    mask_wave(lds, 0, wy, lane);
-    step1_wave(lds, wy, lane, acc1);
-    if (n > 1) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      dma_a1_wave(a, smp(1), lds, wy, lane);
-    }
-    lds_barrier();   // #2
-    if (n > 1) commit_da(pa, lds, ty, b2a);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) sa[i] = pa[i];
-    lds_barrier();   // #3
-    for (int k = 0; k < n; ++k) {
-      // ---- P_k
-      CB_STAMP(1, k, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own a1 channels of s_{k+1}, screens of s_k
-#if !CB_XPH_X
-      commit_x_ws(pxr, lds, ty);
-#endif
-      load_da2(a, smp(k + 2), ty, pa);
-      if (k + 1 < n) {
-        mask_wave(lds, (k + 1) & 1, wy, lane);
-        step1_wave(lds, wy, lane, acc1);
-        if (k + 2 < n) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          dma_a1_wave(a, smp(k + 2), lds, wy, lane);
-        }
-      }
-#if !CB_XPH_X
-      prefetch_x_ws(a, r0, smp(k + 1), ty, pxr);   // after (1): its registers are not live across it
-#endif
-      CB_STAMP(1, k, 1);
-      lds_barrier();
-      // ---- Q_k
-      CB_STAMP(1, k, 2);
-      if (k + 1 < n) commit_d2(sa, lds, ty);
-      if (k + 2 < n) commit_da(pa, lds, ty, b2a);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) sa[i] = pa[i];
-      CB_STAMP(1, k, 3);
-      lds_barrier();
-    }
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          slab_store(out + (16 * mt + g * 4 + r) * 256 + 16 * (2 * wy + j) + col, acc1[mt][j][r]);
-    __syncthreads();
-    if (ty < GI)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) red[ty * 8 + k] = b2a[k];
-  }
-  __syncthreads();
-  if (tid < 32) {
-    float t = 0.f;
-    for (int c = 0; c < 121; ++c) t = __fadd_rn(t, red[((tid >> 3) * 121 + c) * 8 + (tid & 7)]);
-    out[SLAB_B2 + tid] = t;
-  } else if (tid >= 64 && tid < 80) {
-    const int o = tid - 64;
-    float t = 0.f;
-    for (int c = 0; c < 128; ++c) t = __fadd_rn(t, red1[o * 128 + c]);
-    out[SLAB_B1 + o] = t;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Wave-specialised form without the skew (conv_bwd_ws2_kernel): both halves work on sample s_k.
-//   P_k  X: the a1 > 0 bits of its (2) tiles, read straight from A1 (no mask pass), then an LDS arrival
-//           count; (2) of s_k; screens of s_k -> XPH (planes CB_XPH_X0 .. 3; Y commits the others)
-//        Y: (1) of s_k; once the 8 X arrivals of s_k are in, its own two a1 channels of s_{k+1} by LDS-DMA
-//   Q_k  X: (3) of s_k
-//        Y: da2 of s_{k+1} -> D2 and DA; waits for its DMA before the barrier
-// No fill phase and no mask buffers; the a1 DMA is in flight from the end of (1) to the end of Q_k.
-namespace {
-constexpr int L3_D1 = 0;
-constexpr int L3_XPH = L3_D1 + 3 * D1P;
-constexpr int L3_D2 = L3_XPH + 4 * 84 * 4 * XR;
-constexpr int L3_A1 = L3_D2 + 3 * D2P;
-constexpr int L3_DA = L3_A1 + C1_OC * A1C * 4 + 4 * A1R * 4;
-constexpr int L3_END = L3_DA + 3 * DAP;   // 155,520
-static_assert(L3_END <= 160 * 1024 && L3_A1 == L2_A1 && L3_DA == L2_DA && L3_D2 == L2_D2 && L3_XPH == L2_XPH,
-              "the shared helpers address the L2_ regions");
-}  // namespace
-#ifndef CB_XPH_X0
-#define CB_XPH_X0 4   // screens planes X commits: CB_XPH_X0 .. 3 (4: none)
-#endif
-#ifndef CB_DMA_X
-#define CB_DMA_X 0    // 1: the X waves issue the a1 DMA of s_{k+1} at Q_k's start and wait for it after (3)
-#endif
-#ifndef CB_W2_LDS
-#define CB_W2_LDS 1   // 1: W2 staged through LDS by coalesced loads (the fragments' direct loads touch a 64-B
-                      // segment per lane: 64 L2 requests per instruction)
-#endif
-// W2 staging in the da1 region before the first sample: (oc, ic, tap) at oc * W2S_OC + ic * W2S_IC + tap; the
-// fragment reads (lanes: ic = col, oc = 8 g + j) hit 32 distinct banks (W2S_IC = 17, 8 W2S_OC = 16 mod 32)
-constexpr int W2S_IC = 17, W2S_OC = 16 * W2S_IC + 2;   // 274 floats
-static_assert(32 * W2S_OC * 4 <= 3 * D1P, "W2 staging fits the da1 region");
-
-// screens planes [C0, C0 + NC) of sample s (prefetch_x_ws restricted to those planes)
-template <int NC>
-struct PrefetchXn {
-  uint4 x[NC > 0 ? NC : 1];
-  int nv;
-};
-template <int C0, int NC>
-__device__ inline void prefetch_xn(const ConvBwdArgs& a, int r0, int s, int ty_, PrefetchXn<NC>& r) {
-  const int ty = opaque(ty_);
-  const int t = s / a.n, e = s - t * a.n;
-  const int rs = (r0 + t) % a.R;
-  r.nv = a.nvalid[(int64_t)rs * a.n + min(e + (ty & 63), a.n - 1)];
-  const int it = ty < 504 ? ty : 0;
-  const int y = it / 6, q = it - 6 * (it / 6);
-  const int off = y * 84 + (q < 5 ? 16 * q : 68);
-#pragma unroll
-  for (int j = 0; j < NC; ++j) {
-    const int c = C0 + j;
-    const int64_t pl = a.layout == FRAMES_STACK ? ((int64_t)rs * a.n + e) * 4 + c
-                       : a.layout == FRAMES_RGB ? ((int64_t)rs * a.n + e) * 3 + (c > 0 ? c - 1 : 0)
-                                                : (int64_t)((rs + a.R - 3 + c) % a.R) * a.n + e;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.frames + pl * PLANE + off);
-    r.x[j] = make_uint4(src[0], src[1], src[2], src[3]);
-  }
-}
-template <int C0, int NC>
-__device__ inline void commit_xn(const PrefetchXn<NC>& r, uint8_t* lds, int ty_) {
-  const int ty = opaque(ty_);
-  const int nv = __shfl(r.nv, 0);
-  if (ty >= 504) return;
-  const int y = ty / 6, q = ty - 6 * (ty / 6);
-#pragma unroll
-  for (int j = 0; j < NC; ++j) {
-    const int c = C0 + j;
-    uint4 v = r.x[j];
-    if (q == 5) v = make_uint4(v.w, 0, 0, 0);
-    if (c < 4 - nv) v = make_uint4(0, 0, 0, 0);
-    const uint32_t lo01 = __builtin_amdgcn_perm(v.y, v.x, 0x05010400u);
-    const uint32_t hi01 = __builtin_amdgcn_perm(v.y, v.x, 0x07030602u);
-    const uint32_t lo23 = __builtin_amdgcn_perm(v.w, v.z, 0x05010400u);
-    const uint32_t hi23 = __builtin_amdgcn_perm(v.w, v.z, 0x07030602u);
-    uint8_t* d = lds + L2_XPH + (c * 84 + y) * 4 * XR + 4 * q;
-    *reinterpret_cast<uint32_t*>(d) = __builtin_amdgcn_perm(lo23, lo01, 0x05040100u);
-    *reinterpret_cast<uint32_t*>(d + XR) = __builtin_amdgcn_perm(lo23, lo01, 0x07060302u);
-    *reinterpret_cast<uint32_t*>(d + 2 * XR) = __builtin_amdgcn_perm(hi23, hi01, 0x05040100u);
-    *reinterpret_cast<uint32_t*>(d + 3 * XR) = __builtin_amdgcn_perm(hi23, hi01, 0x07060302u);
-  }
-}
-
-__global__ void __launch_bounds__(NT2)
-conv_bwd_ws2_kernel(ConvBwdArgs a) {
-  constexpr int XC0 = CB_XPH_X0, XNC = 4 - CB_XPH_X0;   // screens planes of X: [XC0, 4); of Y: [0, XC0)
-  __shared__ __attribute__((aligned(16))) uint8_t lds[L3_END];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: SGPR values
-  const int g = lane >> 4, col = lane & 15;
-  const int b = blockIdx.x, G = a.G;
-  const int n = (a.S - 1 - b) / G + 1;
-  auto smp = [&](int k) { return b + min(k, n - 1) * G; };
-  auto zero_d1_pads = [&](int t0, int nt) {
-    for (int i = t0; i < 3 * 16 * 20; i += nt) {
-      const int pl = i / 320, r = i - pl * 320;
-      *reinterpret_cast<uint2*>(lds + L3_D1 + pl * D1P + (r / 20) * D1_OC + (r % 20) * D1_ROW + 40) = make_uint2(0, 0);
-    }
-  };
-  if (!CB_W2_LDS) zero_d1_pads(tid, NT2);
-  for (int i = tid; i < 3 * DAP / 16; i += NT2) reinterpret_cast<uint4*>(lds + L3_DA)[i] = make_uint4(0, 0, 0, 0);
-  if (tid < 4 * A1R / 4)
-    reinterpret_cast<uint4*>(lds + L3_A1 + C1_OC * A1C * 4)[tid] = make_uint4(0, 0, 0, 0);
-  float* out = a.slab + (int64_t)b * SLAB;
-  float* red = reinterpret_cast<float*>(lds + L_RED);
-  float* red1 = red + GI * 8;
-
-  if (wave < 8) {
-    // ================================================================ X: (2) and (3)
-    const int wx = wave;
-    const int cls = wx & 3, py = cls >> 1, px = cls & 1;
-    float* w2s = reinterpret_cast<float*>(lds + L3_D1);
-    if (CB_W2_LDS) {   // W2 (32 x 16 x 16 f32): 4 float4 a thread, coalesced
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int f = tid + 512 * j, oc = f >> 6, ic = (f >> 2) & 15, t4 = (f & 3) * 4;
-        const float4 w = reinterpret_cast<const float4*>(a.W2)[f];
-        float* d = w2s + oc * W2S_OC + ic * W2S_IC + t4;
-        d[0] = w.x;
-        d[1] = w.y;
-        d[2] = w.z;
-        d[3] = w.w;
-      }
-    }
-    PrefetchXn<XNC> pxr;
-    int r0 = 0;
-    if constexpr (XNC > 0) {
-      r0 = (int)(a.ctl[CTL_STEP] % a.R);
-      prefetch_xn<XC0, XNC>(a, r0, smp(0), tid, pxr);
-    }
-    if (CB_W2_LDS) lds_barrier();   // #0: W2 staged
-    bf16x8 w2h[4], w2m[4], w2l[4];
-    {
-      const float* w2src = a.W2 + (8 * g * 16 + col) * 16 + py * 4 + px;
-      const float* w2l_ = w2s + (8 * g) * W2S_OC + col * W2S_IC + py * 4 + px;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          v[j] = CB_W2_LDS ? w2l_[j * W2S_OC + (ks >> 1) * 8 + 2 * (ks & 1)]
-                           : w2src[j * 256 + (ks >> 1) * 8 + 2 * (ks & 1)];
-        uint32_t h[4], m[4], l[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) split3_pack(v[2 * j], v[2 * j + 1], h[j], m[j], l[j]);
-        w2h[ks] = frag_from_pairs(h[0], h[1], h[2], h[3]);
-        w2m[ks] = frag_from_pairs(m[0], m[1], m[2], m[3]);
-        w2l[ks] = frag_from_pairs(l[0], l[1], l[2], l[3]);
-      }
-    }
-    f32x4 big3[2], sml3[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) big3[i] = sml3[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float b1s[4] = {0.f, 0.f, 0.f, 0.f};
-    const int xrow3 = L3_XPH + (((wx >> 1) * 84 + 4 * (wx & 1) + (col >> 2)) * 4 + (col & 3)) * XR;
+    const int xrow3 = LW_XPH + (((wx >> 1) * 84 + 4 * (wx & 1) + (col >> 2)) * 4 + (col & 3)) * XR;
     const int mt0 = wx < 4 ? 0 : 4, mt1 = wx < 4 ? 4 : 7;
-    if (CB_W2_LDS) {
-      lds_barrier();   // #0b: every X wave has its W2 fragments; the da1 pads are re-zeroed over the staging
-      zero_d1_pads(tid, NT2 / 2);
+    lds_barrier();   // #0b: every X wave holds its W2 fragments: the da1 pads are zeroed over the staging
+    for (int i = tid; i < 3 * 16 * 20; i += NT2 / 2) {
+      const int pl = i / 320, r = i - pl * 320;
+      *reinterpret_cast<uint2*>(lds + LW_D1 + pl * D1P + (r / 20) * D1_OC + (r % 20) * D1_ROW + 40) = make_uint2(0, 0);
     }
     CB_STAMP(0, 15, 0);
     lds_barrier();   // #1: zeroed pads, D2 / DA / A1 of s_0
@@ -1119,8 +731,7 @@ conv_bwd_ws2_kernel(ConvBwdArgs a) {
     for (int k = 0; k < n; ++k) {
       // ---- P_k: (2) of s_k
       CB_STAMP(0, k, 0);
-      if constexpr (XNC > 0) commit_xn<XC0, XNC>(pxr, lds, tid);
-      const float* a1m = reinterpret_cast<const float*>(lds + L3_A1) + (4 * g) * A1C;
+      const float* a1m = reinterpret_cast<const float*>(lds + LW_A1) + (4 * g) * A1C;
 #pragma unroll 1
       for (int mt = mt0; mt < mt1; ++mt) {
         const int cell = 12 + 16 * mt + col;
@@ -1134,13 +745,13 @@ conv_bwd_ws2_kernel(ConvBwdArgs a) {
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           const int dcell = (ks >> 1) * 11 + (ks & 1);
-          const int o = L3_D2 + d2_slot(cell < 121 ? cell - dcell : 0, g);
+          const int o = LW_D2 + d2_slot(cell < 121 ? cell - dcell : 0, g);
           const bf16x8 bh = lds_load<bf16x8>(lds, o), bm = lds_load<bf16x8>(lds, o + D2P),
                        bl = lds_load<bf16x8>(lds, o + 2 * D2P);
           mfma_x6(w2h[ks], w2m[ks], w2l[ks], bh, bm, bl, big, sml);
         }
         if (keep) {
-          uint8_t* d = lds + L3_D1 + (4 * g) * D1_OC + oy * D1_ROW + ox * 2;
+          uint8_t* d = lds + LW_D1 + (4 * g) * D1_OC + oy * D1_ROW + ox * 2;
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             float v = __fadd_rn(big[rr], sml[rr]);
@@ -1154,16 +765,14 @@ conv_bwd_ws2_kernel(ConvBwdArgs a) {
           }
         }
       }
-      if constexpr (XNC > 0) prefetch_xn<XC0, XNC>(a, r0, smp(k + 1), tid, pxr);
       CB_STAMP(0, k, 1);
       lds_barrier();
-      // ---- Q_k: (3) of s_k (CB_DMA_X: a1 of s_{k+1} -> A1 by this wave's LDS-DMA meanwhile)
+      // ---- Q_k: (3) of s_k
       CB_STAMP(0, k, 2);
-      if (CB_DMA_X && k + 1 < n) dma_a1_wave(a, smp(k + 1), lds, wx, lane);
-#pragma unroll CB_S3_UNROLL
+#pragma unroll 3
       for (int ks = 0; ks < 15; ++ks) {
         const int Gk = 4 * ks + g, oy = Gk / 3, c = Gk - 3 * oy;
-        const int ob = L3_D1 + col * D1_OC + oy * D1_ROW + 16 * c;
+        const int ob = LW_D1 + col * D1_OC + oy * D1_ROW + 16 * c;
         const bf16x8 bh = lds_load<bf16x8>(lds, ob), bm = lds_load<bf16x8>(lds, ob + D1P),
                      bl = lds_load<bf16x8>(lds, ob + 2 * D1P);
         const int oa = xrow3 + oy * 16 * XR + 8 * c;
@@ -1186,7 +795,6 @@ conv_bwd_ws2_kernel(ConvBwdArgs a) {
         }
       }
       CB_STAMP(0, k, 3);
-      if (CB_DMA_X && k + 1 < n) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // a1 of s_{k+1} has landed
       lds_barrier();
     }
 #pragma unroll
@@ -1209,39 +817,36 @@ conv_bwd_ws2_kernel(ConvBwdArgs a) {
     for (int i = 0; i < 2; ++i) acc1[0][i] = acc1[1][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     float b2a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float pa[8];
-    PrefetchXn<XC0> pxr;
+    PrefetchX pxr;
     CB_STAMP(1, 15, 0);
     dma_a1_wave(a, smp(0), lds, wy, lane);
     load_da2(a, smp(0), ty, pa);
-    int r0 = 0;
-    if constexpr (XC0 > 0) {
-      r0 = (int)(a.ctl[CTL_STEP] % a.R);   // after the loads that do not need it
-      prefetch_xn<0, XC0>(a, r0, smp(0), ty, pxr);
-    }
+    const int r0 = (int)(a.ctl[CTL_STEP] % a.R);   // after the loads that do not need it
+    prefetch_x_ws(a, r0, smp(0), ty, pxr);
     CB_STAMP(1, 15, 1);
-    if (CB_W2_LDS) lds_barrier();   // #0
+    lds_barrier();   // #0
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     CB_STAMP(1, 15, 2);
     commit_d2_da(pa, lds, ty, b2a);
     CB_STAMP(1, 15, 3);
-    if (CB_W2_LDS) lds_barrier();   // #0b
+    lds_barrier();   // #0b
     lds_barrier();   // #1
     for (int k = 0; k < n; ++k) {
       // ---- P_k
       CB_STAMP(1, k, 0);
       load_da2(a, smp(k + 1), ty, pa);   // for Q_k
-      if constexpr (XC0 > 0) commit_xn<0, XC0>(pxr, lds, ty);
+      commit_x_ws(pxr, lds, ty);
       step1_wave(lds, wy, lane, acc1);
-      if constexpr (XC0 > 0) prefetch_xn<0, XC0>(a, r0, smp(k + 1), ty, pxr);
+      prefetch_x_ws(a, r0, smp(k + 1), ty, pxr);   // after (1): its registers are not live across it
       CB_STAMP(1, k, 1);
       lds_barrier();
       // ---- Q_k
       CB_STAMP(1, k, 2);
       if (k + 1 < n) {
-        if (!CB_DMA_X) dma_a1_wave(a, smp(k + 1), lds, wy, lane);
+        dma_a1_wave(a, smp(k + 1), lds, wy, lane);
         commit_d2_da(pa, lds, ty, b2a);
         CB_STAMP(1, k, 5);
-        if (!CB_DMA_X) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // a1 of s_{k+1} has landed
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // a1 of s_{k+1} has landed
       }
       CB_STAMP(1, k, 3);
       lds_barrier();
@@ -1259,11 +864,11 @@ conv_bwd_ws2_kernel(ConvBwdArgs a) {
       for (int k = 0; k < 8; ++k) red[ty * 8 + k] = b2a[k];
   }
   __syncthreads();
-  if (tid < 32) {
+  if (tid < 32) {   // conv2 bias: channel oc adds its group's 121 cells in order
     float t = 0.f;
     for (int c = 0; c < 121; ++c) t = __fadd_rn(t, red[((tid >> 3) * 121 + c) * 8 + (tid & 7)]);
     out[SLAB_B2 + tid] = t;
-  } else if (tid >= 64 && tid < 80) {
+  } else if (tid >= 64 && tid < 80) {   // conv1 bias
     const int o = tid - 64;
     float t = 0.f;
     for (int c = 0; c < 128; ++c) t = __fadd_rn(t, red1[o * 128 + c]);
@@ -1357,13 +962,11 @@ hipError_t launch_conv_bwd(const uint8_t* frames, const uint8_t* nvalid, const i
   if (S <= 0) return hipSuccess;
   const int G = conv_bwd_blocks(S);
   ConvBwdArgs a{frames, nvalid, ctl, n, R, a1, da2, W2, S, G, slab, layout};
-  static const char* ws = getenv("ARL_CB_WS");   // wave-specialised form (bit-identical slabs)
-  if (ws != nullptr && ws[0] == '1')
-    hipLaunchKernelGGL(conv_bwd_ws_kernel, dim3(G), dim3(NT2), 0, s, a);
-  else if (ws != nullptr && ws[0] == '2')
-    hipLaunchKernelGGL(conv_bwd_ws2_kernel, dim3(G), dim3(NT2), 0, s, a);
-  else
+  static const char* ws = getenv("ARL_CB_WS");   // "0": the 512-thread kernel (the bitwise test arm)
+  if (ws != nullptr && ws[0] == '0')
     hipLaunchKernelGGL(conv_bwd_kernel, dim3(G), dim3(NT), 0, s, a);
+  else
+    hipLaunchKernelGGL(conv_bwd_ws_kernel, dim3(G), dim3(NT2), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !reduce) return e;
   return launch_conv_reduce(slab, S, gW2, gb2, gW1, gb1, s, layout, nf);

@@ -729,16 +729,16 @@ def test_conv_fwd_two_envs_identical(gpu, tmp_path, n_envs):
     too -- also at 1 and 33 envs; the last arm issues the window step by step
     with the fusion off (ARL_FUSE_RETURNS=0: the separate returns_heads_kernel
     launch), so the fused launch is checked bitwise against the unfused one.
-    ARL_CB_WS=1: conv_bwd.hip's wave-specialised form (1,024 threads, (1) one
-    sample ahead of (2) / (3)) against the 512-thread kernel."""
+    ARL_CB_WS=0: conv_bwd.hip's 512-thread kernel against the default
+    wave-specialised one (1,024 threads, (1) beside (2) and (3) on the other
+    half of each SIMD's waves)."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     outs = []
     for i, arm in enumerate(({"ARL_CONV_EPW": "1", "ARL_FC_BIG": "0"}, {"ARL_CONV_EPW": "2", "ARL_FC_BIG": "0"},
                              {"ARL_CONV_EPW": "1", "ARL_FC_BIG": "1"}, {"ARL_WINDOW_C": "0"},
-                             {"ARL_WINDOW_C": "0", "ARL_FUSE_RETURNS": "0"}, {"ARL_CB_WS": "1"},
-                             {"ARL_CB_WS": "2"})):
+                             {"ARL_WINDOW_C": "0", "ARL_FUSE_RETURNS": "0"}, {"ARL_CB_WS": "0"})):
         f = str(tmp_path / f"arm_{i}.npz")
         env = dict(os.environ, **arm)
         subprocess.run([sys.executable, os.path.join(here, "conv_epw_worker.py"), f, str(n_envs)], env=env,
