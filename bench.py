@@ -867,7 +867,8 @@ def main(a):
              N * (hid_bytes + 12 * A + 12) + (0 if (nat or lstm) else N * (FC_SPLIT + 1) * hid_bytes)),
             ("fc_bwd", "gemm_kernel x2 + reduce_grad_kernel" if nat else "fc_bwd_kernel (dW + da2 + heads dW)",
              lambda i: net.run_stage("fc_bwd", 0, stream=stream), 1, "mfma", 2 * fc_fwd_flop * S),
-            ("conv_bwd", "gemm_kernel x9 + reduce_grad_kernel x3" if nat else "conv_bwd_kernel",
+            ("conv_bwd", "gemm_kernel x9 + reduce_grad_kernel x3" if nat else
+             ("conv_bwd_kernel" if os.environ.get("ARL_CB_WS", "") == "0" else "conv_bwd_ws_kernel"),
              lambda i: net.run_stage("conv_bwd", 0, stream=stream), 1, "mfma", S * conv_bwd_flop),
             # LSTM: the gate kernel (LSTM_XRED: it also forms x from the FC's partials), the
             # truncated-BPTT steps, the gate weight gradients + dfc (a3c_ale.py:50-51,62)

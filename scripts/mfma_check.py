@@ -23,6 +23,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import bench  # noqa: E402
 
 STAGE_OF = [("conv_fwd_kernel", "conv_fwd"), ("fc_fwd_kernel", "fc_fwd"), ("conv_bwd_kernel", "conv_bwd"),
+            ("conv_bwd_ws_kernel", "conv_bwd"),
             ("lstm_gates_kernel", "lstm_gates"), ("lstm_bptt_kernel", "lstm_bptt")]
 
 
